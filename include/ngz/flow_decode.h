@@ -1,0 +1,181 @@
+/*
+ * netgauze_amd — MI355X-native IPFIX (v10) / NetFlow v9 data-record decoder.
+ *
+ * C ABI (plain pointers and sizes, no HIP or torch types in the signatures).
+ * This is the drop-in boundary for the reference's decode path:
+ *
+ *   ngz_ctx                 ≙ netgauze_flow_pkt::codec::FlowInfoCodec
+ *                             (crates/flow-pkt/src/codec.rs:68-73): one per
+ *                             exporter peer, owns the NetFlow v9 and IPFIX
+ *                             TemplatesMap (ipfix.rs:73, netflow.rs).
+ *   ngz_decode_batch        ≙ FlowCollectorActor::decode_pkt applied to each
+ *                             datagram of a batch, in order
+ *                             (crates/flow-service/src/flow_actor.rs:342-411):
+ *                             one FlowInfoCodec::decode (codec.rs:189-220)
+ *                             per datagram -> IpfixPacket::parse
+ *                             (wire/deserializer/ipfix.rs:54-104) /
+ *                             NetFlowV9Packet::parse (netflow.rs:56-114) ->
+ *                             Set::parse -> DataRecord::parse ->
+ *                             Field::parse (generated, generator.rs:2901-2980).
+ *                             Decoded fields land in per-template columnar
+ *                             arrays in HBM instead of Box<[Field]> per record.
+ *   ngz_template_counts     ≙ DecodingTemplate::processed_count /
+ *                             reset_processed_count (ipfix.rs:55-69), read by
+ *                             flow_actor.rs:362-381.
+ *   ngz_dgram_error_json    ≙ serde_json::to_string(&FlowInfoCodecDecoderError)
+ *                             for a datagram whose decode returned Err.
+ *
+ * Error convention (mirrors the reference): the first error aborts the whole
+ * message; template definitions parsed before the error persist.  Return codes
+ * are ints (0 = ok, <0 = NGZ_E_*); no exceptions cross the ABI.  A context is
+ * not thread-safe; distinct contexts may be used concurrently.
+ */
+#ifndef NGZ_FLOW_DECODE_H
+#define NGZ_FLOW_DECODE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NGZ_ABI_VERSION 1
+
+/* return codes */
+#define NGZ_OK 0
+#define NGZ_E_INVALID (-1)     /* bad argument */
+#define NGZ_E_DEVICE (-2)      /* HIP runtime error */
+#define NGZ_E_NOMEM (-3)       /* device allocation failed */
+#define NGZ_E_LIMIT (-4)       /* batch exceeds a compiled limit */
+
+/* per-datagram status (ngz_dgram_hdr.status) */
+#define NGZ_DG_OK 0            /* Ok(Some(FlowInfo)) */
+#define NGZ_DG_NEED_MORE 1     /* Ok(None): shorter than 16 B or than the header length */
+#define NGZ_DG_ERROR 2         /* Err(FlowInfoCodecDecoderError), see ngz_dgram_error_json */
+#define NGZ_DG_UNSUPPORTED 3   /* needs a path not built yet (variable-length data records) */
+
+/* field decode kinds (ngz_field_info.kind); column encodings in DESIGN.md */
+#define NGZ_K_UINT 1      /* big-endian unsigned, reduced size, zero-extended to width */
+#define NGZ_K_TCPFLAGS 2  /* tcpControlBits: u16 (len 1|2) truncated to u8 */
+#define NGZ_K_SINT 3      /* big-endian signed, sign-extended to width */
+#define NGZ_K_BOOL 4      /* u8 0/1 */
+#define NGZ_K_BYTES 5     /* raw wire bytes, width = wire length */
+#define NGZ_K_U256 6      /* <=32 bytes left-aligned, zero-padded to 32 */
+#define NGZ_K_DTMS 7      /* dateTimeMilliseconds -> i64 millis, range-checked */
+#define NGZ_K_DTFRAC 8    /* dateTimeMicro/Nanoseconds -> {u32 secs, u32 nanos} */
+#define NGZ_K_STR 9       /* fixed string: raw bytes, NUL-truncated prefix UTF-8 checked */
+#define NGZ_K_SCOPE32 10  /* NFv9 System/Interface/LineCard scope: reduced u32 (len<=4) */
+#define NGZ_K_VLEN 11     /* variable-length field (not decodable on device yet) */
+#define NGZ_K_FAIL 12     /* always fails with a template-constant error */
+
+typedef struct ngz_ctx ngz_ctx;
+
+/* One batch of datagrams already resident in device memory.  `offsets` and
+ * `lengths` are device arrays of n entries; datagram i is
+ * bytes[offsets[i] .. offsets[i]+lengths[i]).  bytes_size bounds every read. */
+typedef struct {
+    const uint8_t *bytes;
+    uint64_t bytes_size;
+    const uint64_t *offsets;
+    const uint32_t *lengths;
+    uint32_t n;
+} ngz_batch_in;
+
+/* Per-datagram message header + status (device array in ngz_batch_out). */
+typedef struct {
+    uint8_t status;       /* NGZ_DG_* */
+    uint8_t version;      /* 10 = IPFIX, 9 = NetFlow v9, 0 otherwise */
+    uint16_t length;      /* IPFIX header length / NFv9 header count */
+    uint32_t time;        /* IPFIX export_time / NFv9 unix_time (seconds) */
+    uint32_t sequence;    /* sequence_number */
+    uint32_t domain;      /* IPFIX observation_domain_id / NFv9 source_id */
+    uint32_t sys_up_time; /* NFv9 only */
+    uint32_t n_sets;      /* sets parsed (all kinds) */
+    uint64_t err_key;     /* first error, internal encoding; ~0 if none */
+} ngz_dgram_hdr;
+
+/* One data set, in stream order (device array in ngz_batch_out). */
+typedef struct {
+    uint32_t dgram;       /* datagram index */
+    uint16_t set_pos;     /* byte offset of the set header in the datagram */
+    uint16_t slot;        /* batch template slot (ngz_slot_info) */
+    uint32_t rec0;        /* first record's row in the slot's columns */
+    uint32_t n;           /* records */
+} ngz_set_info;
+
+/* Where one template version's records landed. */
+typedef struct {
+    uint32_t version_id;  /* context-unique template version id */
+    uint16_t template_id;
+    uint8_t proto;        /* 10 or 9 */
+    uint8_t n_fields;     /* scope + non-scope fields (columns) */
+    uint32_t n_records;   /* rows filled in this batch */
+    uint32_t capacity;    /* rows allocated (column stride is capacity*width) */
+    uint8_t *columns;     /* device base; column f at columns + capacity*col_off[f] */
+} ngz_slot_info;
+
+typedef struct {
+    uint16_t wire_offset;  /* offset inside the record (0xFFFF after a vlen field) */
+    uint16_t wire_length;  /* declared length (65535 = variable) */
+    uint16_t width;        /* column bytes per record */
+    uint8_t kind;          /* NGZ_K_* */
+    uint8_t is_scope;
+    uint32_t col_off;      /* column offset factor (bytes per row before this column) */
+    uint32_t pen;          /* IE enterprise number (0 = IANA) */
+    uint16_t ie_id;        /* IE id (NFv9 scope ids keep their raw code) */
+    uint16_t reserved;
+} ngz_field_info;
+
+typedef struct {
+    uint32_t n_dgrams;
+    uint32_t n_sets;
+    uint32_t n_slots;
+    uint64_t n_records;          /* all records of all slots (incl. failed messages) */
+    const ngz_dgram_hdr *dgrams; /* device, n_dgrams */
+    const ngz_set_info *sets;    /* device, n_sets */
+    const ngz_slot_info *slots;  /* HOST array, n_slots */
+    uint32_t n_template_dgrams;  /* datagrams with (options) template sets */
+} ngz_batch_out;
+
+/* --- context ------------------------------------------------------------ */
+int ngz_ctx_create(int device, ngz_ctx **out);
+void ngz_ctx_destroy(ngz_ctx *ctx);
+const char *ngz_last_error(ngz_ctx *ctx);
+
+/* --- decode ------------------------------------------------------------- */
+/* Decode every datagram of `in` in order against the context's template
+ * state.  Synchronous: on return the device arrays in *out are complete and
+ * stay valid until the next ngz_decode_batch on this context.
+ * hip_stream: a hipStream_t (NULL = the context's own stream). */
+int ngz_decode_batch(ngz_ctx *ctx, const ngz_batch_in *in, ngz_batch_out *out, void *hip_stream);
+
+/* Same, with the datagrams in host memory (pinned staging, H2D included). */
+int ngz_decode_batch_host(ngz_ctx *ctx, const uint8_t *bytes, uint64_t bytes_size,
+                          const uint64_t *offsets, const uint32_t *lengths, uint32_t n,
+                          ngz_batch_out *out);
+
+/* Column layout of a batch slot (valid with the last batch). */
+int ngz_slot_fields(ngz_ctx *ctx, uint32_t slot, ngz_field_info *fields, uint32_t cap);
+
+/* serde_json text of the datagram's FlowInfoCodecDecoderError (status ERROR).
+ * Returns the string length (excluding NUL) or <0. */
+int ngz_dgram_error_json(ngz_ctx *ctx, uint32_t dgram, char *buf, size_t cap);
+
+/* Template introspection: serde_json text of the current template map for one
+ * protocol (10 or 9): [{"id":..,"scope_field_specifiers":[..],"field_specifiers":[..]},..]. */
+int ngz_templates_json(ngz_ctx *ctx, int proto, char *buf, size_t cap);
+
+/* processed_count of the current templates of one protocol (10 or 9):
+ * fills ids[i], counts[i] for up to cap templates; reset != 0 zeroes them
+ * afterwards (reset_processed_count).  Returns the number of templates. */
+int ngz_template_counts(ngz_ctx *ctx, int proto, uint16_t *ids, uint64_t *counts, uint32_t cap, int reset);
+
+/* Timing of the last ngz_decode_batch: device milliseconds of the record
+ * decode kernel and of the whole device pipeline (HIP events). */
+int ngz_last_timing(ngz_ctx *ctx, float *decode_ms, float *pipeline_ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

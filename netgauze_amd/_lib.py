@@ -1,0 +1,105 @@
+"""ctypes binding of the C ABI in include/ngz/flow_decode.h (libngz.so).
+
+The library is built in-tree by __graft_entry__.build() (hipcc, gfx950).  If
+it is missing this module raises at import: there is no CPU fallback.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libngz.so")
+
+NGZ_DG_OK, NGZ_DG_NEED_MORE, NGZ_DG_ERROR, NGZ_DG_UNSUPPORTED = 0, 1, 2, 3
+(K_UINT, K_TCPFLAGS, K_SINT, K_BOOL, K_BYTES, K_U256, K_DTMS, K_DTFRAC, K_STR,
+ K_SCOPE32, K_VLEN, K_FAIL) = range(1, 13)
+
+# every function the header declares (tests check the exports)
+ABI_FUNCTIONS = [
+    "ngz_ctx_create", "ngz_ctx_destroy", "ngz_last_error", "ngz_decode_batch",
+    "ngz_decode_batch_host", "ngz_slot_fields", "ngz_dgram_error_json",
+    "ngz_templates_json", "ngz_template_counts", "ngz_last_timing",
+]
+
+
+class BatchIn(ctypes.Structure):
+    _fields_ = [("bytes", ctypes.c_void_p), ("bytes_size", ctypes.c_uint64),
+                ("offsets", ctypes.c_void_p), ("lengths", ctypes.c_void_p), ("n", ctypes.c_uint32)]
+
+
+class SlotInfo(ctypes.Structure):
+    _fields_ = [("version_id", ctypes.c_uint32), ("template_id", ctypes.c_uint16),
+                ("proto", ctypes.c_uint8), ("n_fields", ctypes.c_uint8),
+                ("n_records", ctypes.c_uint32), ("capacity", ctypes.c_uint32),
+                ("columns", ctypes.c_void_p)]
+
+
+class BatchOut(ctypes.Structure):
+    _fields_ = [("n_dgrams", ctypes.c_uint32), ("n_sets", ctypes.c_uint32), ("n_slots", ctypes.c_uint32),
+                ("n_records", ctypes.c_uint64), ("dgrams", ctypes.c_void_p), ("sets", ctypes.c_void_p),
+                ("slots", ctypes.POINTER(SlotInfo)), ("n_template_dgrams", ctypes.c_uint32)]
+
+
+class FieldInfo(ctypes.Structure):
+    _fields_ = [("wire_offset", ctypes.c_uint16), ("wire_length", ctypes.c_uint16), ("width", ctypes.c_uint16),
+                ("kind", ctypes.c_uint8), ("is_scope", ctypes.c_uint8), ("col_off", ctypes.c_uint32),
+                ("pen", ctypes.c_uint32), ("ie_id", ctypes.c_uint16), ("reserved", ctypes.c_uint16)]
+
+
+DGRAM_HDR_DTYPE = np.dtype([("status", "u1"), ("version", "u1"), ("length", "<u2"), ("time", "<u4"),
+                            ("sequence", "<u4"), ("domain", "<u4"), ("sys_up_time", "<u4"),
+                            ("n_sets", "<u4"), ("err_key", "<u8")])
+SET_INFO_DTYPE = np.dtype([("dgram", "<u4"), ("set_pos", "<u2"), ("slot", "<u2"), ("rec0", "<u4"), ("n", "<u4")])
+assert DGRAM_HDR_DTYPE.itemsize == 32 and SET_INFO_DTYPE.itemsize == 16
+
+
+def load():
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError("netgauze_amd: %s is missing — run __graft_entry__.build() (hipcc, gfx950); "
+                           "there is no CPU fallback" % LIB_PATH)
+    lib = ctypes.CDLL(LIB_PATH)
+    P, U32, U64, I = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
+    lib.ngz_ctx_create.argtypes = [I, ctypes.POINTER(P)]
+    lib.ngz_ctx_create.restype = I
+    lib.ngz_ctx_destroy.argtypes = [P]
+    lib.ngz_ctx_destroy.restype = None
+    lib.ngz_last_error.argtypes = [P]
+    lib.ngz_last_error.restype = ctypes.c_char_p
+    lib.ngz_decode_batch.argtypes = [P, ctypes.POINTER(BatchIn), ctypes.POINTER(BatchOut), P]
+    lib.ngz_decode_batch.restype = I
+    lib.ngz_decode_batch_host.argtypes = [P, P, U64, P, P, U32, ctypes.POINTER(BatchOut)]
+    lib.ngz_decode_batch_host.restype = I
+    lib.ngz_slot_fields.argtypes = [P, U32, ctypes.POINTER(FieldInfo), U32]
+    lib.ngz_slot_fields.restype = I
+    lib.ngz_dgram_error_json.argtypes = [P, U32, ctypes.c_char_p, ctypes.c_size_t]
+    lib.ngz_dgram_error_json.restype = I
+    lib.ngz_templates_json.argtypes = [P, I, ctypes.c_char_p, ctypes.c_size_t]
+    lib.ngz_templates_json.restype = I
+    lib.ngz_template_counts.argtypes = [P, I, ctypes.POINTER(ctypes.c_uint16), ctypes.POINTER(ctypes.c_uint64), U32, I]
+    lib.ngz_template_counts.restype = I
+    lib.ngz_last_timing.argtypes = [P, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
+    lib.ngz_last_timing.restype = I
+    return lib
+
+
+_HIP = None
+
+
+def hip():
+    """libamdhip64 for device->host copies of result arrays."""
+    global _HIP
+    if _HIP is None:
+        _HIP = ctypes.CDLL("libamdhip64.so")
+        _HIP.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        _HIP.hipMemcpy.restype = ctypes.c_int
+    return _HIP
+
+
+def d2h(dev_ptr, nbytes):
+    out = np.empty(nbytes, dtype=np.uint8)
+    if nbytes:
+        rc = hip().hipMemcpy(out.ctypes.data, dev_ptr, nbytes, 2)  # hipMemcpyDeviceToHost
+        if rc != 0:
+            raise RuntimeError("hipMemcpy D2H failed: %d" % rc)
+    return out

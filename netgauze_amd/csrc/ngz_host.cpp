@@ -1,0 +1,1411 @@
+// Host side of netgauze_amd: the C ABI (include/ngz/flow_decode.h), the
+// per-peer template registry (≙ FlowInfoCodec's two TemplatesMap), host
+// framing of the rare datagrams that carry (options) template sets, and the
+// batch pipeline that drives the HIP kernels in ngz_kernels.hip.
+//
+// Reference (NetGauze v0.13.0, paths relative to the checkout):
+//   crates/flow-pkt/src/codec.rs:68-220            FlowInfoCodec
+//   crates/flow-pkt/src/wire/deserializer/mod.rs:50-67   FieldSpecifier::parse
+//   crates/flow-pkt/src/wire/deserializer/ipfix.rs:133-413  sets / templates
+//   crates/flow-pkt/src/wire/deserializer/netflow.rs:143-388 NFv9 sets / templates
+//   crates/flow-pkt/src/lib.rs:147-154, ie.rs:114-149    length_range checks
+//   crates/ipfix-code-generator/src/generator.rs:390-430,1439-1807  IE lookup, decode rules
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <tuple>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "ngz/flow_decode.h"
+#include "ngz_internal.h"
+
+extern "C" int ngz_launch_frame(const BatchDev *B, const uint8_t *hf_flag, const uint32_t *hf_first, hipStream_t st);
+extern "C" int ngz_scan_temp_bytes(uint64_t n_items, size_t *bytes);
+extern "C" int ngz_launch_scan(void *temp, size_t temp_bytes, const uint32_t *in, uint32_t *out, uint64_t n_items,
+                               hipStream_t st);
+extern "C" int ngz_launch_layout_emit(const BatchDev *B, const uint8_t *hf_flag, const uint32_t *hf_first,
+                                      hipStream_t st);
+extern "C" int ngz_launch_decode(const BatchDev *B, uint32_t grid, uint32_t lds_bytes, hipStream_t st);
+extern "C" int ngz_launch_counts(const BatchDev *B, uint64_t set_cap, hipStream_t st);
+
+namespace {
+
+// ------------------------------------------------------------------------
+// IE registry (generated from the reference XML, tools/gen_ie_registry.py)
+// ------------------------------------------------------------------------
+enum DataType : uint8_t {
+    DT_octetArray = 0, DT_unsigned8, DT_unsigned16, DT_unsigned32, DT_unsigned64, DT_signed8, DT_signed16,
+    DT_signed32, DT_signed64, DT_float32, DT_float64, DT_boolean, DT_macAddress, DT_string, DT_dateTimeSeconds,
+    DT_dateTimeMilliseconds, DT_dateTimeMicroseconds, DT_dateTimeNanoseconds, DT_ipv4Address, DT_ipv6Address,
+    DT_basicList, DT_subTemplateList, DT_subTemplateMultiList, DT_unsigned256,
+};
+
+struct IeRow {
+    uint32_t pen;
+    uint16_t id;
+    uint8_t dtype;
+    uint8_t flags;  // 1 mpls, 2 tcpControlBits, 4 sub-registry
+    const char *name;
+};
+struct VendorRow {
+    uint32_t pen;
+    const char *name;
+};
+
+#define NGZ_IE(pen, id, dt, fl, nm) {pen, (uint16_t)(id), (uint8_t)(dt), (uint8_t)(fl), nm},
+#define NGZ_VENDOR(pen, nm)
+const IeRow kIes[] = {
+#include "ie_table.inc"
+};
+#undef NGZ_IE
+#undef NGZ_VENDOR
+#define NGZ_IE(pen, id, dt, fl, nm)
+#define NGZ_VENDOR(pen, nm) {pen, nm},
+const VendorRow kVendors[] = {
+#include "ie_table.inc"
+};
+#undef NGZ_IE
+#undef NGZ_VENDOR
+
+struct IeIndex {
+    std::unordered_map<uint64_t, const IeRow *> by_key;
+    IeIndex() {
+        for (const auto &r : kIes) by_key[((uint64_t)r.pen << 16) | r.id] = &r;
+    }
+    const IeRow *find(uint32_t pen, uint16_t id) const {
+        auto it = by_key.find(((uint64_t)pen << 16) | id);
+        return it == by_key.end() ? nullptr : it->second;
+    }
+    const char *vendor(uint32_t pen) const {
+        for (const auto &v : kVendors)
+            if (v.pen == pen) return v.name;
+        return nullptr;
+    }
+};
+const IeIndex &ies() {
+    static IeIndex idx;
+    return idx;
+}
+
+// length_range per data type (crates/flow-pkt/src/ie.rs:114-149), half open; {0,0} = unchecked
+void length_range(uint8_t dt, int &lo, int &hi) {
+    static const int r[24][2] = {{0, 0}, {1, 2}, {1, 3}, {1, 5}, {1, 9}, {1, 2}, {1, 3}, {1, 5}, {1, 9}, {4, 5},
+                                 {8, 9}, {1, 2}, {6, 7}, {0, 0}, {4, 5}, {8, 9}, {8, 9}, {8, 9}, {4, 5}, {16, 17},
+                                 {0, 0}, {0, 0}, {0, 0}, {1, 33}};
+    lo = r[dt][0];
+    hi = r[dt][1];
+}
+
+// ------------------------------------------------------------------------
+// Template model
+// ------------------------------------------------------------------------
+enum IeKind : uint8_t { IK_IANA, IK_VENDOR, IK_VENDOR_UNKNOWN, IK_UNKNOWN, IK_SCOPE };
+
+struct Spec {
+    IeKind kind;
+    uint8_t dtype;
+    uint8_t flags;
+    bool scope;
+    uint32_t pen;
+    uint16_t id;  // scope: raw code
+    uint16_t length;
+    const char *name;    // IANA/vendor IE name
+    const char *vendor;  // vendor display name
+};
+
+struct Version {
+    uint8_t proto;  // 10 / 9
+    uint16_t tid;
+    std::vector<Spec> specs;  // scope first
+    uint32_t n_scope;
+    DevPlan plan;
+    std::vector<uint8_t> fail_sub;  // per field: 1 InvalidLength, 2 InvalidPaddingLength, 3 scope InvalidLength
+    uint64_t processed = 0;
+};
+
+std::string json_str(const char *s) {
+    std::string o = "\"";
+    for (const unsigned char *p = (const unsigned char *)s; *p; ++p) {
+        unsigned c = *p;
+        if (c == '"') o += "\\\"";
+        else if (c == '\\') o += "\\\\";
+        else if (c == '\n') o += "\\n";
+        else if (c == '\r') o += "\\r";
+        else if (c == '\t') o += "\\t";
+        else if (c == '\b') o += "\\b";
+        else if (c == '\f') o += "\\f";
+        else if (c < 0x20) {
+            char b[8];
+            snprintf(b, sizeof b, "\\u%04x", c);
+            o += b;
+        } else
+            o += (char)c;
+    }
+    return o + "\"";
+}
+
+std::string ie_json(const Spec &s) {
+    char b[96];
+    switch (s.kind) {
+    case IK_IANA: return json_str(s.name);
+    case IK_VENDOR: return std::string("{") + json_str(s.vendor) + ":" + json_str(s.name) + "}";
+    case IK_VENDOR_UNKNOWN:
+        snprintf(b, sizeof b, ":{\"Unknown\":{\"id\":%u}}}", s.id);
+        return std::string("{") + json_str(s.vendor) + b;
+    case IK_UNKNOWN: snprintf(b, sizeof b, "{\"Unknown\":{\"pen\":%u,\"id\":%u}}", s.pen, s.id); return b;
+    case IK_SCOPE: {
+        static const char *nm[] = {nullptr, "System", "Interface", "LineCard", "Cache", "Template"};
+        if (s.pen == 0 && s.id >= 1 && s.id <= 5) return json_str(nm[s.id]);
+        snprintf(b, sizeof b, "{\"Unknown\":{\"pen\":%u,\"id\":%u}}", s.pen, s.id);
+        return b;
+    }
+    }
+    return "null";
+}
+
+std::string spec_json(const Spec &s) {
+    char b[32];
+    snprintf(b, sizeof b, ",\"length\":%u}", s.length);
+    return "{\"element_id\":" + ie_json(s) + b;
+}
+
+// Decode rule of one field (generator.rs:1439-1807 by data type;
+// netflow.rs:443-475 for NFv9 scope fields) -> device kind and column width.
+void field_rule(const Spec &s, uint8_t &kind, uint16_t &width, uint8_t &fail) {
+    const uint32_t L = s.length;
+    fail = 0;
+    auto failk = [&](uint8_t sub) { kind = NGZ_K_FAIL; width = 0; fail = sub; };
+    if (s.kind == IK_SCOPE) {
+        if (s.pen == 0 && s.id >= 1 && s.id <= 3) {
+            if (L > 4) failk(3);
+            else { kind = NGZ_K_SCOPE32; width = 4; }
+        } else { kind = NGZ_K_BYTES; width = (uint16_t)L; }
+        return;
+    }
+    if (s.kind == IK_UNKNOWN || s.kind == IK_VENDOR_UNKNOWN) {
+        if (L == 0xFFFF) { kind = NGZ_K_VLEN; width = 0; }
+        else { kind = NGZ_K_BYTES; width = (uint16_t)L; }
+        return;
+    }
+    switch (s.dtype) {
+    case DT_octetArray:
+        if (s.flags & 1) { if (L != 3) failk(1); else { kind = NGZ_K_BYTES; width = 3; } return; }
+        [[fallthrough]];
+    case DT_basicList:
+    case DT_subTemplateList:
+    case DT_subTemplateMultiList:
+        if (L == 0xFFFF) { kind = NGZ_K_VLEN; width = 0; }
+        else { kind = NGZ_K_BYTES; width = (uint16_t)L; }
+        return;
+    case DT_string:
+        if (L == 0xFFFF) { kind = NGZ_K_VLEN; width = 0; }
+        else { kind = NGZ_K_STR; width = (uint16_t)L; }
+        return;
+    case DT_unsigned8: if (L != 1) failk(1); else { kind = NGZ_K_UINT; width = 1; } return;
+    case DT_unsigned16:
+        if (L != 1 && L != 2) failk(1);
+        else if (s.flags & 2) { kind = NGZ_K_TCPFLAGS; width = 1; }
+        else { kind = NGZ_K_UINT; width = 2; }
+        return;
+    case DT_unsigned32: if (L > 4) failk(1); else { kind = NGZ_K_UINT; width = 4; } return;
+    case DT_unsigned64: if (L > 8) failk(1); else { kind = NGZ_K_UINT; width = 8; } return;
+    case DT_unsigned256: if (L > 32) failk(1); else { kind = NGZ_K_U256; width = 32; } return;
+    case DT_signed8: if (L != 1) failk(1); else { kind = NGZ_K_SINT; width = 1; } return;
+    case DT_signed16: if (L != 1 && L != 2) failk(1); else { kind = NGZ_K_SINT; width = 2; } return;
+    case DT_signed32:
+        if (L > 8) failk(1);
+        else if (L > 4) failk(2);
+        else { kind = NGZ_K_SINT; width = 4; }
+        return;
+    case DT_signed64: if (L > 8) failk(1); else { kind = NGZ_K_SINT; width = 8; } return;
+    case DT_float32: if (L != 4) failk(1); else { kind = NGZ_K_UINT; width = 4; } return;
+    case DT_float64: if (L != 8) failk(1); else { kind = NGZ_K_UINT; width = 8; } return;
+    case DT_boolean: if (L != 1) failk(1); else { kind = NGZ_K_BOOL; width = 1; } return;
+    case DT_macAddress: if (L != 6) failk(1); else { kind = NGZ_K_BYTES; width = 6; } return;
+    case DT_ipv4Address: if (L != 4) failk(1); else { kind = NGZ_K_UINT; width = 4; } return;
+    case DT_ipv6Address: if (L != 16) failk(1); else { kind = NGZ_K_BYTES; width = 16; } return;
+    case DT_dateTimeSeconds: if (L != 4) failk(1); else { kind = NGZ_K_UINT; width = 4; } return;
+    case DT_dateTimeMilliseconds: if (L != 8) failk(1); else { kind = NGZ_K_DTMS; width = 8; } return;
+    case DT_dateTimeMicroseconds:
+    case DT_dateTimeNanoseconds: if (L != 8) failk(1); else { kind = NGZ_K_DTFRAC; width = 8; } return;
+    }
+    failk(1);
+}
+
+// Choose the LDS pad period minimising ds_read_b32 bank conflicts of the
+// strided per-lane field reads (banks = dword address mod 32, lane groups
+// {0-31},{32-63}; MI355X_MICROARCH.md §LDS).
+uint8_t choose_pad_shift(const DevPlan &P) {
+    const uint32_t rpl = P.rpl, rl = P.rec_len;
+    static const uint8_t cands[] = {31, 8, 7, 6, 5, 4, 3};
+    uint64_t best_cost = ~0ull;
+    uint8_t best = 31;
+    for (uint8_t ps : cands) {
+        uint64_t cost = 0;
+        for (uint32_t f = 0; f < P.n_fields; ++f) {
+            const DevField &fd = P.f[f];
+            if (fd.kind == NGZ_K_FAIL || fd.kind == NGZ_K_VLEN) continue;
+            const uint32_t nd = fd.len <= 4 ? 2 : 3;
+            for (uint32_t sh = 0; sh < 16; sh += 4) {
+                for (uint32_t k = 0; k < rpl; ++k) {
+                    for (uint32_t j = 0; j < nd; ++j) {
+                        for (uint32_t g = 0; g < 2; ++g) {
+                            uint32_t hist[32] = {0};
+                            uint32_t addrs[32];
+                            uint32_t na = 0;
+                            for (uint32_t l = 32 * g; l < 32 * g + 32; ++l) {
+                                const uint32_t x = sh + (l * rpl + k) * rl + fd.off;
+                                const uint32_t q = (x >> 2) + j;
+                                const uint32_t a = q + (q >> ps);
+                                bool dup = false;
+                                for (uint32_t t = 0; t < na; ++t)
+                                    if (addrs[t] == a) { dup = true; break; }
+                                if (dup) continue;
+                                addrs[na++] = a;
+                                hist[a & 31]++;
+                            }
+                            uint32_t m = 0;
+                            for (uint32_t b = 0; b < 32; ++b) m = std::max(m, hist[b]);
+                            cost += m;
+                        }
+                    }
+                }
+            }
+        }
+        if (cost < best_cost) { best_cost = cost; best = ps; }
+    }
+    return best;
+}
+
+void build_plan(Version &v) {
+    DevPlan &P = v.plan;
+    memset(&P, 0, sizeof P);
+    P.proto = v.proto;
+    P.template_id = v.tid;
+    P.pad_shift = 31;
+    v.fail_sub.assign(v.specs.size(), 0);
+    uint32_t off = 0, col = 0, rl = 0;
+    bool vlen = false, devok = v.specs.size() <= NGZ_MAXF;
+    for (size_t i = 0; i < v.specs.size(); ++i) {
+        const Spec &s = v.specs[i];
+        uint8_t kind, fail;
+        uint16_t width;
+        field_rule(s, kind, width, fail);
+        if (v.proto == 10 && s.length == 0xFFFF) vlen = true;
+        // a fixed read of 65535 bytes (IE::Unknown, generator.rs:2971-2974)
+        if (v.proto == 10 && s.length == 0xFFFF && kind != NGZ_K_VLEN) devok = false;
+        // min_record_length counts a vlen field as 1 (ipfix.rs:193-214); NFv9 literal (netflow.rs:201-210)
+        rl += (v.proto == 10 && s.length == 0xFFFF) ? 1 : s.length;
+        if (i < NGZ_MAXF) {
+            DevField &fd = P.f[i];
+            fd.off = (uint16_t)(vlen ? 0xFFFF : off);
+            fd.len = s.length;
+            fd.width = width;
+            fd.kind = kind;
+            fd.flags = fail;
+            fd.col_off = col;
+        }
+        v.fail_sub[i] = fail;
+        off += s.length;
+        col += width;
+    }
+    P.n_fields = (uint16_t)std::min<size_t>(v.specs.size(), NGZ_MAXF);
+    P.rec_len = rl;
+    P.row_bytes = col;
+    P.has_vlen = vlen;
+    for (uint32_t i = 0; i < P.n_fields; ++i)
+        if (P.f[i].kind == NGZ_K_DTMS || P.f[i].kind == NGZ_K_DTFRAC || P.f[i].kind == NGZ_K_STR ||
+            P.f[i].kind == NGZ_K_FAIL)
+            P.has_err = 1;
+    uint32_t rpl = 0;
+    if (devok && !(v.proto == 10 && vlen)) {
+        if (rl <= 64) rpl = 4;
+        else if (rl <= 128) rpl = 2;
+        else if (rl <= NGZ_MAX_REC_LEN) rpl = 1;
+    }
+    P.rpl = (uint8_t)rpl;
+    P.window = rpl ? 64 * rpl : 64;
+    if (rpl) P.pad_shift = choose_pad_shift(P);
+}
+
+uint32_t lds_bytes_for(const DevPlan &P) {
+    if (!P.rpl) return 0;
+    const uint32_t bytes = 16 + P.window * P.rec_len + 16;
+    const uint32_t q = (bytes + 3) / 4 + 4;
+    return 4 * (q + (q >> P.pad_shift) + 4);
+}
+
+struct ErrInfo {  // host-side framing error
+    std::string json;
+};
+
+// ------------------------------------------------------------------------
+// Context
+// ------------------------------------------------------------------------
+template <class T>
+struct DevBuf {
+    T *p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t n) {
+        if (n <= cap) return 0;
+        if (p) hipFree(p);
+        p = nullptr;
+        size_t c = std::max(n, cap + cap / 2);
+        if (hipMalloc((void **)&p, c * sizeof(T) + 64) != hipSuccess) {
+            cap = 0;
+            return -1;
+        }
+        cap = c;
+        return 0;
+    }
+    void release() {
+        if (p) hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+}  // namespace
+
+struct ngz_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string last_error;
+    std::vector<Version> versions;              // append-only
+    std::vector<int32_t> cur[2];                // [proto idx][template id] -> version or -1
+    // batch
+    std::vector<int32_t> slot_version;          // slot -> version
+    std::vector<int32_t> version_slot;          // version -> slot (this batch) or -1
+    DevBuf<DevPlan> d_plans;
+    DevBuf<uint16_t> d_cur_slot;
+    DevBuf<uint32_t> d_tl_key, d_tl_dgram;
+    DevBuf<uint16_t> d_tl_slot;
+    DevBuf<uint8_t> d_hf_flag;
+    DevBuf<uint32_t> d_hf_first;
+    DevBuf<HostSet> d_hf_sets;
+    DevBuf<ngz_dgram_hdr> d_hdr;
+    DevBuf<uint32_t> d_counts, d_scan;
+    DevBuf<uint8_t> d_scan_tmp;
+    DevBuf<SlotRT> d_slots;
+    DevBuf<Chunk> d_chunks;
+    DevBuf<ngz_set_info> d_sets;
+    DevBuf<uint8_t> d_arena;
+    DevBuf<unsigned long long> d_proc;
+    DevBuf<BatchSummary> d_summary;
+    // host staging for ngz_decode_batch_host
+    DevBuf<uint8_t> d_in_bytes;
+    DevBuf<uint64_t> d_in_off;
+    DevBuf<uint32_t> d_in_len;
+    // results of the last batch
+    std::vector<ngz_slot_info> slot_infos;
+    std::vector<SlotRT> slot_rt;
+    std::vector<ErrInfo> host_errors;
+    BatchSummary summary{};
+    ngz_batch_in last_in{};
+    hipEvent_t ev[4]{};
+    float t_decode = 0, t_pipeline = 0;
+    bool plans_dirty = true;
+    uint32_t n_template_dgrams = 0;
+    uint64_t tmpl_gen = 1, uploaded_gen = 0;  // template-state generation vs the device tables
+};
+
+namespace {
+
+int fail(ngz_ctx *c, int code, const char *msg) {
+    if (c) c->last_error = msg;
+    return code;
+}
+
+#define HIPCHK(x)                                                                   \
+    do {                                                                            \
+        hipError_t e_ = (x);                                                        \
+        if (e_ != hipSuccess) {                                                     \
+            ctx->last_error = std::string(#x) + ": " + hipGetErrorString(e_);       \
+            return NGZ_E_DEVICE;                                                    \
+        }                                                                           \
+    } while (0)
+
+uint32_t rd16(const uint8_t *p) { return ((uint32_t)p[0] << 8) | p[1]; }
+uint32_t rd32(const uint8_t *p) { return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3]; }
+
+// ------------------------------------------------------------------------
+// Host framing of a template-bearing datagram (stream order).  Restates
+// Set::parse for template / options-template sets and the framing of data
+// sets; records themselves are decoded on the device.
+// ------------------------------------------------------------------------
+struct HostFrameOut {
+    ngz_dgram_hdr hdr{};
+    std::vector<HostSet> sets;
+    std::vector<std::pair<uint32_t, int32_t>> defs;  // (set position, version) defined here
+};
+
+struct Eof {
+    uint32_t offset, needed, available;
+};
+
+std::string eof_json(const Eof &e) {
+    char b[128];
+    snprintf(b, sizeof b, "{\"Parse\":{\"UnexpectedEof\":{\"offset\":%u,\"needed\":%u,\"available\":%u}}}", e.offset,
+             e.needed, e.available);
+    return b;
+}
+
+struct Cur {
+    const uint8_t *p;
+    uint32_t pos, end;
+    bool need(uint32_t n, Eof &e) const {
+        if (end - pos < n) { e = {pos, n, end - pos}; return false; }
+        return true;
+    }
+};
+
+// FieldSpecifier::parse (deserializer/mod.rs:53-66) -> json error on failure
+bool parse_field_spec(Cur &c, Spec &out, std::string &err) {
+    Eof e;
+    if (!c.need(2, e)) { err = eof_json(e); return false; }
+    uint32_t code = rd16(c.p + c.pos); c.pos += 2;
+    if (!c.need(2, e)) { err = eof_json(e); return false; }
+    uint32_t len = rd16(c.p + c.pos); c.pos += 2;
+    uint32_t pen = 0;
+    if (code & 0x8000) {
+        if (!c.need(4, e)) { err = eof_json(e); return false; }
+        pen = rd32(c.p + c.pos); c.pos += 4;
+        code &= 0x7FFF;
+    }
+    Spec s{};
+    s.pen = pen;
+    s.length = (uint16_t)len;
+    s.scope = false;
+    if (pen == 0) {
+        const IeRow *r = ies().find(0, (uint16_t)code);
+        if (!r) {
+            char b[96];
+            snprintf(b, sizeof b, "{\"IEError\":{\"UndefinedIANAIE\":%u}}", code);
+            err = b;
+            return false;
+        }
+        s.kind = IK_IANA; s.id = (uint16_t)code; s.dtype = r->dtype; s.flags = r->flags; s.name = r->name;
+    } else if (const char *vn = ies().vendor(pen)) {
+        const uint16_t id = (uint16_t)(code & 0x7FFF);
+        const IeRow *r = ies().find(pen, id);
+        s.vendor = vn; s.id = id;
+        if (r) { s.kind = IK_VENDOR; s.dtype = r->dtype; s.flags = r->flags; s.name = r->name; }
+        else { s.kind = IK_VENDOR_UNKNOWN; s.dtype = DT_octetArray; s.flags = 0; }
+    } else {
+        s.kind = IK_UNKNOWN; s.id = (uint16_t)code; s.dtype = DT_octetArray; s.flags = 0;
+    }
+    int lo, hi;
+    length_range(s.dtype, lo, hi);
+    if (hi && !((int)len >= lo && (int)len < hi)) {  // lib.rs:147-154
+        char b[64];
+        snprintf(b, sizeof b, "{\"FieldSpecifierError\":{\"InvalidLength\":[%u,", len);
+        err = std::string(b) + ie_json(s) + "]}}";
+        return false;
+    }
+    out = s;
+    return true;
+}
+
+// ScopeFieldSpecifier::parse (netflow.rs:368-388)
+bool parse_scope_spec(Cur &c, Spec &out, std::string &err) {
+    Eof e;
+    const uint32_t off = c.pos;
+    if (!c.need(2, e)) { err = eof_json(e); return false; }
+    uint32_t code = rd16(c.p + c.pos); c.pos += 2;
+    if (!c.need(2, e)) { err = eof_json(e); return false; }
+    uint32_t len = rd16(c.p + c.pos); c.pos += 2;
+    uint32_t pen = 0;
+    if (code & 0x8000) {
+        if (!c.need(4, e)) { err = eof_json(e); return false; }
+        pen = rd32(c.p + c.pos); c.pos += 4;
+    }
+    Spec s{};
+    s.kind = IK_SCOPE; s.scope = true; s.pen = pen; s.id = (uint16_t)code; s.length = (uint16_t)len;
+    s.dtype = DT_octetArray;
+    if (pen == 0 && (code == 2 || code == 3) && !(len >= 1 && len < 5)) {
+        char b[160];
+        snprintf(b, sizeof b, "{\"InvalidLength\":{\"offset\":%u,\"ie\":%s,\"length\":%u}}", off,
+                 ie_json(s).c_str(), len);
+        err = b;
+        return false;
+    }
+    out = s;
+    return true;
+}
+
+std::string wrap(const char *tag, const std::string &inner) { return std::string("{\"") + tag + "\":" + inner + "}"; }
+
+int32_t define_template(ngz_ctx *ctx, uint8_t proto, uint16_t tid, std::vector<Spec> &&scope, std::vector<Spec> &&fields) {
+    Version v;
+    v.proto = proto;
+    v.tid = tid;
+    v.n_scope = (uint32_t)scope.size();
+    v.specs = std::move(scope);
+    for (auto &f : fields) v.specs.push_back(f);
+    for (uint32_t i = 0; i < v.n_scope; ++i) v.specs[i].scope = true;
+    build_plan(v);
+    ctx->versions.push_back(std::move(v));
+    const int32_t vid = (int32_t)ctx->versions.size() - 1;
+    ctx->cur[proto == 10 ? 0 : 1][tid] = vid;
+    ctx->tmpl_gen++;
+    return vid;
+}
+
+// frame one datagram on the host; `limit` = stop before any set at a position > limit
+void host_frame(ngz_ctx *ctx, const uint8_t *p, uint32_t dl, uint32_t limit, HostFrameOut &o) {
+    ngz_dgram_hdr &h = o.hdr;
+    memset(&h, 0, sizeof h);
+    h.err_key = NGZ_NO_ERR;
+    auto set_err = [&](uint32_t stop, const std::string &json) {
+        ctx->host_errors.push_back({json});
+        h.err_key = ngz_err_key(stop, E_HOST, 0, (uint32_t)ctx->host_errors.size() - 1);
+    };
+    if (dl < 16) { h.status = NGZ_DG_NEED_MORE; return; }
+    const uint32_t ver = rd16(p), len = rd16(p + 2);
+    if (dl < len) { h.status = NGZ_DG_NEED_MORE; return; }
+    h.version = (uint8_t)ver;
+    h.length = (uint16_t)len;
+    char b[256];
+    if (ver == 10) {
+        const char *W = "IpfixParsingError";
+        if (len < 16) {
+            snprintf(b, sizeof b, "{\"InvalidLength\":{\"offset\":2,\"length\":%u}}", len);
+            set_err(2, wrap(W, b));
+            return;
+        }
+        h.time = rd32(p + 4); h.sequence = rd32(p + 8); h.domain = rd32(p + 12);
+        uint32_t pos = 16;
+        while (pos < len) {
+            if (pos > limit) return;
+            const uint32_t rem = len - pos;
+            auto serr = [&](uint32_t stop, const std::string &j) { set_err(stop, wrap(W, wrap("SetParsingError", j))); };
+            if (rem < 2) { serr(pos, eof_json({pos, 2, rem})); return; }
+            const uint32_t id = rd16(p + pos);
+            if (id != 2 && id != 3 && id < 256) {
+                snprintf(b, sizeof b, "{\"InvalidSetId\":{\"offset\":%u,\"id\":%u}}", pos, id);
+                serr(pos, b); return;
+            }
+            if (rem < 4) { serr(pos + 2, eof_json({pos + 2, 2, rem - 2})); return; }
+            const uint32_t sl = rd16(p + pos + 2);
+            if (sl < 4) {
+                snprintf(b, sizeof b, "{\"InvalidLength\":{\"offset\":%u,\"length\":%u}}", pos + 2, sl);
+                serr(pos + 2, b); return;
+            }
+            if (sl - 4 > rem - 4) { serr(pos + 4, eof_json({pos + 4, sl - 4, rem - 4})); return; }
+            h.n_sets++;
+            Cur c{p, pos + 4, pos + sl};
+            if (id == 2) {  // ipfix.rs:162-168, TemplateRecord::parse :384-413
+                while (c.pos < c.end) {
+                    const uint32_t toff = c.pos;
+                    Eof e;
+                    auto terr = [&](const std::string &j) { serr(c.pos, wrap("TemplateRecordError", j)); };
+                    if (!c.need(2, e)) { terr(eof_json(e)); return; }
+                    const uint32_t tid = rd16(p + c.pos);
+                    if (tid < 256) {
+                        snprintf(b, sizeof b, "{\"InvalidTemplateId\":{\"offset\":%u,\"template_id\":%u}}", toff, tid);
+                        terr(b); return;
+                    }
+                    c.pos += 2;
+                    if (!c.need(2, e)) { terr(eof_json(e)); return; }
+                    const uint32_t cnt = rd16(p + c.pos); c.pos += 2;
+                    std::vector<Spec> fields;
+                    for (uint32_t i = 0; i < cnt; ++i) {
+                        Spec s; std::string err;
+                        if (!parse_field_spec(c, s, err)) { terr(wrap("FieldSpecifierError", err)); return; }
+                        fields.push_back(s);
+                    }
+                    o.defs.push_back({toff, define_template(ctx, 10, (uint16_t)tid, {}, std::move(fields))});
+                }
+            } else if (id == 3) {  // ipfix.rs:169-181, OptionsTemplateRecord::parse :276-327
+                while (c.end - c.pos > 3) {
+                    const uint32_t toff = c.pos;
+                    Eof e;
+                    auto terr = [&](const std::string &j) { serr(c.pos, wrap("OptionsTemplateRecordError", j)); };
+                    const uint32_t tid = rd16(p + c.pos);
+                    if (tid < 256) {
+                        snprintf(b, sizeof b, "{\"InvalidTemplateId\":{\"offset\":%u,\"template_id\":%u}}", toff, tid);
+                        terr(b); return;
+                    }
+                    c.pos += 2;
+                    if (!c.need(2, e)) { terr(eof_json(e)); return; }
+                    const uint32_t total = rd16(p + c.pos); c.pos += 2;
+                    const uint32_t soff = c.pos;
+                    if (!c.need(2, e)) { terr(eof_json(e)); return; }
+                    const uint32_t scount = rd16(p + c.pos);
+                    if (scount > total) {
+                        snprintf(b, sizeof b,
+                                 "{\"InvalidScopeFieldsCount\":{\"offset\":%u,\"scope_fields_count\":%u,\"total_fields_count\":%u}}",
+                                 soff, scount, total);
+                        terr(b); return;
+                    }
+                    c.pos += 2;
+                    std::vector<Spec> scope, fields;
+                    for (uint32_t i = 0; i < total; ++i) {
+                        Spec s; std::string err;
+                        if (!parse_field_spec(c, s, err)) { terr(wrap("FieldError", err)); return; }
+                        (i < scount ? scope : fields).push_back(s);
+                    }
+                    o.defs.push_back({toff, define_template(ctx, 10, (uint16_t)tid, std::move(scope), std::move(fields))});
+                }
+                for (uint32_t q = c.pos; q < c.end; ++q)  // check_padding_value (ipfix.rs:240-251)
+                    if (p[q]) {
+                        snprintf(b, sizeof b, "{\"InvalidPaddingValue\":{\"offset\":%u,\"value\":%u}}", q, p[q]);
+                        serr(q, b); return;
+                    }
+            } else {
+                const int32_t vid = ctx->cur[0][id];
+                if (vid < 0) {
+                    snprintf(b, sizeof b, "{\"NoTemplateDefinedFor\":{\"offset\":%u,\"id\":%u}}", pos, id);
+                    serr(pos, b); return;
+                }
+                const Version &v = ctx->versions[vid];
+                const uint32_t ml = v.plan.rec_len;
+                const uint32_t n = ml ? (sl - 4) / ml : 0;
+                if (n && !v.plan.rpl) { h.status = NGZ_DG_UNSUPPORTED; return; }
+                HostSet hs{};
+                hs.set_pos = (uint16_t)pos; hs.reserved2 = (uint32_t)vid; hs.payload_pos = (uint16_t)(pos + 4); hs.n = n;
+                o.sets.push_back(hs);
+            }
+            pos += sl;
+        }
+        return;
+    }
+    if (ver == 9) {
+        const char *W = "NetFlowV9ParingError";
+        if (dl < 20) { set_err(16, wrap(W, eof_json({16, 4, dl - 16}))); return; }
+        h.sys_up_time = rd32(p + 4); h.time = rd32(p + 8); h.sequence = rd32(p + 12); h.domain = rd32(p + 16);
+        const uint32_t count = len;
+        uint32_t i = count, pos = 20;
+        while (i > 0 && dl - pos > 3) {
+            if (pos > limit) return;
+            const uint32_t rem = dl - pos;
+            auto serr = [&](uint32_t stop, const std::string &j) { set_err(stop, wrap(W, wrap("SetError", j))); };
+            const uint32_t id = rd16(p + pos);
+            if (id != 0 && id != 1 && id < 256) {
+                snprintf(b, sizeof b, "{\"InvalidSetId\":{\"offset\":%u,\"id\":%u}}", pos, id);
+                serr(pos, b); return;
+            }
+            const uint32_t sl = rd16(p + pos + 2);
+            if (sl < 4) {
+                snprintf(b, sizeof b, "{\"InvalidLength\":{\"offset\":%u,\"length\":%u}}", pos + 2, sl);
+                serr(pos + 2, b); return;
+            }
+            if (sl - 4 > rem - 4) { serr(pos + 4, eof_json({pos + 4, sl - 4, rem - 4})); return; }
+            h.n_sets++;
+            Cur c{p, pos + 4, pos + sl};
+            if (id == 0) {  // netflow.rs:172-178, TemplateRecord :324-353
+                while (c.pos < c.end) {
+                    const uint32_t toff = c.pos;
+                    Eof e;
+                    auto terr = [&](const std::string &j) { serr(c.pos, wrap("TemplateRecordError", j)); };
+                    if (!c.need(2, e)) { terr(eof_json(e)); return; }
+                    const uint32_t tid = rd16(p + c.pos);
+                    if (tid < 256) {
+                        snprintf(b, sizeof b, "{\"InvalidTemplateId\":{\"offset\":%u,\"template_id\":%u}}", toff, tid);
+                        terr(b); return;
+                    }
+                    c.pos += 2;
+                    if (!c.need(2, e)) { terr(eof_json(e)); return; }
+                    const uint32_t cnt = rd16(p + c.pos); c.pos += 2;
+                    std::vector<Spec> fields;
+                    for (uint32_t k = 0; k < cnt; ++k) {
+                        Spec s; std::string err;
+                        if (!parse_field_spec(c, s, err)) { terr(wrap("FieldSpecifierError", err)); return; }
+                        fields.push_back(s);
+                    }
+                    o.defs.push_back({toff, define_template(ctx, 9, (uint16_t)tid, {}, std::move(fields))});
+                }
+                i -= 1;
+            } else if (id == 1) {  // netflow.rs:179-190, OptionsTemplateRecord :265-310
+                while (c.end - c.pos > 3) {
+                    const uint32_t toff = c.pos;
+                    Eof e;
+                    auto terr = [&](const std::string &j) { serr(c.pos, wrap("OptionsTemplateRecordError", j)); };
+                    const uint32_t tid = rd16(p + c.pos);
+                    if (tid < 256) {
+                        snprintf(b, sizeof b, "{\"InvalidTemplateId\":{\"offset\":%u,\"template_id\":%u}}", toff, tid);
+                        terr(b); return;
+                    }
+                    c.pos += 2;
+                    if (!c.need(2, e)) { terr(eof_json(e)); return; }
+                    const uint32_t slen = rd16(p + c.pos); c.pos += 2;
+                    if (!c.need(2, e)) { terr(eof_json(e)); return; }
+                    const uint32_t olen = rd16(p + c.pos); c.pos += 2;
+                    if (!c.need(slen, e)) { terr(eof_json(e)); return; }
+                    Cur sc{p, c.pos, c.pos + slen};
+                    c.pos += slen;
+                    if (!c.need(olen, e)) { terr(eof_json(e)); return; }
+                    Cur oc{p, c.pos, c.pos + olen};
+                    c.pos += olen;
+                    std::vector<Spec> scope, fields;
+                    while (sc.pos < sc.end) {
+                        Spec s; std::string err;
+                        if (!parse_scope_spec(sc, s, err)) { serr(sc.pos, wrap("OptionsTemplateRecordError", wrap("ScopeFieldSpecifierError", err))); return; }
+                        scope.push_back(s);
+                    }
+                    while (oc.pos < oc.end) {
+                        Spec s; std::string err;
+                        if (!parse_field_spec(oc, s, err)) { serr(oc.pos, wrap("OptionsTemplateRecordError", wrap("FieldSpecifierError", err))); return; }
+                        fields.push_back(s);
+                    }
+                    o.defs.push_back({toff, define_template(ctx, 9, (uint16_t)tid, std::move(scope), std::move(fields))});
+                }
+                for (uint32_t q = c.pos; q < c.end; ++q)
+                    if (p[q]) {
+                        snprintf(b, sizeof b, "{\"InvalidPaddingValue\":{\"offset\":%u,\"value\":%u}}", q, p[q]);
+                        serr(q, b); return;
+                    }
+                i -= 1;
+            } else {
+                const int32_t vid = ctx->cur[1][id];
+                if (vid < 0) {
+                    snprintf(b, sizeof b, "{\"NoTemplateDefinedFor\":{\"offset\":%u,\"id\":%u}}", pos, id);
+                    serr(pos, b); return;
+                }
+                const Version &v = ctx->versions[vid];
+                const uint32_t rl = v.plan.rec_len;
+                const uint32_t n = rl ? (sl - 4) / rl : 0;
+                if (n && !v.plan.rpl) { h.status = NGZ_DG_UNSUPPORTED; return; }
+                HostSet hs{};
+                hs.set_pos = (uint16_t)pos; hs.reserved2 = (uint32_t)vid; hs.payload_pos = (uint16_t)(pos + 4); hs.n = n;
+                o.sets.push_back(hs);
+                for (uint32_t q = pos + 4 + n * rl; q < pos + sl; ++q)
+                    if (p[q]) {
+                        snprintf(b, sizeof b, "{\"InvalidPaddingValue\":{\"offset\":%u,\"value\":%u}}", q, p[q]);
+                        serr(q, b); return;
+                    }
+                if (n > i) {
+                    snprintf(b, sizeof b, "{\"InvalidCount\":{\"offset\":2,\"count\":%u}}", count);
+                    set_err(pos + sl, wrap(W, b)); return;
+                }
+                i -= n;
+            }
+            pos += sl;
+        }
+        return;
+    }
+    snprintf(b, sizeof b, "{\"UnsupportedVersion\":%u}", ver);
+    set_err(0, b);
+}
+
+// ------------------------------------------------------------------------
+// Batch pipeline
+// ------------------------------------------------------------------------
+struct Timeline {
+    std::vector<uint32_t> key, dgram;
+    std::vector<uint16_t> slot;
+};
+
+int assign_slots(ngz_ctx *ctx, const std::vector<int32_t> &extra) {
+    // slots = every current version of both protocols + versions defined in the batch
+    std::vector<int32_t> sv;
+    for (int pi = 0; pi < 2; ++pi)
+        for (uint32_t id = 0; id < 65536; ++id)
+            if (ctx->cur[pi][id] >= 0) sv.push_back(ctx->cur[pi][id]);
+    for (int32_t v : extra) sv.push_back(v);
+    std::sort(sv.begin(), sv.end());
+    sv.erase(std::unique(sv.begin(), sv.end()), sv.end());
+    if (sv.size() > NGZ_MAX_SLOTS) return fail(ctx, NGZ_E_LIMIT, "too many live template versions in one batch");
+    if (sv != ctx->slot_version) {
+        ctx->slot_version = sv;
+        ctx->plans_dirty = true;
+    }
+    ctx->version_slot.assign(ctx->versions.size(), -1);
+    for (size_t s = 0; s < sv.size(); ++s) ctx->version_slot[sv[s]] = (int32_t)s;
+    return 0;
+}
+
+int upload_slots(ngz_ctx *ctx, const std::vector<int32_t> cur_start[2], hipStream_t st) {
+    const size_t S = ctx->slot_version.size();
+    if (ctx->d_plans.ensure(std::max<size_t>(S, 1)) || ctx->d_cur_slot.ensure(2 * 65536))
+        return fail(ctx, NGZ_E_NOMEM, "device alloc (plans)");
+    std::vector<DevPlan> plans(S);
+    for (size_t s = 0; s < S; ++s) plans[s] = ctx->versions[ctx->slot_version[s]].plan;
+    std::vector<uint16_t> cs(2 * 65536, NGZ_NO_SLOT);
+    for (int pi = 0; pi < 2; ++pi)
+        for (uint32_t id = 0; id < 65536; ++id)
+            if (cur_start[pi][id] >= 0) cs[pi * 65536 + id] = (uint16_t)ctx->version_slot[cur_start[pi][id]];
+    HIPCHK(hipMemcpyAsync(ctx->d_plans.p, plans.data(), S * sizeof(DevPlan), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(ctx->d_cur_slot.p, cs.data(), cs.size() * 2, hipMemcpyHostToDevice, st));
+    HIPCHK(hipStreamSynchronize(st));  // host vectors go out of scope
+    ctx->plans_dirty = false;
+    return 0;
+}
+
+struct HostFramed {
+    std::vector<uint8_t> flag;        // per datagram
+    std::vector<uint32_t> first;      // CSR
+    std::vector<HostSet> sets;
+    std::vector<std::pair<uint32_t, ngz_dgram_hdr>> hdrs;
+    Timeline tl;
+};
+
+int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const HostFramed *hf) {
+    const uint32_t N = in->n;
+    const uint32_t S = (uint32_t)ctx->slot_version.size();
+    const uint64_t n_items = (uint64_t)(S + 2) * N + 1;
+    if (n_items > 0x7FFFFFF0ull) return fail(ctx, NGZ_E_LIMIT, "batch too large for the count matrix");
+    size_t scan_tmp = 0;
+    if (ngz_scan_temp_bytes(n_items, &scan_tmp)) return fail(ctx, NGZ_E_DEVICE, "scan temp size");
+    // capacities (overflow is detected on device and retried with more room)
+    uint64_t chunk_cap = std::max<uint64_t>(ctx->d_chunks.cap, in->bytes_size / 4096 + 3ull * N + 1024);
+    uint64_t set_cap = std::max<uint64_t>(ctx->d_sets.cap, 2ull * N + 1024);
+    double ratio = 1.0;
+    uint32_t lds = 64, maxwin_row = 0;
+    for (uint32_t s = 0; s < S; ++s) {
+        const DevPlan &P = ctx->versions[ctx->slot_version[s]].plan;
+        if (P.rec_len) ratio = std::max(ratio, (double)P.row_bytes / (double)P.rec_len);
+        lds = std::max(lds, lds_bytes_for(P));
+        maxwin_row = std::max<uint32_t>(maxwin_row, P.window * P.row_bytes);
+    }
+    uint64_t arena_cap = (uint64_t)(ratio * (double)in->bytes_size) + (uint64_t)S * (maxwin_row + 256) + 4096;
+    arena_cap = std::max<uint64_t>(arena_cap, ctx->d_arena.cap);
+    if (ctx->d_hdr.ensure(std::max<uint32_t>(N, 1)) || ctx->d_counts.ensure(n_items) || ctx->d_scan.ensure(n_items) ||
+        ctx->d_scan_tmp.ensure(scan_tmp + 1) || ctx->d_slots.ensure(std::max<uint32_t>(S, 1)) ||
+        ctx->d_chunks.ensure(chunk_cap) || ctx->d_sets.ensure(set_cap) || ctx->d_arena.ensure(arena_cap) ||
+        ctx->d_proc.ensure(std::max<uint32_t>(S, 1)) || ctx->d_summary.ensure(1))
+        return fail(ctx, NGZ_E_NOMEM, "device alloc (batch)");
+    // host-framed inputs
+    const uint8_t *hf_flag = nullptr;
+    const uint32_t *hf_first = nullptr;
+    BatchDev B{};
+    if (hf) {
+        if (ctx->d_hf_flag.ensure(N) || ctx->d_hf_first.ensure(N + 1) || ctx->d_hf_sets.ensure(hf->sets.size() + 1) ||
+            ctx->d_tl_key.ensure(hf->tl.key.size() + 1) || ctx->d_tl_dgram.ensure(hf->tl.key.size() + 1) ||
+            ctx->d_tl_slot.ensure(hf->tl.key.size() + 1))
+            return fail(ctx, NGZ_E_NOMEM, "device alloc (host framing)");
+        HIPCHK(hipMemcpyAsync(ctx->d_hf_flag.p, hf->flag.data(), N, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(ctx->d_hf_first.p, hf->first.data(), (N + 1) * 4, hipMemcpyHostToDevice, st));
+        if (!hf->sets.empty())
+            HIPCHK(hipMemcpyAsync(ctx->d_hf_sets.p, hf->sets.data(), hf->sets.size() * sizeof(HostSet),
+                                  hipMemcpyHostToDevice, st));
+        if (!hf->tl.key.empty()) {
+            HIPCHK(hipMemcpyAsync(ctx->d_tl_key.p, hf->tl.key.data(), hf->tl.key.size() * 4, hipMemcpyHostToDevice, st));
+            HIPCHK(hipMemcpyAsync(ctx->d_tl_dgram.p, hf->tl.dgram.data(), hf->tl.dgram.size() * 4, hipMemcpyHostToDevice, st));
+            HIPCHK(hipMemcpyAsync(ctx->d_tl_slot.p, hf->tl.slot.data(), hf->tl.slot.size() * 2, hipMemcpyHostToDevice, st));
+        }
+        hf_flag = ctx->d_hf_flag.p;
+        hf_first = ctx->d_hf_first.p;
+        B.tl_key = ctx->d_tl_key.p;
+        B.tl_dgram = ctx->d_tl_dgram.p;
+        B.tl_slot = ctx->d_tl_slot.p;
+        B.tl_n = (uint32_t)hf->tl.key.size();
+        B.hf_first = hf_first;
+        B.hf_sets = ctx->d_hf_sets.p;
+    }
+    B.bytes = in->bytes;
+    B.bytes_size = in->bytes_size;
+    B.offsets = in->offsets;
+    B.lengths = in->lengths;
+    B.n = N;
+    B.n_slots = S;
+    B.plans = ctx->d_plans.p;
+    B.cur_slot = ctx->d_cur_slot.p;
+    B.hdr = ctx->d_hdr.p;
+    B.counts = ctx->d_counts.p;
+    B.scan = ctx->d_scan.p;
+    B.slots = ctx->d_slots.p;
+    B.chunks = ctx->d_chunks.p;
+    B.chunk_cap = ctx->d_chunks.cap;
+    B.sets = ctx->d_sets.p;
+    B.set_cap = ctx->d_sets.cap;
+    B.arena = ctx->d_arena.p;
+    B.arena_cap = ctx->d_arena.cap;
+    B.proc_counts = ctx->d_proc.p;
+    B.summary = ctx->d_summary.p;
+
+    HIPCHK(hipEventRecord(ctx->ev[0], st));
+    HIPCHK(hipMemsetAsync(ctx->d_counts.p, 0, n_items * 4, st));
+    HIPCHK(hipMemsetAsync(ctx->d_summary.p, 0, sizeof(BatchSummary), st));
+    HIPCHK(hipMemsetAsync(ctx->d_proc.p, 0, std::max<uint32_t>(S, 1) * 8, st));
+    if (ngz_launch_frame(&B, hf_flag, hf_first, st)) return fail(ctx, NGZ_E_DEVICE, "k_frame launch");
+    if (hf)
+        for (const auto &ph : hf->hdrs)
+            HIPCHK(hipMemcpyAsync(ctx->d_hdr.p + ph.first, &ph.second, sizeof(ngz_dgram_hdr), hipMemcpyHostToDevice, st));
+    if (ngz_launch_scan(ctx->d_scan_tmp.p, scan_tmp, ctx->d_counts.p, ctx->d_scan.p, n_items, st))
+        return fail(ctx, NGZ_E_DEVICE, "scan launch");
+    if (ngz_launch_layout_emit(&B, hf_flag, hf_first, st)) return fail(ctx, NGZ_E_DEVICE, "layout/emit launch");
+    HIPCHK(hipEventRecord(ctx->ev[1], st));
+    int dev_cus = 256;
+    hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, ctx->device);
+    const uint32_t per_cu = std::max<uint32_t>(1, std::min<uint32_t>(16, 160 * 1024 / std::max<uint32_t>(lds, 1)));
+    const uint32_t grid = (uint32_t)dev_cus * per_cu * 4;
+    if (ngz_launch_decode(&B, grid, lds, st)) return fail(ctx, NGZ_E_DEVICE, "decode launch");
+    HIPCHK(hipEventRecord(ctx->ev[2], st));
+    if (ngz_launch_counts(&B, ctx->d_sets.cap, st)) return fail(ctx, NGZ_E_DEVICE, "counts launch");
+    HIPCHK(hipEventRecord(ctx->ev[3], st));
+    HIPCHK(hipMemcpyAsync(&ctx->summary, ctx->d_summary.p, sizeof(BatchSummary), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    hipEventElapsedTime(&ctx->t_decode, ctx->ev[1], ctx->ev[2]);
+    hipEventElapsedTime(&ctx->t_pipeline, ctx->ev[0], ctx->ev[3]);
+    if (ctx->summary.overflow) {
+        if (ctx->summary.overflow & 1) ctx->d_arena.ensure(ctx->summary.arena_used + 4096);
+        if (ctx->summary.overflow & 2) ctx->d_chunks.ensure(ctx->summary.n_chunks + 1024);
+        if (ctx->summary.overflow & 4) ctx->d_sets.ensure(ctx->summary.n_sets + 1024);
+        return 1;  // retry
+    }
+    return 0;
+}
+
+int finish_batch(ngz_ctx *ctx, const ngz_batch_in *in, ngz_batch_out *out, hipStream_t st) {
+    const uint32_t S = (uint32_t)ctx->slot_version.size();
+    ctx->slot_rt.resize(S);
+    std::vector<unsigned long long> proc(S);
+    if (S) {
+        HIPCHK(hipMemcpyAsync(ctx->slot_rt.data(), ctx->d_slots.p, S * sizeof(SlotRT), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(proc.data(), ctx->d_proc.p, S * 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+    }
+    ctx->slot_infos.resize(S);
+    for (uint32_t s = 0; s < S; ++s) {
+        Version &v = ctx->versions[ctx->slot_version[s]];
+        v.processed += proc[s];
+        ngz_slot_info &si = ctx->slot_infos[s];
+        si.version_id = (uint32_t)ctx->slot_version[s];
+        si.template_id = v.tid;
+        si.proto = v.proto;
+        si.n_fields = (uint8_t)std::min<size_t>(v.specs.size(), 255);
+        si.n_records = ctx->slot_rt[s].total;
+        si.capacity = ctx->slot_rt[s].cap;
+        si.columns = ctx->d_arena.p + ctx->slot_rt[s].block;
+    }
+    out->n_dgrams = in->n;
+    out->n_sets = ctx->summary.n_sets;
+    out->n_slots = S;
+    out->n_records = ctx->summary.n_records_total;
+    out->dgrams = ctx->d_hdr.p;
+    out->sets = ctx->d_sets.p;
+    out->slots = ctx->slot_infos.data();
+    out->n_template_dgrams = ctx->n_template_dgrams;
+    ctx->last_in = *in;
+    return 0;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------
+// C ABI
+// ------------------------------------------------------------------------
+extern "C" {
+
+int ngz_ctx_create(int device, ngz_ctx **out) {
+    if (!out) return NGZ_E_INVALID;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return NGZ_E_DEVICE;
+    if (hipSetDevice(device) != hipSuccess) return NGZ_E_DEVICE;
+    ngz_ctx *ctx = new ngz_ctx();
+    ctx->device = device;
+    ctx->cur[0].assign(65536, -1);
+    ctx->cur[1].assign(65536, -1);
+    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete ctx;
+        return NGZ_E_DEVICE;
+    }
+    for (auto &e : ctx->ev) hipEventCreate(&e);
+    *out = ctx;
+    return NGZ_OK;
+}
+
+void ngz_ctx_destroy(ngz_ctx *ctx) {
+    if (!ctx) return;
+    hipSetDevice(ctx->device);
+    hipStreamSynchronize(ctx->stream);
+    ctx->d_plans.release(); ctx->d_cur_slot.release(); ctx->d_tl_key.release(); ctx->d_tl_dgram.release();
+    ctx->d_tl_slot.release(); ctx->d_hf_flag.release(); ctx->d_hf_first.release(); ctx->d_hf_sets.release();
+    ctx->d_hdr.release(); ctx->d_counts.release(); ctx->d_scan.release(); ctx->d_scan_tmp.release();
+    ctx->d_slots.release(); ctx->d_chunks.release(); ctx->d_sets.release(); ctx->d_arena.release();
+    ctx->d_proc.release(); ctx->d_summary.release(); ctx->d_in_bytes.release(); ctx->d_in_off.release();
+    ctx->d_in_len.release();
+    for (auto &e : ctx->ev) hipEventDestroy(e);
+    hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+const char *ngz_last_error(ngz_ctx *ctx) { return ctx ? ctx->last_error.c_str() : "null context"; }
+
+int ngz_decode_batch(ngz_ctx *ctx, const ngz_batch_in *in, ngz_batch_out *out, void *hip_stream) {
+    if (!ctx || !in || !out) return NGZ_E_INVALID;
+    if (in->n && (!in->bytes || !in->offsets || !in->lengths)) return fail(ctx, NGZ_E_INVALID, "null batch arrays");
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : ctx->stream;
+    ctx->host_errors.clear();
+    memset(out, 0, sizeof *out);
+    // snapshot of the template state at batch start (for the slow path)
+    const size_t nver0 = ctx->versions.size();
+    std::vector<int32_t> cur0[2] = {ctx->cur[0], ctx->cur[1]};
+    int rc = assign_slots(ctx, {});
+    if (rc) return rc;
+    if (ctx->plans_dirty || ctx->uploaded_gen != ctx->tmpl_gen) {
+        rc = upload_slots(ctx, cur0, st);
+        if (rc) return rc;
+        ctx->uploaded_gen = ctx->tmpl_gen;
+    }
+    // fast path: no template sets expected
+    for (int tries = 0; (rc = run_pipeline(ctx, in, st, nullptr)) == 1 && tries < 4; ++tries) {}
+    if (rc < 0) return rc;
+    if (rc == 1) return fail(ctx, NGZ_E_NOMEM, "batch buffers kept overflowing");
+    ctx->n_template_dgrams = ctx->summary.n_host;
+    if (ctx->summary.n_host == 0) return finish_batch(ctx, in, out, st);
+
+    // slow path: frame template-bearing datagrams on the host, in stream order
+    const uint32_t N = in->n;
+    std::vector<ngz_dgram_hdr> hdr(N);
+    std::vector<uint64_t> offs(N);
+    std::vector<uint32_t> lens(N);
+    HIPCHK(hipMemcpyAsync(hdr.data(), ctx->d_hdr.p, N * sizeof(ngz_dgram_hdr), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(offs.data(), in->offsets, N * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(lens.data(), in->lengths, N * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    std::vector<uint32_t> host_idx;
+    for (uint32_t d = 0; d < N; ++d)
+        if (hdr[d].status == NGZ_FR_HOST) host_idx.push_back(d);
+    std::vector<std::vector<uint8_t>> dbytes(host_idx.size());
+    for (size_t i = 0; i < host_idx.size(); ++i) {
+        const uint32_t d = host_idx[i];
+        dbytes[i].resize(lens[d] + 8);
+        HIPCHK(hipMemcpy(dbytes[i].data(), in->bytes + offs[d], lens[d], hipMemcpyDeviceToHost));
+    }
+    ctx->n_template_dgrams = (uint32_t)host_idx.size();
+    std::vector<uint32_t> limit(host_idx.size(), 0xFFFFFFFFu);
+    for (int round = 0; round < 16; ++round) {
+        // roll the template state back to the batch start
+        ctx->uploaded_gen = 0;  // device tables will describe the batch start, not the end state
+        ctx->versions.resize(nver0);
+        ctx->cur[0] = cur0[0];
+        ctx->cur[1] = cur0[1];
+        ctx->host_errors.clear();
+        HostFramed hf;
+        hf.flag.assign(N, 0);
+        hf.first.assign(N + 1, 0);
+        std::vector<std::vector<std::pair<uint32_t, int32_t>>> defs(host_idx.size());
+        std::vector<std::pair<uint32_t, uint32_t>> tl_entries;  // (version, dgram)
+        std::vector<std::pair<uint32_t, std::vector<HostSet>>> per;
+        for (size_t i = 0; i < host_idx.size(); ++i) {
+            const uint32_t d = host_idx[i];
+            HostFrameOut o;
+            host_frame(ctx, dbytes[i].data(), lens[d], limit[i], o);
+            hf.flag[d] = 1;
+            hf.hdrs.push_back({d, o.hdr});
+            per.push_back({d, std::move(o.sets)});
+            defs[i] = o.defs;
+            for (auto &df : o.defs) tl_entries.push_back({(uint32_t)df.second, d});
+        }
+        std::vector<int32_t> extra;
+        for (auto &t : tl_entries) extra.push_back((int32_t)t.first);
+        for (int pi = 0; pi < 2; ++pi)
+            for (uint32_t id = 0; id < 65536; ++id)
+                if (cur0[pi][id] >= 0) extra.push_back(cur0[pi][id]);
+        rc = assign_slots(ctx, extra);
+        if (rc) return rc;
+        // slot ids inside host sets are version ids until now
+        for (auto &pr : per)
+            for (auto &hs : pr.second) hs.slot = (uint16_t)ctx->version_slot[hs.reserved2];
+        uint32_t at = 0, pi = 0;
+        for (uint32_t d = 0; d < N; ++d) {
+            hf.first[d] = at;
+            if (pi < per.size() && per[pi].first == d) {
+                for (auto &hs : per[pi].second) hf.sets.push_back(hs);
+                at += (uint32_t)per[pi].second.size();
+                ++pi;
+            }
+        }
+        hf.first[N] = at;
+        // timeline sorted by (proto<<16|id, dgram)
+        std::vector<std::tuple<uint32_t, uint32_t, uint16_t>> tl;
+        for (auto &t : tl_entries) {
+            const Version &v = ctx->versions[t.first];
+            tl.emplace_back(((v.proto == 10 ? 0u : 1u) << 16) | v.tid, t.second, (uint16_t)ctx->version_slot[t.first]);
+        }
+        std::stable_sort(tl.begin(), tl.end(), [](const auto &a, const auto &b) {
+            return std::get<0>(a) != std::get<0>(b) ? std::get<0>(a) < std::get<0>(b) : std::get<1>(a) < std::get<1>(b);
+        });
+        // several definitions of one id inside one datagram: keep the last
+        std::vector<std::tuple<uint32_t, uint32_t, uint16_t>> tl2;
+        for (auto &e : tl) {
+            if (!tl2.empty() && std::get<0>(tl2.back()) == std::get<0>(e) && std::get<1>(tl2.back()) == std::get<1>(e))
+                tl2.back() = e;
+            else
+                tl2.push_back(e);
+        }
+        for (auto &e : tl2) {
+            hf.tl.key.push_back(std::get<0>(e));
+            hf.tl.dgram.push_back(std::get<1>(e));
+            hf.tl.slot.push_back(std::get<2>(e));
+        }
+        rc = upload_slots(ctx, cur0, st);
+        if (rc) return rc;
+        if (getenv("NGZ_DEBUG")) {
+            fprintf(stderr, "[ngz] slow path round %d: host dgrams %zu, slots %zu, timeline %zu\n", round,
+                    host_idx.size(), ctx->slot_version.size(), hf.tl.key.size());
+            for (size_t i = 0; i < hf.tl.key.size(); ++i)
+                fprintf(stderr, "[ngz]   tl key %u dgram %u slot %u\n", hf.tl.key[i], hf.tl.dgram[i], hf.tl.slot[i]);
+            for (size_t s2 = 0; s2 < ctx->slot_version.size(); ++s2) {
+                const DevPlan &P = ctx->versions[ctx->slot_version[s2]].plan;
+                fprintf(stderr, "[ngz]   slot %zu version %d tid %u rec_len %u rpl %u nf %u ps %u\n", s2,
+                        ctx->slot_version[s2], P.template_id, P.rec_len, P.rpl, P.n_fields, P.pad_shift);
+            }
+        }
+        for (int tries = 0; (rc = run_pipeline(ctx, in, st, &hf)) == 1 && tries < 4; ++tries) {}
+        if (rc < 0) return rc;
+        if (rc == 1) return fail(ctx, NGZ_E_NOMEM, "batch buffers kept overflowing");
+        // a device-found record error that precedes a template set voids that
+        // definition (the reference stops parsing the message there)
+        std::vector<ngz_dgram_hdr> h2(N);
+        HIPCHK(hipMemcpy(h2.data(), ctx->d_hdr.p, N * sizeof(ngz_dgram_hdr), hipMemcpyDeviceToHost));
+        bool redo = false;
+        for (size_t i = 0; i < host_idx.size(); ++i) {
+            const uint64_t k = h2[host_idx[i]].err_key;
+            if (k == NGZ_NO_ERR) continue;
+            const uint32_t stop = (uint32_t)(k >> 48);
+            const uint32_t code = (uint32_t)(k >> 40) & 0xFF;
+            if (code == E_HOST) continue;
+            bool later_def = false;
+            for (auto &df : defs[i])
+                if (df.first > stop) later_def = true;
+            if (later_def && limit[i] != stop) {
+                limit[i] = stop;
+                redo = true;
+            }
+        }
+        if (!redo) break;
+    }
+    return finish_batch(ctx, in, out, st);
+}
+
+int ngz_decode_batch_host(ngz_ctx *ctx, const uint8_t *bytes, uint64_t bytes_size, const uint64_t *offsets,
+                          const uint32_t *lengths, uint32_t n, ngz_batch_out *out) {
+    if (!ctx || !out || (n && (!bytes || !offsets || !lengths))) return NGZ_E_INVALID;
+    HIPCHK(hipSetDevice(ctx->device));
+    if (ctx->d_in_bytes.ensure(bytes_size + 16) || ctx->d_in_off.ensure(n + 1) || ctx->d_in_len.ensure(n + 1))
+        return fail(ctx, NGZ_E_NOMEM, "device alloc (input)");
+    HIPCHK(hipMemcpyAsync(ctx->d_in_bytes.p, bytes, bytes_size, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipMemcpyAsync(ctx->d_in_off.p, offsets, n * 8ull, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipMemcpyAsync(ctx->d_in_len.p, lengths, n * 4ull, hipMemcpyHostToDevice, ctx->stream));
+    ngz_batch_in in{ctx->d_in_bytes.p, bytes_size, ctx->d_in_off.p, ctx->d_in_len.p, n};
+    return ngz_decode_batch(ctx, &in, out, nullptr);
+}
+
+int ngz_slot_fields(ngz_ctx *ctx, uint32_t slot, ngz_field_info *fields, uint32_t cap) {
+    if (!ctx || slot >= ctx->slot_version.size()) return NGZ_E_INVALID;
+    const Version &v = ctx->versions[ctx->slot_version[slot]];
+    const uint32_t n = (uint32_t)v.specs.size();
+    for (uint32_t i = 0; i < n && i < cap; ++i) {
+        ngz_field_info &f = fields[i];
+        const Spec &s = v.specs[i];
+        memset(&f, 0, sizeof f);
+        f.wire_length = s.length;
+        f.is_scope = i < v.n_scope;
+        f.pen = s.pen;
+        f.ie_id = s.id;
+        if (i < NGZ_MAXF) {
+            f.wire_offset = v.plan.f[i].off;
+            f.width = v.plan.f[i].width;
+            f.kind = v.plan.f[i].kind;
+            f.col_off = v.plan.f[i].col_off;
+        }
+    }
+    return (int)n;
+}
+
+int ngz_last_timing(ngz_ctx *ctx, float *decode_ms, float *pipeline_ms) {
+    if (!ctx) return NGZ_E_INVALID;
+    if (decode_ms) *decode_ms = ctx->t_decode;
+    if (pipeline_ms) *pipeline_ms = ctx->t_pipeline;
+    return 0;
+}
+
+int ngz_template_counts(ngz_ctx *ctx, int proto, uint16_t *ids, uint64_t *counts, uint32_t cap, int reset) {
+    if (!ctx || (proto != 9 && proto != 10)) return NGZ_E_INVALID;
+    const int pi = proto == 10 ? 0 : 1;
+    uint32_t n = 0;
+    for (uint32_t id = 0; id < 65536; ++id) {
+        const int32_t v = ctx->cur[pi][id];
+        if (v < 0) continue;
+        if (n < cap) {
+            if (ids) ids[n] = (uint16_t)id;
+            if (counts) counts[n] = ctx->versions[v].processed;
+        }
+        if (reset) ctx->versions[v].processed = 0;
+        ++n;
+    }
+    return (int)n;
+}
+
+int ngz_templates_json(ngz_ctx *ctx, int proto, char *buf, size_t cap) {
+    if (!ctx || (proto != 9 && proto != 10)) return NGZ_E_INVALID;
+    const int pi = proto == 10 ? 0 : 1;
+    std::string s = "[";
+    bool first = true;
+    for (uint32_t id = 0; id < 65536; ++id) {
+        const int32_t vid = ctx->cur[pi][id];
+        if (vid < 0) continue;
+        const Version &v = ctx->versions[vid];
+        if (!first) s += ",";
+        first = false;
+        char b[64];
+        snprintf(b, sizeof b, "{\"id\":%u,", id);
+        s += b;
+        s += "\"scope_field_specifiers\":[";
+        for (uint32_t i = 0; i < v.n_scope; ++i) s += (i ? "," : "") + spec_json(v.specs[i]);
+        s += "],\"field_specifiers\":[";
+        for (uint32_t i = v.n_scope; i < v.specs.size(); ++i) s += (i > v.n_scope ? "," : "") + spec_json(v.specs[i]);
+        s += "]}";
+    }
+    s += "]";
+    if (buf && cap) {
+        const size_t m = std::min(cap - 1, s.size());
+        memcpy(buf, s.data(), m);
+        buf[m] = 0;
+    }
+    return (int)s.size();
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------------
+// Error rendering (serde_json text of FlowInfoCodecDecoderError)
+// ------------------------------------------------------------------------
+namespace {
+
+std::string utf8_error_msg(const uint8_t *s, uint32_t n) {
+    // core::str::Utf8Error Display
+    uint32_t i = 0;
+    while (i < n) {
+        const uint32_t c = s[i];
+        if (c < 0x80) { ++i; continue; }
+        uint32_t need, lo = 0x80, hi = 0xBF;
+        if (c >= 0xC2 && c <= 0xDF) need = 1;
+        else if (c >= 0xE0 && c <= 0xEF) { need = 2; if (c == 0xE0) lo = 0xA0; if (c == 0xED) hi = 0x9F; }
+        else if (c >= 0xF0 && c <= 0xF4) { need = 3; if (c == 0xF0) lo = 0x90; if (c == 0xF4) hi = 0x8F; }
+        else {
+            char b[96];
+            snprintf(b, sizeof b, "invalid utf-8 sequence of 1 bytes from index %u", i);
+            return b;
+        }
+        uint32_t t = 1;
+        for (; t <= need; ++t) {
+            if (i + t >= n) {
+                char b[96];
+                snprintf(b, sizeof b, "incomplete utf-8 byte sequence from index %u", i);
+                return b;
+            }
+            const uint32_t bb = s[i + t];
+            const uint32_t l2 = t == 1 ? lo : 0x80, h2 = t == 1 ? hi : 0xBF;
+            if (bb < l2 || bb > h2) {
+                char b[96];
+                snprintf(b, sizeof b, "invalid utf-8 sequence of %u bytes from index %u", t, i);
+                return b;
+            }
+        }
+        i += need + 1;
+    }
+    return "";
+}
+
+}  // namespace
+
+extern "C" int ngz_dgram_error_json(ngz_ctx *ctx, uint32_t dgram, char *buf, size_t cap) {
+    if (!ctx || dgram >= ctx->last_in.n) return NGZ_E_INVALID;
+    ngz_dgram_hdr h;
+    if (hipMemcpy(&h, ctx->d_hdr.p + dgram, sizeof h, hipMemcpyDeviceToHost) != hipSuccess) return NGZ_E_DEVICE;
+    if (h.err_key == NGZ_NO_ERR) return NGZ_E_INVALID;
+    const uint32_t stop = (uint32_t)(h.err_key >> 48);
+    const uint32_t code = (uint32_t)(h.err_key >> 40) & 0xFF;
+    const uint32_t a = (uint32_t)(h.err_key >> 24) & 0xFFFF;
+    const uint32_t bval = (uint32_t)h.err_key & 0xFFFFFF;
+    std::string s;
+    char b[256];
+    if (code == E_HOST) {
+        s = bval < ctx->host_errors.size() ? ctx->host_errors[bval].json : "null";
+    } else {
+        uint64_t off = 0;
+        uint32_t len = 0;
+        hipMemcpy(&off, ctx->last_in.offsets + dgram, 8, hipMemcpyDeviceToHost);
+        hipMemcpy(&len, ctx->last_in.lengths + dgram, 4, hipMemcpyDeviceToHost);
+        std::vector<uint8_t> p(len + 16, 0);
+        hipMemcpy(p.data(), ctx->last_in.bytes + off, len, hipMemcpyDeviceToHost);
+        const bool v10 = h.version == 10;
+        const char *W = v10 ? "IpfixParsingError" : "NetFlowV9ParingError";
+        const char *SW = v10 ? "SetParsingError" : "SetError";
+        auto set_wrap = [&](const std::string &j) { return wrap(W, wrap(SW, j)); };
+        switch (code) {
+        case E_CODEC_UNSUPPORTED_VERSION: snprintf(b, sizeof b, "{\"UnsupportedVersion\":%u}", a); s = b; break;
+        case E_IPFIX_INVALID_LENGTH:
+            snprintf(b, sizeof b, "{\"InvalidLength\":{\"offset\":2,\"length\":%u}}", bval); s = wrap(W, b); break;
+        case E_HDR_EOF: s = wrap(W, eof_json({stop, a, bval})); break;
+        case E_SET_EOF_ID: case E_SET_EOF_LEN: s = set_wrap(eof_json({stop, a, bval})); break;
+        case E_SET_EOF_BODY: s = set_wrap(eof_json({stop, a, bval})); break;
+        case E_SET_INVALID_ID: snprintf(b, sizeof b, "{\"InvalidSetId\":{\"offset\":%u,\"id\":%u}}", stop, a); s = set_wrap(b); break;
+        case E_SET_INVALID_LENGTH:
+            snprintf(b, sizeof b, "{\"InvalidLength\":{\"offset\":%u,\"length\":%u}}", stop, bval); s = set_wrap(b); break;
+        case E_SET_NO_TEMPLATE:
+            snprintf(b, sizeof b, "{\"NoTemplateDefinedFor\":{\"offset\":%u,\"id\":%u}}", stop, a); s = set_wrap(b); break;
+        case E_SET_PADDING:
+            snprintf(b, sizeof b, "{\"InvalidPaddingValue\":{\"offset\":%u,\"value\":%u}}", stop, bval); s = set_wrap(b); break;
+        case E_NF_INVALID_COUNT:
+            snprintf(b, sizeof b, "{\"InvalidCount\":{\"offset\":2,\"count\":%u}}", bval); s = wrap(W, b); break;
+        case E_REC_DTMS: case E_REC_DTFRAC: case E_REC_UTF8: case E_REC_FAIL: {
+            // find the set and version holding the failing field
+            uint32_t nsets = ctx->summary.n_sets;
+            std::vector<ngz_set_info> sets(nsets);
+            hipMemcpy(sets.data(), ctx->d_sets.p, nsets * sizeof(ngz_set_info), hipMemcpyDeviceToHost);
+            const Version *v = nullptr;
+            for (auto &si : sets)
+                if (si.dgram == dgram && si.set_pos < stop && stop < si.set_pos + rd16(p.data() + si.set_pos + 2))
+                    v = &ctx->versions[ctx->slot_version[si.slot]];
+            if (!v || a >= v->specs.size()) { s = "null"; break; }
+            const Spec &sp = v->specs[a];
+            std::string fe;
+            const char *name = sp.name ? sp.name : "";
+            if (code == E_REC_DTMS) {
+                unsigned long long ms = 0;
+                for (int i = 0; i < 8; ++i) ms = (ms << 8) | p[stop + i];
+                snprintf(b, sizeof b, "{\"InvalidTimestampMillis\":{\"offset\":%u,\"ie_name\":%s,\"millis\":%llu}}", stop,
+                         json_str(name).c_str(), ms);
+                fe = b;
+            } else if (code == E_REC_DTFRAC) {
+                snprintf(b, sizeof b,
+                         "{\"InvalidTimestampFraction\":{\"offset\":%u,\"ie_name\":%s,\"seconds\":%u,\"fraction\":%u}}",
+                         stop, json_str(name).c_str(), rd32(p.data() + stop), rd32(p.data() + stop + 4));
+                fe = b;
+            } else if (code == E_REC_UTF8) {
+                uint32_t n = 0;
+                while (n < sp.length && p[stop + n]) ++n;
+                snprintf(b, sizeof b, "{\"Utf8Error\":{\"offset\":%u,\"ie_name\":%s,\"error\":", stop, json_str(name).c_str());
+                fe = std::string(b) + json_str(utf8_error_msg(p.data() + stop, n).c_str()) + "}}";
+            } else {
+                const uint8_t sub = v->fail_sub[a];
+                if (sub == 3) {
+                    snprintf(b, sizeof b, "{\"ScopeFieldError\":{\"InvalidLength\":{\"offset\":%u,\"length\":%u}}}", stop, sp.length);
+                    s = set_wrap(wrap("DataRecordError", b));
+                    break;
+                }
+                if (sub == 2)
+                    snprintf(b, sizeof b, "{\"Parse\":{\"InvalidPaddingLength\":{\"offset\":%u,\"requested\":%u,\"ret_len\":4}}}",
+                             stop, sp.length);
+                else
+                    snprintf(b, sizeof b, "{\"InvalidLength\":{\"offset\":%u,\"ie_name\":%s,\"length\":%u}}", stop,
+                             json_str(name).c_str(), sp.length);
+                fe = b;
+            }
+            if (sp.kind == IK_VENDOR) fe = wrap((std::string(sp.vendor) + "Error").c_str(), fe);
+            s = set_wrap(wrap("DataRecordError", wrap("FieldError", fe)));
+            break;
+        }
+        default: s = "null";
+        }
+    }
+    if (buf && cap) {
+        const size_t m = std::min(cap - 1, s.size());
+        memcpy(buf, s.data(), m);
+        buf[m] = 0;
+    }
+    return (int)s.size();
+}

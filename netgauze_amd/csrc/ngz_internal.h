@@ -1,0 +1,145 @@
+// Internal structures shared by the host orchestration (ngz_host.cpp) and the
+// HIP kernels (ngz_kernels.hip).  Not part of the C ABI.
+#pragma once
+#include <stdint.h>
+
+#define NGZ_MAXF 128          // fields (scope + non-scope) a device plan can hold
+#define NGZ_MAX_SLOTS 1024    // template versions live in one batch
+#define NGZ_NO_SLOT 0xFFFFu
+#define NGZ_NO_ERR (~0ull)
+#define NGZ_MAX_REC_LEN 2048  // longest fixed record the LDS-staged decode takes
+
+// datagram frame state (k_frame -> host)
+#define NGZ_FR_OK 0
+#define NGZ_FR_NEED_MORE 1
+#define NGZ_FR_ERROR 2
+#define NGZ_FR_UNSUPPORTED 3
+#define NGZ_FR_HOST 4        // contains template sets: framed on the host
+
+// Error codes packed into the 64-bit error key.  Key layout (min wins =
+// first error in parse order):
+//   [63:48] stop position in the datagram (cursor where parsing stopped)
+//   [47:40] code
+//   [39:24] a (field index / set id / ...)
+//   [23:0]  b (length / count / value / ...)
+enum NgzErr : uint32_t {
+    E_NONE = 0,
+    E_CODEC_UNSUPPORTED_VERSION = 1,  // a = version
+    E_IPFIX_INVALID_LENGTH = 2,       // b = length
+    E_HDR_EOF = 3,                    // packet-level UnexpectedEof, b = available
+    E_SET_EOF_ID = 4,                 // peek set id, b = available
+    E_SET_EOF_LEN = 5,                // peek set length, b = available
+    E_SET_INVALID_ID = 6,             // a = id
+    E_SET_INVALID_LENGTH = 7,         // b = length
+    E_SET_EOF_BODY = 8,               // take_slice, a = needed, b = available
+    E_SET_NO_TEMPLATE = 9,            // a = id
+    E_SET_PADDING = 10,               // b = value
+    E_NF_INVALID_COUNT = 11,          // b = count
+    E_REC_DTMS = 12,                  // a = field index (value re-read by host)
+    E_REC_DTFRAC = 13,                // a = field index
+    E_REC_UTF8 = 14,                  // a = field index
+    E_REC_FAIL = 15,                  // a = field index (template-constant failure)
+    E_HOST = 16,                      // host-framed datagram error: b = index in host error table
+};
+
+static inline __host__ __device__ uint64_t ngz_err_key(uint32_t stop, uint32_t code, uint32_t a, uint32_t b) {
+    return ((uint64_t)(stop & 0xFFFF) << 48) | ((uint64_t)(code & 0xFF) << 40) | ((uint64_t)(a & 0xFFFF) << 24) |
+           (uint64_t)(b & 0xFFFFFF);
+}
+
+struct DevField {        // 16 B
+    uint16_t off;        // offset inside the record
+    uint16_t len;        // wire length
+    uint16_t width;      // column width
+    uint8_t kind;        // NGZ_K_*
+    uint8_t flags;
+    uint32_t col_off;    // bytes per row before this column
+    uint32_t reserved;
+};
+
+struct DevPlan {
+    uint32_t rec_len;    // exact wire bytes per record (0 = no records)
+    uint32_t row_bytes;  // sum of column widths
+    uint16_t n_fields;
+    uint8_t proto;       // 10 / 9
+    uint8_t rpl;         // records per lane: 4, 2, 1; 0 = not device-decodable
+    uint8_t pad_shift;   // LDS: one pad dword per 2^pad_shift dwords (31 = none)
+    uint8_t has_vlen;
+    uint8_t has_err;
+    uint8_t reserved0;
+    uint32_t window;     // records per chunk window = 64*rpl
+    uint32_t template_id;
+    uint32_t reserved1[2];
+    DevField f[NGZ_MAXF];
+};
+
+struct SlotRT {          // per batch slot, computed on device by k_layout
+    uint64_t block;      // byte offset of the slot's columns in the arena
+    uint32_t cap;        // rows allocated
+    uint32_t total;      // rows used
+    uint32_t base;       // first element of the slot's row in the scanned count matrix
+    uint32_t reserved;
+};
+
+struct Chunk {           // 32 B, one wave of work
+    uint64_t src;        // batch byte offset of the first record
+    uint32_t rec0;       // first row in the slot's columns
+    uint32_t dgram;
+    uint16_t n;          // records (0 = empty slot)
+    uint16_t slot;
+    uint16_t pos0;       // first record's offset inside the datagram
+    uint16_t reserved;
+    uint32_t reserved2;
+};
+
+// host-framed data set (template-bearing datagrams framed on the host)
+struct HostSet {
+    uint16_t set_pos;
+    uint16_t slot;
+    uint16_t payload_pos; // offset of the first record
+    uint16_t reserved;
+    uint32_t n;
+    uint32_t reserved2;
+};
+
+struct BatchSummary {    // device -> host at the end of a batch
+    uint32_t n_records_total;
+    uint32_t n_chunks;
+    uint32_t n_sets;
+    uint32_t n_host;        // datagrams needing host framing (template sets)
+    uint32_t overflow;      // 1: arena, 2: chunks, 4: sets
+    uint32_t n_unsupported;
+    uint64_t arena_used;
+};
+
+struct BatchDev {        // device pointers of one batch
+    const uint8_t *bytes;
+    uint64_t bytes_size;
+    const uint64_t *offsets;
+    const uint32_t *lengths;
+    uint32_t n;
+    uint32_t n_slots;
+    const DevPlan *plans;      // [n_slots]
+    const uint16_t *cur_slot;  // [2][65536]: proto index 0 = v10, 1 = v9
+    // timeline of template definitions inside this batch (slow path)
+    const uint32_t *tl_key;    // (proto_idx<<16)|id, sorted by (key, dgram)
+    const uint32_t *tl_dgram;
+    const uint16_t *tl_slot;
+    uint32_t tl_n;
+    // host-framed datagrams
+    const uint32_t *hf_first;  // [n+1] CSR into hf_sets, or null
+    const HostSet *hf_sets;
+    const uint64_t *hf_err;    // [n] host error key per datagram
+    void *hdr;                 // ngz_dgram_hdr[n]
+    uint32_t *counts;          // [(n_slots+2)*n + 1]
+    uint32_t *scan;            // same length
+    SlotRT *slots;             // [n_slots]
+    Chunk *chunks;
+    uint64_t chunk_cap;
+    void *sets;                // ngz_set_info[set_cap]
+    uint64_t set_cap;
+    uint8_t *arena;
+    uint64_t arena_cap;
+    unsigned long long *proc_counts; // [n_slots] processed_count increments
+    BatchSummary *summary;
+};

@@ -1,0 +1,149 @@
+"""Host-side mirror of the reference decode interface, over the C ABI.
+
+`FlowInfoCodec` plays the role of netgauze_flow_pkt::codec::FlowInfoCodec
+(crates/flow-pkt/src/codec.rs:68-220): one instance per exporter peer, owning
+the NetFlow v9 and IPFIX template maps.  `decode_batch` applies
+`Decoder::decode` to every datagram of a batch, in order, the way
+FlowCollectorActor::decode_pkt does (crates/flow-service/src/flow_actor.rs:
+342-411), with the records decoded by the HIP kernels into per-template
+columns in HBM.  `template_counts(reset=True)` is reset_processed_count
+(crates/flow-pkt/src/ipfix.rs:65-69).
+"""
+import ctypes
+import json
+
+import numpy as np
+
+from . import _lib
+from ._lib import DGRAM_HDR_DTYPE, SET_INFO_DTYPE, d2h
+
+_LIB = None
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        _LIB = _lib.load()
+    return _LIB
+
+
+class NgzError(RuntimeError):
+    pass
+
+
+class Slot:
+    """Columns of one template version in the last batch."""
+
+    def __init__(self, codec, index, info):
+        self.index = index
+        self.version_id = info.version_id
+        self.template_id = info.template_id
+        self.proto = info.proto
+        self.n_records = info.n_records
+        self.capacity = info.capacity
+        self.columns_ptr = info.columns
+        n = lib().ngz_slot_fields(codec._ctx, index, None, 0)
+        arr = (_lib.FieldInfo * max(n, 1))()
+        lib().ngz_slot_fields(codec._ctx, index, arr, n)
+        self.fields = [arr[i] for i in range(n)]
+
+    def column_ptr(self, f):
+        return self.columns_ptr + self.capacity * self.fields[f].col_off
+
+    def column_bytes(self, f, rows=None):
+        """Host copy of column f: uint8 array of shape (rows, width)."""
+        w = self.fields[f].width
+        rows = self.n_records if rows is None else rows
+        return d2h(self.column_ptr(f), rows * w).reshape(rows, w)
+
+
+class DecodedBatch:
+    def __init__(self, codec, out):
+        self._codec = codec
+        self.out = out
+        self.n_dgrams = out.n_dgrams
+        self.n_sets = out.n_sets
+        self.n_records = out.n_records
+        self.n_template_dgrams = out.n_template_dgrams
+        self.slots = [Slot(codec, i, out.slots[i]) for i in range(out.n_slots)]
+
+    def dgram_headers(self):
+        return d2h(self.out.dgrams, self.n_dgrams * 32).view(DGRAM_HDR_DTYPE)
+
+    def sets(self):
+        return d2h(self.out.sets, self.n_sets * 16).view(SET_INFO_DTYPE)
+
+    def error_json(self, d):
+        n = lib().ngz_dgram_error_json(self._codec._ctx, d, None, 0)
+        if n < 0:
+            return None
+        buf = ctypes.create_string_buffer(n + 1)
+        lib().ngz_dgram_error_json(self._codec._ctx, d, buf, n + 1)
+        return buf.value.decode("utf-8")
+
+    def error(self, d):
+        s = self.error_json(d)
+        return None if s is None else json.loads(s)
+
+
+class FlowInfoCodec:
+    def __init__(self, device=0):
+        ctx = ctypes.c_void_p()
+        rc = lib().ngz_ctx_create(device, ctypes.byref(ctx))
+        if rc != 0:
+            raise NgzError("ngz_ctx_create(%d) failed: %d (no HIP device?)" % (device, rc))
+        self._ctx = ctx
+
+    def close(self):
+        if self._ctx:
+            lib().ngz_ctx_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc != 0:
+            raise NgzError("netgauze_amd: %d: %s" % (rc, lib().ngz_last_error(self._ctx).decode()))
+
+    def decode_batch(self, data, offsets, lengths, n=None, stream=None):
+        """data/offsets/lengths: device tensors (uint8 / int64 / int32), already in HBM."""
+        n = int(offsets.numel()) if n is None else n
+        bi = _lib.BatchIn(data.data_ptr(), data.numel(), offsets.data_ptr(), lengths.data_ptr(), n)
+        out = _lib.BatchOut()
+        self._check(lib().ngz_decode_batch(self._ctx, ctypes.byref(bi), ctypes.byref(out),
+                                           ctypes.c_void_p(stream) if stream else None))
+        return DecodedBatch(self, out)
+
+    def decode_datagrams(self, datagrams):
+        """Host-memory datagrams (list of bytes): H2D through the library."""
+        lens = np.array([len(d) for d in datagrams], dtype=np.uint32)
+        offs = np.zeros(len(datagrams), dtype=np.uint64)
+        if len(datagrams):
+            offs[1:] = np.cumsum(lens[:-1].astype(np.uint64))
+        blob = np.frombuffer(b"".join(datagrams) + b"\0" * 16, dtype=np.uint8)
+        out = _lib.BatchOut()
+        self._check(lib().ngz_decode_batch_host(self._ctx, blob.ctypes.data, int(lens.sum()), offs.ctypes.data,
+                                                lens.ctypes.data, len(datagrams), ctypes.byref(out)))
+        return DecodedBatch(self, out)
+
+    def templates(self, proto):
+        n = lib().ngz_templates_json(self._ctx, proto, None, 0)
+        buf = ctypes.create_string_buffer(n + 1)
+        lib().ngz_templates_json(self._ctx, proto, buf, n + 1)
+        return json.loads(buf.value.decode())
+
+    def template_counts(self, proto, reset=False):
+        n = lib().ngz_template_counts(self._ctx, proto, None, None, 0, 0)
+        ids = (ctypes.c_uint16 * max(n, 1))()
+        cnt = (ctypes.c_uint64 * max(n, 1))()
+        lib().ngz_template_counts(self._ctx, proto, ids, cnt, n, 1 if reset else 0)
+        return {ids[i]: cnt[i] for i in range(n)}
+
+    def last_timing(self):
+        a, b = ctypes.c_float(), ctypes.c_float()
+        lib().ngz_last_timing(self._ctx, ctypes.byref(a), ctypes.byref(b))
+        return a.value, b.value

@@ -1,0 +1,132 @@
+"""Synthetic IPFIX / NetFlow v9 exporter streams (benchmark and test input).
+
+Deterministic: record bytes come from a counter-based splitmix64 stream, so
+the same (template, seed, n) gives identical bytes on CPU (tests, oracle) and
+on the GPU (bench, generated in HBM without an H2D copy).  Layout per
+SURVEY.md §8(d): one template message, then data messages of up to
+`rec_per_msg` records in one data set (1023 x 64-byte T20 records = a
+65,492-byte message), export time 1,700,000,000 + message index, sequence
+number = records sent before the message, observation domain 1.
+"""
+import struct
+
+import torch
+
+SEED_CFG2 = 0x4E475A4500000002
+SEED_CFG3 = 0x4E475A4500000003
+
+# T20: 20 fixed-width IANA fields, 64 bytes (modelled on
+# wire/tests/ipfix.rs:212-236)
+T20 = [
+    (8, 4), (12, 4), (15, 4), (10, 4), (14, 4), (2, 8), (1, 8), (22, 4), (21, 4),
+    (7, 2), (11, 2), (6, 2), (4, 1), (5, 1), (9, 1), (13, 1), (16, 4), (17, 4), (61, 1), (60, 1),
+]
+T20_ID = 256
+
+
+def _i64(c):
+    return c - (1 << 64) if c >= (1 << 63) else c
+
+
+_G = _i64(0x9E3779B97F4A7C15)
+_M1 = _i64(0xBF58476D1CE4E5B9)
+_M2 = _i64(0x94D049BB133111EB)
+
+
+def _lsr(x, k):
+    return (x >> k) & ((1 << (64 - k)) - 1)
+
+
+def splitmix64(idx, seed):
+    """splitmix64 of (seed + idx) for an int64 tensor of counters."""
+    z = idx + _i64(seed & 0xFFFFFFFFFFFFFFFF) + _G
+    z = (z ^ _lsr(z, 30)) * _M1
+    z = (z ^ _lsr(z, 27)) * _M2
+    return z ^ _lsr(z, 31)
+
+
+def field_offsets(fields):
+    offs, o = [], 0
+    for _, ln in fields:
+        offs.append(o)
+        o += ln
+    return offs, o
+
+
+def t20_records(n, seed=SEED_CFG2, device="cpu", first=0):
+    """(n, 64) uint8 tensor of T20 records (wire order, big endian fields)."""
+    words = splitmix64(torch.arange(first * 8, (first + n) * 8, dtype=torch.int64, device=device), seed)
+    rec = words.view(torch.uint8).view(n, 64).clone()
+    offs, _ = field_offsets(T20)
+    o = dict(zip([f for f, _ in T20], offs))
+    proto_tab = torch.tensor([6, 17, 1], dtype=torch.uint8, device=device)
+    rec[:, o[4]] = proto_tab[(rec[:, o[4]].to(torch.int64) % 3)]
+    rec[:, o[9]] = (rec[:, o[9]].to(torch.int64) % 33).to(torch.uint8)
+    rec[:, o[13]] = (rec[:, o[13]].to(torch.int64) % 33).to(torch.uint8)
+    rec[:, o[61]] = rec[:, o[61]] & 1
+    rec[:, o[60]] = 4
+    return rec
+
+
+def template_message(tid=T20_ID, fields=T20, export_time=1_700_000_000, seq=0, domain=1):
+    body = struct.pack(">HH", tid, len(fields)) + b"".join(struct.pack(">HH", i, ln) for i, ln in fields)
+    sset = struct.pack(">HH", 2, 4 + len(body)) + body
+    return struct.pack(">HHIII", 10, 16 + len(sset), export_time, seq, domain) + sset
+
+
+def ipfix_data_stream(records, rec_len, tid=T20_ID, rec_per_msg=1023, export_time0=1_700_000_000, seq0=0,
+                      domain=1):
+    """Pack an (n, rec_len) uint8 tensor into IPFIX data messages, one data
+    set per message.  Returns (bytes uint8 tensor, offsets int64, lengths int32)
+    on the records' device."""
+    dev = records.device
+    n = records.shape[0]
+    n_msgs = (n + rec_per_msg - 1) // rec_per_msg
+    full = n // rec_per_msg
+    msg_len_full = 20 + rec_per_msg * rec_len
+    tail = n - full * rec_per_msg
+    total = full * msg_len_full + (20 + tail * rec_len if tail else 0)
+    buf = torch.zeros(total + 16, dtype=torch.uint8, device=dev)
+    m = torch.arange(n_msgs, dtype=torch.int64, device=dev)
+    k = torch.full((n_msgs,), rec_per_msg, dtype=torch.int64, device=dev)
+    if tail:
+        k[-1] = tail
+    lens = 20 + k * rec_len
+    offs = torch.zeros(n_msgs, dtype=torch.int64, device=dev)
+    if n_msgs > 1:
+        offs[1:] = torch.cumsum(lens[:-1], 0)
+    # headers: version, length, export time, sequence, domain, set id, set length
+    hdr = torch.zeros(n_msgs, 20, dtype=torch.uint8, device=dev)
+
+    def put_be(col, width, vals):
+        for b in range(width):
+            hdr[:, col + b] = _lsr(vals, 8 * (width - 1 - b)).bitwise_and(0xFF).to(torch.uint8)
+
+    put_be(0, 2, torch.full_like(m, 10))
+    put_be(2, 2, lens)
+    put_be(4, 4, (export_time0 + m) & 0xFFFFFFFF)
+    put_be(8, 4, (seq0 + m * rec_per_msg) & 0xFFFFFFFF)
+    put_be(12, 4, torch.full_like(m, domain))
+    put_be(16, 2, torch.full_like(m, tid))
+    put_be(18, 2, 4 + k * rec_len)
+    idx = offs.unsqueeze(1) + torch.arange(20, device=dev).unsqueeze(0)
+    buf[idx.reshape(-1)] = hdr.reshape(-1)
+    if full:
+        body = buf[: full * msg_len_full].view(full, msg_len_full)
+        body[:, 20:] = records[: full * rec_per_msg].reshape(full, rec_per_msg * rec_len)
+    if tail:
+        start = full * msg_len_full + 20
+        buf[start:start + tail * rec_len] = records[full * rec_per_msg:].reshape(-1)
+    return buf, offs, lens.to(torch.int32)
+
+
+def host_batch(datagrams, device="cpu"):
+    """List of bytes -> (bytes uint8, offsets int64, lengths int32) tensors."""
+    lens = [len(d) for d in datagrams]
+    offs = [0] * len(datagrams)
+    for i in range(1, len(datagrams)):
+        offs[i] = offs[i - 1] + lens[i - 1]
+    blob = b"".join(datagrams) + b"\0" * 16
+    return (torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(device),
+            torch.tensor(offs, dtype=torch.int64, device=device),
+            torch.tensor(lens, dtype=torch.int32, device=device))

@@ -1,0 +1,51 @@
+"""CPU checks of the C-ABI library: it is built, it loads, and it exports
+every function include/ngz/flow_decode.h declares (no compute calls here)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "ngz", "flow_decode.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(ngz_[a-z_0-9]+)\s*\(", text, re.M)))
+
+
+def test_header_declares_abi():
+    from netgauze_amd import _lib
+    assert declared_functions() == sorted(_lib.ABI_FUNCTIONS)
+
+
+def test_library_exports_every_declared_symbol():
+    from netgauze_amd import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.fail("libngz.so not built: run __graft_entry__.build()")
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+    _lib.load()
+
+
+def test_ctx_create_without_device_fails_cleanly():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("device present")
+    from netgauze_amd import _lib
+    lib = _lib.load()
+    ctx = ctypes.c_void_p()
+    assert lib.ngz_ctx_create(0, ctypes.byref(ctx)) != 0
+    assert not ctx.value
+
+
+def test_product_does_not_import_oracle():
+    """The product path never routes through the CPU oracle."""
+    pkg = os.path.join(ROOT, "netgauze_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".cpp", ".hip", ".h")):
+                text = open(os.path.join(dirpath, f), errors="ignore").read()
+                assert "ngz_oracle" not in text and "oracle/" not in text, f
