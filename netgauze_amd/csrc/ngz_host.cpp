@@ -25,11 +25,11 @@
 #include "ngz/flow_decode.h"
 #include "ngz_internal.h"
 
-extern "C" int ngz_launch_frame(const BatchDev *B, const uint8_t *hf_flag, const uint32_t *hf_first, hipStream_t st);
+extern "C" int ngz_launch_frame(const BatchDev *B, const uint32_t *hf_flag, const uint32_t *hf_first, hipStream_t st);
 extern "C" int ngz_scan_temp_bytes(uint64_t n_items, size_t *bytes);
 extern "C" int ngz_launch_scan(void *temp, size_t temp_bytes, const uint32_t *in, uint32_t *out, uint64_t n_items,
                                hipStream_t st);
-extern "C" int ngz_launch_layout_emit(const BatchDev *B, const uint8_t *hf_flag, const uint32_t *hf_first,
+extern "C" int ngz_launch_layout_emit(const BatchDev *B, const uint32_t *hf_flag, const uint32_t *hf_first,
                                       hipStream_t st);
 extern "C" int ngz_launch_decode(const BatchDev *B, uint32_t grid, uint32_t lds_bytes, hipStream_t st);
 extern "C" int ngz_launch_counts(const BatchDev *B, uint64_t set_cap, hipStream_t st);
@@ -386,7 +386,8 @@ struct ngz_ctx {
     DevBuf<uint16_t> d_cur_slot;
     DevBuf<uint32_t> d_tl_key, d_tl_dgram;
     DevBuf<uint16_t> d_tl_slot;
-    DevBuf<uint8_t> d_hf_flag;
+    DevBuf<uint32_t> d_hf_flag;
+    DevBuf<ngz_dgram_hdr> d_hf_hdr;
     DevBuf<uint32_t> d_hf_first;
     DevBuf<HostSet> d_hf_sets;
     DevBuf<ngz_dgram_hdr> d_hdr;
@@ -839,10 +840,10 @@ int upload_slots(ngz_ctx *ctx, const std::vector<int32_t> cur_start[2], hipStrea
 }
 
 struct HostFramed {
-    std::vector<uint8_t> flag;        // per datagram
+    std::vector<uint32_t> flag;       // per datagram: 0, or 1 + index into hdrs
     std::vector<uint32_t> first;      // CSR
     std::vector<HostSet> sets;
-    std::vector<std::pair<uint32_t, ngz_dgram_hdr>> hdrs;
+    std::vector<ngz_dgram_hdr> hdrs;
     Timeline tl;
 };
 
@@ -872,15 +873,19 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
         ctx->d_proc.ensure(std::max<uint32_t>(S, 1)) || ctx->d_summary.ensure(1))
         return fail(ctx, NGZ_E_NOMEM, "device alloc (batch)");
     // host-framed inputs
-    const uint8_t *hf_flag = nullptr;
+    const uint32_t *hf_flag = nullptr;
     const uint32_t *hf_first = nullptr;
     BatchDev B{};
     if (hf) {
         if (ctx->d_hf_flag.ensure(N) || ctx->d_hf_first.ensure(N + 1) || ctx->d_hf_sets.ensure(hf->sets.size() + 1) ||
+            ctx->d_hf_hdr.ensure(hf->hdrs.size() + 1) ||
             ctx->d_tl_key.ensure(hf->tl.key.size() + 1) || ctx->d_tl_dgram.ensure(hf->tl.key.size() + 1) ||
             ctx->d_tl_slot.ensure(hf->tl.key.size() + 1))
             return fail(ctx, NGZ_E_NOMEM, "device alloc (host framing)");
-        HIPCHK(hipMemcpyAsync(ctx->d_hf_flag.p, hf->flag.data(), N, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(ctx->d_hf_flag.p, hf->flag.data(), N * 4ull, hipMemcpyHostToDevice, st));
+        if (!hf->hdrs.empty())
+            HIPCHK(hipMemcpyAsync(ctx->d_hf_hdr.p, hf->hdrs.data(), hf->hdrs.size() * sizeof(ngz_dgram_hdr),
+                                  hipMemcpyHostToDevice, st));
         HIPCHK(hipMemcpyAsync(ctx->d_hf_first.p, hf->first.data(), (N + 1) * 4, hipMemcpyHostToDevice, st));
         if (!hf->sets.empty())
             HIPCHK(hipMemcpyAsync(ctx->d_hf_sets.p, hf->sets.data(), hf->sets.size() * sizeof(HostSet),
@@ -897,6 +902,7 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
         B.tl_slot = ctx->d_tl_slot.p;
         B.tl_n = (uint32_t)hf->tl.key.size();
         B.hf_first = hf_first;
+        B.hf_hdr = ctx->d_hf_hdr.p;
         B.hf_sets = ctx->d_hf_sets.p;
     }
     B.bytes = in->bytes;
@@ -925,9 +931,6 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
     HIPCHK(hipMemsetAsync(ctx->d_summary.p, 0, sizeof(BatchSummary), st));
     HIPCHK(hipMemsetAsync(ctx->d_proc.p, 0, std::max<uint32_t>(S, 1) * 8, st));
     if (ngz_launch_frame(&B, hf_flag, hf_first, st)) return fail(ctx, NGZ_E_DEVICE, "k_frame launch");
-    if (hf)
-        for (const auto &ph : hf->hdrs)
-            HIPCHK(hipMemcpyAsync(ctx->d_hdr.p + ph.first, &ph.second, sizeof(ngz_dgram_hdr), hipMemcpyHostToDevice, st));
     if (ngz_launch_scan(ctx->d_scan_tmp.p, scan_tmp, ctx->d_counts.p, ctx->d_scan.p, n_items, st))
         return fail(ctx, NGZ_E_DEVICE, "scan launch");
     if (ngz_launch_layout_emit(&B, hf_flag, hf_first, st)) return fail(ctx, NGZ_E_DEVICE, "layout/emit launch");
@@ -1018,7 +1021,7 @@ void ngz_ctx_destroy(ngz_ctx *ctx) {
     hipSetDevice(ctx->device);
     hipStreamSynchronize(ctx->stream);
     ctx->d_plans.release(); ctx->d_cur_slot.release(); ctx->d_tl_key.release(); ctx->d_tl_dgram.release();
-    ctx->d_tl_slot.release(); ctx->d_hf_flag.release(); ctx->d_hf_first.release(); ctx->d_hf_sets.release();
+    ctx->d_tl_slot.release(); ctx->d_hf_flag.release(); ctx->d_hf_hdr.release(); ctx->d_hf_first.release(); ctx->d_hf_sets.release();
     ctx->d_hdr.release(); ctx->d_counts.release(); ctx->d_scan.release(); ctx->d_scan_tmp.release();
     ctx->d_slots.release(); ctx->d_chunks.release(); ctx->d_sets.release(); ctx->d_arena.release();
     ctx->d_proc.release(); ctx->d_summary.release(); ctx->d_in_bytes.release(); ctx->d_in_off.release();
@@ -1091,8 +1094,8 @@ int ngz_decode_batch(ngz_ctx *ctx, const ngz_batch_in *in, ngz_batch_out *out, v
             const uint32_t d = host_idx[i];
             HostFrameOut o;
             host_frame(ctx, dbytes[i].data(), lens[d], limit[i], o);
-            hf.flag[d] = 1;
-            hf.hdrs.push_back({d, o.hdr});
+            hf.hdrs.push_back(o.hdr);
+            hf.flag[d] = (uint32_t)hf.hdrs.size();
             per.push_back({d, std::move(o.sets)});
             defs[i] = o.defs;
             for (auto &df : o.defs) tl_entries.push_back({(uint32_t)df.second, d});
@@ -1160,6 +1163,11 @@ int ngz_decode_batch(ngz_ctx *ctx, const ngz_batch_in *in, ngz_batch_out *out, v
         std::vector<ngz_dgram_hdr> h2(N);
         HIPCHK(hipMemcpy(h2.data(), ctx->d_hdr.p, N * sizeof(ngz_dgram_hdr), hipMemcpyDeviceToHost));
         bool redo = false;
+        if (getenv("NGZ_DEBUG"))
+            for (size_t i = 0; i < host_idx.size(); ++i)
+                fprintf(stderr, "[ngz]   host dgram %u flag %u status %u err %016llx limit %u defs %zu\n", host_idx[i],
+                        hf.flag[host_idx[i]], h2[host_idx[i]].status, (unsigned long long)h2[host_idx[i]].err_key,
+                        limit[i], defs[i].size());
         for (size_t i = 0; i < host_idx.size(); ++i) {
             const uint64_t k = h2[host_idx[i]].err_key;
             if (k == NGZ_NO_ERR) continue;

@@ -129,7 +129,7 @@ struct BatchDev {        // device pointers of one batch
     // host-framed datagrams
     const uint32_t *hf_first;  // [n+1] CSR into hf_sets, or null
     const HostSet *hf_sets;
-    const uint64_t *hf_err;    // [n] host error key per datagram
+    const void *hf_hdr;        // [hosts] ngz_dgram_hdr of host-framed datagrams (hf_flag[d]-1 indexes)
     void *hdr;                 // ngz_dgram_hdr[n]
     uint32_t *counts;          // [(n_slots+2)*n + 1]
     uint32_t *scan;            // same length

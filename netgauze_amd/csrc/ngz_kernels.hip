@@ -51,7 +51,7 @@ __device__ __forceinline__ uint16_t resolve_slot(const BatchDev &B, uint32_t pid
 // gets the set header position, the template slot, the record count and the
 // position of the first record.  Template sets end the walk with NGZ_FR_HOST.
 template <class V>
-__device__ void walk_datagram(const BatchDev &B, const uint8_t *__restrict__ hf_flag, const uint32_t *__restrict__ hf_first,
+__device__ void walk_datagram(const BatchDev &B, const uint32_t *__restrict__ hf_flag, const uint32_t *__restrict__ hf_first,
                               uint32_t d, WalkOut &o, V &vis) {
     o.status = NGZ_FR_OK;
     o.version = o.length = o.time = o.seq = o.domain = o.sysup = o.nsets = 0;
@@ -159,6 +159,28 @@ __device__ void walk_datagram(const BatchDev &B, const uint8_t *__restrict__ hf_
     o.err = ngz_err_key(0, E_CODEC_UNSUPPORTED_VERSION, ver, 0);
 }
 
+// Does the datagram's set chain contain a (options) template set anywhere?
+// Structural only (independent of template state and of NFv9 record counts),
+// so it over-approximates which datagrams must be framed on the host.
+__device__ bool has_template_sets(const BatchDev &B, uint32_t d) {
+    const uint8_t *p = B.bytes + B.offsets[d];
+    const uint32_t dl = B.lengths[d];
+    if (dl < 16) return false;
+    const uint32_t ver = be16(p), len = be16(p + 2);
+    if (dl < len) return false;
+    uint32_t pos, end;
+    if (ver == 10) { pos = 16; end = len; }
+    else if (ver == 9) { pos = 20; end = dl; }
+    else return false;
+    while (pos + 4 <= end) {
+        const uint32_t id = be16(p + pos), sl = be16(p + pos + 2);
+        if (ver == 10 ? (id == 2 || id == 3) : (id <= 1)) return true;
+        if (sl < 4 || sl > end - pos) return false;
+        pos += sl;
+    }
+    return false;
+}
+
 struct CountVis {
     uint32_t *counts;
     uint32_t N, S, d;
@@ -171,12 +193,13 @@ struct CountVis {
     }
 };
 
-__global__ void k_frame(BatchDev B, const uint8_t *hf_flag, const uint32_t *hf_first) {
+__global__ void k_frame(BatchDev B, const uint32_t *hf_flag, const uint32_t *hf_first) {
     const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
     if (d >= B.n) return;
     CountVis vis{B.counts, B.n, B.n_slots, d, 0, 0, B.plans};
     WalkOut o;
     walk_datagram(B, hf_flag, hf_first, d, o, vis);
+    if (o.status != NGZ_FR_HOST && !(hf_flag && hf_flag[d]) && has_template_sets(B, d)) o.status = NGZ_FR_HOST;
     const uint64_t N = B.n;
     B.counts[(uint64_t)B.n_slots * N + d] = vis.chunks;
     B.counts[(uint64_t)(B.n_slots + 1) * N + d] = vis.sets;
@@ -190,6 +213,7 @@ __global__ void k_frame(BatchDev B, const uint8_t *hf_flag, const uint32_t *hf_f
     h.sys_up_time = o.sysup;
     h.n_sets = o.nsets;
     h.err_key = o.err;
+    if (hf_flag && hf_flag[d]) h = ((const ngz_dgram_hdr *)B.hf_hdr)[hf_flag[d] - 1];
     ((ngz_dgram_hdr *)B.hdr)[d] = h;
     if (o.status == NGZ_FR_HOST && !(hf_flag && hf_flag[d])) atomicAdd(&B.summary->n_host, 1u);
     if (o.status == NGZ_FR_UNSUPPORTED) atomicAdd(&B.summary->n_unsupported, 1u);
@@ -282,7 +306,7 @@ struct EmitVis {
     }
 };
 
-__global__ void k_emit(BatchDev B, const uint8_t *hf_flag, const uint32_t *hf_first) {
+__global__ void k_emit(BatchDev B, const uint32_t *hf_flag, const uint32_t *hf_first) {
     const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
     if (d >= B.n) return;
     if (B.summary->overflow) return;
@@ -657,7 +681,7 @@ __global__ void k_finalize(BatchDev B) {
 // ---------------------------------------------------------------------------
 // launch wrappers (C linkage, used by ngz_host.cpp)
 // ---------------------------------------------------------------------------
-extern "C" int ngz_launch_frame(const BatchDev *B, const uint8_t *hf_flag, const uint32_t *hf_first, hipStream_t st) {
+extern "C" int ngz_launch_frame(const BatchDev *B, const uint32_t *hf_flag, const uint32_t *hf_first, hipStream_t st) {
     const uint32_t nb = (B->n + 255) / 256;
     if (nb) hipLaunchKernelGGL(k_frame, dim3(nb), dim3(256), 0, st, *B, hf_flag, hf_first);
     return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -676,7 +700,7 @@ extern "C" int ngz_launch_scan(void *temp, size_t temp_bytes, const uint32_t *in
     return hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, in, out, (int)n_items, st) == hipSuccess ? 0 : -1;
 }
 
-extern "C" int ngz_launch_layout_emit(const BatchDev *B, const uint8_t *hf_flag, const uint32_t *hf_first,
+extern "C" int ngz_launch_layout_emit(const BatchDev *B, const uint32_t *hf_flag, const uint32_t *hf_first,
                                       hipStream_t st) {
     hipLaunchKernelGGL(k_layout, dim3(1), dim3(64), 0, st, *B);
     const uint32_t nb = (B->n + 255) / 256;

@@ -187,7 +187,7 @@ def test_record_errors(dev):
         ipfix_msg([ipfix_set(400, good), ipfix_set(400, rec(1, 1, 1, b"\x80" * 8))]),     # error in 2nd set
     ]
     stats, batch, codec, oc = run_both(dgrams)
-    assert stats["err"] == 5 and stats["ok"] == 4
+    assert stats["err"] == 6 and stats["ok"] == 3
     assert codec.template_counts(10) == {400: oc.ipfix_templates[400].processed_count}
 
 
