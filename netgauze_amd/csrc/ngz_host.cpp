@@ -338,7 +338,7 @@ uint32_t lds_bytes_for(const DevPlan &P) {
     if (!P.rpl) return 0;
     const uint32_t bytes = 16 + P.window * P.rec_len + 16;
     const uint32_t q = (bytes + 3) / 4 + 4;
-    return 4 * (q + (q >> P.pad_shift) + 4);
+    return 16 * NGZ_MAXF + 4 * (q + (q >> P.pad_shift) + 4);  // field table + staged chunk
 }
 
 struct ErrInfo {  // host-side framing error

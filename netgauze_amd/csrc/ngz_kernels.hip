@@ -475,12 +475,26 @@ __device__ bool utf8_valid_prefix(const uint32_t *lds, uint32_t x, uint32_t len,
     return true;
 }
 
+__device__ __forceinline__ uint32_t sgpr(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+constexpr int STAGE_BATCH = 16;  // 16 x 1 KiB per wave in flight
+
+struct ChunkS {  // chunk descriptor in SGPRs
+    uint64_t src;
+    uint32_t rec0, dgram, n, slot, pos0;
+};
+
+struct PlanS {  // plan header in SGPRs
+    uint32_t rec_len, n_fields, rpl, ps;
+};
+
 template <int RPL>
-__device__ void decode_chunk(const BatchDev &B, const Chunk &c, const DevPlan *__restrict__ P, uint32_t *lds) {
+__device__ void decode_chunk(const BatchDev &B, const ChunkS &c, const PlanS &P, const uint4 *ftab, uint32_t *lds) {
     const uint32_t lane = threadIdx.x;
     const uint32_t n = c.n;
-    const uint32_t rl = P->rec_len;
-    const uint32_t ps = P->pad_shift;
+    const uint32_t rl = P.rec_len;
+    const uint32_t ps = P.ps;
     // ---- stage the chunk's bytes into LDS (16-byte buffer loads) ----
     const uint64_t a0 = c.src & ~15ull;
     const uint32_t sh = (uint32_t)(c.src - a0);
@@ -490,13 +504,26 @@ __device__ void decode_chunk(const BatchDev &B, const Chunk &c, const DevPlan *_
     __amdgpu_buffer_rsrc_t rsrc =
         __builtin_amdgcn_make_buffer_rsrc((void *)(B.bytes + a0), (short)0, (int)avail, 0x00020000);
     const uint32_t nq = (total + 15) >> 4;
-    for (uint32_t q = lane; q < nq; q += 64) {
-        const auto v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, q * 16, 0, 0);
-        const uint32_t b = 4 * q;
-        lds[pidx(b, ps)] = v[0];
-        lds[pidx(b + 1, ps)] = v[1];
-        lds[pidx(b + 2, ps)] = v[2];
-        lds[pidx(b + 3, ps)] = v[3];
+    // issue up to 16 x 16-byte loads per lane before the first LDS write, so a
+    // 16 KB chunk costs one HBM round trip (not one per load)
+    for (uint32_t q0 = 0; q0 < nq; q0 += 64 * STAGE_BATCH) {
+        v4u v[STAGE_BATCH];
+#pragma unroll
+        for (int j = 0; j < STAGE_BATCH; ++j) {
+            const uint32_t q = q0 + j * 64 + lane;
+            v[j] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, q * 16, 0, 0);  // OOB -> 0
+        }
+#pragma unroll
+        for (int j = 0; j < STAGE_BATCH; ++j) {
+            const uint32_t q = q0 + j * 64 + lane;
+            if (q < nq) {
+                const uint32_t b = 4 * q;
+                lds[pidx(b, ps)] = v[j][0];
+                lds[pidx(b + 1, ps)] = v[j][1];
+                lds[pidx(b + 2, ps)] = v[j][2];
+                lds[pidx(b + 3, ps)] = v[j][3];
+            }
+        }
     }
     __syncthreads();
     // ---- this lane's rows ----
@@ -514,12 +541,15 @@ __device__ void decode_chunk(const BatchDev &B, const Chunk &c, const DevPlan *_
     }
     if (vmask) {
         const SlotRT rt = B.slots[c.slot];
-        uint8_t *blk = B.arena + rt.block;
-        const uint32_t nf = P->n_fields;
+        uint8_t *blk = B.arena + sgpr((uint32_t)rt.block) + ((uint64_t)sgpr((uint32_t)(rt.block >> 32)) << 32);
+        const uint32_t cap = sgpr(rt.cap);
+        const uint32_t nf = P.n_fields;
         for (uint32_t f = 0; f < nf; ++f) {
-            const DevField fd = P->f[f];
-            uint8_t *col = blk + (uint64_t)rt.cap * fd.col_off;
-            const uint32_t kind = fd.kind, len = fd.len, width = fd.width, off = fd.off;
+            const uint4 fdv = ftab[f];  // LDS broadcast read of the field descriptor
+            const uint32_t off = sgpr(fdv.x & 0xFFFF), len = sgpr(fdv.x >> 16);
+            const uint32_t width = sgpr(fdv.y & 0xFFFF), kind = sgpr((fdv.y >> 16) & 0xFF);
+            const uint32_t col_off = sgpr(fdv.z);
+            uint8_t *col = blk + (uint64_t)cap * col_off;
             uint32_t x[RPL];
 #pragma unroll
             for (int k = 0; k < RPL; ++k) x[k] = xr[k] + off;
@@ -624,18 +654,40 @@ __device__ void decode_chunk(const BatchDev &B, const Chunk &c, const DevPlan *_
     __syncthreads();  // LDS reused by the next chunk
 }
 
+// one wave per workgroup; LDS = [field table of the current slot][staged chunk]
 __global__ void __launch_bounds__(64) k_decode(BatchDev B) {
-    extern __shared__ uint32_t lds[];
-    const uint32_t nchunks = B.summary->n_chunks;
-    if (B.summary->overflow) return;
+    extern __shared__ uint32_t lds_all[];
+    uint4 *ftab = (uint4 *)lds_all;
+    uint32_t *lds = lds_all + 4 * NGZ_MAXF;
+    const uint32_t nchunks = sgpr(B.summary->n_chunks);
+    if (sgpr(B.summary->overflow)) return;
+    uint32_t cached = 0xFFFFFFFFu;
+    PlanS P{};
     for (uint32_t ci = blockIdx.x; ci < nchunks; ci += gridDim.x) {
-        const Chunk c = B.chunks[ci];
+        const uint4 *cp = (const uint4 *)&B.chunks[ci];
+        const uint4 c0 = cp[0], c1 = cp[1];
+        ChunkS c;
+        c.src = (uint64_t)sgpr(c0.x) | ((uint64_t)sgpr(c0.y) << 32);
+        c.rec0 = sgpr(c0.z);
+        c.dgram = sgpr(c0.w);
+        c.n = sgpr(c1.x & 0xFFFF);
+        c.slot = sgpr(c1.x >> 16);
+        c.pos0 = sgpr(c1.y & 0xFFFF);
         if (c.n == 0) continue;
-        const DevPlan *P = &B.plans[c.slot];
-        const uint32_t rpl = P->rpl;
-        if (rpl == 4) decode_chunk<4>(B, c, P, lds);
-        else if (rpl == 2) decode_chunk<2>(B, c, P, lds);
-        else decode_chunk<1>(B, c, P, lds);
+        if (c.slot != cached) {
+            const DevPlan *pl = &B.plans[c.slot];
+            const uint4 h0 = ((const uint4 *)pl)[0], h1 = ((const uint4 *)pl)[1];
+            P.rec_len = sgpr(h0.x);
+            P.n_fields = sgpr(h0.z & 0xFFFF);
+            P.rpl = sgpr((h0.z >> 24) & 0xFF);
+            P.ps = sgpr(h0.w & 0xFF);
+            (void)h1;
+            for (uint32_t i = threadIdx.x; i < P.n_fields; i += 64) ftab[i] = ((const uint4 *)pl->f)[i];
+            cached = c.slot;
+        }
+        if (P.rpl == 4) decode_chunk<4>(B, c, P, ftab, lds);
+        else if (P.rpl == 2) decode_chunk<2>(B, c, P, ftab, lds);
+        else decode_chunk<1>(B, c, P, ftab, lds);
     }
 }
 
