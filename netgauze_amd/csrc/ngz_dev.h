@@ -1,0 +1,274 @@
+// Device-side record decode primitives, shared by the ahead-of-time generic
+// decode kernel (ngz_kernels.hip) and the per-template kernels generated and
+// compiled at run time with hiprtc (ngz_rtc.cpp embeds this file's text).
+//
+// Reference behaviour restated (file:line relative to the NetGauze checkout):
+//   crates/flow-pkt/src/wire/deserializer/ipfix.rs:335-370 (DataRecord::parse),
+//   netflow.rs:399-475 (NFv9 DataRecord / ScopeField), and the generated
+//   Field::parse rules in crates/flow-pkt/ipfix-code-generator/src/generator.rs:
+//   reduced-size unsigned/signed reads :1468-1562 via parse-utils/src/reader.rs:214-295,
+//   tcpControlBits :1416-1417 (iana/src/tcp.rs:165-168), bool :1607-1619,
+//   fixed strings :1635-1672, dateTimeMilliseconds :1725-1746,
+//   dateTimeMicro/Nanoseconds :1748-1773, u256 :1498-1518.
+//
+// Record model: one lane decodes one record.  A lane holds an 80-byte window
+// of its record in 20 VGPRs (five 16-byte buffer loads), re-aligned so that
+// window byte 0 is record byte `wb`.  All field offsets are wave-uniform, so
+// extraction is register selection (constant-folded in generated kernels,
+// s_set_gpr_idx-indexed in the generic kernel), v_perm/v_alignbyte and shifts.
+#pragma once
+#include <stdint.h>
+
+#include "ngz/flow_decode.h"
+#include "ngz_internal.h"
+
+namespace ngzdev {
+
+typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+
+constexpr int WIN_DW = 20;      // dwords loaded per window (5 x 16 B)
+constexpr uint32_t WIN_B = 76;  // record bytes usable in a window after re-alignment (19 dwords)
+
+// chrono NaiveDate range (0.4.45): -262143-01-01 .. +262142-12-31, in ms
+constexpr int64_t kMinMillis = -8334601315200000LL;  // days_from_civil(-262143,1,1)*86400000
+constexpr int64_t kMaxMillis = 8210266876799999LL;   // (days_from_civil(262142,12,31)+1)*86400000-1
+
+__device__ __forceinline__ uint32_t sgpr(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// 4 wire bytes at uniform window byte offset o, as a little-endian dword
+__device__ __forceinline__ uint32_t rdw(const uint32_t (&R)[WIN_DW], uint32_t o) {
+    uint32_t q = o >> 2;
+    q = q < WIN_DW - 2 ? q : WIN_DW - 2;
+    if ((o & 3) == 0) return R[q];
+    return __builtin_amdgcn_alignbyte(R[q + 1], R[q], o & 3);
+}
+
+__device__ __forceinline__ uint32_t rbyte(const uint32_t (&R)[WIN_DW], uint32_t o) {
+    uint32_t q = o >> 2;
+    q = q < WIN_DW - 1 ? q : WIN_DW - 1;
+    return (R[q] >> (8 * (o & 3))) & 0xFF;
+}
+
+// big-endian unsigned of `len` (0..8) bytes at window byte offset o
+// (read_unsigned32_be / read_unsigned64_be: right-aligned reduced size)
+// Touches exactly window dwords [o/4, (o+len-1)/4].
+__device__ __forceinline__ uint64_t rbe(const uint32_t (&R)[WIN_DW], uint32_t o, uint32_t len) {
+    if (len == 0) return 0;
+    if ((o & 3) + len <= 4) {  // inside one dword
+        uint32_t q = o >> 2;
+        q = q < WIN_DW - 1 ? q : WIN_DW - 1;
+        return __builtin_bswap32(R[q] >> (8 * (o & 3))) >> (32 - 8 * len);
+    }
+    const uint32_t a = __builtin_bswap32(rdw(R, o));
+    if (len <= 4) return a >> (32 - 8 * len);
+    const uint32_t b = __builtin_bswap32(rdw(R, o + 4));
+    return (((uint64_t)a << 32) | b) >> (64 - 8 * len);
+}
+
+// Everything one pass (64 rows, one per lane) needs; uniform except the
+// per-lane row / record position / alignment.
+struct Pass {
+    __amdgpu_buffer_rsrc_t rsrc;  // the chunk's bytes (OOB reads return 0)
+    uint8_t *blk;                 // slot's column block
+    uint32_t cap;                 // rows per column
+    uint32_t rbase;               // this lane's record start, dword aligned, relative to rsrc
+    uint32_t sh;                  // this lane's record misalignment (0..3)
+    bool any_sh;                  // some lane misaligned (uniform)
+    bool valid;                   // this lane's row belongs to the chunk
+    uint32_t row;                 // this lane's output row
+    uint32_t prow;                // first row of the pass (uniform; row = prow + lane)
+    uint32_t lane;
+    uint32_t rec0;                // first row of the chunk
+    uint32_t dgram;               // datagram of the chunk
+    uint32_t recpos;              // this lane's record offset in the datagram
+    uint32_t pos0;                // chunk's first record offset in the datagram
+    void *hdr;                    // ngz_dgram_hdr[] (errors)
+};
+
+// Load record dwords [wb/4, wb/4 + ND) of this lane's record into R[0, ND)
+// (ND <= WIN_DW - 1): ceil(ND/4) 16-byte loads, plus one dword when some
+// lane's record is not dword-aligned and the last load has no spare dword.
+template <int ND>
+__device__ __forceinline__ void win_load(uint32_t (&R)[WIN_DW], const Pass &P, uint32_t wb) {
+    constexpr int NB = (ND + 3) / 4;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+        const v4u v = __builtin_amdgcn_raw_buffer_load_b128(P.rsrc, P.rbase + wb + 16 * i, 0, 0);
+        R[4 * i] = v[0];
+        R[4 * i + 1] = v[1];
+        R[4 * i + 2] = v[2];
+        R[4 * i + 3] = v[3];
+    }
+#pragma unroll
+    for (int i = 4 * NB; i < WIN_DW; ++i) R[i] = 0;
+    if (P.any_sh) {  // records not dword-aligned: shift the window to the record start
+        if constexpr (4 * NB == ND)
+            R[ND] = __builtin_amdgcn_raw_buffer_load_b32(P.rsrc, P.rbase + wb + 4 * ND, 0, 0);
+#pragma unroll
+        for (int j = 0; j < ND; ++j) R[j] = __builtin_amdgcn_alignbyte(R[j + 1], R[j], P.sh);
+    }
+}
+
+__device__ __forceinline__ void rec_error(const Pass &P, uint32_t pos, uint32_t code, uint32_t f) {
+    atomicMin((unsigned long long *)&((ngz_dgram_hdr *)P.hdr)[P.dgram].err_key,
+              (unsigned long long)ngz_err_key(pos, code, f, 0));
+}
+
+// Column `col_off` rows [prow, prow+64) start at a uniform address; lanes add
+// a small 32-bit offset (global_store with an SGPR base).
+__device__ __forceinline__ uint8_t *pass_col(const Pass &P, uint32_t col_off, uint32_t width) {
+    return P.blk + (uint64_t)P.cap * col_off + (uint64_t)P.prow * width;
+}
+
+__device__ __forceinline__ void store_w(uint8_t *pcol, uint32_t lane, uint32_t width, uint64_t v) {
+    if (width == 1) pcol[lane] = (uint8_t)v;
+    else if (width == 2) *(uint16_t *)(pcol + 2 * lane) = (uint16_t)v;
+    else if (width == 4) *(uint32_t *)(pcol + 4 * lane) = (uint32_t)v;
+    else *(uint2 *)(pcol + 8 * lane) = make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+}
+
+// Numeric field (UINT/SCOPE32/TCPFLAGS/SINT/BOOL/DTMS/DTFRAC) at window offset o.
+__device__ __forceinline__ void dec_num(const uint32_t (&R)[WIN_DW], const Pass &P, uint32_t o, uint32_t off,
+                                        uint32_t f, uint32_t len, uint32_t width, uint32_t kind, uint32_t col_off) {
+    uint8_t *pcol = pass_col(P, col_off, width);
+    uint64_t v;
+    if (kind == NGZ_K_BOOL) {
+        v = rbyte(R, o) != 0;
+    } else if (kind == NGZ_K_DTFRAC) {
+        const uint32_t secs = (uint32_t)rbe(R, o, 4);
+        const uint32_t frac = (uint32_t)rbe(R, o + 4, 4);
+        // (1_000_000_000f64 * (fraction as f64 / u32::MAX as f64)) as u32 (generator.rs:1764)
+        const double q = (double)frac / 4294967295.0;
+        const uint32_t ns = (uint32_t)(1000000000.0 * q);
+        // chrono timestamp_opt: ns >= 1e9 only as a leap second (secs % 60 == 59)
+        if (P.valid && ns >= 1000000000u && (secs % 60u) != 59u) rec_error(P, P.recpos + off, E_REC_DTFRAC, f);
+        v = (uint64_t)secs | ((uint64_t)ns << 32);
+    } else {
+        v = rbe(R, o, kind == NGZ_K_DTMS ? 8 : len);
+        if (kind == NGZ_K_TCPFLAGS) v &= 0xFF;  // TCPHeaderFlags::from(u16) keeps the low byte
+        if (kind == NGZ_K_SINT) {
+            const uint32_t s2 = len ? 64 - 8 * len : 0;
+            v = (uint64_t)(((int64_t)(v << s2)) >> s2);
+        }
+        if (P.valid && kind == NGZ_K_DTMS && ((int64_t)v < kMinMillis || (int64_t)v > kMaxMillis))
+            rec_error(P, P.recpos + off, E_REC_DTMS, f);
+    }
+    if (P.valid) store_w(pcol, P.lane, width, v);
+}
+
+struct WindowBytes {
+    const uint32_t (&R)[WIN_DW];
+    uint32_t o;
+    __device__ uint32_t operator()(uint32_t i) const { return rbyte(R, o + i); }
+};
+
+struct GlobalBytes {
+    __amdgpu_buffer_rsrc_t rsrc;
+    uint32_t base;  // this lane's byte, relative to the resource
+    __device__ uint32_t operator()(uint32_t i) const { return __builtin_amdgcn_raw_buffer_load_b8(rsrc, base + i, 0, 0); }
+};
+
+template <class F>
+__device__ bool utf8_valid_prefix(const F &byte_at, uint32_t len) {
+    // std::str::from_utf8 of the bytes up to the first NUL (generator.rs:1651-1668)
+    uint32_t i = 0;
+    while (i < len) {
+        const uint32_t c = byte_at(i);
+        if (c == 0) return true;
+        if (c < 0x80) { ++i; continue; }
+        uint32_t need, lo = 0x80, hi = 0xBF;
+        if (c >= 0xC2 && c <= 0xDF) need = 1;
+        else if (c >= 0xE0 && c <= 0xEF) { need = 2; if (c == 0xE0) lo = 0xA0; if (c == 0xED) hi = 0x9F; }
+        else if (c >= 0xF0 && c <= 0xF4) { need = 3; if (c == 0xF0) lo = 0x90; if (c == 0xF4) hi = 0x8F; }
+        else return false;
+        for (uint32_t t = 1; t <= need; ++t) {
+            if (i + t >= len) return false;
+            const uint32_t b = byte_at(i + t);
+            const uint32_t l2 = (t == 1) ? lo : 0x80, h2 = (t == 1) ? hi : 0xBF;
+            if (b < l2 || b > h2) return false;
+        }
+        i += need + 1;
+    }
+    return true;
+}
+
+// UTF-8 check of a fixed string field (errors only; the bytes go through dec_raw)
+__device__ __forceinline__ void check_str(const uint32_t (&R)[WIN_DW], const Pass &P, uint32_t o, uint32_t off,
+                                          uint32_t f, uint32_t len, bool in_window) {
+    if (!P.valid) return;
+    const bool ok = in_window ? utf8_valid_prefix(WindowBytes{R, o}, len)
+                              : utf8_valid_prefix(GlobalBytes{P.rsrc, P.rbase + P.sh + off}, len);
+    if (!ok) rec_error(P, P.recpos + off, E_REC_UTF8, f);
+}
+
+// Copy `piece` (<= 64) raw wire bytes at window offset o to column bytes
+// [j, j+piece) of this lane's row; `pad_to` > 0 zero-fills [j+piece, pad_to)
+// (u256: left-aligned, zero padded).
+__device__ __forceinline__ void dec_raw(const uint32_t (&R)[WIN_DW], const Pass &P, uint32_t o, uint32_t j,
+                                        uint32_t piece, uint32_t width, uint32_t col_off, uint32_t pad_to) {
+    if (!P.valid) return;
+    uint8_t *dst = pass_col(P, col_off, width) + P.lane * width + j;
+    const bool dw = (width & 3) == 0 && (j & 3) == 0;
+    uint32_t t = 0;
+    if (dw && (width & 15) == 0 && (j & 15) == 0) {
+        for (; t + 16 <= piece; t += 16)
+            *(uint4 *)(dst + t) = make_uint4(rdw(R, o + t), rdw(R, o + t + 4), rdw(R, o + t + 8), rdw(R, o + t + 12));
+    }
+    if (dw)
+        for (; t + 4 <= piece; t += 4) *(uint32_t *)(dst + t) = rdw(R, o + t);
+    for (; t < piece; ++t) dst[t] = (uint8_t)rbyte(R, o + t);
+    for (uint32_t z = j + piece; z < pad_to; ++z) dst[z - j] = 0;
+}
+
+// Walk chunks [c_begin, c_end) of the batch's chunk array, one wave per chunk
+// (wave-strided), 64 rows per pass.  want(slot) decides (and may load per-slot
+// state) whether a chunk's slot is handled here; rec_len(slot) gives its
+// record length; pass(P) decodes the 64 rows of one pass.
+template <class Want, class RecLen, class PassFn>
+__device__ __forceinline__ void run_chunks(const BatchDev &B, uint32_t c_begin, uint32_t c_end, Want &&want,
+                                           RecLen &&rec_len, PassFn &&pass) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wpb = blockDim.x >> 6;
+    const uint32_t wid = sgpr(blockIdx.x * wpb + (threadIdx.x >> 6));
+    const uint32_t nw = gridDim.x * wpb;
+    for (uint32_t ci = c_begin + wid; ci < c_end; ci += nw) {
+        const uint4 *cp = (const uint4 *)&B.chunks[ci];
+        const uint4 c0 = cp[0], c1 = cp[1];
+        const uint32_t n = sgpr(c1.x & 0xFFFF);
+        if (n == 0) continue;  // padding chunk
+        const uint32_t slot = sgpr(c1.x >> 16);
+        if (!want(slot)) continue;
+        const uint32_t rl = rec_len(slot);
+        const uint64_t src = (uint64_t)sgpr(c0.x) | ((uint64_t)sgpr(c0.y) << 32);
+        Pass P;
+        P.rec0 = sgpr(c0.z);
+        P.dgram = sgpr(c0.w);
+        P.pos0 = sgpr(c1.y & 0xFFFF);
+        P.hdr = B.hdr;
+        const SlotRT rt = B.slots[slot];
+        P.blk = B.arena + sgpr((uint32_t)rt.block) + ((uint64_t)sgpr((uint32_t)(rt.block >> 32)) << 32);
+        P.cap = sgpr(rt.cap);
+        const uint64_t a0 = src & ~3ull;
+        const uint64_t avail64 = B.bytes_size - a0;
+        const uint32_t avail = avail64 > 0x7FFFFFF0ull ? 0x7FFFFFF0u : (uint32_t)avail64;
+        P.rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)(B.bytes + a0), (short)0, (int)avail, 0x00020000);
+        const uint32_t wbase = P.rec0 & ~(uint32_t)(NGZ_REG_WINDOW - 1);
+        for (uint32_t p = 0; p < NGZ_REG_WINDOW; p += 64) {
+            const uint32_t pr0 = wbase + p;
+            if (pr0 + 64 <= P.rec0 || pr0 >= P.rec0 + n) continue;  // no row of this pass in the chunk
+            P.prow = pr0;
+            P.lane = lane;
+            P.row = pr0 + lane;
+            P.valid = P.row >= P.rec0 && P.row < P.rec0 + n;
+            const uint32_t k = P.valid ? P.row - P.rec0 : 0;
+            const uint32_t rel = k * rl + (uint32_t)(src & 3);
+            P.rbase = rel & ~3u;
+            P.sh = rel & 3u;
+            P.any_sh = __builtin_amdgcn_ballot_w64(P.sh != 0) != 0;
+            P.recpos = P.pos0 + k * rl;
+            pass(P);
+        }
+    }
+}
+
+}  // namespace ngzdev

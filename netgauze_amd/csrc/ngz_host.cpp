@@ -31,7 +31,9 @@ extern "C" int ngz_launch_scan(void *temp, size_t temp_bytes, const uint32_t *in
                                hipStream_t st);
 extern "C" int ngz_launch_layout_emit(const BatchDev *B, const uint32_t *hf_flag, const uint32_t *hf_first,
                                       hipStream_t st);
-extern "C" int ngz_launch_decode(const BatchDev *B, uint32_t grid, uint32_t lds_bytes, hipStream_t st);
+extern "C" int ngz_launch_decode_generic(const BatchDev *B, uint32_t grid, hipStream_t st);
+void *ngz_rtc_kernel(int device, const DevPlan &P);
+int ngz_rtc_launch(void *fn, const BatchDev *B, uint32_t slot, uint32_t grid, hipStream_t st);
 extern "C" int ngz_launch_counts(const BatchDev *B, uint64_t set_cap, hipStream_t st);
 
 namespace {
@@ -127,6 +129,8 @@ struct Version {
     DevPlan plan;
     std::vector<uint8_t> fail_sub;  // per field: 1 InvalidLength, 2 InvalidPaddingLength, 3 scope InvalidLength
     uint64_t processed = 0;
+    int rtc_state = 0;              // specialised kernel: 0 not looked up, 1 ready, 2 unavailable
+    void *rtc_fn = nullptr;
 };
 
 std::string json_str(const char *s) {
@@ -238,57 +242,11 @@ void field_rule(const Spec &s, uint8_t &kind, uint16_t &width, uint8_t &fail) {
     failk(1);
 }
 
-// Choose the LDS pad period minimising ds_read_b32 bank conflicts of the
-// strided per-lane field reads (banks = dword address mod 32, lane groups
-// {0-31},{32-63}; MI355X_MICROARCH.md §LDS).
-uint8_t choose_pad_shift(const DevPlan &P) {
-    const uint32_t rpl = P.rpl, rl = P.rec_len;
-    static const uint8_t cands[] = {31, 8, 7, 6, 5, 4, 3};
-    uint64_t best_cost = ~0ull;
-    uint8_t best = 31;
-    for (uint8_t ps : cands) {
-        uint64_t cost = 0;
-        for (uint32_t f = 0; f < P.n_fields; ++f) {
-            const DevField &fd = P.f[f];
-            if (fd.kind == NGZ_K_FAIL || fd.kind == NGZ_K_VLEN) continue;
-            const uint32_t nd = fd.len <= 4 ? 2 : 3;
-            for (uint32_t sh = 0; sh < 16; sh += 4) {
-                for (uint32_t k = 0; k < rpl; ++k) {
-                    for (uint32_t j = 0; j < nd; ++j) {
-                        for (uint32_t g = 0; g < 2; ++g) {
-                            uint32_t hist[32] = {0};
-                            uint32_t addrs[32];
-                            uint32_t na = 0;
-                            for (uint32_t l = 32 * g; l < 32 * g + 32; ++l) {
-                                const uint32_t x = sh + (l * rpl + k) * rl + fd.off;
-                                const uint32_t q = (x >> 2) + j;
-                                const uint32_t a = q + (q >> ps);
-                                bool dup = false;
-                                for (uint32_t t = 0; t < na; ++t)
-                                    if (addrs[t] == a) { dup = true; break; }
-                                if (dup) continue;
-                                addrs[na++] = a;
-                                hist[a & 31]++;
-                            }
-                            uint32_t m = 0;
-                            for (uint32_t b = 0; b < 32; ++b) m = std::max(m, hist[b]);
-                            cost += m;
-                        }
-                    }
-                }
-            }
-        }
-        if (cost < best_cost) { best_cost = cost; best = ps; }
-    }
-    return best;
-}
-
 void build_plan(Version &v) {
     DevPlan &P = v.plan;
     memset(&P, 0, sizeof P);
     P.proto = v.proto;
     P.template_id = v.tid;
-    P.pad_shift = 31;
     v.fail_sub.assign(v.specs.size(), 0);
     uint32_t off = 0, col = 0, rl = 0;
     bool vlen = false, devok = v.specs.size() <= NGZ_MAXF;
@@ -323,22 +281,11 @@ void build_plan(Version &v) {
         if (P.f[i].kind == NGZ_K_DTMS || P.f[i].kind == NGZ_K_DTFRAC || P.f[i].kind == NGZ_K_STR ||
             P.f[i].kind == NGZ_K_FAIL)
             P.has_err = 1;
-    uint32_t rpl = 0;
-    if (devok && !(v.proto == 10 && vlen)) {
-        if (rl <= 64) rpl = 4;
-        else if (rl <= 128) rpl = 2;
-        else if (rl <= NGZ_MAX_REC_LEN) rpl = 1;
-    }
-    P.rpl = (uint8_t)rpl;
-    P.window = rpl ? 64 * rpl : 64;
-    if (rpl) P.pad_shift = choose_pad_shift(P);
-}
-
-uint32_t lds_bytes_for(const DevPlan &P) {
-    if (!P.rpl) return 0;
-    const uint32_t bytes = 16 + P.window * P.rec_len + 16;
-    const uint32_t q = (bytes + 3) / 4 + 4;
-    return 16 * NGZ_MAXF + 4 * (q + (q >> P.pad_shift) + 4);  // field table + staged chunk
+    // rpl != 0: device-decodable (every fixed-length record; IPFIX templates
+    // with variable-length fields are not yet)
+    P.rpl = 0;
+    P.window = NGZ_REG_WINDOW;
+    if (devok && !(v.proto == 10 && vlen) && rl <= NGZ_MAX_REC_LEN) P.rpl = 1;
 }
 
 struct ErrInfo {  // host-side framing error
@@ -410,6 +357,10 @@ struct ngz_ctx {
     BatchSummary summary{};
     ngz_batch_in last_in{};
     hipEvent_t ev[4]{};
+    int n_cus = 256;
+    int specialize = 1;                         // NGZ_OPT_SPECIALIZE
+    BatchSummary *h_summary = nullptr;          // pinned
+    SlotRT *h_slots = nullptr;                  // pinned, NGZ_MAX_SLOTS
     float t_decode = 0, t_pipeline = 0;
     bool plans_dirty = true;
     uint32_t n_template_dgrams = 0;
@@ -827,7 +778,18 @@ int upload_slots(ngz_ctx *ctx, const std::vector<int32_t> cur_start[2], hipStrea
     if (ctx->d_plans.ensure(std::max<size_t>(S, 1)) || ctx->d_cur_slot.ensure(2 * 65536))
         return fail(ctx, NGZ_E_NOMEM, "device alloc (plans)");
     std::vector<DevPlan> plans(S);
-    for (size_t s = 0; s < S; ++s) plans[s] = ctx->versions[ctx->slot_version[s]].plan;
+    for (size_t s = 0; s < S; ++s) {
+        Version &v = ctx->versions[ctx->slot_version[s]];
+        plans[s] = v.plan;
+        plans[s].spec = 0;
+        if (ctx->specialize && v.plan.rpl) {
+            if (v.rtc_state == 0) {
+                v.rtc_fn = ngz_rtc_kernel(ctx->device, v.plan);
+                v.rtc_state = v.rtc_fn ? 1 : 2;
+            }
+            plans[s].spec = v.rtc_state == 1;
+        }
+    }
     std::vector<uint16_t> cs(2 * 65536, NGZ_NO_SLOT);
     for (int pi = 0; pi < 2; ++pi)
         for (uint32_t id = 0; id < 65536; ++id)
@@ -850,7 +812,7 @@ struct HostFramed {
 int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const HostFramed *hf) {
     const uint32_t N = in->n;
     const uint32_t S = (uint32_t)ctx->slot_version.size();
-    const uint64_t n_items = (uint64_t)(S + 2) * N + 1;
+    const uint64_t n_items = (uint64_t)(2 * S + 1) * N + 1;
     if (n_items > 0x7FFFFFF0ull) return fail(ctx, NGZ_E_LIMIT, "batch too large for the count matrix");
     size_t scan_tmp = 0;
     if (ngz_scan_temp_bytes(n_items, &scan_tmp)) return fail(ctx, NGZ_E_DEVICE, "scan temp size");
@@ -858,11 +820,10 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
     uint64_t chunk_cap = std::max<uint64_t>(ctx->d_chunks.cap, in->bytes_size / 4096 + 3ull * N + 1024);
     uint64_t set_cap = std::max<uint64_t>(ctx->d_sets.cap, 2ull * N + 1024);
     double ratio = 1.0;
-    uint32_t lds = 64, maxwin_row = 0;
+    uint32_t maxwin_row = 0;
     for (uint32_t s = 0; s < S; ++s) {
         const DevPlan &P = ctx->versions[ctx->slot_version[s]].plan;
         if (P.rec_len) ratio = std::max(ratio, (double)P.row_bytes / (double)P.rec_len);
-        lds = std::max(lds, lds_bytes_for(P));
         maxwin_row = std::max<uint32_t>(maxwin_row, P.window * P.row_bytes);
     }
     uint64_t arena_cap = (uint64_t)(ratio * (double)in->bytes_size) + (uint64_t)S * (maxwin_row + 256) + 4096;
@@ -935,24 +896,38 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
         return fail(ctx, NGZ_E_DEVICE, "scan launch");
     if (ngz_launch_layout_emit(&B, hf_flag, hf_first, st)) return fail(ctx, NGZ_E_DEVICE, "layout/emit launch");
     HIPCHK(hipEventRecord(ctx->ev[1], st));
-    int dev_cus = 256;
-    hipDeviceGetAttribute(&dev_cus, hipDeviceAttributeMultiprocessorCount, ctx->device);
-    const uint32_t per_cu = std::max<uint32_t>(1, std::min<uint32_t>(16, 160 * 1024 / std::max<uint32_t>(lds, 1)));
-    const uint32_t grid = (uint32_t)dev_cus * per_cu * 4;
-    if (ngz_launch_decode(&B, grid, lds, st)) return fail(ctx, NGZ_E_DEVICE, "decode launch");
-    HIPCHK(hipEventRecord(ctx->ev[2], st));
-    if (ngz_launch_counts(&B, ctx->d_sets.cap, st)) return fail(ctx, NGZ_E_DEVICE, "counts launch");
-    HIPCHK(hipEventRecord(ctx->ev[3], st));
-    HIPCHK(hipMemcpyAsync(&ctx->summary, ctx->d_summary.p, sizeof(BatchSummary), hipMemcpyDeviceToHost, st));
+    // per-slot chunk ranges and capacities decide which decode kernels run
+    HIPCHK(hipMemcpyAsync(ctx->h_summary, ctx->d_summary.p, sizeof(BatchSummary), hipMemcpyDeviceToHost, st));
+    if (S) HIPCHK(hipMemcpyAsync(ctx->h_slots, ctx->d_slots.p, S * sizeof(SlotRT), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
-    hipEventElapsedTime(&ctx->t_decode, ctx->ev[1], ctx->ev[2]);
-    hipEventElapsedTime(&ctx->t_pipeline, ctx->ev[0], ctx->ev[3]);
+    ctx->summary = *ctx->h_summary;
     if (ctx->summary.overflow) {
         if (ctx->summary.overflow & 1) ctx->d_arena.ensure(ctx->summary.arena_used + 4096);
         if (ctx->summary.overflow & 2) ctx->d_chunks.ensure(ctx->summary.n_chunks + 1024);
         if (ctx->summary.overflow & 4) ctx->d_sets.ensure(ctx->summary.n_sets + 1024);
         return 1;  // retry
     }
+    const uint32_t grid = (uint32_t)ctx->n_cus * 8;  // 256-thread blocks: up to 32 waves per CU
+    bool generic = false;
+    for (uint32_t s = 0; s < S; ++s) {
+        if (!ctx->h_slots[s].nchunks) continue;
+        const Version &v = ctx->versions[ctx->slot_version[s]];
+        if (!v.plan.rpl) continue;
+        if (ctx->specialize && v.rtc_state == 1) {
+            // one specialised kernel per active template, over that slot's chunks only
+            const uint32_t g = std::min<uint32_t>(grid, (ctx->h_slots[s].nchunks + 3) / 4);
+            if (ngz_rtc_launch(v.rtc_fn, &B, s, g, st)) return fail(ctx, NGZ_E_DEVICE, "specialised decode launch");
+        } else {
+            generic = true;
+        }
+    }
+    if (generic && ngz_launch_decode_generic(&B, grid, st)) return fail(ctx, NGZ_E_DEVICE, "decode launch");
+    HIPCHK(hipEventRecord(ctx->ev[2], st));
+    if (ngz_launch_counts(&B, ctx->d_sets.cap, st)) return fail(ctx, NGZ_E_DEVICE, "counts launch");
+    HIPCHK(hipEventRecord(ctx->ev[3], st));
+    HIPCHK(hipStreamSynchronize(st));
+    hipEventElapsedTime(&ctx->t_decode, ctx->ev[1], ctx->ev[2]);
+    hipEventElapsedTime(&ctx->t_pipeline, ctx->ev[0], ctx->ev[3]);
     return 0;
 }
 
@@ -1012,6 +987,13 @@ int ngz_ctx_create(int device, ngz_ctx **out) {
         return NGZ_E_DEVICE;
     }
     for (auto &e : ctx->ev) hipEventCreate(&e);
+    hipDeviceGetAttribute(&ctx->n_cus, hipDeviceAttributeMultiprocessorCount, device);
+    if (hipHostMalloc((void **)&ctx->h_summary, sizeof(BatchSummary), 0) != hipSuccess ||
+        hipHostMalloc((void **)&ctx->h_slots, NGZ_MAX_SLOTS * sizeof(SlotRT), 0) != hipSuccess) {
+        ngz_ctx_destroy(ctx);
+        return NGZ_E_NOMEM;
+    }
+    if (const char *e = getenv("NGZ_SPECIALIZE")) ctx->specialize = atoi(e);
     *out = ctx;
     return NGZ_OK;
 }
@@ -1027,6 +1009,8 @@ void ngz_ctx_destroy(ngz_ctx *ctx) {
     ctx->d_proc.release(); ctx->d_summary.release(); ctx->d_in_bytes.release(); ctx->d_in_off.release();
     ctx->d_in_len.release();
     for (auto &e : ctx->ev) hipEventDestroy(e);
+    if (ctx->h_summary) hipHostFree(ctx->h_summary);
+    if (ctx->h_slots) hipHostFree(ctx->h_slots);
     hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -1151,8 +1135,8 @@ int ngz_decode_batch(ngz_ctx *ctx, const ngz_batch_in *in, ngz_batch_out *out, v
                 fprintf(stderr, "[ngz]   tl key %u dgram %u slot %u\n", hf.tl.key[i], hf.tl.dgram[i], hf.tl.slot[i]);
             for (size_t s2 = 0; s2 < ctx->slot_version.size(); ++s2) {
                 const DevPlan &P = ctx->versions[ctx->slot_version[s2]].plan;
-                fprintf(stderr, "[ngz]   slot %zu version %d tid %u rec_len %u rpl %u nf %u ps %u\n", s2,
-                        ctx->slot_version[s2], P.template_id, P.rec_len, P.rpl, P.n_fields, P.pad_shift);
+                fprintf(stderr, "[ngz]   slot %zu version %d tid %u rec_len %u rpl %u nf %u spec %u\n", s2,
+                        ctx->slot_version[s2], P.template_id, P.rec_len, P.rpl, P.n_fields, P.spec);
             }
         }
         for (int tries = 0; (rc = run_pipeline(ctx, in, st, &hf)) == 1 && tries < 4; ++tries) {}

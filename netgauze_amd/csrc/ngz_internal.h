@@ -7,7 +7,8 @@
 #define NGZ_MAX_SLOTS 1024    // template versions live in one batch
 #define NGZ_NO_SLOT 0xFFFFu
 #define NGZ_NO_ERR (~0ull)
-#define NGZ_MAX_REC_LEN 2048  // longest fixed record the LDS-staged decode takes
+#define NGZ_MAX_REC_LEN 65535 // longest fixed record the device decode takes
+#define NGZ_REG_WINDOW 256    // records per chunk window (4 passes of 64 lanes)
 
 // datagram frame state (k_frame -> host)
 #define NGZ_FR_OK 0
@@ -62,12 +63,12 @@ struct DevPlan {
     uint32_t row_bytes;  // sum of column widths
     uint16_t n_fields;
     uint8_t proto;       // 10 / 9
-    uint8_t rpl;         // records per lane: 4, 2, 1; 0 = not device-decodable
-    uint8_t pad_shift;   // LDS: one pad dword per 2^pad_shift dwords (31 = none)
+    uint8_t rpl;         // 1 = device-decodable (fixed-length records), 0 = not
+    uint8_t reserved0;
     uint8_t has_vlen;
     uint8_t has_err;
-    uint8_t reserved0;
-    uint32_t window;     // records per chunk window = 64*rpl
+    uint8_t spec;        // 1 = decoded by a run-time specialised kernel (the generic kernel skips it)
+    uint32_t window;     // records per chunk window (NGZ_REG_WINDOW)
     uint32_t template_id;
     uint32_t reserved1[2];
     DevField f[NGZ_MAXF];
@@ -78,6 +79,8 @@ struct SlotRT {          // per batch slot, computed on device by k_layout
     uint32_t cap;        // rows allocated
     uint32_t total;      // rows used
     uint32_t base;       // first element of the slot's row in the scanned count matrix
+    uint32_t chunk0;     // first chunk of the slot (chunks are slot-major)
+    uint32_t nchunks;    // chunks of the slot (incl. empty padding chunks)
     uint32_t reserved;
 };
 
@@ -88,7 +91,7 @@ struct Chunk {           // 32 B, one wave of work
     uint16_t n;          // records (0 = empty slot)
     uint16_t slot;
     uint16_t pos0;       // first record's offset inside the datagram
-    uint16_t reserved;
+    uint16_t cls;        // reserved (0)
     uint32_t reserved2;
 };
 
@@ -131,7 +134,7 @@ struct BatchDev {        // device pointers of one batch
     const HostSet *hf_sets;
     const void *hf_hdr;        // [hosts] ngz_dgram_hdr of host-framed datagrams (hf_flag[d]-1 indexes)
     void *hdr;                 // ngz_dgram_hdr[n]
-    uint32_t *counts;          // [(n_slots+2)*n + 1]
+    uint32_t *counts;          // [(2*n_slots+1)*n + 1]
     uint32_t *scan;            // same length
     SlotRT *slots;             // [n_slots]
     Chunk *chunks;

@@ -1,5 +1,8 @@
-// HIP kernels for gfx950 (CDNA4): datagram framing, record counting/layout
-// and the LDS-staged columnar record decode.
+// HIP kernels for gfx950 (CDNA4): datagram framing, record counting/layout,
+// the generic (field-table driven) columnar record decode and the
+// processed-count bookkeeping.  Per-template specialised decode kernels are
+// generated and compiled at run time (ngz_rtc.cpp) from the same primitives
+// (ngz_dev.h).
 //
 // Reference behaviour restated (file:line relative to the NetGauze checkout):
 //   framing   crates/flow-pkt/src/codec.rs:189-220 (decode gate),
@@ -12,9 +15,11 @@
 #include <hipcub/hipcub.hpp>
 
 #include "ngz/flow_decode.h"
+#include "ngz_dev.h"
 #include "ngz_internal.h"
 
 namespace {
+using namespace ngzdev;
 
 __device__ __forceinline__ uint32_t ld8(const uint8_t *p) { return p[0]; }
 __device__ __forceinline__ uint32_t be16(const uint8_t *p) { return ((uint32_t)p[0] << 8) | p[1]; }
@@ -181,14 +186,18 @@ __device__ bool has_template_sets(const BatchDev &B, uint32_t d) {
     return false;
 }
 
+// Count matrix, slot-major rows of N datagrams (scanned in one pass):
+//   rows [0, S)      records of slot s in datagram d
+//   rows [S, 2S)     decode chunks of slot s in datagram d
+//   row  2S          data sets in datagram d
 struct CountVis {
     uint32_t *counts;
     uint32_t N, S, d;
-    uint32_t chunks, sets;
+    uint32_t sets;
     const DevPlan *plans;
     __device__ void on_set(uint32_t, uint32_t slot, uint32_t n, uint32_t, uint32_t) {
         counts[(uint64_t)slot * N + d] += n;
-        if (n) chunks += (n + plans[slot].window - 1) / plans[slot].window + 1;
+        if (n) counts[(uint64_t)(S + slot) * N + d] += (n + plans[slot].window - 1) / plans[slot].window + 1;
         sets += 1;
     }
 };
@@ -196,13 +205,12 @@ struct CountVis {
 __global__ void k_frame(BatchDev B, const uint32_t *hf_flag, const uint32_t *hf_first) {
     const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
     if (d >= B.n) return;
-    CountVis vis{B.counts, B.n, B.n_slots, d, 0, 0, B.plans};
+    CountVis vis{B.counts, B.n, B.n_slots, d, 0, B.plans};
     WalkOut o;
     walk_datagram(B, hf_flag, hf_first, d, o, vis);
     if (o.status != NGZ_FR_HOST && !(hf_flag && hf_flag[d]) && has_template_sets(B, d)) o.status = NGZ_FR_HOST;
     const uint64_t N = B.n;
-    B.counts[(uint64_t)B.n_slots * N + d] = vis.chunks;
-    B.counts[(uint64_t)(B.n_slots + 1) * N + d] = vis.sets;
+    B.counts[(uint64_t)(2 * B.n_slots) * N + d] = vis.sets;
     ngz_dgram_hdr h;
     h.status = (uint8_t)o.status;
     h.version = (uint8_t)o.version;
@@ -226,6 +234,7 @@ __global__ void k_layout(BatchDev B) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     const uint64_t N = B.n;
     const uint32_t S = B.n_slots;
+    const uint32_t chunk_base = B.scan[(uint64_t)S * N];
     uint64_t off = 0;
     for (uint32_t s = 0; s < S; ++s) {
         const uint32_t base = B.scan[(uint64_t)s * N];
@@ -238,15 +247,15 @@ __global__ void k_layout(BatchDev B) {
         rt.cap = cap;
         rt.total = total;
         rt.base = base;
+        rt.chunk0 = B.scan[(uint64_t)(S + s) * N] - chunk_base;
+        rt.nchunks = B.scan[(uint64_t)(S + s + 1) * N] - B.scan[(uint64_t)(S + s) * N];
         rt.reserved = 0;
         B.slots[s] = rt;
         off += ((uint64_t)cap * B.plans[s].row_bytes + 255) & ~255ull;
     }
-    const uint64_t last = (uint64_t)(S + 2) * N;
-    const uint32_t grand = B.scan[last];
-    const uint32_t rec_total = B.scan[(uint64_t)S * N];
-    const uint32_t chunks = B.scan[(uint64_t)(S + 1) * N] - rec_total;
-    const uint32_t sets = grand - B.scan[(uint64_t)(S + 1) * N];
+    const uint32_t rec_total = chunk_base;
+    const uint32_t chunks = B.scan[(uint64_t)(2 * S) * N] - chunk_base;
+    const uint32_t sets = B.scan[(uint64_t)(2 * S + 1) * N] - B.scan[(uint64_t)(2 * S) * N];
     B.summary->n_records_total = rec_total;
     B.summary->n_chunks = chunks;
     B.summary->n_sets = sets;
@@ -262,7 +271,7 @@ struct EmitVis {
     const BatchDev *B;
     uint32_t d;
     uint64_t dg_off;
-    uint32_t chunk_at, set_at;
+    uint32_t set_at;
     bool ok;
     __device__ void on_set(uint32_t set_pos, uint32_t slot, uint32_t n, uint32_t payload_pos, uint32_t rl) {
         const uint64_t N = B->n;
@@ -280,6 +289,9 @@ struct EmitVis {
         if (!n) return;
         const uint32_t W = B->plans[slot].window;
         const uint32_t reserved = (n + W - 1) / W + 1;
+        uint32_t *ccell = &B->scan[(uint64_t)(B->n_slots + slot) * N + d];  // this slot's chunk cursor
+        const uint32_t chunk_at = *ccell - B->scan[(uint64_t)B->n_slots * N];
+        *ccell += reserved;
         uint32_t r = 0, used = 0;
         while (r < n) {
             const uint32_t cstart = rec0 + r;
@@ -292,7 +304,7 @@ struct EmitVis {
             c.n = (uint16_t)take;
             c.slot = (uint16_t)slot;
             c.pos0 = (uint16_t)(payload_pos + r * rl);
-            c.reserved = 0;
+            c.cls = 0;
             c.reserved2 = 0;
             B->chunks[chunk_at + used] = c;
             ++used;
@@ -302,7 +314,6 @@ struct EmitVis {
             Chunk c = {};
             B->chunks[chunk_at + used] = c;
         }
-        chunk_at += reserved;
     }
 };
 
@@ -316,405 +327,124 @@ __global__ void k_emit(BatchDev B, const uint32_t *hf_flag, const uint32_t *hf_f
     vis.B = &B;
     vis.d = d;
     vis.dg_off = B.offsets[d];
-    vis.chunk_at = B.scan[(uint64_t)S * N + d] - B.scan[(uint64_t)S * N];
-    vis.set_at = B.scan[(uint64_t)(S + 1) * N + d] - B.scan[(uint64_t)(S + 1) * N];
+    vis.set_at = B.scan[(uint64_t)(2 * S) * N + d] - B.scan[(uint64_t)(2 * S) * N];
     vis.ok = true;
     WalkOut o;
     walk_datagram(B, hf_flag, hf_first, d, o, vis);
 }
 
 // ---------------------------------------------------------------------------
-// Record decode: one wave (workgroup of 64) per chunk of <= 64*RPL records.
-// 1) the chunk's bytes are staged HBM -> LDS with 16-byte buffer loads (one
-//    pad dword per 2^pad_shift dwords to spread the strided reads over banks);
-// 2) lane l owns RPL consecutive rows of every column: it reads each field of
-//    its records from LDS, byte-swaps/widens in VGPRs and writes RPL*width
-//    contiguous bytes per column, so a wave stores 64*RPL*width contiguous bytes.
+// Generic record decode (any fixed-length template; the fallback for slots
+// without a specialised run-time-compiled kernel).  One wave per chunk
+// (<= NGZ_REG_WINDOW rows of one output window), 64 rows per pass, one record
+// per lane (ngz_dev.h).  The template's field table is held one descriptor per
+// lane and fetched with v_readlane into SGPRs, so every field's offset,
+// length and kind is wave-uniform; the 80-byte register window slides along
+// the record as fields require (fields are in record order).  Every lane runs
+// the whole field walk (uniform control flow: the register-indexing
+// sequences assume it); only lanes whose row belongs to the chunk store.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t pidx(uint32_t q, uint32_t ps) { return q + (q >> ps); }
-
-__device__ __forceinline__ uint32_t lds_dw(const uint32_t *lds, uint32_t q, uint32_t ps) { return lds[pidx(q, ps)]; }
-
-// big-endian unsigned of `len` (0..8) bytes starting at staged byte x
-__device__ __forceinline__ uint64_t read_be(const uint32_t *lds, uint32_t x, uint32_t len, uint32_t ps) {
-    const uint32_t q = x >> 2, s = x & 3;
-    const uint32_t d0 = lds_dw(lds, q, ps), d1 = lds_dw(lds, q + 1, ps);
-    const uint32_t lo = __builtin_amdgcn_alignbyte(d1, d0, s);
-    if (len <= 4) {
-        if (len == 0) return 0;
-        return __builtin_bswap32(lo) >> (32 - 8 * len);
-    }
-    const uint32_t d2 = lds_dw(lds, q + 2, ps);
-    const uint32_t hi = __builtin_amdgcn_alignbyte(d2, d1, s);
-    const uint64_t v = ((uint64_t)__builtin_bswap32(lo) << 32) | __builtin_bswap32(hi);
-    return v >> (64 - 8 * len);
-}
-
-__device__ __forceinline__ uint32_t read_byte(const uint32_t *lds, uint32_t x, uint32_t ps) {
-    return (lds_dw(lds, x >> 2, ps) >> (8 * (x & 3))) & 0xFF;
-}
-
-// 4 raw bytes at staged byte x as a little-endian dword (wire order)
-__device__ __forceinline__ uint32_t read_raw4(const uint32_t *lds, uint32_t x, uint32_t ps) {
-    const uint32_t q = x >> 2;
-    return __builtin_amdgcn_alignbyte(lds_dw(lds, q + 1, ps), lds_dw(lds, q, ps), x & 3);
-}
-
-// chrono NaiveDate range (0.4.45): -262143-01-01 .. +262142-12-31, in ms
-__device__ constexpr int64_t kMinMillis = -8334601315200000LL;  // days_from_civil(-262143,1,1)*86400000
-__device__ constexpr int64_t kMaxMillis = 8210266876799999LL;   // (days_from_civil(262142,12,31)+1)*86400000-1
-
-template <int RPL>
-__device__ __forceinline__ void store_num(uint8_t *col, uint32_t row0, uint32_t width, const uint64_t (&v)[RPL], uint32_t vmask) {
-    constexpr uint32_t full = (1u << RPL) - 1;
-    if (vmask == full) {
-        if (width == 1) {
-            if constexpr (RPL == 4) {
-                *(uint32_t *)(col + row0) = (uint32_t)(v[0] & 0xFF) | ((uint32_t)(v[1] & 0xFF) << 8) |
-                                            ((uint32_t)(v[2] & 0xFF) << 16) | ((uint32_t)(v[3] & 0xFF) << 24);
-            } else if constexpr (RPL == 2) {
-                *(uint16_t *)(col + row0) = (uint16_t)((v[0] & 0xFF) | ((v[1] & 0xFF) << 8));
-            } else {
-                col[row0] = (uint8_t)v[0];
-            }
-        } else if (width == 2) {
-            if constexpr (RPL == 4) {
-                uint2 w;
-                w.x = (uint32_t)(v[0] & 0xFFFF) | ((uint32_t)(v[1] & 0xFFFF) << 16);
-                w.y = (uint32_t)(v[2] & 0xFFFF) | ((uint32_t)(v[3] & 0xFFFF) << 16);
-                *(uint2 *)(col + 2 * row0) = w;
-            } else if constexpr (RPL == 2) {
-                *(uint32_t *)(col + 2 * row0) = (uint32_t)(v[0] & 0xFFFF) | ((uint32_t)(v[1] & 0xFFFF) << 16);
-            } else {
-                *(uint16_t *)(col + 2 * row0) = (uint16_t)v[0];
-            }
-        } else if (width == 4) {
-            if constexpr (RPL == 4) {
-                uint4 w = make_uint4((uint32_t)v[0], (uint32_t)v[1], (uint32_t)v[2], (uint32_t)v[3]);
-                *(uint4 *)(col + 4 * row0) = w;
-            } else if constexpr (RPL == 2) {
-                *(uint2 *)(col + 4 * row0) = make_uint2((uint32_t)v[0], (uint32_t)v[1]);
-            } else {
-                *(uint32_t *)(col + 4 * row0) = (uint32_t)v[0];
-            }
-        } else {  // 8
-            if constexpr (RPL == 4) {
-                uint4 a = make_uint4((uint32_t)v[0], (uint32_t)(v[0] >> 32), (uint32_t)v[1], (uint32_t)(v[1] >> 32));
-                uint4 b = make_uint4((uint32_t)v[2], (uint32_t)(v[2] >> 32), (uint32_t)v[3], (uint32_t)(v[3] >> 32));
-                *(uint4 *)(col + 8 * row0) = a;
-                *(uint4 *)(col + 8 * row0 + 16) = b;
-            } else if constexpr (RPL == 2) {
-                *(uint4 *)(col + 8 * row0) =
-                    make_uint4((uint32_t)v[0], (uint32_t)(v[0] >> 32), (uint32_t)v[1], (uint32_t)(v[1] >> 32));
-            } else {
-                *(uint2 *)(col + 8 * row0) = make_uint2((uint32_t)v[0], (uint32_t)(v[0] >> 32));
-            }
-        }
-        return;
-    }
-#pragma unroll
-    for (int k = 0; k < RPL; ++k) {
-        if (!(vmask >> k & 1)) continue;
-        uint8_t *dst = col + (uint64_t)(row0 + k) * width;
-        if (width == 1) *dst = (uint8_t)v[k];
-        else if (width == 2) *(uint16_t *)dst = (uint16_t)v[k];
-        else if (width == 4) *(uint32_t *)dst = (uint32_t)v[k];
-        else *(uint64_t *)dst = v[k];
-    }
-}
-
-// raw byte columns (mac, mpls, ipv6, octets, strings, u256): `len` wire bytes
-// copied to `width` column bytes (zero padded when width > len)
-template <int RPL>
-__device__ __forceinline__ void store_bytes(uint8_t *col, uint32_t row0, uint32_t width, uint32_t len,
-                                            const uint32_t *lds, const uint32_t (&x)[RPL], uint32_t vmask,
-                                            uint32_t ps) {
-    constexpr uint32_t full = (1u << RPL) - 1;
-    if (vmask == full && (width & 3) == 0 && len == width) {
-        // every output dword lies inside one record
-        uint32_t *dst = (uint32_t *)(col + (uint64_t)row0 * width);
-        const uint32_t wd = width >> 2;
-#pragma unroll
-        for (int k = 0; k < RPL; ++k)
-            for (uint32_t j = 0; j < wd; ++j) dst[k * wd + j] = read_raw4(lds, x[k] + 4 * j, ps);
-        return;
-    }
-#pragma unroll
-    for (int k = 0; k < RPL; ++k) {
-        if (!(vmask >> k & 1)) continue;
-        uint8_t *dst = col + (uint64_t)(row0 + k) * width;
-        uint32_t j = 0;
-        if ((width & 3) == 0 && (((uintptr_t)dst) & 3) == 0) {
-            for (; j + 4 <= len; j += 4) *(uint32_t *)(dst + j) = read_raw4(lds, x[k] + j, ps);
-        }
-        for (; j < len; ++j) dst[j] = (uint8_t)read_byte(lds, x[k] + j, ps);
-        for (; j < width; ++j) dst[j] = 0;
-    }
-}
-
-__device__ bool utf8_valid_prefix(const uint32_t *lds, uint32_t x, uint32_t len, uint32_t ps) {
-    // validate bytes up to the first NUL (generator.rs:1651-1668)
-    uint32_t i = 0;
-    while (i < len) {
-        const uint32_t c = read_byte(lds, x + i, ps);
-        if (c == 0) return true;
-        if (c < 0x80) { ++i; continue; }
-        uint32_t need, lo = 0x80, hi = 0xBF;
-        if (c >= 0xC2 && c <= 0xDF) need = 1;
-        else if (c >= 0xE0 && c <= 0xEF) { need = 2; if (c == 0xE0) lo = 0xA0; if (c == 0xED) hi = 0x9F; }
-        else if (c >= 0xF0 && c <= 0xF4) { need = 3; if (c == 0xF0) lo = 0x90; if (c == 0xF4) hi = 0x8F; }
-        else return false;
-        for (uint32_t t = 1; t <= need; ++t) {
-            if (i + t >= len) return false;
-            const uint32_t b = read_byte(lds, x + i + t, ps);
-            const uint32_t l2 = (t == 1) ? lo : 0x80, h2 = (t == 1) ? hi : 0xBF;
-            if (b < l2 || b > h2) return false;
-        }
-        i += need + 1;
-    }
-    return true;
-}
-
-__device__ __forceinline__ uint32_t sgpr(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
-
-typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-constexpr int STAGE_BATCH = 16;  // 16 x 1 KiB per wave in flight
-
-struct ChunkS {  // chunk descriptor in SGPRs
-    uint64_t src;
-    uint32_t rec0, dgram, n, slot, pos0;
-};
-
-struct PlanS {  // plan header in SGPRs
-    uint32_t rec_len, n_fields, rpl, ps;
-};
-
-template <int RPL>
-__device__ void decode_chunk(const BatchDev &B, const ChunkS &c, const PlanS &P, const uint4 *ftab, uint32_t *lds) {
-    const uint32_t lane = threadIdx.x;
-    const uint32_t n = c.n;
-    const uint32_t rl = P.rec_len;
-    const uint32_t ps = P.ps;
-    // ---- stage the chunk's bytes into LDS (16-byte buffer loads) ----
-    const uint64_t a0 = c.src & ~15ull;
-    const uint32_t sh = (uint32_t)(c.src - a0);
-    const uint32_t total = sh + n * rl;
-    const uint64_t avail64 = B.bytes_size - a0;
-    const uint32_t avail = avail64 > 0x7FFFFFF0ull ? 0x7FFFFFF0u : (uint32_t)avail64;
-    __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void *)(B.bytes + a0), (short)0, (int)avail, 0x00020000);
-    const uint32_t nq = (total + 15) >> 4;
-    // issue up to 16 x 16-byte loads per lane before the first LDS write, so a
-    // 16 KB chunk costs one HBM round trip (not one per load)
-    for (uint32_t q0 = 0; q0 < nq; q0 += 64 * STAGE_BATCH) {
-        v4u v[STAGE_BATCH];
-#pragma unroll
-        for (int j = 0; j < STAGE_BATCH; ++j) {
-            const uint32_t q = q0 + j * 64 + lane;
-            v[j] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, q * 16, 0, 0);  // OOB -> 0
-        }
-#pragma unroll
-        for (int j = 0; j < STAGE_BATCH; ++j) {
-            const uint32_t q = q0 + j * 64 + lane;
-            if (q < nq) {
-                const uint32_t b = 4 * q;
-                lds[pidx(b, ps)] = v[j][0];
-                lds[pidx(b + 1, ps)] = v[j][1];
-                lds[pidx(b + 2, ps)] = v[j][2];
-                lds[pidx(b + 3, ps)] = v[j][3];
-            }
-        }
-    }
-    __syncthreads();
-    // ---- this lane's rows ----
-    const uint32_t W = 64 * RPL;
-    const uint32_t wbase = c.rec0 & ~(W - 1);
-    const uint32_t row0 = wbase + lane * RPL;  // first row this lane owns
-    uint32_t vmask = 0;
-    uint32_t xr[RPL];  // staged byte of each record
-#pragma unroll
-    for (int k = 0; k < RPL; ++k) {
-        const int32_t r = (int32_t)(row0 + k) - (int32_t)c.rec0;
-        const bool ok = r >= 0 && (uint32_t)r < n;
-        vmask |= (ok ? 1u : 0u) << k;
-        xr[k] = ok ? sh + (uint32_t)r * rl : sh;
-    }
-    if (vmask) {
-        const SlotRT rt = B.slots[c.slot];
-        uint8_t *blk = B.arena + sgpr((uint32_t)rt.block) + ((uint64_t)sgpr((uint32_t)(rt.block >> 32)) << 32);
-        const uint32_t cap = sgpr(rt.cap);
-        const uint32_t nf = P.n_fields;
-        for (uint32_t f = 0; f < nf; ++f) {
-            const uint4 fdv = ftab[f];  // LDS broadcast read of the field descriptor
-            const uint32_t off = sgpr(fdv.x & 0xFFFF), len = sgpr(fdv.x >> 16);
-            const uint32_t width = sgpr(fdv.y & 0xFFFF), kind = sgpr((fdv.y >> 16) & 0xFF);
-            const uint32_t col_off = sgpr(fdv.z);
-            uint8_t *col = blk + (uint64_t)cap * col_off;
-            uint32_t x[RPL];
-#pragma unroll
-            for (int k = 0; k < RPL; ++k) x[k] = xr[k] + off;
-            switch (kind) {
-            case NGZ_K_UINT:
-            case NGZ_K_SCOPE32: {
-                uint64_t v[RPL];
-#pragma unroll
-                for (int k = 0; k < RPL; ++k) v[k] = read_be(lds, x[k], len, ps);
-                store_num<RPL>(col, row0, width, v, vmask);
-                break;
-            }
-            case NGZ_K_TCPFLAGS: {
-                uint64_t v[RPL];
-#pragma unroll
-                for (int k = 0; k < RPL; ++k) v[k] = read_be(lds, x[k], len, ps) & 0xFF;
-                store_num<RPL>(col, row0, width, v, vmask);
-                break;
-            }
-            case NGZ_K_SINT: {
-                uint64_t v[RPL];
-#pragma unroll
-                for (int k = 0; k < RPL; ++k) {
-                    const uint64_t u = read_be(lds, x[k], len, ps);
-                    const uint32_t sh2 = len ? 64 - 8 * len : 0;
-                    v[k] = (uint64_t)(((int64_t)(u << sh2)) >> sh2);
-                }
-                store_num<RPL>(col, row0, width, v, vmask);
-                break;
-            }
-            case NGZ_K_BOOL: {
-                uint64_t v[RPL];
-#pragma unroll
-                for (int k = 0; k < RPL; ++k) v[k] = read_byte(lds, x[k], ps) != 0;
-                store_num<RPL>(col, row0, width, v, vmask);
-                break;
-            }
-            case NGZ_K_DTMS: {
-                uint64_t v[RPL];
-#pragma unroll
-                for (int k = 0; k < RPL; ++k) {
-                    v[k] = read_be(lds, x[k], 8, ps);
-                    const int64_t ms = (int64_t)v[k];
-                    if ((vmask >> k & 1) && (ms < kMinMillis || ms > kMaxMillis)) {
-                        const uint32_t pos = c.pos0 + (row0 + k - c.rec0) * rl + off;
-                        atomicMin((unsigned long long *)&((ngz_dgram_hdr *)B.hdr)[c.dgram].err_key,
-                                  (unsigned long long)ngz_err_key(pos, E_REC_DTMS, f, 0));
-                    }
-                }
-                store_num<RPL>(col, row0, width, v, vmask);
-                break;
-            }
-            case NGZ_K_DTFRAC: {
-                uint64_t v[RPL];
-#pragma unroll
-                for (int k = 0; k < RPL; ++k) {
-                    const uint32_t secs = (uint32_t)read_be(lds, x[k], 4, ps);
-                    const uint32_t frac = (uint32_t)read_be(lds, x[k] + 4, 4, ps);
-                    // (1_000_000_000f64 * (fraction as f64 / u32::MAX as f64)) as u32 (generator.rs:1764)
-                    const double q = (double)frac / 4294967295.0;
-                    const uint32_t ns = (uint32_t)(1000000000.0 * q);
-                    v[k] = (uint64_t)secs | ((uint64_t)ns << 32);
-                    if ((vmask >> k & 1) && ns >= 1000000000u && (secs % 60u) != 59u) {
-                        const uint32_t pos = c.pos0 + (row0 + k - c.rec0) * rl + off;
-                        atomicMin((unsigned long long *)&((ngz_dgram_hdr *)B.hdr)[c.dgram].err_key,
-                                  (unsigned long long)ngz_err_key(pos, E_REC_DTFRAC, f, 0));
-                    }
-                }
-                store_num<RPL>(col, row0, 8, v, vmask);
-                break;
-            }
-            case NGZ_K_STR: {
-#pragma unroll
-                for (int k = 0; k < RPL; ++k) {
-                    if ((vmask >> k & 1) && !utf8_valid_prefix(lds, x[k], len, ps)) {
-                        const uint32_t pos = c.pos0 + (row0 + k - c.rec0) * rl + off;
-                        atomicMin((unsigned long long *)&((ngz_dgram_hdr *)B.hdr)[c.dgram].err_key,
-                                  (unsigned long long)ngz_err_key(pos, E_REC_UTF8, f, 0));
-                    }
-                }
-                store_bytes<RPL>(col, row0, width, len, lds, x, vmask, ps);
-                break;
-            }
-            case NGZ_K_BYTES:
-            case NGZ_K_U256:
-                store_bytes<RPL>(col, row0, width, len, lds, x, vmask, ps);
-                break;
-            case NGZ_K_FAIL: {
-                // template-constant failure: only the chunk's first record matters
-                if ((vmask & 1) && row0 == c.rec0) {
-                    const uint32_t pos = c.pos0 + off;
-                    atomicMin((unsigned long long *)&((ngz_dgram_hdr *)B.hdr)[c.dgram].err_key,
-                              (unsigned long long)ngz_err_key(pos, E_REC_FAIL, f, 0));
-                }
-                break;
-            }
-            default:
-                break;
-            }
-        }
-    }
-    __syncthreads();  // LDS reused by the next chunk
-}
-
-// one wave per workgroup; LDS = [field table of the current slot][staged chunk]
-__global__ void __launch_bounds__(64) k_decode(BatchDev B) {
-    extern __shared__ uint32_t lds_all[];
-    uint4 *ftab = (uint4 *)lds_all;
-    uint32_t *lds = lds_all + 4 * NGZ_MAXF;
-    const uint32_t nchunks = sgpr(B.summary->n_chunks);
+__global__ void __launch_bounds__(256) k_decode_generic(BatchDev B) {
     if (sgpr(B.summary->overflow)) return;
-    uint32_t cached = 0xFFFFFFFFu;
-    PlanS P{};
-    for (uint32_t ci = blockIdx.x; ci < nchunks; ci += gridDim.x) {
-        const uint4 *cp = (const uint4 *)&B.chunks[ci];
-        const uint4 c0 = cp[0], c1 = cp[1];
-        ChunkS c;
-        c.src = (uint64_t)sgpr(c0.x) | ((uint64_t)sgpr(c0.y) << 32);
-        c.rec0 = sgpr(c0.z);
-        c.dgram = sgpr(c0.w);
-        c.n = sgpr(c1.x & 0xFFFF);
-        c.slot = sgpr(c1.x >> 16);
-        c.pos0 = sgpr(c1.y & 0xFFFF);
-        if (c.n == 0) continue;
-        if (c.slot != cached) {
-            const DevPlan *pl = &B.plans[c.slot];
-            const uint4 h0 = ((const uint4 *)pl)[0], h1 = ((const uint4 *)pl)[1];
-            P.rec_len = sgpr(h0.x);
-            P.n_fields = sgpr(h0.z & 0xFFFF);
-            P.rpl = sgpr((h0.z >> 24) & 0xFF);
-            P.ps = sgpr(h0.w & 0xFF);
-            (void)h1;
-            for (uint32_t i = threadIdx.x; i < P.n_fields; i += 64) ftab[i] = ((const uint4 *)pl->f)[i];
-            cached = c.slot;
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t cached = 0xFFFFFFFFu, rl = 0, nf = 0, skip = 0;
+    uint4 fA = make_uint4(0, 0, 0, 0), fB = make_uint4(0, 0, 0, 0);  // field descriptors f = lane, lane + 64
+    auto want = [&](uint32_t slot) {
+        if (slot != cached) {
+            const DevPlan *pl = &B.plans[slot];
+            const uint4 h0 = ((const uint4 *)pl)[0];
+            rl = sgpr(h0.x);
+            nf = sgpr(h0.z & 0xFFFF);
+            skip = sgpr((h0.w >> 24) & 0xFF);  // DevPlan::spec: decoded by its own kernel
+            const uint4 *ft = (const uint4 *)pl->f;
+            fA = lane < nf ? ft[lane] : make_uint4(0, 0, 0, 0);
+            fB = lane + 64 < nf ? ft[lane + 64] : make_uint4(0, 0, 0, 0);
+            cached = slot;
         }
-        if (P.rpl == 4) decode_chunk<4>(B, c, P, ftab, lds);
-        else if (P.rpl == 2) decode_chunk<2>(B, c, P, ftab, lds);
-        else decode_chunk<1>(B, c, P, ftab, lds);
-    }
+        return skip == 0;
+    };
+    auto pass = [&](const Pass &P) {
+        uint32_t R[WIN_DW];
+        uint32_t wb = 0xFFFFFFFFu;  // record offset of the window held in R (uniform)
+        for (uint32_t f = 0; f < nf; ++f) {
+            const uint4 &fs = f < 64 ? fA : fB;
+            const uint32_t fl = f & 63;
+            const uint32_t dx = __builtin_amdgcn_readlane(fs.x, fl), dy = __builtin_amdgcn_readlane(fs.y, fl);
+            const uint32_t col_off = __builtin_amdgcn_readlane(fs.z, fl);
+            const uint32_t off = dx & 0xFFFF, len = dx >> 16, width = dy & 0xFFFF, kind = (dy >> 16) & 0xFF;
+            if (kind == NGZ_K_FAIL) {
+                // template-constant failure: only the chunk's first record matters
+                if (P.valid && P.row == P.rec0) rec_error(P, P.pos0 + off, E_REC_FAIL, f);
+                continue;
+            }
+            if (kind == NGZ_K_VLEN || kind == 0) continue;
+            const bool raw = kind == NGZ_K_STR || kind == NGZ_K_BYTES || kind == NGZ_K_U256;
+            if (kind == NGZ_K_STR && len > 64) check_str(R, P, 0, off, f, len, false);
+            // one window per field, or per 64-byte piece of a raw field
+            for (uint32_t j = 0;; j += 64) {
+                const uint32_t piece = raw ? min(64u, len - j) : 8u;
+                const uint32_t lo = off + j, hi = lo + ((piece + 3) & ~3u);
+                if (wb == 0xFFFFFFFFu || lo < wb || hi > wb + WIN_B) {  // slide the window
+                    wb = lo & ~3u;
+                    win_load<WIN_DW - 1>(R, P, wb);
+                }
+                const uint32_t o = lo - wb;
+                if (!raw) {
+                    dec_num(R, P, o, off, f, len, width, kind, col_off);
+                    break;
+                }
+                if (kind == NGZ_K_STR && len <= 64) check_str(R, P, o, off, f, len, true);
+                const bool last = j + 64 >= len;
+                dec_raw(R, P, o, j, piece, width, col_off, last ? width : 0);
+                if (last) break;
+            }
+        }
+    };
+    run_chunks(B, 0, sgpr(B.summary->n_chunks), want, [&](uint32_t) { return rl; }, pass);
 }
 
-// processed_count increments (ipfix.rs:223 once per set; netflow.rs:218 once
-// per record), honouring where each message's parse stopped.
-__global__ void k_counts(BatchDev B) {
+__device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, 64);
+    return v;
+}
+
+__global__ void __launch_bounds__(256) k_counts(BatchDev B) {
     const uint32_t nsets = B.summary->n_sets;
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (B.summary->overflow || i >= nsets) return;
-    const ngz_set_info s = ((const ngz_set_info *)B.sets)[i];
-    const ngz_dgram_hdr h = ((const ngz_dgram_hdr *)B.hdr)[s.dgram];
-    if (h.status == NGZ_FR_NEED_MORE || h.status == NGZ_FR_UNSUPPORTED) return;
-    const uint32_t stop = h.err_key == NGZ_NO_ERR ? 0x10000u : (uint32_t)(h.err_key >> 48);
-    const DevPlan &pl = B.plans[s.slot];
-    const uint8_t *p = B.bytes + B.offsets[s.dgram];
-    const uint32_t set_len = be16(p + s.set_pos + 2);
-    if (pl.proto == 10) {
-        if (stop >= s.set_pos + set_len) atomicAdd(&B.proc_counts[s.slot], 1ull);
-    } else {
-        // records fully parsed before the stop position
-        const uint32_t first = s.set_pos + 4, rl = pl.rec_len;
-        uint64_t k = 0;
-        if (rl && stop > first) {
-            k = (stop - first) / rl;
-            if (k > s.n) k = s.n;
+    if (B.summary->overflow) return;
+    uint32_t slot = 0;
+    uint64_t inc = 0;
+    if (i < nsets) {
+        const ngz_set_info s = ((const ngz_set_info *)B.sets)[i];
+        const ngz_dgram_hdr h = ((const ngz_dgram_hdr *)B.hdr)[s.dgram];
+        slot = s.slot;
+        if (h.status != NGZ_FR_NEED_MORE && h.status != NGZ_FR_UNSUPPORTED) {
+            const uint32_t stop = h.err_key == NGZ_NO_ERR ? 0x10000u : (uint32_t)(h.err_key >> 48);
+            const DevPlan &pl = B.plans[s.slot];
+            const uint8_t *p = B.bytes + B.offsets[s.dgram];
+            const uint32_t set_len = be16(p + s.set_pos + 2);
+            if (pl.proto == 10) {
+                inc = stop >= s.set_pos + set_len ? 1 : 0;
+            } else {
+                // records fully parsed before the stop position
+                const uint32_t first = s.set_pos + 4, rl = pl.rec_len;
+                if (rl && stop > first) {
+                    inc = (stop - first) / rl;
+                    if (inc > s.n) inc = s.n;
+                }
+            }
         }
-        if (k) atomicAdd(&B.proc_counts[s.slot], (unsigned long long)k);
+    }
+    // one atomic per (wave, slot): consecutive sets mostly share a template
+    uint64_t pending = __ballot(inc != 0);
+    while (pending) {
+        const uint32_t leader = (uint32_t)__ffsll((unsigned long long)pending) - 1;
+        const uint32_t s0 = __builtin_amdgcn_readlane(slot, leader);
+        const bool mine = inc != 0 && slot == s0;
+        const uint64_t sum = wave_sum(mine ? inc : 0);
+        if ((threadIdx.x & 63) == leader) atomicAdd(&B.proc_counts[s0], (unsigned long long)sum);
+        pending &= ~__ballot(mine);
     }
 }
 
@@ -760,13 +490,13 @@ extern "C" int ngz_launch_layout_emit(const BatchDev *B, const uint32_t *hf_flag
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-extern "C" int ngz_launch_decode(const BatchDev *B, uint32_t grid, uint32_t lds_bytes, hipStream_t st) {
-    if (grid) hipLaunchKernelGGL(k_decode, dim3(grid), dim3(64), lds_bytes, st, *B);
+extern "C" int ngz_launch_decode_generic(const BatchDev *B, uint32_t grid, hipStream_t st) {
+    if (grid) hipLaunchKernelGGL(k_decode_generic, dim3(grid), dim3(256), 0, st, *B);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 extern "C" int ngz_launch_counts(const BatchDev *B, uint64_t set_cap, hipStream_t st) {
-    const uint64_t nb = (set_cap + 255) / 256;
+    const uint64_t nb = (set_cap + 255) / 256;  // n_sets is known on device only
     if (nb) hipLaunchKernelGGL(k_counts, dim3((uint32_t)nb), dim3(256), 0, st, *B);
     const uint32_t nd = (B->n + 255) / 256;
     if (nd) hipLaunchKernelGGL(k_finalize, dim3(nd), dim3(256), 0, st, *B);

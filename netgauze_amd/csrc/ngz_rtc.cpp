@@ -1,0 +1,252 @@
+// Per-template decode kernels, generated and compiled at run time (hiprtc).
+//
+// A template's decode plan (DevPlan: record length + per-field offset,
+// length, column width, decode kind) is turned into HIP source in which every
+// field is a constant: the generated kernel walks only that template's chunks
+// and, per 64-record pass, loads exactly the record dwords its fields touch
+// into VGPRs (statically planned 80-byte windows), then extracts, byte-swaps,
+// widens and stores each field with constant register indices and shifts.
+// It is the north star's "one kernel specialised per active template ID";
+// the generic field-table kernel (ngz_kernels.hip) decodes the same plans and
+// is used when specialisation is off or a compile fails.
+//
+// Kernels are cached process-wide by (device, plan signature): every template
+// with the same layout -- the same template re-announced by an exporter, or
+// the same layout on another exporter peer -- shares one code object.
+#include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "ngz/flow_decode.h"
+#include "ngz_internal.h"
+
+namespace {
+
+// texts of flow_decode.h, ngz_internal.h and ngz_dev.h (tools/embed_sources.py)
+#include "ngz_rtc_sources.inc"
+
+constexpr uint32_t kWinDw = 19;  // usable dwords of a register window (ngz_dev.h WIN_DW - 1)
+
+struct Item {           // one extraction step of the generated pass body
+    int type;           // 0 numeric, 1 raw piece, 2 string check (window), 3 string check (global), 4 fail
+    uint32_t f, off, len, width, kind, col_off;
+    uint32_t j, piece, pad_to;  // raw pieces
+    uint32_t d0, d1;    // record dwords touched (inclusive), types 0-2
+};
+
+std::string signature(const DevPlan &P) {
+    std::string s = "rl" + std::to_string(P.rec_len);
+    char b[96];
+    for (uint32_t f = 0; f < P.n_fields; ++f) {
+        const DevField &d = P.f[f];
+        snprintf(b, sizeof b, ";%u,%u,%u,%u,%u", d.off, d.len, d.width, d.kind, d.col_off);
+        s += b;
+    }
+    return s;
+}
+
+std::string generate(const DevPlan &P) {
+    std::vector<Item> items;
+    for (uint32_t f = 0; f < P.n_fields; ++f) {
+        const DevField &d = P.f[f];
+        Item it{};
+        it.f = f;
+        it.off = d.off;
+        it.len = d.len;
+        it.width = d.width;
+        it.kind = d.kind;
+        it.col_off = d.col_off;
+        switch (d.kind) {
+        case NGZ_K_FAIL:
+            it.type = 4;
+            items.push_back(it);
+            break;
+        case NGZ_K_UINT: case NGZ_K_SCOPE32: case NGZ_K_TCPFLAGS: case NGZ_K_SINT:
+        case NGZ_K_BOOL: case NGZ_K_DTMS: case NGZ_K_DTFRAC: {
+            uint32_t L = d.len;
+            if (d.kind == NGZ_K_DTMS || d.kind == NGZ_K_DTFRAC) L = 8;
+            if (d.kind == NGZ_K_BOOL) L = 1;
+            if (L == 0) L = 1;
+            it.type = 0;
+            it.d0 = d.off >> 2;
+            it.d1 = (d.off + L - 1) >> 2;
+            items.push_back(it);
+            break;
+        }
+        case NGZ_K_STR: case NGZ_K_BYTES: case NGZ_K_U256: {
+            if (d.kind == NGZ_K_STR) {
+                Item c = it;
+                c.type = d.len <= 64 ? 2 : 3;
+                c.d0 = d.off >> 2;
+                c.d1 = d.len ? (d.off + d.len - 1) >> 2 : c.d0;
+                items.push_back(c);
+            }
+            for (uint32_t j = 0;; j += 64) {
+                Item r = it;
+                r.type = 1;
+                r.j = j;
+                r.piece = std::min<uint32_t>(64, d.len - j);
+                const bool last = j + 64 >= d.len;
+                r.pad_to = last ? d.width : 0;
+                r.d0 = (d.off + j) >> 2;
+                r.d1 = r.piece ? (d.off + j + r.piece - 1) >> 2 : r.d0;
+                items.push_back(r);
+                if (last) break;
+            }
+            break;
+        }
+        default:
+            break;  // vlen: not device-decodable (plan.rpl == 0 never reaches here)
+        }
+    }
+    // windows: greedy in record order; a window spans <= kWinDw dwords
+    std::vector<std::pair<uint32_t, uint32_t>> wins;  // (first dword, dword count)
+    std::vector<int> item_win(items.size(), -1);
+    for (size_t i = 0; i < items.size(); ++i) {
+        const Item &it = items[i];
+        if (it.type == 3 || it.type == 4) continue;
+        if (wins.empty() || it.d0 < wins.back().first || it.d1 >= wins.back().first + kWinDw) wins.push_back({it.d0, 1});
+        auto &w = wins.back();
+        w.second = std::max(w.second, it.d1 - w.first + 1);
+        item_win[i] = (int)wins.size() - 1;
+    }
+    std::string body;
+    char b[512];
+    int cur = -1;
+    for (size_t i = 0; i < items.size(); ++i) {
+        const Item &it = items[i];
+        if (item_win[i] >= 0 && item_win[i] != cur) {
+            cur = item_win[i];
+            snprintf(b, sizeof b, "        win_load<%u>(R, P, %uu);\n", wins[cur].second, 4 * wins[cur].first);
+            body += b;
+        }
+        const uint32_t wb = cur >= 0 ? 4 * wins[cur].first : 0;
+        switch (it.type) {
+        case 0:
+            snprintf(b, sizeof b, "        dec_num(R, P, %uu, %uu, %uu, %uu, %uu, %uu, %uu);\n", it.off - wb, it.off, it.f,
+                     it.len, it.width, it.kind, it.col_off);
+            break;
+        case 1:
+            snprintf(b, sizeof b, "        dec_raw(R, P, %uu, %uu, %uu, %uu, %uu, %uu);\n", it.off + it.j - wb, it.j,
+                     it.piece, it.width, it.col_off, it.pad_to);
+            break;
+        case 2:
+            snprintf(b, sizeof b, "        check_str(R, P, %uu, %uu, %uu, %uu, true);\n", it.off - wb, it.off, it.f, it.len);
+            break;
+        case 3:
+            snprintf(b, sizeof b, "        check_str(R, P, 0u, %uu, %uu, %uu, false);\n", it.off, it.f, it.len);
+            break;
+        case 4:
+            snprintf(b, sizeof b, "        if (P.valid && P.row == P.rec0) rec_error(P, P.pos0 + %uu, E_REC_FAIL, %uu);\n",
+                     it.off, it.f);
+            break;
+        }
+        body += b;
+    }
+    std::string src;
+    src += "// generated by ngz_rtc.cpp for plan " + signature(P) + "\n";
+    src += "#include \"ngz_dev.h\"\nusing namespace ngzdev;\n";
+    src += "extern \"C\" __global__ void __launch_bounds__(256) ngz_tpl(BatchDev B, uint32_t slot) {\n";
+    src += "    if (sgpr(B.summary->overflow)) return;\n";
+    src += "    const SlotRT *rtp = &B.slots[slot];\n";
+    src += "    const uint32_t c0 = sgpr(rtp->chunk0), nc = sgpr(rtp->nchunks);\n";
+    src += "    run_chunks(B, c0, c0 + nc, [](uint32_t) { return true; }, [](uint32_t) { return " +
+           std::to_string(P.rec_len) + "u; },\n";
+    src += "               [&](const Pass &P) {\n        uint32_t R[WIN_DW];\n";
+    src += body;
+    src += "    });\n}\n";
+    return src;
+}
+
+struct Entry {
+    hipModule_t mod = nullptr;
+    hipFunction_t fn = nullptr;
+    bool failed = false;
+};
+
+std::mutex g_mu;
+std::map<std::pair<int, std::string>, Entry> g_cache;
+
+bool compile(const std::string &src, std::vector<char> &code, std::string &log) {
+    hiprtcProgram prog;
+    // hiprtc supplies stdint.h but not stddef.h (flow_decode.h only needs size_t)
+    static const char kStddef[] = "#pragma once\ntypedef __SIZE_TYPE__ size_t;\n";
+    const char *hdrs[] = {kSrcFlowDecode, kSrcInternal, kSrcDev, kStddef};
+    const char *names[] = {"ngz/flow_decode.h", "ngz_internal.h", "ngz_dev.h", "stddef.h"};
+    if (hiprtcCreateProgram(&prog, src.c_str(), "ngz_tpl.hip", 4, hdrs, names) != HIPRTC_SUCCESS) return false;
+    const char *opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off"};
+    const hiprtcResult rc = hiprtcCompileProgram(prog, 4, opts);
+    size_t ls = 0;
+    hiprtcGetProgramLogSize(prog, &ls);
+    if (ls > 1) {
+        log.resize(ls);
+        hiprtcGetProgramLog(prog, &log[0]);
+    }
+    bool ok = rc == HIPRTC_SUCCESS;
+    if (ok) {
+        size_t cs = 0;
+        ok = hiprtcGetCodeSize(prog, &cs) == HIPRTC_SUCCESS && cs > 0;
+        if (ok) {
+            code.resize(cs);
+            ok = hiprtcGetCode(prog, code.data()) == HIPRTC_SUCCESS;
+        }
+    }
+    hiprtcDestroyProgram(&prog);
+    return ok;
+}
+
+}  // namespace
+
+// Specialised kernel for a plan on `device` (compiled on first use, cached);
+// nullptr when compilation failed (the caller falls back to the generic kernel).
+void *ngz_rtc_kernel(int device, const DevPlan &P) {
+    const std::string sig = signature(P);
+    std::lock_guard<std::mutex> lk(g_mu);
+    Entry &e = g_cache[{device, sig}];
+    if (e.fn || e.failed) return (void *)e.fn;
+    const std::string src = generate(P);
+    std::vector<char> code;
+    std::string log;
+    if (getenv("NGZ_RTC_DUMP")) fprintf(stderr, "[ngz rtc] source:\n%s\n", src.c_str());
+    if (!compile(src, code, log)) {
+        fprintf(stderr, "[ngz rtc] compile failed for %s:\n%s\n", sig.c_str(), log.c_str());
+        e.failed = true;
+        return nullptr;
+    }
+    if (hipModuleLoadData(&e.mod, code.data()) != hipSuccess ||
+        hipModuleGetFunction(&e.fn, e.mod, "ngz_tpl") != hipSuccess) {
+        fprintf(stderr, "[ngz rtc] module load failed for %s\n", sig.c_str());
+        e.failed = true;
+        e.fn = nullptr;
+        return nullptr;
+    }
+    return (void *)e.fn;
+}
+
+// The generated source for a plan (introspection / tests).
+std::string ngz_rtc_source(const DevPlan &P) { return generate(P); }
+
+// Launch a specialised kernel over one slot's chunks.
+int ngz_rtc_launch(void *fn, const BatchDev *B, uint32_t slot, uint32_t grid, hipStream_t st) {
+    BatchDev b = *B;
+    uint32_t s = slot;
+    void *args[] = {&b, &s};
+    return hipModuleLaunchKernel((hipFunction_t)fn, grid, 1, 1, 256, 1, 1, 0, st, args, nullptr) == hipSuccess ? 0 : -1;
+}
+
+// Generate and compile without loading (no device needed): 0 ok, -1 failed.
+int ngz_rtc_compile_only(const DevPlan &P, std::string *log_out) {
+    std::vector<char> code;
+    std::string log;
+    const bool ok = compile(generate(P), code, log);
+    if (log_out) *log_out = log;
+    return ok ? 0 : -1;
+}

@@ -16,8 +16,8 @@ print("== rocprofv3 --kernel-trace --stats (pipeline kernels)")
 print("%-40s %8s %14s %14s" % ("kernel", "calls", "avg_ns", "total_ns"))
 for r in rows:
     name = r["Name"]
-    short = name.split("(")[0].replace("(anonymous namespace)::", "")
-    if any(k in name for k in ("k_decode", "k_frame", "k_emit", "k_layout", "k_counts", "k_finalize", "rocprim", "fillBuffer")):
+    short = name.replace("(anonymous namespace)::", "").split("(")[0]
+    if any(k in name for k in ("k_decode", "ngz_tpl", "k_frame", "k_emit", "k_layout", "k_counts", "k_finalize", "rocprim", "fillBuffer")):
         print("%-40s %8s %14.0f %14s" % (short[:40], r["Calls"], float(r["AverageNs"]), r["TotalDurationNs"]))
 out = {}
 for c in ("FETCH_SIZE", "WRITE_SIZE"):
