@@ -53,6 +53,22 @@ def cpu_baseline(seconds_budget=12.0, sample_records=4_000_000):
                       % (reps, sample_records, int(offs.numel()), threads, dt)}
 
 
+def committed_traffic(records):
+    """Per-launch HBM bytes of the decode kernel from the newest committed
+    rocprofv3 PMC profile of this same workload (profiles/*/traffic.json,
+    written by tools/summarize_profile.py), or None."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "traffic.json"))):
+        try:
+            t = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if t.get("records") == records:
+            best = (t["traffic_bytes"], os.path.relpath(f, ROOT))
+    return best
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -60,7 +76,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--records", type=int, default=100_000_000, help="T20 records per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--e2e", action="store_true",
+                    help="host-to-host rate instead: pinned host datagrams -> H2D -> decode -> D2H of all columns")
     args = ap.parse_args()
+    if args.e2e:
+        return main_e2e(args)
 
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -118,6 +138,7 @@ def main():
     dec_avg = sum(dec_ms) / len(dec_ms)
     alg_bytes = n * (BYTES_PER_RECORD_IN + BYTES_PER_RECORD_OUT)
     achieved = alg_bytes / (dec_avg * 1e-3) / 1e9
+    traffic = committed_traffic(n)
     out = {
         "metric": "IPFIX flow records/sec + GB/s (device-resident), 20-field fixed template",
         "value": value,
@@ -136,9 +157,11 @@ def main():
                    "parallelism": "shard-per-gpu" if world > 1 else "single"},
         "gbps_step": total_records * (BYTES_PER_RECORD_IN + BYTES_PER_RECORD_OUT) / elapsed / 1e9,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "k_decode", "kernel_ms": dec_avg,
-                     "alg_bytes_per_launch": alg_bytes},
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic[0] if traffic else None,
+                     "traffic_src": traffic[1] if traffic else None,
+                     "kernel": "ngz_tpl (per-template decode kernel, T20)", "kernel_ms": dec_avg,
+                     "alg_bytes_per_launch": alg_bytes,
+                     "read_gbps": n * BYTES_PER_RECORD_IN / (dec_avg * 1e-3) / 1e9},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline()
@@ -146,6 +169,59 @@ def main():
         print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def main_e2e(args):
+    """Host-resident path (north star: UDP/PCAP -> decoded record arrays in host
+    memory): the batch sits in pinned host memory, ngz_decode_batch_host copies
+    it H2D, decodes, and every column block is copied back D2H.  Reported in
+    DESIGN.md; never the headline value."""
+    import torch
+    from netgauze_amd import synth
+    from netgauze_amd.flow import FlowInfoCodec
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    codec = FlowInfoCodec(0)
+    codec.decode_datagrams([synth.template_message()])
+    n = args.records
+    rec = synth.t20_records(n, seed=synth.SEED_CFG2, device=dev, first=0)
+    buf, offs, lens = synth.ipfix_data_stream(rec, 64)
+    del rec
+    hb = torch.empty(buf.numel(), dtype=torch.uint8, pin_memory=True)
+    hb.copy_(buf)
+    ho = torch.empty(offs.numel(), dtype=torch.int64, pin_memory=True)
+    ho.copy_(offs)
+    hl = torch.empty(lens.numel(), dtype=torch.int32, pin_memory=True)
+    hl.copy_(lens)
+    del buf, offs, lens
+    torch.cuda.synchronize()
+    out = torch.empty(n * BYTES_PER_RECORD_OUT + (1 << 20), dtype=torch.uint8, pin_memory=True)
+
+    def step():
+        b = codec.decode_host_buffers(hb.data_ptr(), hb.numel(), ho.data_ptr(), hl.data_ptr(), ho.numel())
+        moved = 0
+        for sl in b.slots:
+            if sl.n_records:
+                moved += sl.copy_block_to_host(out.data_ptr() + moved)
+        return b, moved
+
+    for _ in range(args.warmup):
+        b, moved = step()
+    assert b.n_records == n
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    print(json.dumps({
+        "metric": "IPFIX flow records/sec host-to-host (pinned H2D + decode + D2H of all columns), T20",
+        "value": n * args.steps / el, "unit": "records/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": el / args.steps * 1e3, "higher_is_better": True,
+        "dtype": "u8", "data": "synthetic T20, pinned host memory",
+        "config": {"workload": "T20 x %d records, 1023 per message" % n, "h2d_bytes": int(hb.numel()),
+                   "d2h_bytes": int(moved)},
+        "pcie_gbps": (hb.numel() + moved) * args.steps / el / 1e9}), flush=True)
 
 
 if __name__ == "__main__":

@@ -143,6 +143,13 @@ int ngz_ctx_create(int device, ngz_ctx **out);
 void ngz_ctx_destroy(ngz_ctx *ctx);
 const char *ngz_last_error(ngz_ctx *ctx);
 
+/* Context options (ngz_ctx_set_option). */
+#define NGZ_OPT_SPECIALIZE 1    /* 1 (default): decode each template with its own kernel, generated and
+                                   compiled at run time (hiprtc) and cached by layout; 0: the generic
+                                   field-table kernel for every template */
+#define NGZ_OPT_BLOCKS_PER_CU 2 /* decode grid size: 256-thread blocks per CU (default 4) */
+int ngz_ctx_set_option(ngz_ctx *ctx, int opt, int64_t value);
+
 /* --- decode ------------------------------------------------------------- */
 /* Decode every datagram of `in` in order against the context's template
  * state.  Synchronous: on return the device arrays in *out are complete and

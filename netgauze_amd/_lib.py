@@ -19,7 +19,7 @@ NGZ_DG_OK, NGZ_DG_NEED_MORE, NGZ_DG_ERROR, NGZ_DG_UNSUPPORTED = 0, 1, 2, 3
 ABI_FUNCTIONS = [
     "ngz_ctx_create", "ngz_ctx_destroy", "ngz_last_error", "ngz_decode_batch",
     "ngz_decode_batch_host", "ngz_slot_fields", "ngz_dgram_error_json",
-    "ngz_templates_json", "ngz_template_counts", "ngz_last_timing",
+    "ngz_templates_json", "ngz_template_counts", "ngz_last_timing", "ngz_ctx_set_option",
 ]
 
 
@@ -80,6 +80,8 @@ def load():
     lib.ngz_template_counts.restype = I
     lib.ngz_last_timing.argtypes = [P, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
     lib.ngz_last_timing.restype = I
+    lib.ngz_ctx_set_option.argtypes = [P, I, ctypes.c_int64]
+    lib.ngz_ctx_set_option.restype = I
     return lib
 
 

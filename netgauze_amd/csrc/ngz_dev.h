@@ -76,7 +76,8 @@ struct Pass {
     bool any_sh;                  // some lane misaligned (uniform)
     bool valid;                   // this lane's row belongs to the chunk
     uint32_t row;                 // this lane's output row
-    uint32_t prow;                // first row of the pass (uniform; row = prow + lane)
+    uint32_t prow;                // first row of the pass (uniform; row = prow + lrow)
+    uint32_t lrow;                // this lane's row within the pass
     uint32_t lane;
     uint32_t rec0;                // first row of the chunk
     uint32_t dgram;               // datagram of the chunk
@@ -127,10 +128,10 @@ __device__ __forceinline__ void store_w(uint8_t *pcol, uint32_t lane, uint32_t w
     else *(uint2 *)(pcol + 8 * lane) = make_uint2((uint32_t)v, (uint32_t)(v >> 32));
 }
 
-// Numeric field (UINT/SCOPE32/TCPFLAGS/SINT/BOOL/DTMS/DTFRAC) at window offset o.
-__device__ __forceinline__ void dec_num(const uint32_t (&R)[WIN_DW], const Pass &P, uint32_t o, uint32_t off,
-                                        uint32_t f, uint32_t len, uint32_t width, uint32_t kind, uint32_t col_off) {
-    uint8_t *pcol = pass_col(P, col_off, width);
+// Value of a numeric field (UINT/SCOPE32/TCPFLAGS/SINT/BOOL/DTMS/DTFRAC) at
+// window offset o, in its column encoding; reports the field's errors.
+__device__ __forceinline__ uint64_t num_value(const uint32_t (&R)[WIN_DW], const Pass &P, uint32_t o, uint32_t off,
+                                              uint32_t f, uint32_t len, uint32_t kind) {
     uint64_t v;
     if (kind == NGZ_K_BOOL) {
         v = rbyte(R, o) != 0;
@@ -153,7 +154,62 @@ __device__ __forceinline__ void dec_num(const uint32_t (&R)[WIN_DW], const Pass 
         if (P.valid && kind == NGZ_K_DTMS && ((int64_t)v < kMinMillis || (int64_t)v > kMaxMillis))
             rec_error(P, P.recpos + off, E_REC_DTMS, f);
     }
-    if (P.valid) store_w(pcol, P.lane, width, v);
+    return v;
+}
+
+// Numeric field of one record per lane: one store of `width` bytes per lane.
+__device__ __forceinline__ void dec_num(const uint32_t (&R)[WIN_DW], const Pass &P, uint32_t o, uint32_t off,
+                                        uint32_t f, uint32_t len, uint32_t width, uint32_t kind, uint32_t col_off) {
+    const uint64_t v = num_value(R, P, o, off, f, len, kind);
+    if (P.valid) store_w(pass_col(P, col_off, width), P.lrow, width, v);
+}
+
+// Numeric field of C consecutive rows per lane (run_chunks<C, true>): the C
+// values are packed into one C*width-byte store per lane when all C rows
+// belong to the chunk (a wave writes 64*C*width contiguous bytes).
+template <int C>
+__device__ __forceinline__ void dec_num_c(const uint32_t (&R)[C][WIN_DW], const Pass (&P)[C], uint32_t o, uint32_t off,
+                                          uint32_t f, uint32_t len, uint32_t width, uint32_t kind, uint32_t col_off) {
+    uint64_t v[C];
+    bool full = true;
+#pragma unroll
+    for (int k = 0; k < C; ++k) {
+        v[k] = num_value(R[k], P[k], o, off, f, len, kind);
+        full = full && P[k].valid;
+    }
+    uint8_t *pcol = pass_col(P[0], col_off, width);
+    if (full) {
+        uint8_t *dst = pcol + (uint64_t)P[0].lrow * width;  // lrow of record 0 = C*lane
+        if (width == 1) {
+            uint32_t w = 0;
+#pragma unroll
+            for (int k = 0; k < C; ++k) w |= (uint32_t)(v[k] & 0xFF) << (8 * k);
+            if (C == 4) *(uint32_t *)dst = w;
+            else if (C == 2) *(uint16_t *)dst = (uint16_t)w;
+            else *dst = (uint8_t)w;
+        } else if (width == 2) {
+            uint32_t w[2] = {0, 0};
+#pragma unroll
+            for (int k = 0; k < C; ++k) w[k >> 1] |= (uint32_t)(v[k] & 0xFFFF) << (16 * (k & 1));
+            if (C == 4) *(uint2 *)dst = make_uint2(w[0], w[1]);
+            else if (C == 2) *(uint32_t *)dst = w[0];
+            else *(uint16_t *)dst = (uint16_t)w[0];
+        } else if (width == 4) {
+            if (C == 4) *(uint4 *)dst = make_uint4((uint32_t)v[0], (uint32_t)v[1 % C], (uint32_t)v[2 % C], (uint32_t)v[3 % C]);
+            else if (C == 2) *(uint2 *)dst = make_uint2((uint32_t)v[0], (uint32_t)v[1 % C]);
+            else *(uint32_t *)dst = (uint32_t)v[0];
+        } else {
+#pragma unroll
+            for (int k = 0; k + 1 < C; k += 2)
+                *(uint4 *)(dst + 8 * k) = make_uint4((uint32_t)v[k], (uint32_t)(v[k] >> 32), (uint32_t)v[k + 1],
+                                                     (uint32_t)(v[k + 1] >> 32));
+            if (C == 1) *(uint2 *)dst = make_uint2((uint32_t)v[0], (uint32_t)(v[0] >> 32));
+        }
+        return;
+    }
+#pragma unroll
+    for (int k = 0; k < C; ++k)
+        if (P[k].valid) store_w(pcol, P[k].lrow, width, v[k]);
 }
 
 struct WindowBytes {
@@ -207,7 +263,7 @@ __device__ __forceinline__ void check_str(const uint32_t (&R)[WIN_DW], const Pas
 __device__ __forceinline__ void dec_raw(const uint32_t (&R)[WIN_DW], const Pass &P, uint32_t o, uint32_t j,
                                         uint32_t piece, uint32_t width, uint32_t col_off, uint32_t pad_to) {
     if (!P.valid) return;
-    uint8_t *dst = pass_col(P, col_off, width) + P.lane * width + j;
+    uint8_t *dst = pass_col(P, col_off, width) + P.lrow * width + j;
     const bool dw = (width & 3) == 0 && (j & 3) == 0;
     uint32_t t = 0;
     if (dw && (width & 15) == 0 && (j & 15) == 0) {
@@ -221,12 +277,16 @@ __device__ __forceinline__ void dec_raw(const uint32_t (&R)[WIN_DW], const Pass 
 }
 
 // Walk chunks [c_begin, c_end) of the batch's chunk array, one wave per chunk
-// (wave-strided), 64 rows per pass.  want(slot) decides (and may load per-slot
-// state) whether a chunk's slot is handled here; rec_len(slot) gives its
-// record length; pass(P) decodes the 64 rows of one pass.
-template <class Want, class RecLen, class PassFn>
+// (wave-strided).  A chunk's window of NGZ_REG_WINDOW rows is covered in
+// groups of 64*RPL rows, RPL records per lane (all their loads in flight at
+// once): with CONSEC lane l owns the RPL consecutive rows prow + RPL*l + k
+// (so narrow columns pack into wide stores), otherwise rows prow + 64*k + l.  want(slot) decides (and
+// may load per-slot state) whether a chunk's slot is handled here;
+// rec_len(slot) gives its record length; pass(P) decodes one group.
+template <int RPL, bool CONSEC, class Want, class RecLen, class PassFn>
 __device__ __forceinline__ void run_chunks(const BatchDev &B, uint32_t c_begin, uint32_t c_end, Want &&want,
                                            RecLen &&rec_len, PassFn &&pass) {
+    static_assert(RPL == 1 || RPL == 2 || RPL == 4, "RPL");
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wpb = blockDim.x >> 6;
     const uint32_t wid = sgpr(blockIdx.x * wpb + (threadIdx.x >> 6));
@@ -240,32 +300,40 @@ __device__ __forceinline__ void run_chunks(const BatchDev &B, uint32_t c_begin, 
         if (!want(slot)) continue;
         const uint32_t rl = rec_len(slot);
         const uint64_t src = (uint64_t)sgpr(c0.x) | ((uint64_t)sgpr(c0.y) << 32);
-        Pass P;
-        P.rec0 = sgpr(c0.z);
-        P.dgram = sgpr(c0.w);
-        P.pos0 = sgpr(c1.y & 0xFFFF);
-        P.hdr = B.hdr;
+        Pass P[RPL];
+        P[0].rec0 = sgpr(c0.z);
+        P[0].dgram = sgpr(c0.w);
+        P[0].pos0 = sgpr(c1.y & 0xFFFF);
+        P[0].hdr = B.hdr;
         const SlotRT rt = B.slots[slot];
-        P.blk = B.arena + sgpr((uint32_t)rt.block) + ((uint64_t)sgpr((uint32_t)(rt.block >> 32)) << 32);
-        P.cap = sgpr(rt.cap);
+        P[0].blk = B.arena + sgpr((uint32_t)rt.block) + ((uint64_t)sgpr((uint32_t)(rt.block >> 32)) << 32);
+        P[0].cap = sgpr(rt.cap);
         const uint64_t a0 = src & ~3ull;
         const uint64_t avail64 = B.bytes_size - a0;
         const uint32_t avail = avail64 > 0x7FFFFFF0ull ? 0x7FFFFFF0u : (uint32_t)avail64;
-        P.rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)(B.bytes + a0), (short)0, (int)avail, 0x00020000);
-        const uint32_t wbase = P.rec0 & ~(uint32_t)(NGZ_REG_WINDOW - 1);
-        for (uint32_t p = 0; p < NGZ_REG_WINDOW; p += 64) {
+        P[0].rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)(B.bytes + a0), (short)0, (int)avail, 0x00020000);
+        P[0].lane = lane;
+#pragma unroll
+        for (int k = 1; k < RPL; ++k) P[k] = P[0];
+        const uint32_t rec0 = P[0].rec0;
+        const uint32_t wbase = rec0 & ~(uint32_t)(NGZ_REG_WINDOW - 1);
+        for (uint32_t p = 0; p < NGZ_REG_WINDOW; p += 64 * RPL) {
             const uint32_t pr0 = wbase + p;
-            if (pr0 + 64 <= P.rec0 || pr0 >= P.rec0 + n) continue;  // no row of this pass in the chunk
-            P.prow = pr0;
-            P.lane = lane;
-            P.row = pr0 + lane;
-            P.valid = P.row >= P.rec0 && P.row < P.rec0 + n;
-            const uint32_t k = P.valid ? P.row - P.rec0 : 0;
-            const uint32_t rel = k * rl + (uint32_t)(src & 3);
-            P.rbase = rel & ~3u;
-            P.sh = rel & 3u;
-            P.any_sh = __builtin_amdgcn_ballot_w64(P.sh != 0) != 0;
-            P.recpos = P.pos0 + k * rl;
+            if (pr0 + 64 * RPL <= rec0 || pr0 >= rec0 + n) continue;  // no row of this group in the chunk
+#pragma unroll
+            for (int k = 0; k < RPL; ++k) {
+                Pass &Q = P[k];
+                Q.prow = CONSEC ? pr0 : pr0 + 64 * k;
+                Q.lrow = CONSEC ? RPL * lane + k : lane;
+                Q.row = Q.prow + Q.lrow;
+                Q.valid = Q.row >= rec0 && Q.row < rec0 + n;
+                const uint32_t r = Q.valid ? Q.row - rec0 : 0;
+                const uint32_t rel = r * rl + (uint32_t)(src & 3);
+                Q.rbase = rel & ~3u;
+                Q.sh = rel & 3u;
+                Q.any_sh = __builtin_amdgcn_ballot_w64(Q.sh != 0) != 0;
+                Q.recpos = Q.pos0 + r * rl;
+            }
             pass(P);
         }
     }

@@ -359,6 +359,7 @@ struct ngz_ctx {
     hipEvent_t ev[4]{};
     int n_cus = 256;
     int specialize = 1;                         // NGZ_OPT_SPECIALIZE
+    uint32_t blocks_per_cu = 4;                 // decode grid: 4 x 256 threads per CU
     BatchSummary *h_summary = nullptr;          // pinned
     SlotRT *h_slots = nullptr;                  // pinned, NGZ_MAX_SLOTS
     float t_decode = 0, t_pipeline = 0;
@@ -895,7 +896,6 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
     if (ngz_launch_scan(ctx->d_scan_tmp.p, scan_tmp, ctx->d_counts.p, ctx->d_scan.p, n_items, st))
         return fail(ctx, NGZ_E_DEVICE, "scan launch");
     if (ngz_launch_layout_emit(&B, hf_flag, hf_first, st)) return fail(ctx, NGZ_E_DEVICE, "layout/emit launch");
-    HIPCHK(hipEventRecord(ctx->ev[1], st));
     // per-slot chunk ranges and capacities decide which decode kernels run
     HIPCHK(hipMemcpyAsync(ctx->h_summary, ctx->d_summary.p, sizeof(BatchSummary), hipMemcpyDeviceToHost, st));
     if (S) HIPCHK(hipMemcpyAsync(ctx->h_slots, ctx->d_slots.p, S * sizeof(SlotRT), hipMemcpyDeviceToHost, st));
@@ -907,8 +907,9 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
         if (ctx->summary.overflow & 4) ctx->d_sets.ensure(ctx->summary.n_sets + 1024);
         return 1;  // retry
     }
-    const uint32_t grid = (uint32_t)ctx->n_cus * 8;  // 256-thread blocks: up to 32 waves per CU
+    const uint32_t grid = (uint32_t)ctx->n_cus * ctx->blocks_per_cu;  // 256-thread blocks
     bool generic = false;
+    HIPCHK(hipEventRecord(ctx->ev[1], st));
     for (uint32_t s = 0; s < S; ++s) {
         if (!ctx->h_slots[s].nchunks) continue;
         const Version &v = ctx->versions[ctx->slot_version[s]];
@@ -994,6 +995,7 @@ int ngz_ctx_create(int device, ngz_ctx **out) {
         return NGZ_E_NOMEM;
     }
     if (const char *e = getenv("NGZ_SPECIALIZE")) ctx->specialize = atoi(e);
+    if (const char *e = getenv("NGZ_BLOCKS_PER_CU")) ctx->blocks_per_cu = std::max(1, std::min(32, atoi(e)));
     *out = ctx;
     return NGZ_OK;
 }
@@ -1016,6 +1018,22 @@ void ngz_ctx_destroy(ngz_ctx *ctx) {
 }
 
 const char *ngz_last_error(ngz_ctx *ctx) { return ctx ? ctx->last_error.c_str() : "null context"; }
+
+int ngz_ctx_set_option(ngz_ctx *ctx, int opt, int64_t value) {
+    if (!ctx) return NGZ_E_INVALID;
+    switch (opt) {
+    case NGZ_OPT_SPECIALIZE:
+        if (value != 0 && value != 1) return fail(ctx, NGZ_E_INVALID, "NGZ_OPT_SPECIALIZE takes 0 or 1");
+        if (ctx->specialize != (int)value) ctx->plans_dirty = true;  // device plans carry the spec flag
+        ctx->specialize = (int)value;
+        return NGZ_OK;
+    case NGZ_OPT_BLOCKS_PER_CU:
+        if (value < 1 || value > 32) return fail(ctx, NGZ_E_INVALID, "NGZ_OPT_BLOCKS_PER_CU takes 1..32");
+        ctx->blocks_per_cu = (uint32_t)value;
+        return NGZ_OK;
+    }
+    return fail(ctx, NGZ_E_INVALID, "unknown option");
+}
 
 int ngz_decode_batch(ngz_ctx *ctx, const ngz_batch_in *in, ngz_batch_out *out, void *hip_stream) {
     if (!ctx || !in || !out) return NGZ_E_INVALID;

@@ -363,7 +363,8 @@ __global__ void __launch_bounds__(256) k_decode_generic(BatchDev B) {
         }
         return skip == 0;
     };
-    auto pass = [&](const Pass &P) {
+    auto pass = [&](const Pass (&PP)[1]) {
+        const Pass &P = PP[0];
         uint32_t R[WIN_DW];
         uint32_t wb = 0xFFFFFFFFu;  // record offset of the window held in R (uniform)
         for (uint32_t f = 0; f < nf; ++f) {
@@ -400,7 +401,7 @@ __global__ void __launch_bounds__(256) k_decode_generic(BatchDev B) {
             }
         }
     };
-    run_chunks(B, 0, sgpr(B.summary->n_chunks), want, [&](uint32_t) { return rl; }, pass);
+    run_chunks<1, false>(B, 0, sgpr(B.summary->n_chunks), want, [&](uint32_t) { return rl; }, pass);
 }
 
 __device__ __forceinline__ uint64_t wave_sum(uint64_t v) {

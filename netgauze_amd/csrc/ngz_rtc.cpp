@@ -118,39 +118,78 @@ std::string generate(const DevPlan &P) {
         w.second = std::max(w.second, it.d1 - w.first + 1);
         item_win[i] = (int)wins.size() - 1;
     }
+    // Rows per lane and their layout (NGZ_RTC_LAYOUT overrides for experiments):
+    // "c4"/"c2" = 4/2 consecutive rows per lane, numeric columns packed into
+    // one wide store per lane; "r1"/"r2"/"r4" = 1/2/4 rows per lane, 64 apart.
+    int rpl = 4;
+    bool consec = true;
+    if (const char *e = getenv("NGZ_RTC_LAYOUT")) {
+        if (e[0] == 'c' || e[0] == 'r') {
+            consec = e[0] == 'c';
+            rpl = atoi(e + 1);
+        }
+        if (rpl != 1 && rpl != 2 && rpl != 4) rpl = 4;
+    }
     std::string body;
     char b[512];
-    int cur = -1;
-    for (size_t i = 0; i < items.size(); ++i) {
-        const Item &it = items[i];
-        if (item_win[i] >= 0 && item_win[i] != cur) {
-            cur = item_win[i];
-            snprintf(b, sizeof b, "        win_load<%u>(R, P, %uu);\n", wins[cur].second, 4 * wins[cur].first);
-            body += b;
-        }
-        const uint32_t wb = cur >= 0 ? 4 * wins[cur].first : 0;
+    auto emit_item = [&](const Item &it, uint32_t wb, int k) {
+        const std::string R = "R[" + std::to_string(k) + "]", P = "P[" + std::to_string(k) + "]";
         switch (it.type) {
         case 0:
-            snprintf(b, sizeof b, "        dec_num(R, P, %uu, %uu, %uu, %uu, %uu, %uu, %uu);\n", it.off - wb, it.off, it.f,
-                     it.len, it.width, it.kind, it.col_off);
+            snprintf(b, sizeof b, "        dec_num(%s, %s, %uu, %uu, %uu, %uu, %uu, %uu, %uu);\n", R.c_str(), P.c_str(),
+                     it.off - wb, it.off, it.f, it.len, it.width, it.kind, it.col_off);
             break;
         case 1:
-            snprintf(b, sizeof b, "        dec_raw(R, P, %uu, %uu, %uu, %uu, %uu, %uu);\n", it.off + it.j - wb, it.j,
-                     it.piece, it.width, it.col_off, it.pad_to);
+            snprintf(b, sizeof b, "        dec_raw(%s, %s, %uu, %uu, %uu, %uu, %uu, %uu);\n", R.c_str(), P.c_str(),
+                     it.off + it.j - wb, it.j, it.piece, it.width, it.col_off, it.pad_to);
             break;
         case 2:
-            snprintf(b, sizeof b, "        check_str(R, P, %uu, %uu, %uu, %uu, true);\n", it.off - wb, it.off, it.f, it.len);
+            snprintf(b, sizeof b, "        check_str(%s, %s, %uu, %uu, %uu, %uu, true);\n", R.c_str(), P.c_str(),
+                     it.off - wb, it.off, it.f, it.len);
             break;
         case 3:
-            snprintf(b, sizeof b, "        check_str(R, P, 0u, %uu, %uu, %uu, false);\n", it.off, it.f, it.len);
+            snprintf(b, sizeof b, "        check_str(%s, %s, 0u, %uu, %uu, %uu, false);\n", R.c_str(), P.c_str(), it.off,
+                     it.f, it.len);
             break;
         case 4:
-            snprintf(b, sizeof b, "        if (P.valid && P.row == P.rec0) rec_error(P, P.pos0 + %uu, E_REC_FAIL, %uu);\n",
-                     it.off, it.f);
+            snprintf(b, sizeof b,
+                     "        if (%s.valid && %s.row == %s.rec0) rec_error(%s, %s.pos0 + %uu, E_REC_FAIL, %uu);\n",
+                     P.c_str(), P.c_str(), P.c_str(), P.c_str(), P.c_str(), it.off, it.f);
             break;
         }
         body += b;
+    };
+    // per window: the loads of all rows first, then its items
+    size_t i = 0;
+    while (i < items.size()) {
+        size_t e = i + 1;
+        while (e < items.size() && item_win[e] == item_win[i]) ++e;
+        const int w = item_win[i];
+        if (w >= 0) {
+            for (int k = 0; k < rpl; ++k) {
+                snprintf(b, sizeof b, "        win_load<%u>(R[%d], P[%d], %uu);\n", wins[w].second, k, k, 4 * wins[w].first);
+                body += b;
+            }
+        }
+        const uint32_t wb = w >= 0 ? 4 * wins[w].first : 0;
+        if (consec) {
+            for (size_t t = i; t < e; ++t) {
+                const Item &it = items[t];
+                if (it.type == 0) {
+                    snprintf(b, sizeof b, "        dec_num_c<%d>(R, P, %uu, %uu, %uu, %uu, %uu, %uu, %uu);\n", rpl,
+                             it.off - wb, it.off, it.f, it.len, it.width, it.kind, it.col_off);
+                    body += b;
+                } else {
+                    for (int k = 0; k < rpl; ++k) emit_item(it, wb, k);
+                }
+            }
+        } else {
+            for (int k = 0; k < rpl; ++k)
+                for (size_t t = i; t < e; ++t) emit_item(items[t], wb, k);
+        }
+        i = e;
     }
+    const std::string RPL = std::to_string(rpl);
     std::string src;
     src += "// generated by ngz_rtc.cpp for plan " + signature(P) + "\n";
     src += "#include \"ngz_dev.h\"\nusing namespace ngzdev;\n";
@@ -158,9 +197,11 @@ std::string generate(const DevPlan &P) {
     src += "    if (sgpr(B.summary->overflow)) return;\n";
     src += "    const SlotRT *rtp = &B.slots[slot];\n";
     src += "    const uint32_t c0 = sgpr(rtp->chunk0), nc = sgpr(rtp->nchunks);\n";
-    src += "    run_chunks(B, c0, c0 + nc, [](uint32_t) { return true; }, [](uint32_t) { return " +
-           std::to_string(P.rec_len) + "u; },\n";
-    src += "               [&](const Pass &P) {\n        uint32_t R[WIN_DW];\n";
+    src += "    run_chunks<" + RPL + ", " + (consec ? "true" : "false") +
+           ">(B, c0, c0 + nc, [](uint32_t) { return true; }, [](uint32_t) { return " + std::to_string(P.rec_len) +
+           "u; },\n";
+    src += "               [&](const Pass (&P)[" + RPL + "]) {\n";
+    src += "        uint32_t R[" + RPL + "][WIN_DW];\n";
     src += body;
     src += "    });\n}\n";
     return src;

@@ -50,6 +50,19 @@ class Slot:
     def column_ptr(self, f):
         return self.columns_ptr + self.capacity * self.fields[f].col_off
 
+    def block_bytes(self):
+        """Bytes of this slot's column block (every column, capacity rows)."""
+        return self.capacity * sum(fi.width for fi in self.fields)
+
+    def copy_block_to_host(self, host_ptr):
+        """D2H of the whole column block (columns are contiguous in it)."""
+        n = self.block_bytes()
+        if n:
+            rc = _lib.hip().hipMemcpy(host_ptr, self.columns_ptr, n, 2)
+            if rc != 0:
+                raise RuntimeError("hipMemcpy D2H failed: %d" % rc)
+        return n
+
     def column_bytes(self, f, rows=None):
         """Host copy of column f: uint8 array of shape (rows, width)."""
         w = self.fields[f].width
@@ -86,13 +99,22 @@ class DecodedBatch:
         return None if s is None else json.loads(s)
 
 
+OPT_SPECIALIZE = 1
+OPT_BLOCKS_PER_CU = 2
+
+
 class FlowInfoCodec:
-    def __init__(self, device=0):
+    def __init__(self, device=0, specialize=None):
         ctx = ctypes.c_void_p()
         rc = lib().ngz_ctx_create(device, ctypes.byref(ctx))
         if rc != 0:
             raise NgzError("ngz_ctx_create(%d) failed: %d (no HIP device?)" % (device, rc))
         self._ctx = ctx
+        if specialize is not None:
+            self.set_option(OPT_SPECIALIZE, 1 if specialize else 0)
+
+    def set_option(self, opt, value):
+        self._check(lib().ngz_ctx_set_option(self._ctx, opt, int(value)))
 
     def close(self):
         if self._ctx:
@@ -128,6 +150,14 @@ class FlowInfoCodec:
         out = _lib.BatchOut()
         self._check(lib().ngz_decode_batch_host(self._ctx, blob.ctypes.data, int(lens.sum()), offs.ctypes.data,
                                                 lens.ctypes.data, len(datagrams), ctypes.byref(out)))
+        return DecodedBatch(self, out)
+
+    def decode_host_buffers(self, data_ptr, data_size, offsets_ptr, lengths_ptr, n):
+        """Host-resident batch given as raw pointers (pinned memory gives full
+        PCIe rate): H2D through the library, then the device decode."""
+        out = _lib.BatchOut()
+        self._check(lib().ngz_decode_batch_host(self._ctx, data_ptr, data_size, offsets_ptr, lengths_ptr, n,
+                                                ctypes.byref(out)))
         return DecodedBatch(self, out)
 
     def templates(self, proto):
