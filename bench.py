@@ -74,7 +74,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--records", type=int, default=100_000_000, help="T20 records per GPU")
+    ap.add_argument("--records", type=int, default=100_000_000, help="records per GPU")
+    ap.add_argument("--workload", choices=["t20", "mixed8"], default="t20",
+                    help="t20 (headline): one 20-field 64-B template; mixed8: config 3, 8 reference-shaped "
+                         "templates (40-153 B) in interleaved messages")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e", action="store_true",
                     help="host-to-host rate instead: pinned host datagrams -> H2D -> decode -> D2H of all columns")
@@ -97,11 +100,18 @@ def main():
 
     dev = torch.device("cuda", local)
     codec = FlowInfoCodec(local)
-    codec.decode_datagrams([synth.template_message()])  # exporter's template, learnt before timing
     n = args.records
-    rec = synth.t20_records(n, seed=synth.SEED_CFG2 + rank, device=dev, first=0)
-    buf, offs, lens = synth.ipfix_data_stream(rec, 64)
-    del rec
+    if args.workload == "t20":
+        codec.decode_datagrams([synth.template_message()])  # exporter's template, learnt before timing
+        rec = synth.t20_records(n, seed=synth.SEED_CFG2 + rank, device=dev, first=0)
+        buf, offs, lens = synth.ipfix_data_stream(rec, 64)
+        del rec
+        rec_bytes = {256: 64}
+    else:
+        codec.decode_datagrams([synth.templates_message(synth.CFG3_TEMPLATES)])
+        buf, offs, lens, recs = synth.mixed_stream(n, seed=synth.SEED_CFG3 + 16 * rank, device=dev)
+        rec_bytes = {tid: r.shape[1] for tid, r in recs.items()}
+        del recs
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream(dev).cuda_stream
 
@@ -116,6 +126,10 @@ def main():
     for _ in range(args.warmup):
         b = step()
     assert b.n_records == n, (b.n_records, n)
+    # algorithmic bytes per launch: wire bytes read + canonical column bytes written, per template
+    alg_bytes = sum(s.n_records * (rec_bytes[s.template_id] + sum(f.width for f in s.fields))
+                    for s in b.slots if s.n_records)
+    read_bytes = sum(s.n_records * rec_bytes[s.template_id] for s in b.slots if s.n_records)
     dec_ms = []
     if dist is not None:
         dist.barrier()
@@ -136,11 +150,11 @@ def main():
     total_records = n * world * args.steps
     value = total_records / elapsed
     dec_avg = sum(dec_ms) / len(dec_ms)
-    alg_bytes = n * (BYTES_PER_RECORD_IN + BYTES_PER_RECORD_OUT)
     achieved = alg_bytes / (dec_avg * 1e-3) / 1e9
-    traffic = committed_traffic(n)
+    traffic = committed_traffic(n) if args.workload == "t20" else None
     out = {
-        "metric": "IPFIX flow records/sec + GB/s (device-resident), 20-field fixed template",
+        "metric": "IPFIX flow records/sec + GB/s (device-resident), 20-field fixed template"
+                  if args.workload == "t20" else "IPFIX flow records/sec (device-resident), config 3: 8 templates",
         "value": value,
         "unit": "records/s",
         "n_gpus": world,
@@ -151,19 +165,23 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (splitmix64 T20 records, seed 0x4E475A4500000002+rank, generated in HBM)",
-        "config": {"workload": "T20 x %d records/GPU, 1023 records per 65,492-byte IPFIX message" % n,
+        "data": "synthetic (splitmix64 records, seed 0x4E475A450000000%d+rank, generated in HBM)"
+                % (2 if args.workload == "t20" else 3),
+        "config": {"workload": ("T20 x %d records/GPU, 1023 records per 65,492-byte IPFIX message" % n)
+                   if args.workload == "t20" else
+                   ("config 3: %d records/GPU over templates %s, interleaved messages"
+                    % (n, ",".join(str(t) for t, _ in synth.CFG3_TEMPLATES))),
                    "records_per_gpu": n, "messages_per_gpu": int(offs.numel()),
                    "parallelism": "shard-per-gpu" if world > 1 else "single"},
-        "gbps_step": total_records * (BYTES_PER_RECORD_IN + BYTES_PER_RECORD_OUT) / elapsed / 1e9,
+        "gbps_step": alg_bytes * world * args.steps / elapsed / 1e9,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic[0] if traffic else None,
                      "traffic_src": traffic[1] if traffic else None,
-                     "kernel": "ngz_tpl (per-template decode kernel, T20)", "kernel_ms": dec_avg,
+                     "kernel": "ngz_tpl (per-template decode kernels)", "kernel_ms": dec_avg,
                      "alg_bytes_per_launch": alg_bytes,
-                     "read_gbps": n * BYTES_PER_RECORD_IN / (dec_avg * 1e-3) / 1e9},
+                     "read_gbps": read_bytes / (dec_avg * 1e-3) / 1e9},
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "t20":
         out["cpu_baseline"] = cpu_baseline()
     if rank == 0:
         print(json.dumps(out), flush=True)

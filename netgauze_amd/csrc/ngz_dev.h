@@ -276,6 +276,36 @@ __device__ __forceinline__ void dec_raw(const uint32_t (&R)[WIN_DW], const Pass 
     for (uint32_t z = j + piece; z < pad_to; ++z) dst[z - j] = 0;
 }
 
+// Raw field of C consecutive rows per lane (run_chunks<C, true>), whole field
+// in the window and len == width (ipv6, mac, MPLS labels, short octet arrays):
+// the C records' bytes are concatenated in registers and written as
+// C*width/4 dwords (C*width contiguous bytes per lane), instead of per-record
+// byte stores.  Other cases go record by record through dec_raw.
+template <int C>
+__device__ __forceinline__ void dec_raw_c(const uint32_t (&R)[C][WIN_DW], const Pass (&P)[C], uint32_t o,
+                                          uint32_t width, uint32_t col_off) {
+    bool full = true;
+#pragma unroll
+    for (int k = 0; k < C; ++k) full = full && P[k].valid;
+    if (full && C == 4 && width <= 16) {
+        uint8_t *dst = pass_col(P[0], col_off, width) + (uint64_t)P[0].lrow * width;
+        // dword m of the lane's 4*width bytes: byte i comes from record (4m+i)/width,
+        // field byte (4m+i)%width -- constants once width is
+        for (uint32_t m = 0; m < width; ++m) {
+            uint32_t w = 0;
+#pragma unroll
+            for (uint32_t i = 0; i < 4; ++i) {
+                const uint32_t b = 4 * m + i;
+                w |= rbyte(R[b / width], o + b % width) << (8 * i);
+            }
+            *(uint32_t *)(dst + 4 * m) = w;
+        }
+        return;
+    }
+#pragma unroll
+    for (int k = 0; k < C; ++k) dec_raw(R[k], P[k], o, 0, width, width, col_off, 0);
+}
+
 // Walk chunks [c_begin, c_end) of the batch's chunk array, one wave per chunk
 // (wave-strided).  A chunk's window of NGZ_REG_WINDOW rows is covered in
 // groups of 64*RPL rows, RPL records per lane (all their loads in flight at

@@ -81,7 +81,7 @@ struct SlotRT {          // per batch slot, computed on device by k_layout
     uint32_t base;       // first element of the slot's row in the scanned count matrix
     uint32_t chunk0;     // first chunk of the slot (chunks are slot-major)
     uint32_t nchunks;    // chunks of the slot (incl. empty padding chunks)
-    uint32_t reserved;
+    uint32_t chunk_scan0;  // scanned count at the slot's first chunk cell (k_emit cursor base)
 };
 
 struct Chunk {           // 32 B, one wave of work

@@ -249,7 +249,7 @@ __global__ void k_layout(BatchDev B) {
         rt.base = base;
         rt.chunk0 = B.scan[(uint64_t)(S + s) * N] - chunk_base;
         rt.nchunks = B.scan[(uint64_t)(S + s + 1) * N] - B.scan[(uint64_t)(S + s) * N];
-        rt.reserved = 0;
+        rt.chunk_scan0 = B.scan[(uint64_t)(S + s) * N];
         B.slots[s] = rt;
         off += ((uint64_t)cap * B.plans[s].row_bytes + 255) & ~255ull;
     }
@@ -289,8 +289,10 @@ struct EmitVis {
         if (!n) return;
         const uint32_t W = B->plans[slot].window;
         const uint32_t reserved = (n + W - 1) / W + 1;
-        uint32_t *ccell = &B->scan[(uint64_t)(B->n_slots + slot) * N + d];  // this slot's chunk cursor
-        const uint32_t chunk_at = *ccell - B->scan[(uint64_t)B->n_slots * N];
+        // this slot's chunk cursor; the scan row's own first cell is another
+        // thread's cursor, so the row base comes from SlotRT (k_layout)
+        uint32_t *ccell = &B->scan[(uint64_t)(B->n_slots + slot) * N + d];
+        const uint32_t chunk_at = *ccell - B->slots[slot].chunk_scan0 + B->slots[slot].chunk0;
         *ccell += reserved;
         uint32_t r = 0, used = 0;
         while (r < n) {

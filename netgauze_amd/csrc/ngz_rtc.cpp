@@ -179,6 +179,11 @@ std::string generate(const DevPlan &P) {
                     snprintf(b, sizeof b, "        dec_num_c<%d>(R, P, %uu, %uu, %uu, %uu, %uu, %uu, %uu);\n", rpl,
                              it.off - wb, it.off, it.f, it.len, it.width, it.kind, it.col_off);
                     body += b;
+                } else if (it.type == 1 && it.j == 0 && it.piece == it.len && it.len == it.width && it.width <= 16) {
+                    // whole short raw field: packed C-row store
+                    snprintf(b, sizeof b, "        dec_raw_c<%d>(R, P, %uu, %uu, %uu);\n", rpl, it.off - wb, it.width,
+                             it.col_off);
+                    body += b;
                 } else {
                     for (int k = 0; k < rpl; ++k) emit_item(it, wb, k);
                 }

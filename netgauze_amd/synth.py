@@ -130,3 +130,82 @@ def host_batch(datagrams, device="cpu"):
     return (torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(device),
             torch.tensor(offs, dtype=torch.int64, device=device),
             torch.tensor(lens, dtype=torch.int32, device=device))
+
+
+# --- config 3: mixed templates ------------------------------
+# Field lists are the reference's own: 347/348/342/313 as announced in
+# crates/pcap-decoder/tests/data/502-IPFIXv10-BGP-IPv6-CISCO-SRv6-lcomms.pcap,
+# 307 from wire/tests/ipfix.rs:212-236, 1024 from benches/serde_benchmark.rs:36-39.
+_F347 = [(2, 8), (1, 8), (8, 4), (12, 4), (10, 4), (14, 4), (21, 4), (22, 4), (7, 2), (11, 2), (16, 4), (17, 4),
+         (18, 4), (9, 1), (13, 1), (4, 1), (6, 2), (5, 1), (61, 1), (89, 4), (302, 4), (234, 4), (235, 4), (52, 1),
+         (53, 1), (198, 8), (56, 6), (80, 6), (256, 2), (243, 2), (245, 2), (244, 1)]
+_F342 = [(2, 8), (1, 8), (27, 16), (28, 16), (10, 4), (14, 4), (22, 4), (21, 4), (31, 4), (64, 4), (7, 2), (11, 2),
+         (16, 4), (17, 4), (63, 16), (30, 1), (29, 1), (4, 1), (6, 2), (5, 1), (61, 1), (89, 4), (302, 4), (234, 4),
+         (235, 4), (52, 1), (53, 1), (198, 8)]
+_F348 = _F342 + [(56, 6), (80, 6), (256, 2), (243, 2), (245, 2), (244, 1)]
+_F313 = [(70, 3), (71, 3), (72, 3), (73, 3), (74, 3), (75, 3), (10, 4), (14, 4), (1, 8), (2, 8), (21, 4), (22, 4),
+         (47, 4), (140, 16), (27, 16), (28, 16), (31, 4), (91, 1), (64, 4), (8, 4), (12, 4), (7, 2), (11, 2), (46, 1),
+         (89, 4), (61, 1), (5, 1), (4, 1), (6, 2), (302, 4), (234, 4), (235, 4), (198, 8)]
+_F307 = [(8, 4), (12, 4), (5, 1), (4, 1), (7, 2), (11, 2), (32, 2), (10, 4), (16, 4), (17, 4), (18, 4), (14, 4),
+         (1, 4), (2, 4), (22, 4), (21, 4), (15, 4), (9, 1), (13, 1), (6, 1), (60, 1), (152, 8), (153, 8)]
+_F1024 = [(8, 4), (12, 4), (22, 4), (21, 4), (1, 4), (2, 4), (10, 4), (14, 4), (7, 2), (11, 2), (4, 1), (6, 1),
+          (60, 1), (5, 1)]
+# 313 with NFv9-style reduced-size counters (reduced-size encoding, RFC 7011 §6.2)
+_F313R = [(f, {1: 4, 2: 4, 198: 4, 89: 1, 234: 2, 235: 2}.get(f, ln)) for f, ln in _F313]
+
+CFG3_TEMPLATES = [(256, T20), (347, _F347), (348, _F348), (342, _F342), (313, _F313), (307, _F307), (1024, _F1024),
+                  (2313, _F313R)]
+
+_DT_MS = {152, 153, 154, 155, 156, 157, 158, 159}  # dateTime{Milli,Micro,Nano}seconds IEs used here (152/153 ms)
+
+
+def template_records(fields, n, seed, device="cpu", first=0):
+    """(n, rec_len) uint8 tensor of records for an arbitrary fixed-width IANA
+    template: splitmix64 bytes, with dateTimeMilliseconds fields (152/153)
+    moved into chrono's valid range (2023-11-14 + up to ~11.6 days)."""
+    offs, rl = field_offsets(fields)
+    nw = (rl + 7) // 8
+    words = splitmix64(torch.arange(first * nw, (first + n) * nw, dtype=torch.int64, device=device), seed)
+    rec = words.view(torch.uint8).view(n, nw * 8)[:, :rl].clone()
+    for (ie, ln), o in zip(fields, offs):
+        if ie in (152, 153) and ln == 8:
+            ms = 1_700_000_000_000 + (torch.arange(first, first + n, dtype=torch.int64, device=device) * 7919) % 1_000_000_000
+            for b in range(8):
+                rec[:, o + b] = _lsr(ms, 8 * (7 - b)).bitwise_and(0xFF).to(torch.uint8)
+    return rec
+
+
+def templates_message(templates, export_time=1_700_000_000, seq=0, domain=1):
+    """One IPFIX message announcing several templates in one template set."""
+    body = b""
+    for tid, fields in templates:
+        body += struct.pack(">HH", tid, len(fields)) + b"".join(struct.pack(">HH", i, ln) for i, ln in fields)
+    sset = struct.pack(">HH", 2, 4 + len(body)) + body
+    return struct.pack(">HHIII", 10, 16 + len(sset), export_time, seq, domain) + sset
+
+
+def mixed_stream(n, templates=CFG3_TEMPLATES, seed=SEED_CFG3, device="cpu"):
+    """Config 3: n records split evenly over the templates, each template's
+    records packed as many per message as fit in 65,535 bytes, messages
+    interleaved round-robin across templates.  Returns (bytes, offsets,
+    lengths, {template id: records tensor})."""
+    parts, recs = [], {}
+    T = len(templates)
+    for t, (tid, fields) in enumerate(templates):
+        nt = n // T + (1 if t < n % T else 0)
+        _, rl = field_offsets(fields)
+        r = template_records(fields, nt, seed + t, device)
+        recs[tid] = r
+        per = (65535 - 20) // rl
+        parts.append(ipfix_data_stream(r, rl, tid=tid, rec_per_msg=per))
+    bufs, offs, lens, keys = [], [], [], []
+    base = 0
+    for t, (b, o, ln) in enumerate(parts):
+        bufs.append(b[:-16])
+        offs.append(o + base)
+        lens.append(ln)
+        keys.append(torch.arange(o.numel(), dtype=torch.int64, device=o.device) * T + t)
+        base += b.numel() - 16
+    buf = torch.cat(bufs + [torch.zeros(16, dtype=torch.uint8, device=bufs[0].device)])
+    order = torch.argsort(torch.cat(keys))
+    return buf, torch.cat(offs)[order], torch.cat(lens)[order], recs

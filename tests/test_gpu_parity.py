@@ -2,6 +2,7 @@
 
 Bit-exact on every decoded field, every header, every error text.
 """
+import ctypes
 import struct
 
 import numpy as np
@@ -10,6 +11,7 @@ import pytest
 import golden_io
 import ngz_oracle as O
 import parity
+from netgauze_amd import _lib as L
 
 pytestmark = pytest.mark.gpu
 
@@ -111,6 +113,95 @@ def test_t20_device_resident_large(dev):
         else:
             exp = raw[:, ::-1]  # big endian -> little endian, same width
         assert np.array_equal(got, exp), "field %d (ie %d)" % (f, ie)
+
+
+def column_on_device(slot, f, rows):
+    """Device copy (torch, uint8 [rows, width]) of one decoded column: the
+    full-size checks compare on the GPU instead of shipping GBs to the host."""
+    from netgauze_amd import _lib
+    w = slot.fields[f].width
+    out = torch.empty(rows * w, dtype=torch.uint8, device="cuda")
+    if rows * w:
+        hip = _lib.hip()
+        hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        assert hip.hipMemcpy(out.data_ptr(), slot.column_ptr(f), rows * w, 3) == 0  # D2D
+    return out.view(rows, w)
+
+
+def expected_column(rec, fi):
+    """Canonical column of a fixed-width unsigned / ipv4 / tcpControlBits /
+    raw-bytes / dateTimeMilliseconds field, from the wire bytes (torch, on the
+    records' device): the big-endian value re-laid little-endian at the
+    column width (SURVEY.md §8(a) column table)."""
+    off, ln, w = fi.wire_offset, fi.wire_length, fi.width
+    raw = rec[:, off:off + ln]
+    if fi.kind == L.K_BYTES:
+        return raw
+    if fi.kind == L.K_TCPFLAGS:
+        return raw[:, ln - 1:ln]
+    assert fi.kind in (L.K_UINT, L.K_DTMS), fi.kind
+    out = torch.zeros(rec.shape[0], w, dtype=torch.uint8, device=rec.device)
+    out[:, :ln] = torch.flip(raw, dims=[1])
+    return out
+
+
+def check_slot_full(slot, rec):
+    n = rec.shape[0]
+    assert slot.n_records == n
+    for f, fi in enumerate(slot.fields):
+        got = column_on_device(slot, f, n)
+        exp = expected_column(rec, fi)
+        if not torch.equal(got, exp):
+            bad = torch.nonzero((got != exp).any(dim=1)).flatten()
+            raise AssertionError("template %d field %d: %d rows differ, first %s last %s; got %s exp %s" % (
+                slot.template_id, f, bad.numel(), bad[:8].tolist(), bad[-4:].tolist(),
+                got[bad[:2]].tolist(), exp[bad[:2]].tolist()))
+
+
+def test_t20_full_size_1e8(dev):
+    """North-star size: 10^8 T20 records, every column byte compared on the GPU."""
+    from netgauze_amd import synth
+    n = 100_000_000
+    codec = new_codec()
+    codec.decode_datagrams([synth.template_message()])
+    rec = synth.t20_records(n, device=dev)
+    buf, offs, lens = synth.ipfix_data_stream(rec, 64)
+    torch.cuda.synchronize()
+    batch = codec.decode_batch(buf, offs, lens)
+    del buf
+    hdr = batch.dgram_headers()
+    assert (hdr["status"] == 0).all() and len(hdr) == offs.numel()
+    check_slot_full([s for s in batch.slots if s.template_id == 256][0], rec)
+    assert codec.template_counts(10) == {256: offs.numel()}  # one processed_count per data set
+
+
+def test_cfg3_mixed_templates_oracle(dev):
+    """Config 3 shape (8 templates, 40-153 B records, interleaved messages)
+    against the oracle, every field."""
+    from netgauze_amd import synth
+    b, o, ln, _ = synth.mixed_stream(24_000)
+    bb = bytes(b.numpy())
+    dgrams = [synth.templates_message(synth.CFG3_TEMPLATES)] + [bb[x:x + y] for x, y in zip(o.tolist(), ln.tolist())]
+    stats, batch, codec, oc = run_both(dgrams)
+    assert stats["records"] == 24_000 and stats["unsupported"] == 0
+    assert codec.template_counts(10) == {t: oc.ipfix_templates[t].processed_count for t, _ in synth.CFG3_TEMPLATES}
+
+
+def test_cfg3_mixed_templates_1e7(dev):
+    """Config 3 at 10^7 records (1.25e6 per template): every column of every
+    template compared on the GPU with the wire bytes re-laid."""
+    from netgauze_amd import synth
+    codec = new_codec()
+    codec.decode_datagrams([synth.templates_message(synth.CFG3_TEMPLATES)])
+    b, o, ln, recs = synth.mixed_stream(10_000_000, device=dev)
+    torch.cuda.synchronize()
+    batch = codec.decode_batch(b, o, ln)
+    assert batch.n_records == 10_000_000
+    assert (batch.dgram_headers()["status"] == 0).all()
+    by_tid = {s.template_id: s for s in batch.slots if s.n_records}
+    assert set(by_tid) == set(recs)
+    for tid, rec in recs.items():
+        check_slot_full(by_tid[tid], rec)
 
 
 def peers_of(name):
