@@ -83,6 +83,7 @@ struct Pass {
     uint32_t dgram;               // datagram of the chunk
     uint32_t recpos;              // this lane's record offset in the datagram
     uint32_t pos0;                // chunk's first record offset in the datagram
+    uint64_t a0;                  // batch byte offset of the resource base
     void *hdr;                    // ngz_dgram_hdr[] (errors)
 };
 
@@ -110,9 +111,9 @@ __device__ __forceinline__ void win_load(uint32_t (&R)[WIN_DW], const Pass &P, u
     }
 }
 
-__device__ __forceinline__ void rec_error(const Pass &P, uint32_t pos, uint32_t code, uint32_t f) {
+__device__ __forceinline__ void rec_error(const Pass &P, uint32_t pos, uint32_t code, uint32_t f, uint32_t b = 0) {
     atomicMin((unsigned long long *)&((ngz_dgram_hdr *)P.hdr)[P.dgram].err_key,
-              (unsigned long long)ngz_err_key(pos, code, f, 0));
+              (unsigned long long)ngz_err_key(pos, code, f, b));
 }
 
 // Column `col_off` rows [prow, prow+64) start at a uniform address; lanes add
@@ -224,13 +225,14 @@ struct GlobalBytes {
     __device__ uint32_t operator()(uint32_t i) const { return __builtin_amdgcn_raw_buffer_load_b8(rsrc, base + i, 0, 0); }
 };
 
+// std::str::from_utf8 of `len` bytes; with stop_at_nul only the bytes up to
+// the first NUL (fixed-length strings, generator.rs:1651-1668)
 template <class F>
-__device__ bool utf8_valid_prefix(const F &byte_at, uint32_t len) {
-    // std::str::from_utf8 of the bytes up to the first NUL (generator.rs:1651-1668)
+__device__ bool utf8_valid_prefix(const F &byte_at, uint32_t len, bool stop_at_nul = true) {
     uint32_t i = 0;
     while (i < len) {
         const uint32_t c = byte_at(i);
-        if (c == 0) return true;
+        if (c == 0 && stop_at_nul) return true;
         if (c < 0x80) { ++i; continue; }
         uint32_t need, lo = 0x80, hi = 0xBF;
         if (c >= 0xC2 && c <= 0xDF) need = 1;
@@ -310,12 +312,18 @@ __device__ __forceinline__ void dec_raw_c(const uint32_t (&R)[C][WIN_DW], const 
 // (wave-strided).  A chunk's window of NGZ_REG_WINDOW rows is covered in
 // groups of 64*RPL rows, RPL records per lane (all their loads in flight at
 // once): with CONSEC lane l owns the RPL consecutive rows prow + RPL*l + k
-// (so narrow columns pack into wide stores), otherwise rows prow + 64*k + l.  want(slot) decides (and
-// may load per-slot state) whether a chunk's slot is handled here;
-// rec_len(slot) gives its record length; pass(P) decodes one group.
-template <int RPL, bool CONSEC, class Want, class RecLen, class PassFn>
+// (so narrow columns pack into wide stores), otherwise rows prow + 64*k + l.
+// want(slot) decides (and may load per-slot state) whether a chunk's slot is
+// handled here; shape(slot) gives its record shape; pass(P) decodes one group.
+struct RecShape {
+    uint32_t rl;         // record length (fixed templates)
+    uint32_t row_bytes;  // column bytes per row (locates the record-offset array of vlen slots)
+    bool vlen;           // variable-length records: per-row offsets from the record-offset array
+};
+
+template <int RPL, bool CONSEC, class Want, class Shape, class PassFn>
 __device__ __forceinline__ void run_chunks(const BatchDev &B, uint32_t c_begin, uint32_t c_end, Want &&want,
-                                           RecLen &&rec_len, PassFn &&pass) {
+                                           Shape &&shape, PassFn &&pass) {
     static_assert(RPL == 1 || RPL == 2 || RPL == 4, "RPL");
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wpb = blockDim.x >> 6;
@@ -328,7 +336,8 @@ __device__ __forceinline__ void run_chunks(const BatchDev &B, uint32_t c_begin, 
         if (n == 0) continue;  // padding chunk
         const uint32_t slot = sgpr(c1.x >> 16);
         if (!want(slot)) continue;
-        const uint32_t rl = rec_len(slot);
+        const RecShape rs = shape(slot);
+        const uint32_t rl = rs.rl;
         const uint64_t src = (uint64_t)sgpr(c0.x) | ((uint64_t)sgpr(c0.y) << 32);
         Pass P[RPL];
         P[0].rec0 = sgpr(c0.z);
@@ -342,7 +351,9 @@ __device__ __forceinline__ void run_chunks(const BatchDev &B, uint32_t c_begin, 
         const uint64_t avail64 = B.bytes_size - a0;
         const uint32_t avail = avail64 > 0x7FFFFFF0ull ? 0x7FFFFFF0u : (uint32_t)avail64;
         P[0].rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)(B.bytes + a0), (short)0, (int)avail, 0x00020000);
+        P[0].a0 = a0;
         P[0].lane = lane;
+        const uint32_t *ro = rs.vlen ? (const uint32_t *)(P[0].blk + (uint64_t)P[0].cap * rs.row_bytes) : nullptr;
 #pragma unroll
         for (int k = 1; k < RPL; ++k) P[k] = P[0];
         const uint32_t rec0 = P[0].rec0;
@@ -358,11 +369,13 @@ __device__ __forceinline__ void run_chunks(const BatchDev &B, uint32_t c_begin, 
                 Q.row = Q.prow + Q.lrow;
                 Q.valid = Q.row >= rec0 && Q.row < rec0 + n;
                 const uint32_t r = Q.valid ? Q.row - rec0 : 0;
-                const uint32_t rel = r * rl + (uint32_t)(src & 3);
+                // record offset from the chunk's first record
+                const uint32_t d = ro ? (Q.valid ? ro[Q.row] : P[0].pos0) - P[0].pos0 : r * rl;
+                const uint32_t rel = d + (uint32_t)(src & 3);
                 Q.rbase = rel & ~3u;
                 Q.sh = rel & 3u;
                 Q.any_sh = __builtin_amdgcn_ballot_w64(Q.sh != 0) != 0;
-                Q.recpos = Q.pos0 + r * rl;
+                Q.recpos = Q.pos0 + d;
             }
             pass(P);
         }

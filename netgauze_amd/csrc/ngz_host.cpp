@@ -193,7 +193,8 @@ void field_rule(const Spec &s, uint8_t &kind, uint16_t &width, uint8_t &fail) {
         return;
     }
     if (s.kind == IK_UNKNOWN || s.kind == IK_VENDOR_UNKNOWN) {
-        if (L == 0xFFFF) { kind = NGZ_K_VLEN; width = 0; }
+        // IE::Unknown reads 65535 fixed bytes (generator.rs:2971-2974); vendor Unknown is vlen-aware
+        if (L == 0xFFFF && s.kind == IK_VENDOR_UNKNOWN) { kind = NGZ_K_VLEN; width = 16; }
         else { kind = NGZ_K_BYTES; width = (uint16_t)L; }
         return;
     }
@@ -204,11 +205,11 @@ void field_rule(const Spec &s, uint8_t &kind, uint16_t &width, uint8_t &fail) {
     case DT_basicList:
     case DT_subTemplateList:
     case DT_subTemplateMultiList:
-        if (L == 0xFFFF) { kind = NGZ_K_VLEN; width = 0; }
+        if (L == 0xFFFF) { kind = NGZ_K_VLEN; width = 16; }
         else { kind = NGZ_K_BYTES; width = (uint16_t)L; }
         return;
     case DT_string:
-        if (L == 0xFFFF) { kind = NGZ_K_VLEN; width = 0; }
+        if (L == 0xFFFF) { kind = NGZ_K_VLEN; width = 16; fail = 0x80; }
         else { kind = NGZ_K_STR; width = (uint16_t)L; }
         return;
     case DT_unsigned8: if (L != 1) failk(1); else { kind = NGZ_K_UINT; width = 1; } return;
@@ -255,9 +256,9 @@ void build_plan(Version &v) {
         uint8_t kind, fail;
         uint16_t width;
         field_rule(s, kind, width, fail);
+        // IPFIX 65535 = variable length; IE::Unknown reads 65535 fixed bytes instead
+        // (generator.rs:2971-2974), which the record walk always reports as UnexpectedEof
         if (v.proto == 10 && s.length == 0xFFFF) vlen = true;
-        // a fixed read of 65535 bytes (IE::Unknown, generator.rs:2971-2974)
-        if (v.proto == 10 && s.length == 0xFFFF && kind != NGZ_K_VLEN) devok = false;
         // min_record_length counts a vlen field as 1 (ipfix.rs:193-214); NFv9 literal (netflow.rs:201-210)
         rl += (v.proto == 10 && s.length == 0xFFFF) ? 1 : s.length;
         if (i < NGZ_MAXF) {
@@ -281,11 +282,11 @@ void build_plan(Version &v) {
         if (P.f[i].kind == NGZ_K_DTMS || P.f[i].kind == NGZ_K_DTFRAC || P.f[i].kind == NGZ_K_STR ||
             P.f[i].kind == NGZ_K_FAIL)
             P.has_err = 1;
-    // rpl != 0: device-decodable (every fixed-length record; IPFIX templates
-    // with variable-length fields are not yet)
+    // rpl != 0: device-decodable (fixed-length records, and IPFIX records with
+    // variable-length fields through the framing walk + record-offset arrays)
     P.rpl = 0;
     P.window = NGZ_REG_WINDOW;
-    if (devok && !(v.proto == 10 && vlen) && rl <= NGZ_MAX_REC_LEN) P.rpl = 1;
+    if (devok && rl <= NGZ_MAX_REC_LEN) P.rpl = 1;
 }
 
 struct ErrInfo {  // host-side framing error
@@ -619,11 +620,17 @@ void host_frame(ngz_ctx *ctx, const uint8_t *p, uint32_t dl, uint32_t limit, Hos
                 }
                 const Version &v = ctx->versions[vid];
                 const uint32_t ml = v.plan.rec_len;
-                const uint32_t n = ml ? (sl - 4) / ml : 0;
+                uint64_t verr = NGZ_NO_ERR;
+                uint32_t n;
+                if (v.plan.has_vlen && v.plan.rpl)  // record lengths come from the data (ipfix.rs:219-222)
+                    n = ngz_vlen_walk(p, pos + 4, pos + sl, v.plan, &verr, [](uint32_t, uint32_t) {});
+                else
+                    n = ml ? (sl - 4) / ml : 0;
                 if (n && !v.plan.rpl) { h.status = NGZ_DG_UNSUPPORTED; return; }
                 HostSet hs{};
                 hs.set_pos = (uint16_t)pos; hs.reserved2 = (uint32_t)vid; hs.payload_pos = (uint16_t)(pos + 4); hs.n = n;
                 o.sets.push_back(hs);
+                if (verr != NGZ_NO_ERR) { h.err_key = verr; return; }  // rendered like a device-found record error
             }
             pos += sl;
         }
@@ -783,7 +790,7 @@ int upload_slots(ngz_ctx *ctx, const std::vector<int32_t> cur_start[2], hipStrea
         Version &v = ctx->versions[ctx->slot_version[s]];
         plans[s] = v.plan;
         plans[s].spec = 0;
-        if (ctx->specialize && v.plan.rpl) {
+        if (ctx->specialize && v.plan.rpl && !v.plan.has_vlen) {  // vlen templates: generic kernel
             if (v.rtc_state == 0) {
                 v.rtc_fn = ngz_rtc_kernel(ctx->device, v.plan);
                 v.rtc_state = v.rtc_fn ? 1 : 2;
@@ -914,7 +921,7 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
         if (!ctx->h_slots[s].nchunks) continue;
         const Version &v = ctx->versions[ctx->slot_version[s]];
         if (!v.plan.rpl) continue;
-        if (ctx->specialize && v.rtc_state == 1) {
+        if (ctx->specialize && v.rtc_state == 1 && !v.plan.has_vlen) {
             // one specialised kernel per active template, over that slot's chunks only
             const uint32_t g = std::min<uint32_t>(grid, (ctx->h_slots[s].nchunks + 3) / 4);
             if (ngz_rtc_launch(v.rtc_fn, &B, s, g, st)) return fail(ctx, NGZ_E_DEVICE, "specialised decode launch");
@@ -1361,15 +1368,20 @@ extern "C" int ngz_dgram_error_json(ngz_ctx *ctx, uint32_t dgram, char *buf, siz
             snprintf(b, sizeof b, "{\"InvalidPaddingValue\":{\"offset\":%u,\"value\":%u}}", stop, bval); s = set_wrap(b); break;
         case E_NF_INVALID_COUNT:
             snprintf(b, sizeof b, "{\"InvalidCount\":{\"offset\":2,\"count\":%u}}", bval); s = wrap(W, b); break;
-        case E_REC_DTMS: case E_REC_DTFRAC: case E_REC_UTF8: case E_REC_FAIL: {
+        case E_REC_DTMS: case E_REC_DTFRAC: case E_REC_UTF8: case E_REC_FAIL: case E_REC_EOF: {
             // find the set and version holding the failing field
             uint32_t nsets = ctx->summary.n_sets;
             std::vector<ngz_set_info> sets(nsets);
             hipMemcpy(sets.data(), ctx->d_sets.p, nsets * sizeof(ngz_set_info), hipMemcpyDeviceToHost);
             const Version *v = nullptr;
-            for (auto &si : sets)
-                if (si.dgram == dgram && si.set_pos < stop && stop < si.set_pos + rd16(p.data() + si.set_pos + 2))
+            uint32_t set_end = 0;
+            for (auto &si : sets) {
+                const uint32_t e = si.set_pos + rd16(p.data() + si.set_pos + 2);
+                if (si.dgram == dgram && si.set_pos < stop && stop <= e) {
                     v = &ctx->versions[ctx->slot_version[si.slot]];
+                    set_end = e;
+                }
+            }
             if (!v || a >= v->specs.size()) { s = "null"; break; }
             const Spec &sp = v->specs[a];
             std::string fe;
@@ -1385,9 +1397,12 @@ extern "C" int ngz_dgram_error_json(ngz_ctx *ctx, uint32_t dgram, char *buf, siz
                          "{\"InvalidTimestampFraction\":{\"offset\":%u,\"ie_name\":%s,\"seconds\":%u,\"fraction\":%u}}",
                          stop, json_str(name).c_str(), rd32(p.data() + stop), rd32(p.data() + stop + 4));
                 fe = b;
+            } else if (code == E_REC_EOF) {  // variable-length record ran past its set
+                fe = eof_json({stop, bval, set_end - stop});
             } else if (code == E_REC_UTF8) {
                 uint32_t n = 0;
-                while (n < sp.length && p[stop + n]) ++n;
+                if (sp.length == 0xFFFF) n = bval;  // variable-length string: every byte
+                else while (n < sp.length && p[stop + n]) ++n;  // fixed: up to the first NUL
                 snprintf(b, sizeof b, "{\"Utf8Error\":{\"offset\":%u,\"ie_name\":%s,\"error\":", stop, json_str(name).c_str());
                 fe = std::string(b) + json_str(utf8_error_msg(p.data() + stop, n).c_str()) + "}}";
             } else {
@@ -1405,7 +1420,7 @@ extern "C" int ngz_dgram_error_json(ngz_ctx *ctx, uint32_t dgram, char *buf, siz
                              json_str(name).c_str(), sp.length);
                 fe = b;
             }
-            if (sp.kind == IK_VENDOR) fe = wrap((std::string(sp.vendor) + "Error").c_str(), fe);
+            if (sp.kind == IK_VENDOR || sp.kind == IK_VENDOR_UNKNOWN) fe = wrap((std::string(sp.vendor) + "Error").c_str(), fe);
             s = set_wrap(wrap("DataRecordError", wrap("FieldError", fe)));
             break;
         }

@@ -3,6 +3,8 @@
 #pragma once
 #include <stdint.h>
 
+#include "ngz/flow_decode.h"
+
 #define NGZ_MAXF 128          // fields (scope + non-scope) a device plan can hold
 #define NGZ_MAX_SLOTS 1024    // template versions live in one batch
 #define NGZ_NO_SLOT 0xFFFFu
@@ -38,9 +40,10 @@ enum NgzErr : uint32_t {
     E_NF_INVALID_COUNT = 11,          // b = count
     E_REC_DTMS = 12,                  // a = field index (value re-read by host)
     E_REC_DTFRAC = 13,                // a = field index
-    E_REC_UTF8 = 14,                  // a = field index
+    E_REC_UTF8 = 14,                  // a = field index, b = value length (variable-length strings)
     E_REC_FAIL = 15,                  // a = field index (template-constant failure)
     E_HOST = 16,                      // host-framed datagram error: b = index in host error table
+    E_REC_EOF = 17,                   // UnexpectedEof inside a variable-length data record: a = field, b = needed
 };
 
 static inline __host__ __device__ uint64_t ngz_err_key(uint32_t stop, uint32_t code, uint32_t a, uint32_t b) {
@@ -53,7 +56,7 @@ struct DevField {        // 16 B
     uint16_t len;        // wire length
     uint16_t width;      // column width
     uint8_t kind;        // NGZ_K_*
-    uint8_t flags;
+    uint8_t flags;       // NGZ_K_FAIL: failure sub-code; NGZ_K_VLEN: 0x80 = string (UTF-8 checked)
     uint32_t col_off;    // bytes per row before this column
     uint32_t reserved;
 };
@@ -73,6 +76,56 @@ struct DevPlan {
     uint32_t reserved1[2];
     DevField f[NGZ_MAXF];
 };
+
+// Records of one IPFIX data set whose template has variable-length (65535)
+// fields, walked as Set::parse + DataRecord::parse + Field::parse would
+// (ipfix.rs:193-222, 335-370; vlen prefix generator.rs:1775-1793: u8, 255 ->
+// 3-byte length).  p = datagram, [pos, end) = set payload.  Calls
+// on_rec(k, record_offset) for each complete record only (a failing record
+// has no row); returns the number of complete records; on UnexpectedEof / a
+// template-constant field failure sets *err to the error key (parsing stops
+// there).
+template <class F>
+__host__ __device__ inline uint32_t ngz_vlen_walk(const uint8_t *p, uint32_t pos, uint32_t end, const DevPlan &pl,
+                                                  uint64_t *err, F &&on_rec) {
+    const uint32_t minlen = pl.rec_len;  // vlen counted as 1
+    uint32_t n = 0;
+    while (minlen > 0 && end - pos >= minlen) {
+        const uint32_t start = pos;
+        for (uint32_t f = 0; f < pl.n_fields; ++f) {
+            const DevField &fd = pl.f[f];
+            const uint32_t rem = end - pos;
+            if (fd.kind == NGZ_K_FAIL) {  // fails before reading (InvalidLength, ...)
+                *err = ngz_err_key(pos, E_REC_FAIL, f, 0);
+                return n;
+            }
+            if (fd.kind == NGZ_K_VLEN) {
+                if (rem < 1) { *err = ngz_err_key(pos, E_REC_EOF, f, 1); return n; }
+                uint32_t len = p[pos];
+                pos += 1;
+                if (len == 255) {  // read_unsigned32_be(3)
+                    if (end - pos < 3) { *err = ngz_err_key(pos, E_REC_EOF, f, 3); return n; }
+                    len = ((uint32_t)p[pos] << 16) | ((uint32_t)p[pos + 1] << 8) | p[pos + 2];
+                    pos += 3;
+                }
+                if (end - pos < len) { *err = ngz_err_key(pos, E_REC_EOF, f, len); return n; }
+                pos += len;
+                continue;
+            }
+            if (fd.kind == NGZ_K_DTFRAC) {  // two u32 reads (generator.rs:1748-1773)
+                if (rem < 4) { *err = ngz_err_key(pos, E_REC_EOF, f, 4); return n; }
+                if (rem < 8) { *err = ngz_err_key(pos + 4, E_REC_EOF, f, 4); return n; }
+                pos += 8;
+                continue;
+            }
+            if (rem < fd.len) { *err = ngz_err_key(pos, E_REC_EOF, f, fd.len); return n; }
+            pos += fd.len;
+        }
+        on_rec(n, start);
+        ++n;
+    }
+    return n;
+}
 
 struct SlotRT {          // per batch slot, computed on device by k_layout
     uint64_t block;      // byte offset of the slot's columns in the arena

@@ -63,9 +63,15 @@ __device__ void walk_datagram(const BatchDev &B, const uint32_t *__restrict__ hf
     o.err = NGZ_NO_ERR;
     if (hf_flag != nullptr && hf_flag[d]) {
         o.status = NGZ_FR_HOST;
+        const uint8_t *p = B.bytes + B.offsets[d];
         for (uint32_t i = hf_first[d]; i < hf_first[d + 1]; ++i) {
             const HostSet &h = B.hf_sets[i];
-            vis.on_set(h.set_pos, h.slot, h.n, h.payload_pos, B.plans[h.slot].rec_len);
+            const DevPlan &pl = B.plans[h.slot];
+            if (pl.has_vlen && h.n) {  // record offsets (the host walk counted the same records)
+                uint64_t e = NGZ_NO_ERR;
+                vis.vlen(p, h.payload_pos, h.set_pos + be16(p + h.set_pos + 2), h.slot, pl, &e);
+            }
+            vis.on_set(h.set_pos, h.slot, h.n, h.payload_pos, pl.rec_len);
         }
         return;
     }
@@ -106,11 +112,17 @@ __device__ void walk_datagram(const BatchDev &B, const uint32_t *__restrict__ hf
                 o.status = NGZ_FR_ERROR; o.err = ngz_err_key(pos, E_SET_NO_TEMPLATE, id, 0); return;
             }
             const DevPlan &pl = B.plans[slot];
-            const uint32_t minlen = pl.rec_len;  // ipfix.rs:193-214
-            const uint32_t n = minlen ? (sl - 4) / minlen : 0;  // :219 loop bound
+            const uint32_t minlen = pl.rec_len;  // ipfix.rs:193-214 (vlen counted as 1)
+            uint64_t verr = NGZ_NO_ERR;
+            uint32_t n;
+            if (pl.has_vlen && pl.rpl)  // :219-222 record by record: lengths come from the data
+                n = vis.vlen(p, pos + 4, pos + sl, slot, pl, &verr);
+            else
+                n = minlen ? (sl - 4) / minlen : 0;  // :219 loop bound
             if (n && !pl.rpl) { o.status = NGZ_FR_UNSUPPORTED; return; }
             o.nsets++;
             vis.on_set(pos, slot, n, pos + 4, minlen);
+            if (verr != NGZ_NO_ERR) { o.status = NGZ_FR_ERROR; o.err = verr; return; }  // first error aborts
             pos += sl;  // leftover (padding or garbage) ignored: ipfix.rs:224-227
         }
         return;
@@ -195,6 +207,9 @@ struct CountVis {
     uint32_t N, S, d;
     uint32_t sets;
     const DevPlan *plans;
+    __device__ uint32_t vlen(const uint8_t *p, uint32_t pos, uint32_t end, uint32_t, const DevPlan &pl, uint64_t *err) {
+        return ngz_vlen_walk(p, pos, end, pl, err, [](uint32_t, uint32_t) {});
+    }
     __device__ void on_set(uint32_t, uint32_t slot, uint32_t n, uint32_t, uint32_t) {
         counts[(uint64_t)slot * N + d] += n;
         if (n) counts[(uint64_t)(S + slot) * N + d] += (n + plans[slot].window - 1) / plans[slot].window + 1;
@@ -251,7 +266,8 @@ __global__ void k_layout(BatchDev B) {
         rt.nchunks = B.scan[(uint64_t)(S + s + 1) * N] - B.scan[(uint64_t)(S + s) * N];
         rt.chunk_scan0 = B.scan[(uint64_t)(S + s) * N];
         B.slots[s] = rt;
-        off += ((uint64_t)cap * B.plans[s].row_bytes + 255) & ~255ull;
+        const uint64_t rec_off_bytes = B.plans[s].has_vlen ? 4ull * cap : 0;  // vlen: record offsets
+        off += ((uint64_t)cap * B.plans[s].row_bytes + rec_off_bytes + 255) & ~255ull;
     }
     const uint32_t rec_total = chunk_base;
     const uint32_t chunks = B.scan[(uint64_t)(2 * S) * N] - chunk_base;
@@ -273,6 +289,18 @@ struct EmitVis {
     uint64_t dg_off;
     uint32_t set_at;
     bool ok;
+    // variable-length records: their datagram offsets go to the slot's
+    // record-offset array (after its columns), rows rec0.. of this set
+    __device__ uint32_t *recoff(uint32_t slot) const {
+        const SlotRT &rt = B->slots[slot];
+        return (uint32_t *)(B->arena + rt.block + (uint64_t)rt.cap * B->plans[slot].row_bytes);
+    }
+    __device__ uint32_t vlen(const uint8_t *p, uint32_t pos, uint32_t end, uint32_t slot, const DevPlan &pl,
+                             uint64_t *err) {
+        const uint32_t rec0 = B->scan[(uint64_t)slot * B->n + d] - B->slots[slot].base;
+        uint32_t *ro = recoff(slot) + rec0;
+        return ngz_vlen_walk(p, pos, end, pl, err, [&](uint32_t k, uint32_t at) { ro[k] = at; });
+    }
     __device__ void on_set(uint32_t set_pos, uint32_t slot, uint32_t n, uint32_t payload_pos, uint32_t rl) {
         const uint64_t N = B->n;
         uint32_t *cell = &B->scan[(uint64_t)slot * N + d];
@@ -294,18 +322,20 @@ struct EmitVis {
         uint32_t *ccell = &B->scan[(uint64_t)(B->n_slots + slot) * N + d];
         const uint32_t chunk_at = *ccell - B->slots[slot].chunk_scan0 + B->slots[slot].chunk0;
         *ccell += reserved;
+        const uint32_t *ro = B->plans[slot].has_vlen ? recoff(slot) : nullptr;
         uint32_t r = 0, used = 0;
         while (r < n) {
             const uint32_t cstart = rec0 + r;
             const uint32_t wend = (cstart / W + 1) * W;
             const uint32_t take = min(n - r, wend - cstart);
+            const uint32_t at = ro ? ro[cstart] : payload_pos + r * rl;  // first record's offset in the datagram
             Chunk c;
-            c.src = dg_off + payload_pos + (uint64_t)r * rl;
+            c.src = dg_off + at;
             c.rec0 = cstart;
             c.dgram = d;
             c.n = (uint16_t)take;
             c.slot = (uint16_t)slot;
-            c.pos0 = (uint16_t)(payload_pos + r * rl);
+            c.pos0 = (uint16_t)at;
             c.cls = 0;
             c.reserved2 = 0;
             B->chunks[chunk_at + used] = c;
@@ -349,14 +379,16 @@ __global__ void k_emit(BatchDev B, const uint32_t *hf_flag, const uint32_t *hf_f
 __global__ void __launch_bounds__(256) k_decode_generic(BatchDev B) {
     if (sgpr(B.summary->overflow)) return;
     const uint32_t lane = threadIdx.x & 63;
-    uint32_t cached = 0xFFFFFFFFu, rl = 0, nf = 0, skip = 0;
+    uint32_t cached = 0xFFFFFFFFu, rl = 0, nf = 0, skip = 0, row_bytes = 0, has_vlen = 0;
     uint4 fA = make_uint4(0, 0, 0, 0), fB = make_uint4(0, 0, 0, 0);  // field descriptors f = lane, lane + 64
     auto want = [&](uint32_t slot) {
         if (slot != cached) {
             const DevPlan *pl = &B.plans[slot];
             const uint4 h0 = ((const uint4 *)pl)[0];
             rl = sgpr(h0.x);
+            row_bytes = sgpr(h0.y);
             nf = sgpr(h0.z & 0xFFFF);
+            has_vlen = sgpr((h0.w >> 8) & 0xFF);
             skip = sgpr((h0.w >> 24) & 0xFF);  // DevPlan::spec: decoded by its own kernel
             const uint4 *ft = (const uint4 *)pl->f;
             fA = lane < nf ? ft[lane] : make_uint4(0, 0, 0, 0);
@@ -365,45 +397,81 @@ __global__ void __launch_bounds__(256) k_decode_generic(BatchDev B) {
         }
         return skip == 0;
     };
+    auto shape = [&](uint32_t) { return RecShape{rl, row_bytes, has_vlen != 0}; };
     auto pass = [&](const Pass (&PP)[1]) {
-        const Pass &P = PP[0];
+        const Pass &P0 = PP[0];
+        Pass P = P0;               // window loads are relative to the current segment
+        const uint32_t rel0 = P0.rbase + P0.sh;  // record start, relative to the resource
+        uint32_t seg = 0;          // per lane: record offset of the current segment (after the last vlen field)
+        uint32_t so = 0;           // uniform: offset of the next field inside the segment
         uint32_t R[WIN_DW];
-        uint32_t wb = 0xFFFFFFFFu;  // record offset of the window held in R (uniform)
+        uint32_t wb = 0xFFFFFFFFu;  // segment offset of the window held in R (uniform)
+        auto window = [&](uint32_t lo, uint32_t hi) {  // make segment bytes [lo, hi) available
+            if (wb == 0xFFFFFFFFu || lo < wb || hi > wb + WIN_B) {
+                wb = lo & ~3u;
+                win_load<WIN_DW - 1>(R, P, wb);
+            }
+        };
         for (uint32_t f = 0; f < nf; ++f) {
             const uint4 &fs = f < 64 ? fA : fB;
             const uint32_t fl = f & 63;
             const uint32_t dx = __builtin_amdgcn_readlane(fs.x, fl), dy = __builtin_amdgcn_readlane(fs.y, fl);
             const uint32_t col_off = __builtin_amdgcn_readlane(fs.z, fl);
-            const uint32_t off = dx & 0xFFFF, len = dx >> 16, width = dy & 0xFFFF, kind = (dy >> 16) & 0xFF;
+            const uint32_t len = dx >> 16, width = dy & 0xFFFF, kind = (dy >> 16) & 0xFF;
+            const uint32_t off = seg + so;  // record offset of the field (per lane after a vlen field)
             if (kind == NGZ_K_FAIL) {
                 // template-constant failure: only the chunk's first record matters
+                // (vlen templates never get here: the framing walk stops at it)
                 if (P.valid && P.row == P.rec0) rec_error(P, P.pos0 + off, E_REC_FAIL, f);
+                so += len;
                 continue;
             }
-            if (kind == NGZ_K_VLEN || kind == 0) continue;
+            if (kind == NGZ_K_VLEN) {
+                // u8 length, 255 -> 3-byte length (generator.rs:1775-1793); column = {u64 batch offset, u32 len, 0}
+                window(so, so + 4);
+                uint32_t L = rbyte(R, so - wb), hdr = 1;
+                if (L == 255) {
+                    L = (uint32_t)rbe(R, so + 1 - wb, 3);
+                    hdr = 4;
+                }
+                const uint32_t data = off + hdr;  // record offset of the value
+                if (P.valid) {
+                    uint8_t *dst = pass_col(P, col_off, 16) + P.lrow * 16;
+                    const uint64_t at = P0.a0 + rel0 + data;
+                    *(uint4 *)dst = make_uint4((uint32_t)at, (uint32_t)(at >> 32), L, 0);
+                    if ((dy >> 31) && !utf8_valid_prefix(GlobalBytes{P.rsrc, rel0 + data}, L, false))  // vlen string
+                        rec_error(P, P0.recpos + data, E_REC_UTF8, f, L);
+                }
+                seg = data + L;  // the next segment starts after the value
+                so = 0;
+                P.rbase = (rel0 + seg) & ~3u;
+                P.sh = (rel0 + seg) & 3u;
+                P.any_sh = __builtin_amdgcn_ballot_w64(P.sh != 0) != 0;
+                wb = 0xFFFFFFFFu;
+                continue;
+            }
+            if (kind == 0) { so += len; continue; }
             const bool raw = kind == NGZ_K_STR || kind == NGZ_K_BYTES || kind == NGZ_K_U256;
-            if (kind == NGZ_K_STR && len > 64) check_str(R, P, 0, off, f, len, false);
+            if (kind == NGZ_K_STR && len > 64) check_str(R, P0, 0, off, f, len, false);
             // one window per field, or per 64-byte piece of a raw field
             for (uint32_t j = 0;; j += 64) {
                 const uint32_t piece = raw ? min(64u, len - j) : 8u;
-                const uint32_t lo = off + j, hi = lo + ((piece + 3) & ~3u);
-                if (wb == 0xFFFFFFFFu || lo < wb || hi > wb + WIN_B) {  // slide the window
-                    wb = lo & ~3u;
-                    win_load<WIN_DW - 1>(R, P, wb);
-                }
+                const uint32_t lo = so + j;
+                window(lo, lo + ((piece + 3) & ~3u));
                 const uint32_t o = lo - wb;
                 if (!raw) {
-                    dec_num(R, P, o, off, f, len, width, kind, col_off);
+                    dec_num(R, P0, o, off, f, len, width, kind, col_off);
                     break;
                 }
-                if (kind == NGZ_K_STR && len <= 64) check_str(R, P, o, off, f, len, true);
+                if (kind == NGZ_K_STR && len <= 64) check_str(R, P0, o, off, f, len, true);
                 const bool last = j + 64 >= len;
-                dec_raw(R, P, o, j, piece, width, col_off, last ? width : 0);
+                dec_raw(R, P0, o, j, piece, width, col_off, last ? width : 0);
                 if (last) break;
             }
+            so += len;
         }
     };
-    run_chunks<1, false>(B, 0, sgpr(B.summary->n_chunks), want, [&](uint32_t) { return rl; }, pass);
+    run_chunks<1, false>(B, 0, sgpr(B.summary->n_chunks), want, shape, pass);
 }
 
 __device__ __forceinline__ uint64_t wave_sum(uint64_t v) {

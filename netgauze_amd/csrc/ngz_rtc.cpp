@@ -203,8 +203,8 @@ std::string generate(const DevPlan &P) {
     src += "    const SlotRT *rtp = &B.slots[slot];\n";
     src += "    const uint32_t c0 = sgpr(rtp->chunk0), nc = sgpr(rtp->nchunks);\n";
     src += "    run_chunks<" + RPL + ", " + (consec ? "true" : "false") +
-           ">(B, c0, c0 + nc, [](uint32_t) { return true; }, [](uint32_t) { return " + std::to_string(P.rec_len) +
-           "u; },\n";
+           ">(B, c0, c0 + nc, [](uint32_t) { return true; }, [](uint32_t) { return RecShape{" +
+           std::to_string(P.rec_len) + "u, 0u, false}; },\n";
     src += "               [&](const Pass (&P)[" + RPL + "]) {\n";
     src += "        uint32_t R[" + RPL + "][WIN_DW];\n";
     src += body;

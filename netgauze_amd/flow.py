@@ -71,14 +71,26 @@ class Slot:
 
 
 class DecodedBatch:
-    def __init__(self, codec, out):
+    def __init__(self, codec, out, source=None):
         self._codec = codec
+        self._source = source  # the batch bytes: host numpy array or device tensor
         self.out = out
         self.n_dgrams = out.n_dgrams
         self.n_sets = out.n_sets
         self.n_records = out.n_records
         self.n_template_dgrams = out.n_template_dgrams
         self.slots = [Slot(codec, i, out.slots[i]) for i in range(out.n_slots)]
+
+    def input_bytes(self, offset, n):
+        """Bytes [offset, offset+n) of this batch's input: variable-length
+        columns hold {u64 offset into the batch bytes, u32 length} and are
+        valid while the input is (the next batch on the context at most)."""
+        src = self._source
+        if src is None:
+            raise ValueError("batch input not retained")
+        if isinstance(src, np.ndarray):
+            return bytes(src[offset:offset + n])
+        return bytes(d2h(src.data_ptr() + offset, n))
 
     def dgram_headers(self):
         return d2h(self.out.dgrams, self.n_dgrams * 32).view(DGRAM_HDR_DTYPE)
@@ -138,7 +150,7 @@ class FlowInfoCodec:
         out = _lib.BatchOut()
         self._check(lib().ngz_decode_batch(self._ctx, ctypes.byref(bi), ctypes.byref(out),
                                            ctypes.c_void_p(stream) if stream else None))
-        return DecodedBatch(self, out)
+        return DecodedBatch(self, out, data)
 
     def decode_datagrams(self, datagrams):
         """Host-memory datagrams (list of bytes): H2D through the library."""
@@ -150,7 +162,7 @@ class FlowInfoCodec:
         out = _lib.BatchOut()
         self._check(lib().ngz_decode_batch_host(self._ctx, blob.ctypes.data, int(lens.sum()), offs.ctypes.data,
                                                 lens.ctypes.data, len(datagrams), ctypes.byref(out)))
-        return DecodedBatch(self, out)
+        return DecodedBatch(self, out, blob)
 
     def decode_host_buffers(self, data_ptr, data_size, offsets_ptr, lengths_ptr, n):
         """Host-resident batch given as raw pointers (pinned memory gives full

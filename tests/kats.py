@@ -1,0 +1,64 @@
+"""Field-level known-answer vectors transcribed from the reference's own unit
+tests (crates/flow-pkt/src/wire/tests/mod.rs and ipfix.rs).  Each entry is
+(name, ie_id, length, wire bytes, expected oracle value or expected error).
+Expected values are restated in the oracle's value model:
+  unsigned -> int; float64 -> ("f64", raw bits); dateTime -> DateTime(secs, nanos);
+  strings -> str; octet arrays / u256 -> bytes.
+"""
+import calendar
+import struct
+
+import ngz_oracle as O
+
+
+def _utc(y, mo, d, h, mi, s):
+    return calendar.timegm((y, mo, d, h, mi, s, 0, 0, 0))
+
+
+SMALL = "abcdefghijklmnopqrstuvwxyz"
+LARGE = SMALL * 10  # 260 characters
+SMALL_DATA = bytes(range(26))
+LARGE_DATA = bytes((i % 256) for i in range(260))
+
+KATS = [
+    # mod.rs:77-99 test_u8_value: protocolIdentifier 123 (PTP)
+    ("u8_value", 4, 1, bytes([123]), 123),
+    ("u8_invalid_length", 4, 2, bytes([123]),
+     {"InvalidLength": {"offset": 0, "ie_name": "protocolIdentifier", "length": 2}}),
+    # mod.rs:102-129 test_f64_value: samplingProbability 123.4
+    ("f64_value", 311, 8, bytes([64, 94, 217, 153, 153, 153, 153, 154]),
+     ("f64", struct.unpack(">Q", struct.pack(">d", 123.4))[0])),
+    ("f64_invalid_length", 311, 4, bytes([64, 94, 217, 153, 153, 153, 153, 154]),
+     {"InvalidLength": {"offset": 0, "ie_name": "samplingProbability", "length": 4}}),
+    # mod.rs:223-239 test_milli_value: 2016-11-29T20:05:31.519Z
+    ("milli_value", 152, 8, bytes([0, 0, 1, 88, 177, 177, 56, 255]),
+     O.DateTime(_utc(2016, 11, 29, 20, 5, 31), 519_000_000)),
+    # mod.rs:242-295 test_time_fraction_value: full (leap second at :59), half (rounded), zero
+    ("fraction_full_leap", 154, 8, bytes([0x58, 0x3d, 0xdf, 0xa7, 0xff, 0xff, 0xff, 0xff]),
+     O.DateTime(_utc(2016, 11, 29, 20, 5, 59), 1_000_000_000)),
+    ("fraction_half", 154, 8, bytes([0x58, 0x3d, 0xdf, 0x8b, 0x7f, 0xff, 0xff, 0xff]),
+     O.DateTime(_utc(2016, 11, 29, 20, 5, 31), 499_999_999)),
+    ("fraction_zero", 154, 8, bytes([0x58, 0x3d, 0xdf, 0x8b, 0, 0, 0, 0]),
+     O.DateTime(_utc(2016, 11, 29, 20, 5, 31), 0)),
+] + [
+    # mod.rs:423-509 test_u64_reduced_size_encoding: packetDeltaCount, 1..8 bytes
+    ("u64_reduced_%d" % n, 2, n, bytes([0xff, 0xee, 0xdd, 0xcc, 0xbb, 0xaa, 0x99, 0x88][:n]),
+     int.from_bytes(bytes([0xff, 0xee, 0xdd, 0xcc, 0xbb, 0xaa, 0x99, 0x88][:n]), "big"))
+    for n in range(1, 9)
+] + [
+    # mod.rs:512-552 test_u256_value: full, reduced (left-aligned, zero padded), too long
+    ("u256_full", 515, 32, bytes([0x11] * 32), bytes([0x11] * 32)),
+    ("u256_reduced", 515, 8, bytes([0x11] * 8), bytes([0x11] * 8) + bytes(24)),
+    ("u256_invalid_length", 515, 33, bytes([0x11] * 32),
+     {"InvalidLength": {"offset": 0, "ie_name": "ipv6ExtensionHeadersFull", "length": 33}}),
+    # ipfix.rs:1704-1788 test_string_variable_length: applicationName, u8 / 3-byte length, fixed
+    ("string_vlen_small", 96, 0xFFFF, bytes([26]) + SMALL.encode(), SMALL),
+    ("string_fixed_small", 96, 26, SMALL.encode(), SMALL),
+    ("string_vlen_large", 96, 0xFFFF, bytes([0xff, 0x00, 0x01, 0x04]) + LARGE.encode(), LARGE),
+    ("string_fixed_large", 96, 260, LARGE.encode(), LARGE),
+    # ipfix.rs:1791-1875 test_octet_array_variable_length: paddingOctets
+    ("octets_vlen_small", 210, 0xFFFF, bytes([26]) + SMALL_DATA, SMALL_DATA),
+    ("octets_fixed_small", 210, 26, SMALL_DATA, SMALL_DATA),
+    ("octets_vlen_large", 210, 0xFFFF, bytes([0xff, 0x00, 0x01, 0x04]) + LARGE_DATA, LARGE_DATA),
+    ("octets_fixed_large", 210, 260, LARGE_DATA, LARGE_DATA),
+]

@@ -119,7 +119,15 @@ def check_batch(batch, oracle, check_records=True, max_fail=5):
                 for f, fv in enumerate(allf):
                     fi = slot.fields[f]
                     got = bytes(col(int(gs["slot"]), f)[rec0 + r])
-                    if fi.kind == L.K_STR:
+                    if fi.kind == L.K_VLEN:
+                        # {u64 batch offset, u32 length, u32 0} -> the value's bytes in the input batch
+                        off = int.from_bytes(got[:8], "little")
+                        ln = int.from_bytes(got[8:12], "little")
+                        assert got[12:] == bytes(4), (d, r, f, got.hex())
+                        v = fv.value
+                        exp = v.encode("utf-8") if isinstance(v, str) else bytes(v)
+                        assert batch.input_bytes(off, ln) == exp, (d, r, f, off, ln, exp[:32])
+                    elif fi.kind == L.K_STR:
                         raw = got.split(b"\0", 1)[0]
                         exp = fv.value.encode("utf-8")
                         assert raw == exp, (d, r, f, raw, exp)

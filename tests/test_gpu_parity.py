@@ -294,6 +294,78 @@ def test_record_errors(dev):
     assert codec.template_counts(10) == {400: oc.ipfix_templates[400].processed_count}
 
 
+def vl(b):
+    """RFC 7011 s7 variable-length encoding as the reference reads it:
+    u8 length, or 255 + 3-byte length (generator.rs:1775-1793)."""
+    return (bytes([len(b)]) if len(b) < 255 else b"\xff" + len(b).to_bytes(3, "big")) + b
+
+
+def test_variable_length_fields(dev):
+    """IPFIX variable-length (65535) IEs on the device: strings (UTF-8
+    checked, no NUL truncation), octet arrays, vendor-unknown IEs, the 255
+    escape, fields after a vlen field at per-record offsets, and every
+    UnexpectedEof a record walk can hit."""
+    fields = [(8, 4), (82, 65535), (7, 2), (313, 65535), (152, 8), (4, 1), (1000, 65535, 2011)]
+    t = ipfix_msg([ipfix_set(2, tmpl(500, fields))])
+
+    def rec(name, blob, ms=1_700_000_000_000, ven=b"hw", port=443, proto=6, ip=0x0A000001):
+        return (struct.pack(">I", ip) + vl(name) + struct.pack(">H", port) + vl(blob) + struct.pack(">QB", ms, proto)
+                + vl(ven))
+
+    goods = [rec(("if%d" % i).encode() * (i % 7), bytes(range(i % 64)), ms=1_700_000_000_000 + i,
+                 port=i & 0xFFFF, ven=b"v" * (300 if i % 97 == 0 else i % 13)) for i in range(700)]
+    assert len(b"".join(goods[40:700])) < 65000
+    dgrams = [
+        t,
+        ipfix_msg([ipfix_set(500, b"".join(goods[:40]))]),
+        ipfix_msg([ipfix_set(500, b"".join(goods[40:700]))]),                      # > 256 records: several chunks
+        ipfix_msg([ipfix_set(500, rec("grüße €".encode(), b"", ven=b"") + rec(b"a\0b", b"\x00" * 300))]),
+        ipfix_msg([ipfix_set(500, rec(b"ok", b"x") + b"\0\0\0")]),                  # zero padding after records
+        ipfix_msg([ipfix_set(500, rec(b"ok", b"x") + rec(b"\xc3\x28", b"y"))]),       # invalid utf-8 (vlen: no NUL cut)
+        ipfix_msg([ipfix_set(500, rec(b"ok", b"x") + rec(b"ok", b"y", ms=2**63 + 1))]),  # dt-ms after vlen fields
+        ipfix_msg([ipfix_set(500, rec(b"ok", b"x") + struct.pack(">I", 1) + b"\xc8" + b"n" * 20)]),      # data EOF
+        ipfix_msg([ipfix_set(500, rec(b"ok", b"x") + rec(b"ok", b"y", ven=b"")[:-1] + b"\xff\x00\x01")]),  # escape EOF
+        ipfix_msg([ipfix_set(500, rec(b"ok", b"x") + struct.pack(">I", 1) + vl(b"e" * 14))]),              # u16 EOF
+        ipfix_msg([ipfix_set(500, rec(b"ok", b"x") + struct.pack(">I", 1) + b"\xff\x00\x00\x05abcd" + b"\0" * 8)]),
+        ipfix_msg([ipfix_set(500, rec(b"ok", b"x")), ipfix_set(500, rec(b"ok", b"\x01" * 40)[:-3])]),   # 2nd set EOF
+        ipfix_msg([ipfix_set(500, rec(b"ok", b"x")) + ipfix_set(2, tmpl(501, [(8, 4), (82, 65535)]))]),
+        ipfix_msg([ipfix_set(501, struct.pack(">I", 7) + vl(b"z" * 1000)), ipfix_set(500, rec(b"q", b"r"))]),
+    ]
+    stats, batch, codec, oc = run_both(dgrams)
+    assert stats["unsupported"] == 0
+    assert stats["records"] == 700 + 2 + 1 + 1 + 2
+    assert stats["err"] == 7
+    assert codec.template_counts(10) == {t: oc.ipfix_templates[t].processed_count for t in (500, 501)}
+
+
+def test_reference_field_kats(dev):
+    """The reference's field-level unit vectors (tests/kats.py) through the
+    device: each wrapped as [sourceIPv4Address, field, sourceTransportPort]
+    records of its own template, 3 records per message.  (The InvalidLength
+    vectors call Field::parse directly in the reference; on the wire their
+    templates are already rejected by FieldSpecifier::new, so they are pinned
+    on the oracle only, tests/test_oracle_kat.py.)"""
+    import kats
+    dgrams = []
+    good = [k for k in kats.KATS if not isinstance(k[4], dict)]
+    for i, (name, ie_id, length, wire, _) in enumerate(good):
+        tid = 600 + i
+        recs = b"".join(struct.pack(">I", 0x0A000000 + k) + wire + struct.pack(">H", 1000 + k) for k in range(3))
+        dgrams += [ipfix_msg([ipfix_set(2, tmpl(tid, [(8, 4), (ie_id, length), (7, 2)]))]),
+                   ipfix_msg([ipfix_set(tid, recs)])]
+    stats, *_ = run_both(dgrams)
+    assert stats["err"] == 0 and stats["ok"] == 2 * len(good) and stats["records"] == 3 * len(good)
+
+
+def test_unknown_pen_65535_is_eof(dev):
+    """IE::Unknown (unregistered PEN) with length 65535 is read as 65535 fixed
+    bytes (generator.rs:2971-2974): every record hits UnexpectedEof."""
+    t = ipfix_msg([ipfix_set(2, tmpl(510, [(8, 4), (5, 65535, 213)]))])
+    dgrams = [t, ipfix_msg([ipfix_set(510, struct.pack(">I", 1) + b"abc")])]
+    stats, *_ = run_both(dgrams)
+    assert stats["err"] == 1 and stats["unsupported"] == 0
+
+
 def test_template_errors_and_redefinition(dev):
     rec_a = struct.pack(">IH", 0x0A000001, 80)
     rec_b = struct.pack(">HIB", 443, 0xC0A80001, 6)
