@@ -348,7 +348,10 @@ __device__ __forceinline__ void run_chunks(const BatchDev &B, uint32_t c_begin, 
         P[0].blk = B.arena + sgpr((uint32_t)rt.block) + ((uint64_t)sgpr((uint32_t)(rt.block >> 32)) << 32);
         P[0].cap = sgpr(rt.cap);
         const uint64_t a0 = src & ~3ull;
-        const uint64_t avail64 = B.bytes_size - a0;
+        // buffer range checks are per dword (a dword straddling num_records reads 0),
+        // so round up: the <= 3 bytes past bytes_size share the last valid byte's
+        // 4-byte word, hence its page; those bytes are never used
+        const uint64_t avail64 = (B.bytes_size - a0 + 3) & ~3ull;
         const uint32_t avail = avail64 > 0x7FFFFFF0ull ? 0x7FFFFFF0u : (uint32_t)avail64;
         P[0].rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)(B.bytes + a0), (short)0, (int)avail, 0x00020000);
         P[0].a0 = a0;

@@ -496,7 +496,11 @@ __global__ void __launch_bounds__(256) k_counts(BatchDev B) {
             const uint8_t *p = B.bytes + B.offsets[s.dgram];
             const uint32_t set_len = be16(p + s.set_pos + 2);
             if (pl.proto == 10) {
-                inc = stop >= s.set_pos + set_len ? 1 : 0;
+                // the set's records all parsed (ipfix.rs:219-223); an UnexpectedEof at
+                // exactly the set end (available 0) is this set's failing record
+                const uint32_t code = h.err_key == NGZ_NO_ERR ? 0 : (uint32_t)(h.err_key >> 40) & 0xFF;
+                const uint32_t end = s.set_pos + set_len;
+                inc = (stop > end || (stop == end && code != E_REC_EOF)) ? 1 : 0;
             } else {
                 // records fully parsed before the stop position
                 const uint32_t first = s.set_pos + 4, rl = pl.rec_len;
