@@ -35,6 +35,29 @@ constexpr int64_t kMaxMillis = 8210266876799999LL;   // (days_from_civil(262142,
 
 __device__ __forceinline__ uint32_t sgpr(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// v_readlane as an unsigned value (the builtin returns int: widening it
+// directly to 64 bits would sign-extend)
+__device__ __forceinline__ uint32_t lane_u32(uint32_t v, uint32_t lane) {
+    return (uint32_t)__builtin_amdgcn_readlane(v, lane);
+}
+
+// Wave-uniform load through the scalar cache (s_load_*): the pointer is cast to
+// the constant address space, which is sound for tables no kernel writes while
+// the reader runs (chunk descriptors, slot table, plans).  Scalar loads count
+// on lgkmcnt, so they overlap the vector loads instead of queueing behind them.
+template <class T>
+__device__ __forceinline__ T sload(const T *p) {
+    static_assert(sizeof(T) % 4 == 0, "dword-sized tables only");
+    typedef const __attribute__((address_space(4))) uint32_t *cptr;
+    const cptr q = (cptr)p;
+    uint32_t w[sizeof(T) / 4];
+#pragma unroll
+    for (uint32_t i = 0; i < sizeof(T) / 4; ++i) w[i] = q[i];
+    T out;
+    __builtin_memcpy(&out, w, sizeof(T));
+    return out;
+}
+
 // 4 wire bytes at uniform window byte offset o, as a little-endian dword
 __device__ __forceinline__ uint32_t rdw(const uint32_t (&R)[WIN_DW], uint32_t o) {
     uint32_t q = o >> 2;
@@ -329,24 +352,50 @@ __device__ __forceinline__ void run_chunks(const BatchDev &B, uint32_t c_begin, 
     const uint32_t wpb = blockDim.x >> 6;
     const uint32_t wid = sgpr(blockIdx.x * wpb + (threadIdx.x >> 6));
     const uint32_t nw = gridDim.x * wpb;
-    for (uint32_t ci = c_begin + wid; ci < c_end; ci += nw) {
-        const uint4 *cp = (const uint4 *)&B.chunks[ci];
-        const uint4 c0 = cp[0], c1 = cp[1];
-        const uint32_t n = sgpr(c1.x & 0xFFFF);
-        if (n == 0) continue;  // padding chunk
-        const uint32_t slot = sgpr(c1.x >> 16);
+    uint32_t rt_slot = 0xFFFFFFFFu, cap = 0;
+    uint8_t *blk = nullptr;
+    // Chunk descriptors are fetched 64 at a time, one per lane (lane j holds
+    // the wave's j-th next chunk), and read with v_readlane: one descriptor
+    // round trip per 64 chunks instead of one per chunk.  (vmcnt counts loads
+    // and stores in order, so a per-chunk descriptor load would also wait for
+    // the previous chunk's column stores.)
+    for (uint32_t cb = c_begin + wid; cb < c_end; cb += 64 * nw) {
+        const uint32_t mine = cb + lane * nw;
+        uint4 e0 = make_uint4(0, 0, 0, 0), e1 = make_uint4(0, 0, 0, 0);
+        if (mine < c_end) {
+            e0 = ((const uint4 *)&B.chunks[mine])[0];
+            e1 = ((const uint4 *)&B.chunks[mine])[1];
+        }
+        const uint32_t cnt = min(64u, (c_end - cb + nw - 1) / nw);
+      for (uint32_t j = 0; j < cnt; ++j) {
+        Chunk cur;
+        const uint32_t w1x = lane_u32(e1.x, j);
+        cur.n = (uint16_t)(w1x & 0xFFFF);
+        if (cur.n == 0) continue;  // padding chunk
+        cur.slot = (uint16_t)(w1x >> 16);
+        cur.src = (uint64_t)lane_u32(e0.x, j) | ((uint64_t)lane_u32(e0.y, j) << 32);
+        cur.rec0 = lane_u32(e0.z, j);
+        cur.dgram = lane_u32(e0.w, j);
+        cur.pos0 = (uint16_t)(lane_u32(e1.y, j) & 0xFFFF);
+        const uint32_t n = cur.n;
+        const uint32_t slot = cur.slot;
         if (!want(slot)) continue;
         const RecShape rs = shape(slot);
         const uint32_t rl = rs.rl;
-        const uint64_t src = (uint64_t)sgpr(c0.x) | ((uint64_t)sgpr(c0.y) << 32);
+        const uint64_t src = cur.src;
+        if (slot != rt_slot) {
+            const SlotRT rt = sload(&B.slots[slot]);
+            blk = B.arena + rt.block;
+            cap = rt.cap;
+            rt_slot = slot;
+        }
         Pass P[RPL];
-        P[0].rec0 = sgpr(c0.z);
-        P[0].dgram = sgpr(c0.w);
-        P[0].pos0 = sgpr(c1.y & 0xFFFF);
+        P[0].rec0 = cur.rec0;
+        P[0].dgram = cur.dgram;
+        P[0].pos0 = cur.pos0;
         P[0].hdr = B.hdr;
-        const SlotRT rt = B.slots[slot];
-        P[0].blk = B.arena + sgpr((uint32_t)rt.block) + ((uint64_t)sgpr((uint32_t)(rt.block >> 32)) << 32);
-        P[0].cap = sgpr(rt.cap);
+        P[0].blk = blk;
+        P[0].cap = cap;
         const uint64_t a0 = src & ~3ull;
         // buffer range checks are per dword (a dword straddling num_records reads 0),
         // so round up: the <= 3 bytes past bytes_size share the last valid byte's
@@ -382,6 +431,7 @@ __device__ __forceinline__ void run_chunks(const BatchDev &B, uint32_t c_begin, 
             }
             pass(P);
         }
+      }
     }
 }
 

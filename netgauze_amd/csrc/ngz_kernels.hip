@@ -377,19 +377,19 @@ __global__ void k_emit(BatchDev B, const uint32_t *hf_flag, const uint32_t *hf_f
 // sequences assume it); only lanes whose row belongs to the chunk store.
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_decode_generic(BatchDev B) {
-    if (sgpr(B.summary->overflow)) return;
+    if (sload(&B.summary->overflow)) return;
     const uint32_t lane = threadIdx.x & 63;
     uint32_t cached = 0xFFFFFFFFu, rl = 0, nf = 0, skip = 0, row_bytes = 0, has_vlen = 0;
     uint4 fA = make_uint4(0, 0, 0, 0), fB = make_uint4(0, 0, 0, 0);  // field descriptors f = lane, lane + 64
     auto want = [&](uint32_t slot) {
         if (slot != cached) {
             const DevPlan *pl = &B.plans[slot];
-            const uint4 h0 = ((const uint4 *)pl)[0];
-            rl = sgpr(h0.x);
-            row_bytes = sgpr(h0.y);
-            nf = sgpr(h0.z & 0xFFFF);
-            has_vlen = sgpr((h0.w >> 8) & 0xFF);
-            skip = sgpr((h0.w >> 24) & 0xFF);  // DevPlan::spec: decoded by its own kernel
+            const uint4 h0 = sload((const uint4 *)pl);
+            rl = h0.x;
+            row_bytes = h0.y;
+            nf = h0.z & 0xFFFF;
+            has_vlen = (h0.w >> 8) & 0xFF;
+            skip = (h0.w >> 24) & 0xFF;  // DevPlan::spec: decoded by its own kernel
             const uint4 *ft = (const uint4 *)pl->f;
             fA = lane < nf ? ft[lane] : make_uint4(0, 0, 0, 0);
             fB = lane + 64 < nf ? ft[lane + 64] : make_uint4(0, 0, 0, 0);
@@ -415,8 +415,8 @@ __global__ void __launch_bounds__(256) k_decode_generic(BatchDev B) {
         for (uint32_t f = 0; f < nf; ++f) {
             const uint4 &fs = f < 64 ? fA : fB;
             const uint32_t fl = f & 63;
-            const uint32_t dx = __builtin_amdgcn_readlane(fs.x, fl), dy = __builtin_amdgcn_readlane(fs.y, fl);
-            const uint32_t col_off = __builtin_amdgcn_readlane(fs.z, fl);
+            const uint32_t dx = lane_u32(fs.x, fl), dy = lane_u32(fs.y, fl);
+            const uint32_t col_off = lane_u32(fs.z, fl);
             const uint32_t len = dx >> 16, width = dy & 0xFFFF, kind = (dy >> 16) & 0xFF;
             const uint32_t off = seg + so;  // record offset of the field (per lane after a vlen field)
             if (kind == NGZ_K_FAIL) {
@@ -471,7 +471,7 @@ __global__ void __launch_bounds__(256) k_decode_generic(BatchDev B) {
             so += len;
         }
     };
-    run_chunks<1, false>(B, 0, sgpr(B.summary->n_chunks), want, shape, pass);
+    run_chunks<1, false>(B, 0, sload(&B.summary->n_chunks), want, shape, pass);
 }
 
 __device__ __forceinline__ uint64_t wave_sum(uint64_t v) {

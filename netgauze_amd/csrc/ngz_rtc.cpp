@@ -199,9 +199,9 @@ std::string generate(const DevPlan &P) {
     src += "// generated by ngz_rtc.cpp for plan " + signature(P) + "\n";
     src += "#include \"ngz_dev.h\"\nusing namespace ngzdev;\n";
     src += "extern \"C\" __global__ void __launch_bounds__(256) ngz_tpl(BatchDev B, uint32_t slot) {\n";
-    src += "    if (sgpr(B.summary->overflow)) return;\n";
-    src += "    const SlotRT *rtp = &B.slots[slot];\n";
-    src += "    const uint32_t c0 = sgpr(rtp->chunk0), nc = sgpr(rtp->nchunks);\n";
+    src += "    if (sload(&B.summary->overflow)) return;\n";
+    src += "    const SlotRT rt = sload(&B.slots[slot]);\n";
+    src += "    const uint32_t c0 = rt.chunk0, nc = rt.nchunks;\n";
     src += "    run_chunks<" + RPL + ", " + (consec ? "true" : "false") +
            ">(B, c0, c0 + nc, [](uint32_t) { return true; }, [](uint32_t) { return RecShape{" +
            std::to_string(P.rec_len) + "u, 0u, false}; },\n";
