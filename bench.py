@@ -75,9 +75,10 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--records", type=int, default=100_000_000, help="records per GPU")
-    ap.add_argument("--workload", choices=["t20", "mixed8"], default="t20",
+    ap.add_argument("--workload", choices=["t20", "mixed8", "cfg4"], default="t20",
                     help="t20 (headline): one 20-field 64-B template; mixed8: config 3, 8 reference-shaped "
-                         "templates (40-153 B) in interleaved messages")
+                         "templates (40-153 B) in interleaved messages; cfg4: config 4, NetFlow v9 + IPFIX "
+                         "variable-length/enterprise IEs")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e", action="store_true",
                     help="host-to-host rate instead: pinned host datagrams -> H2D -> decode -> D2H of all columns")
@@ -107,11 +108,16 @@ def main():
         buf, offs, lens = synth.ipfix_data_stream(rec, 64)
         del rec
         rec_bytes = {256: 64}
-    else:
+    elif args.workload == "mixed8":
         codec.decode_datagrams([synth.templates_message(synth.CFG3_TEMPLATES)])
         buf, offs, lens, recs = synth.mixed_stream(n, seed=synth.SEED_CFG3 + 16 * rank, device=dev)
         rec_bytes = {tid: r.shape[1] for tid, r in recs.items()}
         del recs
+    else:
+        dg = synth.cfg4_datagrams(n, seed=synth.SEED_CFG4 + 16 * rank)
+        codec.decode_datagrams(dg[:2])  # the NFv9 and IPFIX templates
+        buf, offs, lens = synth.host_batch(dg[2:], device=dev)
+        rec_bytes = None  # variable: the data bytes of the batch stand in for record bytes
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream(dev).cuda_stream
 
@@ -127,9 +133,11 @@ def main():
         b = step()
     assert b.n_records == n, (b.n_records, n)
     # algorithmic bytes per launch: wire bytes read + canonical column bytes written, per template
-    alg_bytes = sum(s.n_records * (rec_bytes[s.template_id] + sum(f.width for f in s.fields))
-                    for s in b.slots if s.n_records)
-    read_bytes = sum(s.n_records * rec_bytes[s.template_id] for s in b.slots if s.n_records)
+    if rec_bytes is not None:
+        read_bytes = sum(s.n_records * rec_bytes[s.template_id] for s in b.slots if s.n_records)
+    else:
+        read_bytes = int(lens.sum())  # every datagram byte (headers are < 1 %)
+    alg_bytes = read_bytes + sum(s.n_records * sum(f.width for f in s.fields) for s in b.slots if s.n_records)
     dec_ms = []
     if dist is not None:
         dist.barrier()
@@ -153,8 +161,10 @@ def main():
     achieved = alg_bytes / (dec_avg * 1e-3) / 1e9
     traffic = committed_traffic(n) if args.workload == "t20" else None
     out = {
-        "metric": "IPFIX flow records/sec + GB/s (device-resident), 20-field fixed template"
-                  if args.workload == "t20" else "IPFIX flow records/sec (device-resident), config 3: 8 templates",
+        "metric": {"t20": "IPFIX flow records/sec + GB/s (device-resident), 20-field fixed template",
+                   "mixed8": "IPFIX flow records/sec (device-resident), config 3: 8 templates",
+                   "cfg4": "flow records/sec (device-resident), config 4: NetFlow v9 + IPFIX variable-length"}
+                  [args.workload],
         "value": value,
         "unit": "records/s",
         "n_gpus": world,
@@ -165,12 +175,13 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (splitmix64 records, seed 0x4E475A450000000%d+rank, generated in HBM)"
-                % (2 if args.workload == "t20" else 3),
-        "config": {"workload": ("T20 x %d records/GPU, 1023 records per 65,492-byte IPFIX message" % n)
-                   if args.workload == "t20" else
-                   ("config 3: %d records/GPU over templates %s, interleaved messages"
-                    % (n, ",".join(str(t) for t, _ in synth.CFG3_TEMPLATES))),
+        "data": "synthetic (splitmix64 records, seed 0x4E475A450000000%d+rank)"
+                % {"t20": 2, "mixed8": 3, "cfg4": 4}[args.workload],
+        "config": {"workload": {"t20": "T20 x %d records/GPU, 1023 records per 65,492-byte IPFIX message" % n,
+                                "mixed8": "config 3: %d records/GPU over templates %s, interleaved messages"
+                                % (n, ",".join(str(t) for t, _ in synth.CFG3_TEMPLATES)),
+                                "cfg4": "config 4: %d records/GPU, NFv9 template 313 (130 B, 10/packet) + IPFIX "
+                                        "template 900 (vlen strings/octets, VMware/Huawei IEs)" % n}[args.workload],
                    "records_per_gpu": n, "messages_per_gpu": int(offs.numel()),
                    "parallelism": "shard-per-gpu" if world > 1 else "single"},
         "gbps_step": alg_bytes * world * args.steps / elapsed / 1e9,

@@ -209,3 +209,147 @@ def mixed_stream(n, templates=CFG3_TEMPLATES, seed=SEED_CFG3, device="cpu"):
     buf = torch.cat(bufs + [torch.zeros(16, dtype=torch.uint8, device=bufs[0].device)])
     order = torch.argsort(torch.cat(keys))
     return buf, torch.cat(offs)[order], torch.cat(lens)[order], recs
+
+
+# --- config 4: NetFlow v9 + IPFIX variable-length / enterprise IEs ------------
+# NFv9 template 313 exactly as announced in the reference capture
+# assets/pcaps/101-NFv9-CISCO-cust_primitives (130-byte records, reduced sizes).
+NF313 = [(70, 3), (71, 3), (72, 3), (73, 3), (74, 3), (75, 3), (10, 4), (14, 4), (1, 4), (2, 4), (21, 4), (22, 4),
+         (47, 4), (140, 16), (27, 16), (28, 16), (31, 3), (91, 1), (64, 4), (8, 4), (12, 4), (7, 2), (11, 2), (46, 1),
+         (89, 1), (61, 1), (5, 1), (4, 1), (6, 1), (48, 2), (234, 4), (235, 4)]
+# IPFIX template with variable-length strings / octets and enterprise IEs:
+# VMware (PEN 6876) tenantProtocol, vmUuid (string, vlen), vifUuid (octets, vlen);
+# Huawei (PEN 2011) unregistered id 1000 (vendor Unknown, vlen-aware).
+V900 = [(8, 4), (12, 4), (82, 0xFFFF), (7, 2), (11, 2), (4, 1), (1, 8), (2, 8), (96, 0xFFFF),
+        (880, 1, 6876), (951, 0xFFFF, 6876), (960, 0xFFFF, 6876), (1000, 0xFFFF, 2011), (152, 8)]
+V900_ID = 900
+NF313_ID = 313
+SEED_CFG4 = 0x4E475A4500000004
+
+
+def _u64s(n, seed, salt):
+    return splitmix64(torch.arange(n, dtype=torch.int64) * 16 + salt, seed).numpy().view("uint64")
+
+
+def vlen_records(n, fields=V900, seed=SEED_CFG4, max_len=40):
+    """n IPFIX records of a template with variable-length fields (numpy, host).
+    Variable-length values are printable ASCII of 0..max_len bytes (valid
+    UTF-8), written with the 1-byte length prefix, every 97th record's first
+    variable field with the 255 + 3-byte escape.  dateTimeMilliseconds stays in
+    chrono's range.  Returns (flat uint8 bytes, record lengths int64)."""
+    import numpy as np
+    lens = []
+    parts = []
+    for k, f in enumerate(fields):
+        ln = f[1]
+        if ln == 0xFFFF:
+            L = (_u64s(n, seed, k) % (max_len + 1)).astype(np.int64)
+            esc = np.zeros(n, dtype=bool)
+            if k == next(i for i, g in enumerate(fields) if g[1] == 0xFFFF):
+                esc = (np.arange(n) % 97) == 0
+            lens.append(L + np.where(esc, 4, 1))
+            parts.append(("v", L, esc, k))
+        else:
+            lens.append(np.full(n, ln, dtype=np.int64))
+            parts.append(("f", ln, f[0], k))
+    rec_len = np.sum(lens, axis=0)
+    starts = np.zeros(n + 1, dtype=np.int64)
+    starts[1:] = np.cumsum(rec_len)
+    out = np.zeros(int(starts[-1]), dtype=np.uint8)
+    cur = starts[:-1].copy()
+    for kind, a, b, k in parts:
+        if kind == "f":
+            ln, ie = a, b
+            if ie in (152, 153) and ln == 8:
+                v = 1_700_000_000_000 + (np.arange(n, dtype=np.int64) * 7919) % 1_000_000_000
+            else:
+                v = _u64s(n, seed, 100 + k)
+            vb = v.astype(">u8").view(np.uint8).reshape(n, 8)[:, 8 - ln:] if ln <= 8 else None
+            for j in range(ln):
+                out[cur + j] = vb[:, j] if vb is not None else (_u64s(n, seed, 200 + 16 * k + j) & 0xFF)
+            cur += ln
+        else:
+            L, esc = a, b
+            out[cur] = np.where(esc, 255, L).astype(np.uint8)
+            e = np.nonzero(esc)[0]
+            out[cur[e] + 1] = 0
+            out[cur[e] + 2] = (L[e] >> 8).astype(np.uint8)
+            out[cur[e] + 3] = (L[e] & 0xFF).astype(np.uint8)
+            cur += np.where(esc, 4, 1)
+            # printable bytes 'a'..'z' for every value byte
+            total = int(L.sum())
+            if total:
+                rep = np.repeat(cur, L)
+                within = np.arange(total) - np.repeat(np.cumsum(L) - L, L)
+                out[rep + within] = (97 + (rep + within) % 26).astype(np.uint8)
+            cur += L
+    return out, rec_len
+
+
+def _pack_ipfix(flat, rec_len, tid, max_msg=65000, export_time0=1_700_000_000, domain=1):
+    import numpy as np
+    starts = np.zeros(len(rec_len) + 1, dtype=np.int64)
+    starts[1:] = np.cumsum(rec_len)
+    msgs = []
+    i = 0
+    n = len(rec_len)
+    while i < n:
+        j = int(np.searchsorted(starts, starts[i] + max_msg - 20, side="right")) - 1
+        j = max(j, i + 1)
+        body = flat[starts[i]:starts[j]].tobytes()
+        msgs.append(struct.pack(">HHIIIHH", 10, 20 + len(body), export_time0 + len(msgs), i, domain, tid,
+                                4 + len(body)) + body)
+        i = j
+    return msgs
+
+
+def nfv9_template_message(tid=NF313_ID, fields=NF313, unix=1_700_000_000, seq=0, src=1):
+    body = struct.pack(">HH", tid, len(fields)) + b"".join(struct.pack(">HH", i, ln) for i, ln in fields)
+    fs = struct.pack(">HH", 0, 4 + len(body)) + body
+    return struct.pack(">HHIIII", 9, 1, 1000, unix, seq, src) + fs
+
+
+def _pack_nfv9(recs, rec_len, tid, per_msg=10, unix0=1_700_000_000, src=1):
+    """NetFlow v9 export packets of per_msg records in one data flowset,
+    zero-padded to 4 bytes (netflow.rs:225,237-248)."""
+    msgs = []
+    n = recs.shape[0]
+    for m, i in enumerate(range(0, n, per_msg)):
+        k = min(per_msg, n - i)
+        body = recs[i:i + k].tobytes()
+        pad = (-(4 + len(body))) % 4
+        fs = struct.pack(">HH", tid, 4 + len(body) + pad) + body + b"\0" * pad
+        msgs.append(struct.pack(">HHIIII", 9, k, 1000 + m, unix0 + m, i, src) + fs)
+    return msgs
+
+
+def cfg4_datagrams(n, seed=SEED_CFG4):
+    """Config 4: n records, half NetFlow v9 (template 313, 130 B, 10 records
+    per packet as Cisco exporters send), half IPFIX with variable-length and
+    enterprise IEs (template 900), packets interleaved.  The two template
+    packets come first.  Returns a list of datagrams (bytes)."""
+    import numpy as np
+    n_nf = n // 2
+    n_v = n - n_nf
+    _, rl = field_offsets(NF313)
+    nf = template_records(NF313, n_nf, seed, "cpu").numpy()
+    nf_msgs = _pack_nfv9(nf, rl, NF313_ID)
+    flat, lens = vlen_records(n_v, V900, seed + 1)
+    v_msgs = _pack_ipfix(flat, lens, V900_ID)
+    out = [nfv9_template_message(), _ipfix_template_v900()]
+    # interleave proportionally: packet i of a stream of m packets at position i/m
+    keys = [(i / len(nf_msgs), 0, i) for i in range(len(nf_msgs))] + [(i / len(v_msgs), 1, i) for i in range(len(v_msgs))]
+    keys.sort()
+    out += [nf_msgs[i] if s == 0 else v_msgs[i] for _, s, i in keys]
+    return out
+
+
+def _ipfix_template_v900():
+    body = struct.pack(">HH", V900_ID, len(V900))
+    for f in V900:
+        if len(f) == 2:
+            body += struct.pack(">HH", f[0], f[1])
+        else:
+            body += struct.pack(">HHI", f[0] | 0x8000, f[1], f[2])
+    sset = struct.pack(">HH", 2, 4 + len(body)) + body
+    return struct.pack(">HHIII", 10, 16 + len(sset), 1_700_000_000, 0, 1) + sset

@@ -357,6 +357,18 @@ def test_reference_field_kats(dev):
     assert stats["err"] == 0 and stats["ok"] == 2 * len(good) and stats["records"] == 3 * len(good)
 
 
+def test_cfg4_netflow_v9_and_variable_length(dev):
+    """Config 4 shape: NetFlow v9 (the reference capture's template 313, 130 B)
+    interleaved with IPFIX records carrying variable-length strings/octets and
+    VMware / Huawei enterprise IEs, against the oracle."""
+    from netgauze_amd import synth
+    dgrams = synth.cfg4_datagrams(6000)
+    stats, batch, codec, oc = run_both(dgrams)
+    assert stats["records"] == 6000 and stats["err"] == 0 and stats["unsupported"] == 0
+    assert codec.template_counts(10) == {900: oc.ipfix_templates[900].processed_count}
+    assert codec.template_counts(9) == {313: oc.netflow_templates[313].processed_count}
+
+
 def test_unknown_pen_65535_is_eof(dev):
     """IE::Unknown (unregistered PEN) with length 65535 is read as 65535 fixed
     bytes (generator.rs:2971-2974): every record hits UnexpectedEof."""
