@@ -104,9 +104,11 @@ struct Pass {
     uint32_t lane;
     uint32_t rec0;                // first row of the chunk
     uint32_t dgram;               // datagram of the chunk
-    uint32_t recpos;              // this lane's record offset in the datagram
+    uint32_t recpos;              // this lane's record offset in the datagram (~0: row mode, derive from rabs)
     uint32_t pos0;                // chunk's first record offset in the datagram
     uint64_t a0;                  // batch byte offset of the resource base
+    uint64_t rabs;                // row mode: this lane's record batch offset
+    const uint64_t *offsets;      // datagram offsets (row-mode error positions)
     void *hdr;                    // ngz_dgram_hdr[] (errors)
 };
 
@@ -134,23 +136,60 @@ __device__ __forceinline__ void win_load(uint32_t (&R)[WIN_DW], const Pass &P, u
     }
 }
 
-__device__ __forceinline__ void rec_error(const Pass &P, uint32_t pos, uint32_t code, uint32_t f, uint32_t b = 0) {
+// Report a record error at byte `rec_off` of this lane's record (the datagram
+// keeps the smallest key = the first error in parse order).
+__device__ __forceinline__ void rec_error(const Pass &P, uint32_t rec_off, uint32_t code, uint32_t f, uint32_t b = 0) {
+    const uint32_t recpos = P.recpos != 0xFFFFFFFFu ? P.recpos : (uint32_t)(P.rabs - P.offsets[P.dgram]);
     atomicMin((unsigned long long *)&((ngz_dgram_hdr *)P.hdr)[P.dgram].err_key,
-              (unsigned long long)ngz_err_key(pos, code, f, b));
+              (unsigned long long)ngz_err_key(recpos + rec_off, code, f, b));
 }
 
-// Column `col_off` rows [prow, prow+64) start at a uniform address; lanes add
-// a small 32-bit offset (global_store with an SGPR base).
+// Template-constant field failure (InvalidLength etc.): the first record of
+// each set fails there; chunk mode reports it from the chunk's first row,
+// row mode from every row (the smallest position per datagram wins).
+__device__ __forceinline__ void fail_field(const Pass &P, uint32_t rec_off, uint32_t f) {
+    if (P.valid && (P.recpos == 0xFFFFFFFFu || P.row == P.rec0)) rec_error(P, rec_off, E_REC_FAIL, f);
+}
+
+// Column `col_off` rows of a pass start at a uniform address: stores go
+// through a buffer resource built from it in SGPRs, lanes add a small 32-bit
+// offset (lrow*width + byte) -- no per-lane 64-bit column addresses, which
+// would otherwise cost 2 VGPRs per column for the whole chunk loop.
+typedef uint32_t v2u __attribute__((ext_vector_type(2)));
+
 __device__ __forceinline__ uint8_t *pass_col(const Pass &P, uint32_t col_off, uint32_t width) {
     return P.blk + (uint64_t)P.cap * col_off + (uint64_t)P.prow * width;
 }
 
-__device__ __forceinline__ void store_w(uint8_t *pcol, uint32_t lane, uint32_t width, uint64_t v) {
-    if (width == 1) pcol[lane] = (uint8_t)v;
-    else if (width == 2) *(uint16_t *)(pcol + 2 * lane) = (uint16_t)v;
-    else if (width == 4) *(uint32_t *)(pcol + 4 * lane) = (uint32_t)v;
-    else *(uint2 *)(pcol + 8 * lane) = make_uint2((uint32_t)v, (uint32_t)(v >> 32));
-}
+struct ColSt {
+    __amdgpu_buffer_rsrc_t r;
+    __device__ __forceinline__ ColSt(const Pass &P, uint32_t col_off, uint32_t width)
+        : r(__builtin_amdgcn_make_buffer_rsrc(pass_col(P, col_off, width), (short)0, 0x7FFFFFF0, 0x00020000)) {}
+    __device__ __forceinline__ void b8(uint32_t off, uint32_t v) const {
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, r, off, 0, 0);
+    }
+    __device__ __forceinline__ void b16(uint32_t off, uint32_t v) const {
+        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)v, r, off, 0, 0);
+    }
+    __device__ __forceinline__ void b32(uint32_t off, uint32_t v) const {
+        __builtin_amdgcn_raw_buffer_store_b32(v, r, off, 0, 0);
+    }
+    __device__ __forceinline__ void b64(uint32_t off, uint32_t lo, uint32_t hi) const {
+        v2u x = {lo, hi};
+        __builtin_amdgcn_raw_buffer_store_b64(x, r, off, 0, 0);
+    }
+    __device__ __forceinline__ void b128(uint32_t off, uint32_t a, uint32_t b, uint32_t c, uint32_t d) const {
+        v4u x = {a, b, c, d};
+        __builtin_amdgcn_raw_buffer_store_b128(x, r, off, 0, 0);
+    }
+    // one value of `width` bytes (1/2/4/8) at row lrow
+    __device__ __forceinline__ void w(uint32_t lrow, uint32_t width, uint64_t v) const {
+        if (width == 1) b8(lrow, (uint32_t)v);
+        else if (width == 2) b16(2 * lrow, (uint32_t)v);
+        else if (width == 4) b32(4 * lrow, (uint32_t)v);
+        else b64(8 * lrow, (uint32_t)v, (uint32_t)(v >> 32));
+    }
+};
 
 // Value of a numeric field (UINT/SCOPE32/TCPFLAGS/SINT/BOOL/DTMS/DTFRAC) at
 // window offset o, in its column encoding; reports the field's errors.
@@ -166,7 +205,7 @@ __device__ __forceinline__ uint64_t num_value(const uint32_t (&R)[WIN_DW], const
         const double q = (double)frac / 4294967295.0;
         const uint32_t ns = (uint32_t)(1000000000.0 * q);
         // chrono timestamp_opt: ns >= 1e9 only as a leap second (secs % 60 == 59)
-        if (P.valid && ns >= 1000000000u && (secs % 60u) != 59u) rec_error(P, P.recpos + off, E_REC_DTFRAC, f);
+        if (P.valid && ns >= 1000000000u && (secs % 60u) != 59u) rec_error(P, off, E_REC_DTFRAC, f);
         v = (uint64_t)secs | ((uint64_t)ns << 32);
     } else {
         v = rbe(R, o, kind == NGZ_K_DTMS ? 8 : len);
@@ -176,7 +215,7 @@ __device__ __forceinline__ uint64_t num_value(const uint32_t (&R)[WIN_DW], const
             v = (uint64_t)(((int64_t)(v << s2)) >> s2);
         }
         if (P.valid && kind == NGZ_K_DTMS && ((int64_t)v < kMinMillis || (int64_t)v > kMaxMillis))
-            rec_error(P, P.recpos + off, E_REC_DTMS, f);
+            rec_error(P, off, E_REC_DTMS, f);
     }
     return v;
 }
@@ -185,7 +224,7 @@ __device__ __forceinline__ uint64_t num_value(const uint32_t (&R)[WIN_DW], const
 __device__ __forceinline__ void dec_num(const uint32_t (&R)[WIN_DW], const Pass &P, uint32_t o, uint32_t off,
                                         uint32_t f, uint32_t len, uint32_t width, uint32_t kind, uint32_t col_off) {
     const uint64_t v = num_value(R, P, o, off, f, len, kind);
-    if (P.valid) store_w(pass_col(P, col_off, width), P.lrow, width, v);
+    if (P.valid) ColSt(P, col_off, width).w(P.lrow, width, v);
 }
 
 // Numeric field of C consecutive rows per lane (run_chunks<C, true>): the C
@@ -201,39 +240,38 @@ __device__ __forceinline__ void dec_num_c(const uint32_t (&R)[C][WIN_DW], const 
         v[k] = num_value(R[k], P[k], o, off, f, len, kind);
         full = full && P[k].valid;
     }
-    uint8_t *pcol = pass_col(P[0], col_off, width);
+    const ColSt cs(P[0], col_off, width);
     if (full) {
-        uint8_t *dst = pcol + (uint64_t)P[0].lrow * width;  // lrow of record 0 = C*lane
+        const uint32_t at = P[0].lrow * width;  // lrow of record 0 = C*lane
         if (width == 1) {
             uint32_t w = 0;
 #pragma unroll
             for (int k = 0; k < C; ++k) w |= (uint32_t)(v[k] & 0xFF) << (8 * k);
-            if (C == 4) *(uint32_t *)dst = w;
-            else if (C == 2) *(uint16_t *)dst = (uint16_t)w;
-            else *dst = (uint8_t)w;
+            if (C == 4) cs.b32(at, w);
+            else if (C == 2) cs.b16(at, w);
+            else cs.b8(at, w);
         } else if (width == 2) {
             uint32_t w[2] = {0, 0};
 #pragma unroll
             for (int k = 0; k < C; ++k) w[k >> 1] |= (uint32_t)(v[k] & 0xFFFF) << (16 * (k & 1));
-            if (C == 4) *(uint2 *)dst = make_uint2(w[0], w[1]);
-            else if (C == 2) *(uint32_t *)dst = w[0];
-            else *(uint16_t *)dst = (uint16_t)w[0];
+            if (C == 4) cs.b64(at, w[0], w[1]);
+            else if (C == 2) cs.b32(at, w[0]);
+            else cs.b16(at, w[0]);
         } else if (width == 4) {
-            if (C == 4) *(uint4 *)dst = make_uint4((uint32_t)v[0], (uint32_t)v[1 % C], (uint32_t)v[2 % C], (uint32_t)v[3 % C]);
-            else if (C == 2) *(uint2 *)dst = make_uint2((uint32_t)v[0], (uint32_t)v[1 % C]);
-            else *(uint32_t *)dst = (uint32_t)v[0];
+            if (C == 4) cs.b128(at, (uint32_t)v[0], (uint32_t)v[1 % C], (uint32_t)v[2 % C], (uint32_t)v[3 % C]);
+            else if (C == 2) cs.b64(at, (uint32_t)v[0], (uint32_t)v[1 % C]);
+            else cs.b32(at, (uint32_t)v[0]);
         } else {
 #pragma unroll
             for (int k = 0; k + 1 < C; k += 2)
-                *(uint4 *)(dst + 8 * k) = make_uint4((uint32_t)v[k], (uint32_t)(v[k] >> 32), (uint32_t)v[k + 1],
-                                                     (uint32_t)(v[k + 1] >> 32));
-            if (C == 1) *(uint2 *)dst = make_uint2((uint32_t)v[0], (uint32_t)(v[0] >> 32));
+                cs.b128(at + 8 * k, (uint32_t)v[k], (uint32_t)(v[k] >> 32), (uint32_t)v[k + 1], (uint32_t)(v[k + 1] >> 32));
+            if (C == 1) cs.b64(at, (uint32_t)v[0], (uint32_t)(v[0] >> 32));
         }
         return;
     }
 #pragma unroll
     for (int k = 0; k < C; ++k)
-        if (P[k].valid) store_w(pcol, P[k].lrow, width, v[k]);
+        if (P[k].valid) cs.w(P[k].lrow, width, v[k]);
 }
 
 struct WindowBytes {
@@ -279,7 +317,7 @@ __device__ __forceinline__ void check_str(const uint32_t (&R)[WIN_DW], const Pas
     if (!P.valid) return;
     const bool ok = in_window ? utf8_valid_prefix(WindowBytes{R, o}, len)
                               : utf8_valid_prefix(GlobalBytes{P.rsrc, P.rbase + P.sh + off}, len);
-    if (!ok) rec_error(P, P.recpos + off, E_REC_UTF8, f);
+    if (!ok) rec_error(P, off, E_REC_UTF8, f);
 }
 
 // Copy `piece` (<= 64) raw wire bytes at window offset o to column bytes
@@ -288,17 +326,17 @@ __device__ __forceinline__ void check_str(const uint32_t (&R)[WIN_DW], const Pas
 __device__ __forceinline__ void dec_raw(const uint32_t (&R)[WIN_DW], const Pass &P, uint32_t o, uint32_t j,
                                         uint32_t piece, uint32_t width, uint32_t col_off, uint32_t pad_to) {
     if (!P.valid) return;
-    uint8_t *dst = pass_col(P, col_off, width) + P.lrow * width + j;
+    const ColSt cs(P, col_off, width);
+    const uint32_t at = P.lrow * width + j;
     const bool dw = (width & 3) == 0 && (j & 3) == 0;
     uint32_t t = 0;
     if (dw && (width & 15) == 0 && (j & 15) == 0) {
-        for (; t + 16 <= piece; t += 16)
-            *(uint4 *)(dst + t) = make_uint4(rdw(R, o + t), rdw(R, o + t + 4), rdw(R, o + t + 8), rdw(R, o + t + 12));
+        for (; t + 16 <= piece; t += 16) cs.b128(at + t, rdw(R, o + t), rdw(R, o + t + 4), rdw(R, o + t + 8), rdw(R, o + t + 12));
     }
     if (dw)
-        for (; t + 4 <= piece; t += 4) *(uint32_t *)(dst + t) = rdw(R, o + t);
-    for (; t < piece; ++t) dst[t] = (uint8_t)rbyte(R, o + t);
-    for (uint32_t z = j + piece; z < pad_to; ++z) dst[z - j] = 0;
+        for (; t + 4 <= piece; t += 4) cs.b32(at + t, rdw(R, o + t));
+    for (; t < piece; ++t) cs.b8(at + t, rbyte(R, o + t));
+    for (uint32_t z = j + piece; z < pad_to; ++z) cs.b8(at + z - j, 0);
 }
 
 // Raw field of C consecutive rows per lane (run_chunks<C, true>), whole field
@@ -313,7 +351,8 @@ __device__ __forceinline__ void dec_raw_c(const uint32_t (&R)[C][WIN_DW], const 
 #pragma unroll
     for (int k = 0; k < C; ++k) full = full && P[k].valid;
     if (full && C == 4 && width <= 16) {
-        uint8_t *dst = pass_col(P[0], col_off, width) + (uint64_t)P[0].lrow * width;
+        const ColSt cs(P[0], col_off, width);
+        const uint32_t at = P[0].lrow * width;
         // dword m of the lane's 4*width bytes: byte i comes from record (4m+i)/width,
         // field byte (4m+i)%width -- constants once width is
         for (uint32_t m = 0; m < width; ++m) {
@@ -323,7 +362,7 @@ __device__ __forceinline__ void dec_raw_c(const uint32_t (&R)[C][WIN_DW], const 
                 const uint32_t b = 4 * m + i;
                 w |= rbyte(R[b / width], o + b % width) << (8 * i);
             }
-            *(uint32_t *)(dst + 4 * m) = w;
+            cs.b32(at + 4 * m, w);
         }
         return;
     }
@@ -404,8 +443,9 @@ __device__ __forceinline__ void run_chunks(const BatchDev &B, uint32_t c_begin, 
         const uint32_t avail = avail64 > 0x7FFFFFF0ull ? 0x7FFFFFF0u : (uint32_t)avail64;
         P[0].rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)(B.bytes + a0), (short)0, (int)avail, 0x00020000);
         P[0].a0 = a0;
+        P[0].rabs = 0;
+        P[0].offsets = B.offsets;
         P[0].lane = lane;
-        const uint32_t *ro = rs.vlen ? (const uint32_t *)(P[0].blk + (uint64_t)P[0].cap * rs.row_bytes) : nullptr;
 #pragma unroll
         for (int k = 1; k < RPL; ++k) P[k] = P[0];
         const uint32_t rec0 = P[0].rec0;
@@ -421,8 +461,7 @@ __device__ __forceinline__ void run_chunks(const BatchDev &B, uint32_t c_begin, 
                 Q.row = Q.prow + Q.lrow;
                 Q.valid = Q.row >= rec0 && Q.row < rec0 + n;
                 const uint32_t r = Q.valid ? Q.row - rec0 : 0;
-                // record offset from the chunk's first record
-                const uint32_t d = ro ? (Q.valid ? ro[Q.row] : P[0].pos0) - P[0].pos0 : r * rl;
+                const uint32_t d = r * rl;  // record offset from the chunk's first record
                 const uint32_t rel = d + (uint32_t)(src & 3);
                 Q.rbase = rel & ~3u;
                 Q.sh = rel & 3u;
@@ -432,6 +471,128 @@ __device__ __forceinline__ void run_chunks(const BatchDev &B, uint32_t c_begin, 
             pass(P);
         }
       }
+    }
+}
+
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        const uint64_t o = __shfl_xor(v, m, 64);
+        v = o < v ? o : v;
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        const uint64_t o = __shfl_xor(v, m, 64);
+        v = o > v ? o : v;
+    }
+    return v;
+}
+
+// Row mode: walk the slot's output in windows of NGZ_REG_WINDOW rows (wave
+// strided), groups of 64*RPL rows as in run_chunks, every row's record found
+// through rowsrc/rowdg (k_emit).  A group's records are read through one
+// buffer resource based at their smallest address; a group whose records
+// span more than the 31-bit offset range (only with far-apart datagram
+// offsets) is decoded one record at a time.
+template <int RPL, bool CONSEC, class Shape, class PassFn>
+__device__ __forceinline__ void run_windows(const BatchDev &B, uint32_t slot, Shape &&shape, PassFn &&pass) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wpb = blockDim.x >> 6;
+    const uint32_t wid = sgpr(blockIdx.x * wpb + (threadIdx.x >> 6));
+    const uint32_t nw = gridDim.x * wpb;
+    const SlotRT rt = sload(&B.slots[slot]);
+    const uint32_t total = rt.total;
+    const uint64_t *rs = (const uint64_t *)(B.arena + rt.rows);
+    const uint32_t *rd = (const uint32_t *)(B.arena + rt.rows + 8ull * rt.cap);
+    const RecShape shp = shape(slot);
+    (void)shp;
+    Pass P[RPL];
+    P[0].blk = B.arena + rt.block;
+    P[0].cap = rt.cap;
+    P[0].hdr = B.hdr;
+    P[0].offsets = B.offsets;
+    P[0].lane = lane;
+    P[0].recpos = 0xFFFFFFFFu;
+    P[0].pos0 = 0;
+    P[0].dgram = 0;
+#pragma unroll
+    for (int k = 1; k < RPL; ++k) P[k] = P[0];
+    const uint32_t nwin = (total + NGZ_REG_WINDOW - 1) / NGZ_REG_WINDOW;
+    for (uint32_t w = wid; w < nwin; w += nw) {
+        for (uint32_t p = 0; p < NGZ_REG_WINDOW; p += 64 * RPL) {
+            const uint32_t pr0 = w * NGZ_REG_WINDOW + p;
+            if (pr0 >= total) break;
+            uint64_t src[RPL];
+            uint64_t lo = ~0ull, hi = 0;
+#pragma unroll
+            for (int k = 0; k < RPL; ++k) {
+                Pass &Q = P[k];
+                Q.prow = CONSEC ? pr0 : pr0 + 64 * k;
+                Q.lrow = CONSEC ? RPL * lane + k : lane;
+                Q.row = Q.prow + Q.lrow;
+                Q.rec0 = pr0;
+                Q.valid = Q.row < total;
+                src[k] = Q.valid ? rs[Q.row] : 0;
+                Q.dgram = Q.valid ? rd[Q.row] : 0;
+                Q.rabs = src[k];
+                if (Q.valid) {
+                    lo = src[k] < lo ? src[k] : lo;
+                    hi = src[k] > hi ? src[k] : hi;
+                }
+            }
+            const uint64_t base = wave_min_u64(lo) & ~3ull;
+            const uint64_t top = wave_max_u64(hi);
+            if (top - base < 0x7FFF0000ull) {
+                const uint64_t avail64 = (B.bytes_size - base + 3) & ~3ull;
+                const uint32_t avail = avail64 > 0x7FFFFFF0ull ? 0x7FFFFFF0u : (uint32_t)avail64;
+                const __amdgpu_buffer_rsrc_t r =
+                    __builtin_amdgcn_make_buffer_rsrc((void *)(B.bytes + base), (short)0, (int)avail, 0x00020000);
+#pragma unroll
+                for (int k = 0; k < RPL; ++k) {
+                    Pass &Q = P[k];
+                    const uint32_t rel = Q.valid ? (uint32_t)(src[k] - base) : 0;
+                    Q.rsrc = r;
+                    Q.a0 = base;
+                    Q.rbase = rel & ~3u;
+                    Q.sh = rel & 3u;
+                    Q.any_sh = __builtin_amdgcn_ballot_w64(Q.sh != 0) != 0;
+                }
+                pass(P);
+            } else {
+                // records too far apart for one resource: one record per pass
+                bool keep[RPL];
+#pragma unroll
+                for (int k = 0; k < RPL; ++k) keep[k] = P[k].valid;
+                for (uint32_t L = 0; L < 64; ++L) {
+#pragma unroll
+                    for (int k0 = 0; k0 < RPL; ++k0) {
+                        if (!__builtin_amdgcn_readlane((int)keep[k0], L)) continue;
+                        const uint64_t b1 = ((uint64_t)lane_u32((uint32_t)src[k0], L) |
+                                             ((uint64_t)lane_u32((uint32_t)(src[k0] >> 32), L) << 32)) & ~3ull;
+                        const uint64_t avail64 = (B.bytes_size - b1 + 3) & ~3ull;
+                        const uint32_t avail = avail64 > 0x7FFFFFF0ull ? 0x7FFFFFF0u : (uint32_t)avail64;
+                        const __amdgpu_buffer_rsrc_t r =
+                            __builtin_amdgcn_make_buffer_rsrc((void *)(B.bytes + b1), (short)0, (int)avail, 0x00020000);
+#pragma unroll
+                        for (int k = 0; k < RPL; ++k) {
+                            Pass &Q = P[k];
+                            Q.valid = k == k0 && lane == L && keep[k];
+                            const uint32_t rel = Q.valid ? (uint32_t)(src[k] - b1) : 0;
+                            Q.rsrc = r;
+                            Q.a0 = b1;
+                            Q.rbase = rel & ~3u;
+                            Q.sh = rel & 3u;
+                            Q.any_sh = __builtin_amdgcn_ballot_w64(Q.sh != 0) != 0;
+                        }
+                        pass(P);
+                    }
+                }
+            }
+        }
     }
 }
 

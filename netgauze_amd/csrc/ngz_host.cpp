@@ -831,7 +831,8 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
     uint32_t maxwin_row = 0;
     for (uint32_t s = 0; s < S; ++s) {
         const DevPlan &P = ctx->versions[ctx->slot_version[s]].plan;
-        if (P.rec_len) ratio = std::max(ratio, (double)P.row_bytes / (double)P.rec_len);
+        // columns + row-mode record table (12 B/row) per wire byte
+        if (P.rec_len) ratio = std::max(ratio, (double)(P.row_bytes + 12) / (double)P.rec_len);
         maxwin_row = std::max<uint32_t>(maxwin_row, P.window * P.row_bytes);
     }
     uint64_t arena_cap = (uint64_t)(ratio * (double)in->bytes_size) + (uint64_t)S * (maxwin_row + 256) + 4096;
@@ -918,12 +919,14 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
     bool generic = false;
     HIPCHK(hipEventRecord(ctx->ev[1], st));
     for (uint32_t s = 0; s < S; ++s) {
-        if (!ctx->h_slots[s].nchunks) continue;
+        const SlotRT &rt = ctx->h_slots[s];
+        if (!rt.total || (rt.mode == NGZ_MODE_CHUNK && !rt.nchunks)) continue;
         const Version &v = ctx->versions[ctx->slot_version[s]];
         if (!v.plan.rpl) continue;
         if (ctx->specialize && v.rtc_state == 1 && !v.plan.has_vlen) {
             // one specialised kernel per active template, over that slot's chunks only
-            const uint32_t g = std::min<uint32_t>(grid, (ctx->h_slots[s].nchunks + 3) / 4);
+            const uint32_t units = rt.mode == NGZ_MODE_ROW ? (rt.total + NGZ_REG_WINDOW - 1) / NGZ_REG_WINDOW : rt.nchunks;
+            const uint32_t g = std::min<uint32_t>(grid, (units + 3) / 4);
             if (ngz_rtc_launch(v.rtc_fn, &B, s, g, st)) return fail(ctx, NGZ_E_DEVICE, "specialised decode launch");
         } else {
             generic = true;

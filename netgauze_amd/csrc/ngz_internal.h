@@ -133,9 +133,21 @@ struct SlotRT {          // per batch slot, computed on device by k_layout
     uint32_t total;      // rows used
     uint32_t base;       // first element of the slot's row in the scanned count matrix
     uint32_t chunk0;     // first chunk of the slot (chunks are slot-major)
-    uint32_t nchunks;    // chunks of the slot (incl. empty padding chunks)
+    uint32_t nchunks;    // chunks of the slot (incl. empty padding chunks); 0 in row mode
     uint32_t chunk_scan0;  // scanned count at the slot's first chunk cell (k_emit cursor base)
+    uint32_t mode;       // NGZ_MODE_*
+    uint32_t reserved;
+    uint64_t rows;       // row mode: arena offset of u64 rowsrc[cap] (batch offset of each record),
+                         // followed by u32 rowdg[cap] (its datagram)
 };
+
+// Decode work of a slot: chunk mode walks set-relative chunks of <= 256 rows
+// (large sets: records of a chunk are contiguous); row mode walks 256-row
+// windows of the slot's output with a per-row source address, so small sets
+// (MTU-sized IPFIX, NetFlow v9 packets of ~10 records) and variable-length
+// records still fill every lane.
+#define NGZ_MODE_CHUNK 0u
+#define NGZ_MODE_ROW 1u
 
 struct Chunk {           // 32 B, one wave of work
     uint64_t src;        // batch byte offset of the first record

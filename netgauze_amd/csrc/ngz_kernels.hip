@@ -265,9 +265,16 @@ __global__ void k_layout(BatchDev B) {
         rt.chunk0 = B.scan[(uint64_t)(S + s) * N] - chunk_base;
         rt.nchunks = B.scan[(uint64_t)(S + s + 1) * N] - B.scan[(uint64_t)(S + s) * N];
         rt.chunk_scan0 = B.scan[(uint64_t)(S + s) * N];
+        // row mode for variable-length records and for sets so small that
+        // set-relative chunks would leave most lanes idle (< 25 % of rows used)
+        rt.mode = (B.plans[s].has_vlen || 4ull * total < (uint64_t)rt.nchunks * w) ? NGZ_MODE_ROW : NGZ_MODE_CHUNK;
+        rt.reserved = 0;
+        const uint64_t col_bytes = ((uint64_t)cap * B.plans[s].row_bytes + 7) & ~7ull;
+        rt.rows = rt.mode == NGZ_MODE_ROW ? off + col_bytes : 0;
+        if (rt.mode == NGZ_MODE_ROW) rt.nchunks = 0;
         B.slots[s] = rt;
-        const uint64_t rec_off_bytes = B.plans[s].has_vlen ? 4ull * cap : 0;  // vlen: record offsets
-        off += ((uint64_t)cap * B.plans[s].row_bytes + rec_off_bytes + 255) & ~255ull;
+        const uint64_t row_bytes_extra = rt.mode == NGZ_MODE_ROW ? 12ull * cap : 0;  // rowsrc + rowdg
+        off += (col_bytes + row_bytes_extra + 255) & ~255ull;
     }
     const uint32_t rec_total = chunk_base;
     const uint32_t chunks = B.scan[(uint64_t)(2 * S) * N] - chunk_base;
@@ -289,17 +296,20 @@ struct EmitVis {
     uint64_t dg_off;
     uint32_t set_at;
     bool ok;
-    // variable-length records: their datagram offsets go to the slot's
-    // record-offset array (after its columns), rows rec0.. of this set
-    __device__ uint32_t *recoff(uint32_t slot) const {
-        const SlotRT &rt = B->slots[slot];
-        return (uint32_t *)(B->arena + rt.block + (uint64_t)rt.cap * B->plans[slot].row_bytes);
+    // row mode: every record's batch offset and datagram, rows rec0.. of this set
+    __device__ uint64_t *rowsrc(uint32_t slot) const { return (uint64_t *)(B->arena + B->slots[slot].rows); }
+    __device__ uint32_t *rowdg(uint32_t slot) const {
+        return (uint32_t *)(B->arena + B->slots[slot].rows + 8ull * B->slots[slot].cap);
     }
     __device__ uint32_t vlen(const uint8_t *p, uint32_t pos, uint32_t end, uint32_t slot, const DevPlan &pl,
                              uint64_t *err) {
         const uint32_t rec0 = B->scan[(uint64_t)slot * B->n + d] - B->slots[slot].base;
-        uint32_t *ro = recoff(slot) + rec0;
-        return ngz_vlen_walk(p, pos, end, pl, err, [&](uint32_t k, uint32_t at) { ro[k] = at; });
+        uint64_t *rs = rowsrc(slot) + rec0;
+        uint32_t *rd = rowdg(slot) + rec0;
+        return ngz_vlen_walk(p, pos, end, pl, err, [&](uint32_t k, uint32_t at) {
+            rs[k] = dg_off + at;
+            rd[k] = d;
+        });
     }
     __device__ void on_set(uint32_t set_pos, uint32_t slot, uint32_t n, uint32_t payload_pos, uint32_t rl) {
         const uint64_t N = B->n;
@@ -315,6 +325,16 @@ struct EmitVis {
         si.n = n;
         ((ngz_set_info *)B->sets)[set_at++] = si;
         if (!n) return;
+        if (B->slots[slot].mode == NGZ_MODE_ROW) {
+            if (B->plans[slot].has_vlen) return;  // the walk (vlen) wrote the rows
+            uint64_t *rs = rowsrc(slot) + rec0;
+            uint32_t *rd = rowdg(slot) + rec0;
+            for (uint32_t k = 0; k < n; ++k) {
+                rs[k] = dg_off + payload_pos + (uint64_t)k * rl;
+                rd[k] = d;
+            }
+            return;
+        }
         const uint32_t W = B->plans[slot].window;
         const uint32_t reserved = (n + W - 1) / W + 1;
         // this slot's chunk cursor; the scan row's own first cell is another
@@ -322,13 +342,12 @@ struct EmitVis {
         uint32_t *ccell = &B->scan[(uint64_t)(B->n_slots + slot) * N + d];
         const uint32_t chunk_at = *ccell - B->slots[slot].chunk_scan0 + B->slots[slot].chunk0;
         *ccell += reserved;
-        const uint32_t *ro = B->plans[slot].has_vlen ? recoff(slot) : nullptr;
         uint32_t r = 0, used = 0;
         while (r < n) {
             const uint32_t cstart = rec0 + r;
             const uint32_t wend = (cstart / W + 1) * W;
             const uint32_t take = min(n - r, wend - cstart);
-            const uint32_t at = ro ? ro[cstart] : payload_pos + r * rl;  // first record's offset in the datagram
+            const uint32_t at = payload_pos + r * rl;  // first record's offset in the datagram
             Chunk c;
             c.src = dg_off + at;
             c.rec0 = cstart;
@@ -422,7 +441,7 @@ __global__ void __launch_bounds__(256) k_decode_generic(BatchDev B) {
             if (kind == NGZ_K_FAIL) {
                 // template-constant failure: only the chunk's first record matters
                 // (vlen templates never get here: the framing walk stops at it)
-                if (P.valid && P.row == P.rec0) rec_error(P, P.pos0 + off, E_REC_FAIL, f);
+                fail_field(P0, off, f);
                 so += len;
                 continue;
             }
@@ -436,11 +455,10 @@ __global__ void __launch_bounds__(256) k_decode_generic(BatchDev B) {
                 }
                 const uint32_t data = off + hdr;  // record offset of the value
                 if (P.valid) {
-                    uint8_t *dst = pass_col(P, col_off, 16) + P.lrow * 16;
                     const uint64_t at = P0.a0 + rel0 + data;
-                    *(uint4 *)dst = make_uint4((uint32_t)at, (uint32_t)(at >> 32), L, 0);
+                    ColSt(P, col_off, 16).b128(P.lrow * 16, (uint32_t)at, (uint32_t)(at >> 32), L, 0);
                     if ((dy >> 31) && !utf8_valid_prefix(GlobalBytes{P.rsrc, rel0 + data}, L, false))  // vlen string
-                        rec_error(P, P0.recpos + data, E_REC_UTF8, f, L);
+                        rec_error(P0, data, E_REC_UTF8, f, L);
                 }
                 seg = data + L;  // the next segment starts after the value
                 so = 0;
@@ -471,7 +489,16 @@ __global__ void __launch_bounds__(256) k_decode_generic(BatchDev B) {
             so += len;
         }
     };
-    run_chunks<1, false>(B, 0, sload(&B.summary->n_chunks), want, shape, pass);
+    // slot by slot: chunk-mode slots through their chunk range, row-mode
+    // slots through their row windows (specialised slots are skipped by want)
+    for (uint32_t s = 0; s < B.n_slots; ++s) {
+        const SlotRT rt = sload(&B.slots[s]);
+        if (rt.total == 0 || !want(s)) continue;
+        if (rt.mode == NGZ_MODE_ROW)
+            run_windows<1, false>(B, s, shape, pass);
+        else
+            run_chunks<1, false>(B, rt.chunk0, rt.chunk0 + rt.nchunks, want, shape, pass);
+    }
 }
 
 __device__ __forceinline__ uint64_t wave_sum(uint64_t v) {

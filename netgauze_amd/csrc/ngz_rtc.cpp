@@ -121,12 +121,18 @@ std::string generate(const DevPlan &P) {
     // Rows per lane and their layout (NGZ_RTC_LAYOUT overrides for experiments):
     // "c4"/"c2" = 4/2 consecutive rows per lane, numeric columns packed into
     // one wide store per lane; "r1"/"r2"/"r4" = 1/2/4 rows per lane, 64 apart.
+    // Default by record length (measured, profiles/): records that fit one
+    // 76-byte register window pack 4 consecutive rows per lane; longer ones
+    // would hold 4 records x several windows of VGPRs, so they take one row
+    // per lane (or 2 consecutive rows up to 152 B with NGZ_RTC_LONG=c2).
     int rpl = 4;
     bool consec = true;
-    if (const char *e = getenv("NGZ_RTC_LAYOUT")) {
-        if (e[0] == 'c' || e[0] == 'r') {
-            consec = e[0] == 'c';
-            rpl = atoi(e + 1);
+    const char *layout = getenv("NGZ_RTC_LAYOUT");
+    if (!layout && P.rec_len > 76) layout = getenv("NGZ_RTC_LONG") ? getenv("NGZ_RTC_LONG") : "r1";
+    if (layout) {
+        if (layout[0] == 'c' || layout[0] == 'r') {
+            consec = layout[0] == 'c';
+            rpl = atoi(layout + 1);
         }
         if (rpl != 1 && rpl != 2 && rpl != 4) rpl = 4;
     }
@@ -152,9 +158,7 @@ std::string generate(const DevPlan &P) {
                      it.f, it.len);
             break;
         case 4:
-            snprintf(b, sizeof b,
-                     "        if (%s.valid && %s.row == %s.rec0) rec_error(%s, %s.pos0 + %uu, E_REC_FAIL, %uu);\n",
-                     P.c_str(), P.c_str(), P.c_str(), P.c_str(), P.c_str(), it.off, it.f);
+            snprintf(b, sizeof b, "        fail_field(%s, %uu, %uu);\n", P.c_str(), it.off, it.f);
             break;
         }
         body += b;
@@ -202,13 +206,14 @@ std::string generate(const DevPlan &P) {
     src += "    if (sload(&B.summary->overflow)) return;\n";
     src += "    const SlotRT rt = sload(&B.slots[slot]);\n";
     src += "    const uint32_t c0 = rt.chunk0, nc = rt.nchunks;\n";
-    src += "    run_chunks<" + RPL + ", " + (consec ? "true" : "false") +
-           ">(B, c0, c0 + nc, [](uint32_t) { return true; }, [](uint32_t) { return RecShape{" +
-           std::to_string(P.rec_len) + "u, 0u, false}; },\n";
-    src += "               [&](const Pass (&P)[" + RPL + "]) {\n";
+    const std::string L = RPL + ", " + (consec ? "true" : "false");
+    src += "    auto shape = [](uint32_t) { return RecShape{" + std::to_string(P.rec_len) + "u, 0u, false}; };\n";
+    src += "    auto pass = [&](const Pass (&P)[" + RPL + "]) {\n";
     src += "        uint32_t R[" + RPL + "][WIN_DW];\n";
     src += body;
-    src += "    });\n}\n";
+    src += "    };\n";
+    src += "    if (rt.mode == NGZ_MODE_ROW) run_windows<" + L + ">(B, slot, shape, pass);\n";
+    src += "    else run_chunks<" + L + ">(B, c0, c0 + nc, [](uint32_t) { return true; }, shape, pass);\n}\n";
     return src;
 }
 

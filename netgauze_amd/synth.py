@@ -323,11 +323,12 @@ def _pack_nfv9(recs, rec_len, tid, per_msg=10, unix0=1_700_000_000, src=1):
     return msgs
 
 
-def cfg4_datagrams(n, seed=SEED_CFG4):
+def cfg4_datagrams(n, seed=SEED_CFG4, ipfix_msg_bytes=1400):
     """Config 4: n records, half NetFlow v9 (template 313, 130 B, 10 records
     per packet as Cisco exporters send), half IPFIX with variable-length and
-    enterprise IEs (template 900), packets interleaved.  The two template
-    packets come first.  Returns a list of datagrams (bytes)."""
+    enterprise IEs (template 900) in MTU-sized messages (~1400 B, ~15
+    records), packets interleaved.  The two template packets come first.
+    Returns a list of datagrams (bytes)."""
     import numpy as np
     n_nf = n // 2
     n_v = n - n_nf
@@ -335,7 +336,7 @@ def cfg4_datagrams(n, seed=SEED_CFG4):
     nf = template_records(NF313, n_nf, seed, "cpu").numpy()
     nf_msgs = _pack_nfv9(nf, rl, NF313_ID)
     flat, lens = vlen_records(n_v, V900, seed + 1)
-    v_msgs = _pack_ipfix(flat, lens, V900_ID)
+    v_msgs = _pack_ipfix(flat, lens, V900_ID, max_msg=ipfix_msg_bytes)
     out = [nfv9_template_message(), _ipfix_template_v900()]
     # interleave proportionally: packet i of a stream of m packets at position i/m
     keys = [(i / len(nf_msgs), 0, i) for i in range(len(nf_msgs))] + [(i / len(v_msgs), 1, i) for i in range(len(v_msgs))]
