@@ -182,6 +182,15 @@ int ngz_template_counts(ngz_ctx *ctx, int proto, uint16_t *ids, uint64_t *counts
  * decode kernel and of the whole device pipeline (HIP events). */
 int ngz_last_timing(ngz_ctx *ctx, float *decode_ms, float *pipeline_ms);
 
+/* Introspection (no device needed): the per-template decode kernel for one
+ * IPFIX template record (template id u16, field count u16, field specifiers;
+ * the body of a template set entry, ipfix.rs:384-413).  Writes the generated
+ * HIP source to buf (NUL-terminated, truncated to cap) and, with compile != 0,
+ * compiles it for gfx950 with hiprtc (the build log follows the source on
+ * failure).  Returns 0 on success, NGZ_E_INVALID if the template does not
+ * parse or is not device-decodable, NGZ_E_DEVICE if compilation failed. */
+int ngz_template_kernel(const uint8_t *tmpl, size_t len, int compile, char *buf, size_t cap);
+
 #ifdef __cplusplus
 }
 #endif

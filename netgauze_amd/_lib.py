@@ -20,6 +20,7 @@ ABI_FUNCTIONS = [
     "ngz_ctx_create", "ngz_ctx_destroy", "ngz_last_error", "ngz_decode_batch",
     "ngz_decode_batch_host", "ngz_slot_fields", "ngz_dgram_error_json",
     "ngz_templates_json", "ngz_template_counts", "ngz_last_timing", "ngz_ctx_set_option",
+    "ngz_template_kernel",
 ]
 
 

@@ -100,6 +100,7 @@ struct Pass {
     bool valid;                   // this lane's row belongs to the chunk
     uint32_t row;                 // this lane's output row
     uint32_t prow;                // first row of the pass (uniform; row = prow + lrow)
+    uint32_t wrow;                // LDS-staged kernels: prow relative to the workgroup window (uniform)
     uint32_t lrow;                // this lane's row within the pass
     uint32_t lane;
     uint32_t rec0;                // first row of the chunk
@@ -113,24 +114,44 @@ struct Pass {
 };
 
 // Load record dwords [wb/4, wb/4 + ND) of this lane's record into R[0, ND)
-// (ND <= WIN_DW - 1): ceil(ND/4) 16-byte loads, plus one dword when some
-// lane's record is not dword-aligned and the last load has no spare dword.
+// (ND <= WIN_DW - 1).  Every load is a 16-byte aligned buffer_load_dwordx4
+// (the resource base is 16-byte aligned): misaligned 16-byte loads cost ~11 %
+// of HBM throughput on gfx950 (tools/hbm_probe2.hip).  The lane's window
+// starts dsh = 0..3 dwords into its first aligned block, so ceil((ND+3)/4)
+// blocks cover it (plus one dword when some lane's record is not
+// dword-aligned and the last block has no spare dword); two v_bfi steps per
+// dword shift the blocks down by dsh (per lane), then v_alignbyte by the
+// record's byte misalignment sh when any lane has one.
 template <int ND>
 __device__ __forceinline__ void win_load(uint32_t (&R)[WIN_DW], const Pass &P, uint32_t wb) {
-    constexpr int NB = (ND + 3) / 4;
+    constexpr int NB = (ND + 3 + 3) / 4;
+    constexpr int NT = 4 * NB + 1;
+    const uint32_t o = P.rbase + wb;  // dword aligned
+    const uint32_t o16 = o & ~15u;
+    uint32_t T[NT];
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
-        const v4u v = __builtin_amdgcn_raw_buffer_load_b128(P.rsrc, P.rbase + wb + 16 * i, 0, 0);
-        R[4 * i] = v[0];
-        R[4 * i + 1] = v[1];
-        R[4 * i + 2] = v[2];
-        R[4 * i + 3] = v[3];
+        const v4u v = __builtin_amdgcn_raw_buffer_load_b128(P.rsrc, o16 + 16 * i, 0, 0);
+        T[4 * i] = v[0];
+        T[4 * i + 1] = v[1];
+        T[4 * i + 2] = v[2];
+        T[4 * i + 3] = v[3];
     }
+    T[NT - 1] = 0;
+    // the byte shift reads dword ND; with dsh = 3 it is block dword ND + 3
+    if (P.any_sh && ND + 3 >= 4 * NB) T[NT - 1] = __builtin_amdgcn_raw_buffer_load_b32(P.rsrc, o16 + 16 * NB, 0, 0);
+    // per-lane dword shift by dsh (bitwise selects: a ternary on array
+    // elements would become a dynamically indexed, scratch-allocated array)
+    const uint32_t m0 = 0u - ((o >> 2) & 1u), m1 = 0u - ((o >> 3) & 1u);
+    uint32_t U[NT - 1];
 #pragma unroll
-    for (int i = 4 * NB; i < WIN_DW; ++i) R[i] = 0;
+    for (int j = 0; j < NT - 1; ++j) U[j] = (T[j + 1] & m0) | (T[j] & ~m0);
+    constexpr int NR = ND + 1 < WIN_DW ? ND + 1 : WIN_DW;
+#pragma unroll
+    for (int j = 0; j < NR; ++j) R[j] = (j + 2 < NT - 1 ? (U[j + 2] & m1) : 0u) | (U[j] & ~m1);
+#pragma unroll
+    for (int j = NR; j < WIN_DW; ++j) R[j] = 0;
     if (P.any_sh) {  // records not dword-aligned: shift the window to the record start
-        if constexpr (4 * NB == ND)
-            R[ND] = __builtin_amdgcn_raw_buffer_load_b32(P.rsrc, P.rbase + wb + 4 * ND, 0, 0);
 #pragma unroll
         for (int j = 0; j < ND; ++j) R[j] = __builtin_amdgcn_alignbyte(R[j + 1], R[j], P.sh);
     }
@@ -161,6 +182,50 @@ __device__ __forceinline__ uint8_t *pass_col(const Pass &P, uint32_t col_off, ui
     return P.blk + (uint64_t)P.cap * col_off + (uint64_t)P.prow * width;
 }
 
+#ifdef NGZ_LDS_WAVES
+// LDS-staged per-template kernels (generated with NGZ_LDS_WAVES / NGZ_LDS_ROWB
+// defined): the decode writes a workgroup window of LDS_ROWS rows into LDS,
+// column-major (column f at LDS_ROWS*col_off, row r at + r*width), and the
+// generated store step writes each column's run to HBM with 16-byte stores.
+constexpr uint32_t LDS_ROWS = NGZ_REG_WINDOW * NGZ_LDS_WAVES;
+__shared__ __attribute__((aligned(16))) uint8_t ngz_lds[LDS_ROWS * NGZ_LDS_ROWB];
+
+struct ColSt {
+    uint32_t base;  // LDS byte offset of this pass's first row in the column
+    __device__ __forceinline__ ColSt(const Pass &P, uint32_t col_off, uint32_t width)
+        : base(LDS_ROWS * col_off + P.wrow * width) {}
+    __device__ __forceinline__ void b8(uint32_t off, uint32_t v) const { ngz_lds[base + off] = (uint8_t)v; }
+    __device__ __forceinline__ void b16(uint32_t off, uint32_t v) const {
+        *(uint16_t *)&ngz_lds[base + off] = (uint16_t)v;
+    }
+    __device__ __forceinline__ void b32(uint32_t off, uint32_t v) const { *(uint32_t *)&ngz_lds[base + off] = v; }
+    __device__ __forceinline__ void b64(uint32_t off, uint32_t lo, uint32_t hi) const {
+        v2u x = {lo, hi};
+        *(v2u *)&ngz_lds[base + off] = x;
+    }
+    __device__ __forceinline__ void b128(uint32_t off, uint32_t a, uint32_t b, uint32_t c, uint32_t d) const {
+        v4u x = {a, b, c, d};
+        *(v4u *)&ngz_lds[base + off] = x;
+    }
+    __device__ __forceinline__ void w(uint32_t lrow, uint32_t width, uint64_t v) const {
+        if (width == 1) b8(lrow, (uint32_t)v);
+        else if (width == 2) b16(2 * lrow, (uint32_t)v);
+        else if (width == 4) b32(4 * lrow, (uint32_t)v);
+        else b64(8 * lrow, (uint32_t)v, (uint32_t)(v >> 32));
+    }
+};
+
+// Store step: `lanes` x 16 B of LDS at lds_off to the column whose run of
+// this window starts at `dst` (uniform), byte `at` of the run.
+__device__ __forceinline__ void lds_flush(uint8_t *dst, uint32_t at, uint32_t lds_off, uint32_t lanes) {
+    const uint32_t lane = threadIdx.x & 63;
+    if (lane < lanes) {
+        const v4u x = *(const v4u *)&ngz_lds[lds_off + 16 * lane];
+        const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, 0x7FFFFFF0, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(x, r, at + 16 * lane, 0, 0);
+    }
+}
+#else
 struct ColSt {
     __amdgpu_buffer_rsrc_t r;
     __device__ __forceinline__ ColSt(const Pass &P, uint32_t col_off, uint32_t width)
@@ -190,6 +255,7 @@ struct ColSt {
         else b64(8 * lrow, (uint32_t)v, (uint32_t)(v >> 32));
     }
 };
+#endif
 
 // Value of a numeric field (UINT/SCOPE32/TCPFLAGS/SINT/BOOL/DTMS/DTFRAC) at
 // window offset o, in its column encoding; reports the field's errors.
@@ -383,6 +449,71 @@ struct RecShape {
     bool vlen;           // variable-length records: per-row offsets from the record-offset array
 };
 
+// Chunk descriptor j of the 64 a wave fetched (lane j holds it; v_readlane)
+__device__ __forceinline__ Chunk chunk_at_lane(const uint4 &e0, const uint4 &e1, uint32_t j) {
+    Chunk cur;
+    const uint32_t w1x = lane_u32(e1.x, j);
+    cur.n = (uint16_t)(w1x & 0xFFFF);
+    cur.slot = (uint16_t)(w1x >> 16);
+    cur.src = (uint64_t)lane_u32(e0.x, j) | ((uint64_t)lane_u32(e0.y, j) << 32);
+    cur.rec0 = lane_u32(e0.z, j);
+    cur.dgram = lane_u32(e0.w, j);
+    cur.pos0 = (uint16_t)(lane_u32(e1.y, j) & 0xFFFF);
+    return cur;
+}
+
+// The passes of one chunk (its rows of one NGZ_REG_WINDOW window); row0 is
+// the first row of the LDS workgroup window (0 for direct stores).
+template <int RPL, bool CONSEC, class PassFn>
+__device__ __forceinline__ void chunk_passes(const BatchDev &B, const Chunk &cur, uint32_t rl, uint8_t *blk,
+                                             uint32_t cap, uint32_t lane, uint32_t row0, PassFn &&pass) {
+    const uint32_t n = cur.n;
+    const uint64_t src = cur.src;
+    Pass P[RPL];
+    P[0].rec0 = cur.rec0;
+    P[0].dgram = cur.dgram;
+    P[0].pos0 = cur.pos0;
+    P[0].hdr = B.hdr;
+    P[0].blk = blk;
+    P[0].cap = cap;
+    const uint64_t a0 = src & ~15ull;  // 16-byte aligned resource base (win_load)
+    // buffer range checks are per dword (a dword straddling num_records reads 0),
+    // so round up: the <= 3 bytes past bytes_size share the last valid byte's
+    // 4-byte word, hence its page; those bytes are never used
+    const uint64_t avail64 = (B.bytes_size - a0 + 3) & ~3ull;
+    const uint32_t avail = avail64 > 0x7FFFFFF0ull ? 0x7FFFFFF0u : (uint32_t)avail64;
+    P[0].rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)(B.bytes + a0), (short)0, (int)avail, 0x00020000);
+    P[0].a0 = a0;
+    P[0].rabs = 0;
+    P[0].offsets = B.offsets;
+    P[0].lane = lane;
+#pragma unroll
+    for (int k = 1; k < RPL; ++k) P[k] = P[0];
+    const uint32_t rec0 = P[0].rec0;
+    const uint32_t wbase = rec0 & ~(uint32_t)(NGZ_REG_WINDOW - 1);
+    for (uint32_t p = 0; p < NGZ_REG_WINDOW; p += 64 * RPL) {
+        const uint32_t pr0 = wbase + p;
+        if (pr0 + 64 * RPL <= rec0 || pr0 >= rec0 + n) continue;  // no row of this group in the chunk
+#pragma unroll
+        for (int k = 0; k < RPL; ++k) {
+            Pass &Q = P[k];
+            Q.prow = CONSEC ? pr0 : pr0 + 64 * k;
+            Q.wrow = Q.prow - row0;
+            Q.lrow = CONSEC ? RPL * lane + k : lane;
+            Q.row = Q.prow + Q.lrow;
+            Q.valid = Q.row >= rec0 && Q.row < rec0 + n;
+            const uint32_t r = Q.valid ? Q.row - rec0 : 0;
+            const uint32_t d = r * rl;  // record offset from the chunk's first record
+            const uint32_t rel = d + (uint32_t)(src & 15);
+            Q.rbase = rel & ~3u;
+            Q.sh = rel & 3u;
+            Q.any_sh = __builtin_amdgcn_ballot_w64(Q.sh != 0) != 0;
+            Q.recpos = Q.pos0 + d;
+        }
+        pass(P);
+    }
+}
+
 template <int RPL, bool CONSEC, class Want, class Shape, class PassFn>
 __device__ __forceinline__ void run_chunks(const BatchDev &B, uint32_t c_begin, uint32_t c_end, Want &&want,
                                            Shape &&shape, PassFn &&pass) {
@@ -406,71 +537,20 @@ __device__ __forceinline__ void run_chunks(const BatchDev &B, uint32_t c_begin, 
             e1 = ((const uint4 *)&B.chunks[mine])[1];
         }
         const uint32_t cnt = min(64u, (c_end - cb + nw - 1) / nw);
-      for (uint32_t j = 0; j < cnt; ++j) {
-        Chunk cur;
-        const uint32_t w1x = lane_u32(e1.x, j);
-        cur.n = (uint16_t)(w1x & 0xFFFF);
-        if (cur.n == 0) continue;  // padding chunk
-        cur.slot = (uint16_t)(w1x >> 16);
-        cur.src = (uint64_t)lane_u32(e0.x, j) | ((uint64_t)lane_u32(e0.y, j) << 32);
-        cur.rec0 = lane_u32(e0.z, j);
-        cur.dgram = lane_u32(e0.w, j);
-        cur.pos0 = (uint16_t)(lane_u32(e1.y, j) & 0xFFFF);
-        const uint32_t n = cur.n;
-        const uint32_t slot = cur.slot;
-        if (!want(slot)) continue;
-        const RecShape rs = shape(slot);
-        const uint32_t rl = rs.rl;
-        const uint64_t src = cur.src;
-        if (slot != rt_slot) {
-            const SlotRT rt = sload(&B.slots[slot]);
-            blk = B.arena + rt.block;
-            cap = rt.cap;
-            rt_slot = slot;
-        }
-        Pass P[RPL];
-        P[0].rec0 = cur.rec0;
-        P[0].dgram = cur.dgram;
-        P[0].pos0 = cur.pos0;
-        P[0].hdr = B.hdr;
-        P[0].blk = blk;
-        P[0].cap = cap;
-        const uint64_t a0 = src & ~3ull;
-        // buffer range checks are per dword (a dword straddling num_records reads 0),
-        // so round up: the <= 3 bytes past bytes_size share the last valid byte's
-        // 4-byte word, hence its page; those bytes are never used
-        const uint64_t avail64 = (B.bytes_size - a0 + 3) & ~3ull;
-        const uint32_t avail = avail64 > 0x7FFFFFF0ull ? 0x7FFFFFF0u : (uint32_t)avail64;
-        P[0].rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)(B.bytes + a0), (short)0, (int)avail, 0x00020000);
-        P[0].a0 = a0;
-        P[0].rabs = 0;
-        P[0].offsets = B.offsets;
-        P[0].lane = lane;
-#pragma unroll
-        for (int k = 1; k < RPL; ++k) P[k] = P[0];
-        const uint32_t rec0 = P[0].rec0;
-        const uint32_t wbase = rec0 & ~(uint32_t)(NGZ_REG_WINDOW - 1);
-        for (uint32_t p = 0; p < NGZ_REG_WINDOW; p += 64 * RPL) {
-            const uint32_t pr0 = wbase + p;
-            if (pr0 + 64 * RPL <= rec0 || pr0 >= rec0 + n) continue;  // no row of this group in the chunk
-#pragma unroll
-            for (int k = 0; k < RPL; ++k) {
-                Pass &Q = P[k];
-                Q.prow = CONSEC ? pr0 : pr0 + 64 * k;
-                Q.lrow = CONSEC ? RPL * lane + k : lane;
-                Q.row = Q.prow + Q.lrow;
-                Q.valid = Q.row >= rec0 && Q.row < rec0 + n;
-                const uint32_t r = Q.valid ? Q.row - rec0 : 0;
-                const uint32_t d = r * rl;  // record offset from the chunk's first record
-                const uint32_t rel = d + (uint32_t)(src & 3);
-                Q.rbase = rel & ~3u;
-                Q.sh = rel & 3u;
-                Q.any_sh = __builtin_amdgcn_ballot_w64(Q.sh != 0) != 0;
-                Q.recpos = Q.pos0 + d;
+        for (uint32_t j = 0; j < cnt; ++j) {
+            const Chunk cur = chunk_at_lane(e0, e1, j);
+            if (cur.n == 0) continue;  // padding chunk
+            const uint32_t slot = cur.slot;
+            if (!want(slot)) continue;
+            const RecShape rs = shape(slot);
+            if (slot != rt_slot) {
+                const SlotRT rt = sload(&B.slots[slot]);
+                blk = B.arena + rt.block;
+                cap = rt.cap;
+                rt_slot = slot;
             }
-            pass(P);
+            chunk_passes<RPL, CONSEC>(B, cur, rs.rl, blk, cap, lane, 0u, pass);
         }
-      }
     }
 }
 
@@ -498,102 +578,276 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
 // buffer resource based at their smallest address; a group whose records
 // span more than the 31-bit offset range (only with far-apart datagram
 // offsets) is decoded one record at a time.
-template <int RPL, bool CONSEC, class Shape, class PassFn>
-__device__ __forceinline__ void run_windows(const BatchDev &B, uint32_t slot, Shape &&shape, PassFn &&pass) {
+// Row source of row mode: the record table k_emit wrote (batch offset and
+// datagram of every row; error positions derived from the batch offset).
+struct RowTableSrc {
+    const uint64_t *rs;
+    const uint32_t *rd;
+    __device__ __forceinline__ bool operator()(Pass &Q, uint64_t &src) const {
+        src = rs[Q.row];
+        Q.dgram = rd[Q.row];
+        Q.recpos = 0xFFFFFFFFu;
+        Q.rec0 = Q.row;
+        return true;
+    }
+    // smallest / largest record address of the group: from the lanes' rows
+    static constexpr bool kRange = false;
+    __device__ __forceinline__ void range(uint64_t &, uint64_t &) const {}
+};
+
+// One NGZ_REG_WINDOW window w of a slot whose every row's record is found by
+// `srcfn(Q, src)` (sets src, Q.dgram, Q.recpos, Q.rec0 for row Q.row; false =
+// no record), so a group's lanes may read records of different sets and
+// datagrams.  P[] is preset by the caller; row0 as in chunk_passes.
+template <int RPL, bool CONSEC, class SrcFn, class PassFn>
+__device__ __forceinline__ void row_window(const BatchDev &B, const SrcFn &srcfn, uint32_t total, uint32_t w, uint32_t row0,
+                                           Pass (&P)[RPL], PassFn &&pass) {
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t wpb = blockDim.x >> 6;
-    const uint32_t wid = sgpr(blockIdx.x * wpb + (threadIdx.x >> 6));
-    const uint32_t nw = gridDim.x * wpb;
-    const SlotRT rt = sload(&B.slots[slot]);
-    const uint32_t total = rt.total;
-    const uint64_t *rs = (const uint64_t *)(B.arena + rt.rows);
-    const uint32_t *rd = (const uint32_t *)(B.arena + rt.rows + 8ull * rt.cap);
-    const RecShape shp = shape(slot);
-    (void)shp;
-    Pass P[RPL];
-    P[0].blk = B.arena + rt.block;
-    P[0].cap = rt.cap;
-    P[0].hdr = B.hdr;
-    P[0].offsets = B.offsets;
-    P[0].lane = lane;
-    P[0].recpos = 0xFFFFFFFFu;
-    P[0].pos0 = 0;
-    P[0].dgram = 0;
+    for (uint32_t p = 0; p < NGZ_REG_WINDOW; p += 64 * RPL) {
+        const uint32_t pr0 = w * NGZ_REG_WINDOW + p;
+        if (pr0 >= total) break;
+        uint64_t src[RPL];
+        uint64_t lo = ~0ull, hi = 0;
 #pragma unroll
-    for (int k = 1; k < RPL; ++k) P[k] = P[0];
-    const uint32_t nwin = (total + NGZ_REG_WINDOW - 1) / NGZ_REG_WINDOW;
-    for (uint32_t w = wid; w < nwin; w += nw) {
-        for (uint32_t p = 0; p < NGZ_REG_WINDOW; p += 64 * RPL) {
-            const uint32_t pr0 = w * NGZ_REG_WINDOW + p;
-            if (pr0 >= total) break;
-            uint64_t src[RPL];
-            uint64_t lo = ~0ull, hi = 0;
+        for (int k = 0; k < RPL; ++k) {
+            Pass &Q = P[k];
+            Q.prow = CONSEC ? pr0 : pr0 + 64 * k;
+            Q.wrow = Q.prow - row0;
+            Q.lrow = CONSEC ? RPL * lane + k : lane;
+            Q.row = Q.prow + Q.lrow;
+            src[k] = 0;
+            Q.valid = Q.row < total && srcfn(Q, src[k]);
+            if (!Q.valid) {
+                src[k] = 0;
+                Q.dgram = 0;
+            }
+            Q.rabs = src[k];
+            if (Q.valid) {
+                lo = src[k] < lo ? src[k] : lo;
+                hi = src[k] > hi ? src[k] : hi;
+            }
+        }
+        uint64_t base, top;
+        if constexpr (SrcFn::kRange) {
+            srcfn.range(base, top);  // uniform, without cross-lane reductions
+            base &= ~15ull;
+        } else {
+            base = wave_min_u64(lo) & ~15ull;
+            top = wave_max_u64(hi);
+        }
+        if (top - base < 0x7FFF0000ull) {
+            const uint64_t avail64 = (B.bytes_size - base + 3) & ~3ull;
+            const uint32_t avail = avail64 > 0x7FFFFFF0ull ? 0x7FFFFFF0u : (uint32_t)avail64;
+            const __amdgpu_buffer_rsrc_t r =
+                __builtin_amdgcn_make_buffer_rsrc((void *)(B.bytes + base), (short)0, (int)avail, 0x00020000);
 #pragma unroll
             for (int k = 0; k < RPL; ++k) {
                 Pass &Q = P[k];
-                Q.prow = CONSEC ? pr0 : pr0 + 64 * k;
-                Q.lrow = CONSEC ? RPL * lane + k : lane;
-                Q.row = Q.prow + Q.lrow;
-                Q.rec0 = pr0;
-                Q.valid = Q.row < total;
-                src[k] = Q.valid ? rs[Q.row] : 0;
-                Q.dgram = Q.valid ? rd[Q.row] : 0;
-                Q.rabs = src[k];
-                if (Q.valid) {
-                    lo = src[k] < lo ? src[k] : lo;
-                    hi = src[k] > hi ? src[k] : hi;
-                }
+                const uint32_t rel = Q.valid ? (uint32_t)(src[k] - base) : 0;
+                Q.rsrc = r;
+                Q.a0 = base;
+                Q.rbase = rel & ~3u;
+                Q.sh = rel & 3u;
+                Q.any_sh = __builtin_amdgcn_ballot_w64(Q.sh != 0) != 0;
             }
-            const uint64_t base = wave_min_u64(lo) & ~3ull;
-            const uint64_t top = wave_max_u64(hi);
-            if (top - base < 0x7FFF0000ull) {
-                const uint64_t avail64 = (B.bytes_size - base + 3) & ~3ull;
-                const uint32_t avail = avail64 > 0x7FFFFFF0ull ? 0x7FFFFFF0u : (uint32_t)avail64;
-                const __amdgpu_buffer_rsrc_t r =
-                    __builtin_amdgcn_make_buffer_rsrc((void *)(B.bytes + base), (short)0, (int)avail, 0x00020000);
+            pass(P);
+        } else {
+            // records too far apart for one resource: one record per pass
+            bool keep[RPL];
 #pragma unroll
-                for (int k = 0; k < RPL; ++k) {
-                    Pass &Q = P[k];
-                    const uint32_t rel = Q.valid ? (uint32_t)(src[k] - base) : 0;
-                    Q.rsrc = r;
-                    Q.a0 = base;
-                    Q.rbase = rel & ~3u;
-                    Q.sh = rel & 3u;
-                    Q.any_sh = __builtin_amdgcn_ballot_w64(Q.sh != 0) != 0;
-                }
-                pass(P);
-            } else {
-                // records too far apart for one resource: one record per pass
-                bool keep[RPL];
+            for (int k = 0; k < RPL; ++k) keep[k] = P[k].valid;
+            for (uint32_t L = 0; L < 64; ++L) {
 #pragma unroll
-                for (int k = 0; k < RPL; ++k) keep[k] = P[k].valid;
-                for (uint32_t L = 0; L < 64; ++L) {
+                for (int k0 = 0; k0 < RPL; ++k0) {
+                    if (!__builtin_amdgcn_readlane((int)keep[k0], L)) continue;
+                    const uint64_t b1 = ((uint64_t)lane_u32((uint32_t)src[k0], L) |
+                                         ((uint64_t)lane_u32((uint32_t)(src[k0] >> 32), L) << 32)) & ~15ull;
+                    const uint64_t avail64 = (B.bytes_size - b1 + 3) & ~3ull;
+                    const uint32_t avail = avail64 > 0x7FFFFFF0ull ? 0x7FFFFFF0u : (uint32_t)avail64;
+                    const __amdgpu_buffer_rsrc_t r =
+                        __builtin_amdgcn_make_buffer_rsrc((void *)(B.bytes + b1), (short)0, (int)avail, 0x00020000);
 #pragma unroll
-                    for (int k0 = 0; k0 < RPL; ++k0) {
-                        if (!__builtin_amdgcn_readlane((int)keep[k0], L)) continue;
-                        const uint64_t b1 = ((uint64_t)lane_u32((uint32_t)src[k0], L) |
-                                             ((uint64_t)lane_u32((uint32_t)(src[k0] >> 32), L) << 32)) & ~3ull;
-                        const uint64_t avail64 = (B.bytes_size - b1 + 3) & ~3ull;
-                        const uint32_t avail = avail64 > 0x7FFFFFF0ull ? 0x7FFFFFF0u : (uint32_t)avail64;
-                        const __amdgpu_buffer_rsrc_t r =
-                            __builtin_amdgcn_make_buffer_rsrc((void *)(B.bytes + b1), (short)0, (int)avail, 0x00020000);
-#pragma unroll
-                        for (int k = 0; k < RPL; ++k) {
-                            Pass &Q = P[k];
-                            Q.valid = k == k0 && lane == L && keep[k];
-                            const uint32_t rel = Q.valid ? (uint32_t)(src[k] - b1) : 0;
-                            Q.rsrc = r;
-                            Q.a0 = b1;
-                            Q.rbase = rel & ~3u;
-                            Q.sh = rel & 3u;
-                            Q.any_sh = __builtin_amdgcn_ballot_w64(Q.sh != 0) != 0;
-                        }
-                        pass(P);
+                    for (int k = 0; k < RPL; ++k) {
+                        Pass &Q = P[k];
+                        Q.valid = k == k0 && lane == L && keep[k];
+                        const uint32_t rel = Q.valid ? (uint32_t)(src[k] - b1) : 0;
+                        Q.rsrc = r;
+                        Q.a0 = b1;
+                        Q.rbase = rel & ~3u;
+                        Q.sh = rel & 3u;
+                        Q.any_sh = __builtin_amdgcn_ballot_w64(Q.sh != 0) != 0;
                     }
+                    pass(P);
                 }
             }
         }
     }
 }
+
+// P[] fields of a row-mode slot that do not change per window
+template <int RPL>
+__device__ __forceinline__ void row_preset(const BatchDev &B, const SlotRT &rt, Pass (&P)[RPL]) {
+    P[0].blk = B.arena + rt.block;
+    P[0].cap = rt.cap;
+    P[0].hdr = B.hdr;
+    P[0].offsets = B.offsets;
+    P[0].lane = threadIdx.x & 63;
+    P[0].recpos = 0xFFFFFFFFu;
+    P[0].pos0 = 0;
+    P[0].dgram = 0;
+#pragma unroll
+    for (int k = 1; k < RPL; ++k) P[k] = P[0];
+}
+
+template <int RPL, bool CONSEC, class Shape, class PassFn>
+__device__ __forceinline__ void run_windows(const BatchDev &B, uint32_t slot, Shape &&shape, PassFn &&pass) {
+    const uint32_t wpb = blockDim.x >> 6;
+    const uint32_t wid = sgpr(blockIdx.x * wpb + (threadIdx.x >> 6));
+    const uint32_t nw = gridDim.x * wpb;
+    const SlotRT rt = sload(&B.slots[slot]);
+    const uint64_t *rs = (const uint64_t *)(B.arena + rt.rows);
+    const uint32_t *rd = (const uint32_t *)(B.arena + rt.rows + 8ull * rt.cap);
+    (void)shape;
+    Pass P[RPL];
+    row_preset<RPL>(B, rt, P);
+    const uint32_t nwin = (rt.total + NGZ_REG_WINDOW - 1) / NGZ_REG_WINDOW;
+    for (uint32_t w = wid; w < nwin; w += nw) row_window<RPL, CONSEC>(B, RowTableSrc{rs, rd}, rt.total, w, 0u, P, pass);
+}
+
+#ifdef NGZ_LDS_WAVES
+// Row source of a chunk-mode window: the window's chunk descriptors, one per
+// lane (e0/e1 as fetched by the wave, cnt valid); a row's record is in the
+// chunk whose row range holds it.
+struct ChunkGatherSrc {
+    uint4 e0, e1;
+    uint32_t cnt;
+    uint32_t rl;
+    __device__ __forceinline__ bool operator()(Pass &Q, uint64_t &src) const {
+        bool hit = false;
+        for (uint32_t j = 0; j < cnt; ++j) {
+            const uint32_t n = lane_u32(e1.x, j) & 0xFFFF;  // 0 = padding chunk
+            const uint32_t r0 = lane_u32(e0.z, j);
+            const uint32_t r = Q.row - r0;
+            if (r < n) {
+                const uint32_t d = r * rl;
+                src = ((uint64_t)lane_u32(e0.x, j) | ((uint64_t)lane_u32(e0.y, j) << 32)) + d;
+                Q.dgram = lane_u32(e0.w, j);
+                Q.recpos = (lane_u32(e1.y, j) & 0xFFFF) + d;
+                Q.rec0 = r0;
+                hit = true;
+            }
+        }
+        return hit;
+    }
+    // the window's record addresses span [first record of the lowest chunk,
+    // last record of the highest]: scalar, over the descriptors
+    static constexpr bool kRange = true;
+    __device__ __forceinline__ void range(uint64_t &lo, uint64_t &hi) const {
+        lo = ~0ull;
+        hi = 0;
+        for (uint32_t j = 0; j < cnt; ++j) {
+            const uint32_t n = lane_u32(e1.x, j) & 0xFFFF;
+            if (!n) continue;
+            const uint64_t a = (uint64_t)lane_u32(e0.x, j) | ((uint64_t)lane_u32(e0.y, j) << 32);
+            lo = a < lo ? a : lo;
+            const uint64_t b = a + (uint64_t)(n - 1) * rl;
+            hi = b > hi ? b : hi;
+        }
+        if (lo > hi) lo = hi = 0;
+    }
+};
+
+// LDS-staged decode of one slot: workgroup window W = rows [W*LDS_ROWS,
+// (W+1)*LDS_ROWS); wave q decodes its NGZ_REG_WINDOW sub-window s into LDS,
+// then the workgroup writes the window's column runs (store(W, blk, cap),
+// generated per template).  The capacity is a multiple of LDS_ROWS
+// (k_layout), so a window's runs never leave the slot's block; rows past the
+// slot's total carry stale bytes nobody reads.
+//
+// Chunk mode: the chunks of sub-window s are [wt[s], wt[s+1]) (k_emit).  A
+// wave holds the window-table entries of its next 64 sub-windows in two
+// VGPRs and fetches the next sub-window's chunk descriptors (one per lane)
+// while it decodes the current one, so the record loads are the only memory
+// latency on a window's path.  Lanes gather their rows' records across the
+// sub-window's chunks (ChunkGatherSrc): one pass per group of 64*RPL rows
+// even where a set ends inside the window.  Sub-windows of more than 64
+// chunks go chunk by chunk.
+template <int RPL, bool CONSEC, class Shape, class PassFn, class StoreFn>
+__device__ __forceinline__ void run_lds(const BatchDev &B, uint32_t slot, Shape &&shape, PassFn &&pass,
+                                        StoreFn &&store) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t q = sgpr(threadIdx.x >> 6);
+    const SlotRT rt = sload(&B.slots[slot]);
+    const uint32_t total = rt.total;
+    const uint32_t nwin = (total + LDS_ROWS - 1) / LDS_ROWS;
+    const uint32_t nsub = (total + NGZ_REG_WINDOW - 1) / NGZ_REG_WINDOW;
+    const RecShape shp = shape(slot);
+    uint8_t *blk = B.arena + rt.block;
+    const uint32_t c_end = rt.chunk0 + rt.nchunks;
+    const uint32_t *wt = (const uint32_t *)(B.arena + rt.wtab);
+    Pass P[RPL];
+    row_preset<RPL>(B, rt, P);
+    if (rt.mode == NGZ_MODE_ROW) {
+        const uint64_t *rs = (const uint64_t *)(B.arena + rt.rows);
+        const uint32_t *rd = (const uint32_t *)(B.arena + rt.rows + 8ull * rt.cap);
+        for (uint32_t W = blockIdx.x; W < nwin; W += gridDim.x) {
+            const uint32_t s = W * NGZ_LDS_WAVES + q;
+            if (s < nsub) row_window<RPL, CONSEC>(B, RowTableSrc{rs, rd}, total, s, W * LDS_ROWS, P, pass);
+            __syncthreads();
+            store(W, blk, rt.cap);
+            __syncthreads();
+        }
+        return;
+    }
+    // window-table entries [cb, ce) of this wave's sub-windows i0 .. i0+63 (lane i)
+    auto wt_fetch = [&](uint32_t i0, uint32_t &ta, uint32_t &tb) {
+        const uint32_t Wl = blockIdx.x + (i0 + lane) * gridDim.x;
+        const uint32_t sl = Wl * NGZ_LDS_WAVES + q;
+        ta = sl < nsub ? wt[sl] : c_end;
+        tb = sl + 1 < nsub ? wt[sl + 1] : c_end;
+    };
+    auto desc_fetch = [&](uint32_t cb, uint32_t ce, uint4 &e0, uint4 &e1) {
+        const uint32_t mine = cb + lane;
+        e0 = make_uint4(0, 0, 0, 0);
+        e1 = make_uint4(0, 0, 0, 0);
+        if (mine < ce) {
+            e0 = ((const uint4 *)&B.chunks[mine])[0];
+            e1 = ((const uint4 *)&B.chunks[mine])[1];
+        }
+    };
+    uint32_t ta = 0, tb = 0;
+    uint4 n0, n1;  // descriptors of the next sub-window
+    wt_fetch(0, ta, tb);
+    desc_fetch(lane_u32(ta, 0), lane_u32(tb, 0), n0, n1);
+    uint32_t i = 0;
+    for (uint32_t W = blockIdx.x; W < nwin; W += gridDim.x, ++i) {
+        const uint32_t s = W * NGZ_LDS_WAVES + q;
+        const uint32_t cb = lane_u32(ta, i & 63), ce = lane_u32(tb, i & 63);
+        const uint4 e0 = n0, e1 = n1;
+        // prefetch: the next sub-window's descriptors (and table entries every 64)
+        if (((i + 1) & 63) == 0) wt_fetch(i + 1, ta, tb);
+        desc_fetch(lane_u32(ta, (i + 1) & 63), lane_u32(tb, (i + 1) & 63), n0, n1);
+        if (s < nsub) {
+            if (ce - cb <= 64) {
+                row_window<RPL, CONSEC>(B, ChunkGatherSrc{e0, e1, ce - cb, shp.rl}, total, s, W * LDS_ROWS, P, pass);
+            } else {
+                for (uint32_t c0 = cb; c0 < ce; c0 += 64) {
+                    uint4 f0, f1;
+                    desc_fetch(c0, ce, f0, f1);
+                    const uint32_t cnt = min(64u, ce - c0);
+                    for (uint32_t j = 0; j < cnt; ++j) {
+                        const Chunk cur = chunk_at_lane(f0, f1, j);
+                        if (cur.n == 0) continue;  // padding chunk
+                        chunk_passes<RPL, CONSEC>(B, cur, shp.rl, blk, rt.cap, lane, W * LDS_ROWS, pass);
+                    }
+                }
+            }
+        }
+        __syncthreads();
+        store(W, blk, rt.cap);
+        __syncthreads();
+    }
+}
+#endif
 
 }  // namespace ngzdev

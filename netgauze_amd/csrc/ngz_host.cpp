@@ -33,7 +33,9 @@ extern "C" int ngz_launch_layout_emit(const BatchDev *B, const uint32_t *hf_flag
                                       hipStream_t st);
 extern "C" int ngz_launch_decode_generic(const BatchDev *B, uint32_t grid, hipStream_t st);
 void *ngz_rtc_kernel(int device, const DevPlan &P);
-int ngz_rtc_launch(void *fn, const BatchDev *B, uint32_t slot, uint32_t grid, hipStream_t st);
+std::string ngz_rtc_source(const DevPlan &P);
+int ngz_rtc_compile_only(const DevPlan &P, std::string *log_out);
+int ngz_rtc_launch(void *fn, const BatchDev *B, uint32_t slot, uint32_t grid, uint32_t block, hipStream_t st);
 extern "C" int ngz_launch_counts(const BatchDev *B, uint64_t set_cap, hipStream_t st);
 
 namespace {
@@ -287,6 +289,10 @@ void build_plan(Version &v) {
     P.rpl = 0;
     P.window = NGZ_REG_WINDOW;
     if (devok && rl <= NGZ_MAX_REC_LEN) P.rpl = 1;
+    // per-template kernels stage the columns of 256*lds_waves rows in LDS
+    // (NGZ_LDS=0: direct column stores, for A/B measurements)
+    static const bool lds_on = !getenv("NGZ_LDS") || atoi(getenv("NGZ_LDS")) != 0;
+    P.lds_waves = (P.rpl && !vlen && lds_on) ? ngz_lds_waves(P.row_bytes) : 0;
 }
 
 struct ErrInfo {  // host-side framing error
@@ -361,6 +367,7 @@ struct ngz_ctx {
     int n_cus = 256;
     int specialize = 1;                         // NGZ_OPT_SPECIALIZE
     uint32_t blocks_per_cu = 4;                 // decode grid: 4 x 256 threads per CU
+    uint32_t lds_blocks_per_cu = 8;             // LDS-staged decode grid (2 resident per CU at 64 KB)
     BatchSummary *h_summary = nullptr;          // pinned
     SlotRT *h_slots = nullptr;                  // pinned, NGZ_MAX_SLOTS
     float t_decode = 0, t_pipeline = 0;
@@ -833,7 +840,7 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
         const DevPlan &P = ctx->versions[ctx->slot_version[s]].plan;
         // columns + row-mode record table (12 B/row) per wire byte
         if (P.rec_len) ratio = std::max(ratio, (double)(P.row_bytes + 12) / (double)P.rec_len);
-        maxwin_row = std::max<uint32_t>(maxwin_row, P.window * P.row_bytes);
+        maxwin_row = std::max<uint32_t>(maxwin_row, P.window * std::max<uint32_t>(P.lds_waves, 1) * P.row_bytes);
     }
     uint64_t arena_cap = (uint64_t)(ratio * (double)in->bytes_size) + (uint64_t)S * (maxwin_row + 256) + 4096;
     arena_cap = std::max<uint64_t>(arena_cap, ctx->d_arena.cap);
@@ -925,9 +932,18 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
         if (!v.plan.rpl) continue;
         if (ctx->specialize && v.rtc_state == 1 && !v.plan.has_vlen) {
             // one specialised kernel per active template, over that slot's chunks only
-            const uint32_t units = rt.mode == NGZ_MODE_ROW ? (rt.total + NGZ_REG_WINDOW - 1) / NGZ_REG_WINDOW : rt.nchunks;
-            const uint32_t g = std::min<uint32_t>(grid, (units + 3) / 4);
-            if (ngz_rtc_launch(v.rtc_fn, &B, s, g, st)) return fail(ctx, NGZ_E_DEVICE, "specialised decode launch");
+            uint32_t g, block = 256;
+            if (v.plan.lds_waves) {
+                // one workgroup per window of 256*lds_waves rows (grid-strided)
+                const uint32_t rows = NGZ_REG_WINDOW * v.plan.lds_waves;
+                g = std::min<uint32_t>((uint32_t)ctx->n_cus * ctx->lds_blocks_per_cu, (rt.total + rows - 1) / rows);
+                block = 64 * v.plan.lds_waves;
+            } else {
+                const uint32_t units =
+                    rt.mode == NGZ_MODE_ROW ? (rt.total + NGZ_REG_WINDOW - 1) / NGZ_REG_WINDOW : rt.nchunks;
+                g = std::min<uint32_t>(grid, (units + 3) / 4);
+            }
+            if (ngz_rtc_launch(v.rtc_fn, &B, s, g, block, st)) return fail(ctx, NGZ_E_DEVICE, "specialised decode launch");
         } else {
             generic = true;
         }
@@ -1006,6 +1022,7 @@ int ngz_ctx_create(int device, ngz_ctx **out) {
     }
     if (const char *e = getenv("NGZ_SPECIALIZE")) ctx->specialize = atoi(e);
     if (const char *e = getenv("NGZ_BLOCKS_PER_CU")) ctx->blocks_per_cu = std::max(1, std::min(32, atoi(e)));
+    if (const char *e = getenv("NGZ_LDS_BLOCKS_PER_CU")) ctx->lds_blocks_per_cu = std::max(1, std::min(512, atoi(e)));
     *out = ctx;
     return NGZ_OK;
 }
@@ -1436,4 +1453,39 @@ extern "C" int ngz_dgram_error_json(ngz_ctx *ctx, uint32_t dgram, char *buf, siz
         buf[m] = 0;
     }
     return (int)s.size();
+}
+
+extern "C" int ngz_template_kernel(const uint8_t *tmpl, size_t len, int compile, char *buf, size_t cap) {
+    if (!tmpl || len < 4 || len > 65535) return NGZ_E_INVALID;
+    Cur c{tmpl, 0, (uint32_t)len};
+    const uint16_t tid = rd16(tmpl);
+    const uint32_t count = rd16(tmpl + 2);
+    c.pos = 4;
+    Version v;
+    v.proto = 10;
+    v.tid = tid;
+    v.n_scope = 0;
+    for (uint32_t i = 0; i < count; ++i) {
+        Spec s;
+        std::string err;
+        if (!parse_field_spec(c, s, err)) return NGZ_E_INVALID;
+        v.specs.push_back(s);
+    }
+    build_plan(v);
+    if (!v.plan.rpl || v.plan.has_vlen) return NGZ_E_INVALID;
+    std::string out = ngz_rtc_source(v.plan);
+    int rc = NGZ_OK;
+    if (compile) {
+        std::string log;
+        if (ngz_rtc_compile_only(v.plan, &log)) {
+            out += "\n// hiprtc log:\n" + log;
+            rc = NGZ_E_DEVICE;
+        }
+    }
+    if (buf && cap) {
+        const size_t n = std::min(cap - 1, out.size());
+        memcpy(buf, out.data(), n);
+        buf[n] = 0;
+    }
+    return rc;
 }

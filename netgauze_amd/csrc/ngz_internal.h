@@ -11,6 +11,18 @@
 #define NGZ_NO_ERR (~0ull)
 #define NGZ_MAX_REC_LEN 65535 // longest fixed record the device decode takes
 #define NGZ_REG_WINDOW 256    // records per chunk window (4 passes of 64 lanes)
+#define NGZ_LDS_BUDGET 65536  // LDS bytes one workgroup may stage columns in
+
+// Workgroup window of the LDS-staged per-template kernels: a workgroup
+// decodes lds_waves consecutive 256-row windows (one per wave) into LDS,
+// column-major, then writes every column's 256*lds_waves rows as one
+// contiguous run of 16-byte stores.  As many waves as the budget allows, at
+// most 4; 0 (rows too wide) = direct stores.
+static inline __host__ __device__ uint32_t ngz_lds_waves(uint32_t row_bytes) {
+    if (!row_bytes) return 0;
+    const uint32_t w = NGZ_LDS_BUDGET / (NGZ_REG_WINDOW * row_bytes);
+    return w > 4 ? 4 : w;
+}
 
 // datagram frame state (k_frame -> host)
 #define NGZ_FR_OK 0
@@ -73,7 +85,9 @@ struct DevPlan {
     uint8_t spec;        // 1 = decoded by a run-time specialised kernel (the generic kernel skips it)
     uint32_t window;     // records per chunk window (NGZ_REG_WINDOW)
     uint32_t template_id;
-    uint32_t reserved1[2];
+    uint32_t lds_waves;  // per-template kernel stages columns in LDS: waves (256-row sub-windows) per
+                         // workgroup window, 0 = direct column stores (ngz_lds_waves)
+    uint32_t reserved1;
     DevField f[NGZ_MAXF];
 };
 
@@ -139,6 +153,8 @@ struct SlotRT {          // per batch slot, computed on device by k_layout
     uint32_t reserved;
     uint64_t rows;       // row mode: arena offset of u64 rowsrc[cap] (batch offset of each record),
                          // followed by u32 rowdg[cap] (its datagram)
+    uint64_t wtab;       // chunk mode: arena offset of u32 wfirst[cap/window]: first chunk of
+                         // every output window (k_emit), for the LDS-staged kernels
 };
 
 // Decode work of a slot: chunk mode walks set-relative chunks of <= 256 rows

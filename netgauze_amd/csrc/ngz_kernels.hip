@@ -256,7 +256,9 @@ __global__ void k_layout(BatchDev B) {
         const uint32_t next = B.scan[(uint64_t)(s + 1) * N];
         const uint32_t total = next - base;
         const uint32_t w = B.plans[s].window ? B.plans[s].window : 64;
-        const uint32_t cap = total ? ((total + w - 1) / w) * w : 0;
+        // LDS-staged kernels store whole workgroup windows: capacity in those
+        const uint32_t wa = B.plans[s].lds_waves ? w * B.plans[s].lds_waves : w;
+        const uint32_t cap = total ? ((total + wa - 1) / wa) * wa : 0;
         SlotRT rt;
         rt.block = off;
         rt.cap = cap;
@@ -271,9 +273,11 @@ __global__ void k_layout(BatchDev B) {
         rt.reserved = 0;
         const uint64_t col_bytes = ((uint64_t)cap * B.plans[s].row_bytes + 7) & ~7ull;
         rt.rows = rt.mode == NGZ_MODE_ROW ? off + col_bytes : 0;
+        rt.wtab = rt.mode == NGZ_MODE_CHUNK ? off + col_bytes : 0;
         if (rt.mode == NGZ_MODE_ROW) rt.nchunks = 0;
         B.slots[s] = rt;
-        const uint64_t row_bytes_extra = rt.mode == NGZ_MODE_ROW ? 12ull * cap : 0;  // rowsrc + rowdg
+        // row mode: rowsrc + rowdg; chunk mode: first chunk per window
+        const uint64_t row_bytes_extra = rt.mode == NGZ_MODE_ROW ? 12ull * cap : 4ull * (cap / w + 1);
         off += (col_bytes + row_bytes_extra + 255) & ~255ull;
     }
     const uint32_t rec_total = chunk_base;
@@ -358,6 +362,8 @@ struct EmitVis {
             c.cls = 0;
             c.reserved2 = 0;
             B->chunks[chunk_at + used] = c;
+            // every window starts with a chunk (sets are cut at window boundaries)
+            if (cstart % W == 0) ((uint32_t *)(B->arena + B->slots[slot].wtab))[cstart / W] = chunk_at + used;
             ++used;
             r += take;
         }

@@ -43,7 +43,7 @@ struct Item {           // one extraction step of the generated pass body
 };
 
 std::string signature(const DevPlan &P) {
-    std::string s = "rl" + std::to_string(P.rec_len);
+    std::string s = "rl" + std::to_string(P.rec_len) + "lw" + std::to_string(P.lds_waves);
     char b[96];
     for (uint32_t f = 0; f < P.n_fields; ++f) {
         const DevField &d = P.f[f];
@@ -127,7 +127,14 @@ std::string generate(const DevPlan &P) {
     // per lane (or 2 consecutive rows up to 152 B with NGZ_RTC_LONG=c2).
     int rpl = 4;
     bool consec = true;
+    //
+    // LDS-staged kernels take rows 64 apart ("r1" by default): a load
+    // instruction's 64 lanes then read 64 adjacent records (one contiguous
+    // span), where 4 consecutive rows per lane spread it over 4x as many
+    // cache lines; T20 at 10^8 records decoded in 2.15 ms (r1) vs 2.55 ms
+    // (c4) on the same box (profiles/r1e).
     const char *layout = getenv("NGZ_RTC_LAYOUT");
+    if (!layout && P.lds_waves) layout = getenv("NGZ_RTC_LDS_LAYOUT") ? getenv("NGZ_RTC_LDS_LAYOUT") : "r1";
     if (!layout && P.rec_len > 76) layout = getenv("NGZ_RTC_LONG") ? getenv("NGZ_RTC_LONG") : "r1";
     if (layout) {
         if (layout[0] == 'c' || layout[0] == 'r') {
@@ -199,10 +206,16 @@ std::string generate(const DevPlan &P) {
         i = e;
     }
     const std::string RPL = std::to_string(rpl);
+    const uint32_t lw = P.lds_waves;
     std::string src;
     src += "// generated by ngz_rtc.cpp for plan " + signature(P) + "\n";
+    if (lw) {
+        src += "#define NGZ_LDS_WAVES " + std::to_string(lw) + "\n";
+        src += "#define NGZ_LDS_ROWB " + std::to_string(P.row_bytes) + "\n";
+    }
     src += "#include \"ngz_dev.h\"\nusing namespace ngzdev;\n";
-    src += "extern \"C\" __global__ void __launch_bounds__(256) ngz_tpl(BatchDev B, uint32_t slot) {\n";
+    src += "extern \"C\" __global__ void __launch_bounds__(" + std::to_string(lw ? 64 * lw : 256) +
+           ") ngz_tpl(BatchDev B, uint32_t slot) {\n";
     src += "    if (sload(&B.summary->overflow)) return;\n";
     src += "    const SlotRT rt = sload(&B.slots[slot]);\n";
     src += "    const uint32_t c0 = rt.chunk0, nc = rt.nchunks;\n";
@@ -212,6 +225,44 @@ std::string generate(const DevPlan &P) {
     src += "        uint32_t R[" + RPL + "][WIN_DW];\n";
     src += body;
     src += "    };\n";
+    if (lw) {
+        // Store step of the LDS-staged kernel: each column's run of the window
+        // (LDS_ROWS*width bytes) cut into 1 KB units (64 lanes x 16 B), dealt
+        // round robin to the waves; every store instruction is one full wave
+        // writing 1 KB of one column.
+        const uint32_t rows = NGZ_REG_WINDOW * lw;
+        std::vector<std::string> per_wave(lw);
+        uint32_t u = 0;
+        for (uint32_t f = 0; f < P.n_fields; ++f) {
+            const DevField &d = P.f[f];
+            if (!d.width) continue;
+            // pieces of one raw field share its column: one run per column
+            bool seen = false;
+            for (uint32_t g = 0; g < f; ++g) seen = seen || (P.f[g].width && P.f[g].col_off == d.col_off);
+            if (seen) continue;
+            const uint32_t run = rows * d.width;
+            for (uint32_t at = 0; at < run; at += 1024, ++u) {
+                const uint32_t lanes = std::min<uint32_t>(1024, run - at) / 16;
+                snprintf(b, sizeof b,
+                         "            lds_flush(blk + (uint64_t)cap * %uu + (uint64_t)W * %uu, %uu, %uu, %uu);\n",
+                         d.col_off, run, at, rows * d.col_off + at, lanes);
+                per_wave[u % lw] += b;
+            }
+        }
+        // NGZ_RTC_EXP=1: no store step (timing experiments only; output invalid)
+        if (getenv("NGZ_RTC_EXP") && (atoi(getenv("NGZ_RTC_EXP")) & 1)) per_wave.assign(lw, "");
+        src += "    auto store = [&](uint32_t W, uint8_t *blk, uint32_t cap) {\n";
+        src += "        const uint32_t q = sgpr(threadIdx.x >> 6);\n";
+        for (uint32_t q = 0; q < lw; ++q) {
+            src += q ? "        else if (q == " + std::to_string(q) + ") {\n" : "        if (q == 0) {\n";
+            src += per_wave[q];
+            src += "        }\n";
+        }
+        src += "    };\n";
+        src += "    (void)c0; (void)nc;\n";
+        src += "    run_lds<" + L + ">(B, slot, shape, pass, store);\n}\n";
+        return src;
+    }
     src += "    if (rt.mode == NGZ_MODE_ROW) run_windows<" + L + ">(B, slot, shape, pass);\n";
     src += "    else run_chunks<" + L + ">(B, c0, c0 + nc, [](uint32_t) { return true; }, shape, pass);\n}\n";
     return src;
@@ -286,11 +337,11 @@ void *ngz_rtc_kernel(int device, const DevPlan &P) {
 std::string ngz_rtc_source(const DevPlan &P) { return generate(P); }
 
 // Launch a specialised kernel over one slot's chunks.
-int ngz_rtc_launch(void *fn, const BatchDev *B, uint32_t slot, uint32_t grid, hipStream_t st) {
+int ngz_rtc_launch(void *fn, const BatchDev *B, uint32_t slot, uint32_t grid, uint32_t block, hipStream_t st) {
     BatchDev b = *B;
     uint32_t s = slot;
     void *args[] = {&b, &s};
-    return hipModuleLaunchKernel((hipFunction_t)fn, grid, 1, 1, 256, 1, 1, 0, st, args, nullptr) == hipSuccess ? 0 : -1;
+    return hipModuleLaunchKernel((hipFunction_t)fn, grid, 1, 1, block, 1, 1, 0, st, args, nullptr) == hipSuccess ? 0 : -1;
 }
 
 // Generate and compile without loading (no device needed): 0 ok, -1 failed.

@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 TAG=${TAG:-r1}
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
-timeout -k 10 900 python -m pytest tests/ -q -m gpu -x > $OUT/pytest_gpu.log 2>&1 || { tail -30 $OUT/pytest_gpu.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests/ -q -m gpu -x --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { tail -30 $OUT/pytest_gpu.log; exit 1; }
 tail -2 $OUT/pytest_gpu.log
 timeout -k 10 600 python bench.py > $OUT/bench.json 2> $OUT/bench.err || exit 2
 cat $OUT/bench.json
