@@ -49,3 +49,21 @@ def test_product_does_not_import_oracle():
             if f.endswith((".py", ".cpp", ".hip", ".h")):
                 text = open(os.path.join(dirpath, f), errors="ignore").read()
                 assert "ngz_oracle" not in text and "oracle/" not in text, f
+
+
+@pytest.mark.parametrize("tid", [t for t, _ in __import__("netgauze_amd.synth", fromlist=["x"]).CFG3_TEMPLATES])
+def test_template_kernels_compile_for_gfx950(tid):
+    """The per-template decode kernel of every config-3 template is generated
+    and compiled for gfx950 by hiprtc (no device needed): LDS-staged where the
+    rows fit the workgroup budget, direct column stores otherwise."""
+    import struct
+    from netgauze_amd import _lib, synth
+    fields = dict(synth.CFG3_TEMPLATES)[tid]
+    rec = struct.pack(">HH", tid, len(fields)) + b"".join(struct.pack(">HH", i, ln) for i, ln in fields)
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    buf = ctypes.create_string_buffer(1 << 20)
+    rc = lib.ngz_template_kernel(rec, len(rec), 1, buf, len(buf))
+    src = buf.value.decode()
+    assert rc == 0, src[-2000:]
+    assert "ngz_tpl" in src
+    assert ("run_lds" in src) == ("NGZ_LDS_WAVES" in src)
