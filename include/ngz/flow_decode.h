@@ -182,6 +182,13 @@ int ngz_template_counts(ngz_ctx *ctx, int proto, uint16_t *ids, uint64_t *counts
  * decode kernel and of the whole device pipeline (HIP events). */
 int ngz_last_timing(ngz_ctx *ctx, float *decode_ms, float *pipeline_ms);
 
+/* D2H of the last batch's columns into host memory `dst` (pinned for full
+ * PCIe rate): the column block of every slot with records, in slot order,
+ * each ngz_slot_info.capacity * (sum of column widths) bytes, starting at a
+ * multiple of 256 bytes.  Copied on the context's stream; returns the bytes
+ * written, or <0 (NGZ_E_INVALID: cap too small). */
+int64_t ngz_columns_to_host(ngz_ctx *ctx, void *dst, uint64_t cap);
+
 /* Introspection (no device needed): the per-template decode kernel for one
  * IPFIX template record (template id u16, field count u16, field specifiers;
  * the body of a template set entry, ipfix.rs:384-413).  Writes the generated

@@ -20,7 +20,7 @@ ABI_FUNCTIONS = [
     "ngz_ctx_create", "ngz_ctx_destroy", "ngz_last_error", "ngz_decode_batch",
     "ngz_decode_batch_host", "ngz_slot_fields", "ngz_dgram_error_json",
     "ngz_templates_json", "ngz_template_counts", "ngz_last_timing", "ngz_ctx_set_option",
-    "ngz_template_kernel",
+    "ngz_template_kernel", "ngz_columns_to_host",
 ]
 
 
@@ -81,6 +81,10 @@ def load():
     lib.ngz_template_counts.restype = I
     lib.ngz_last_timing.argtypes = [P, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
     lib.ngz_last_timing.restype = I
+    lib.ngz_columns_to_host.argtypes = [P, P, U64]
+    lib.ngz_columns_to_host.restype = ctypes.c_int64
+    lib.ngz_template_kernel.argtypes = [P, ctypes.c_size_t, I, ctypes.c_char_p, ctypes.c_size_t]
+    lib.ngz_template_kernel.restype = I
     lib.ngz_ctx_set_option.argtypes = [P, I, ctypes.c_int64]
     lib.ngz_ctx_set_option.restype = I
     return lib

@@ -370,10 +370,15 @@ struct ngz_ctx {
     uint32_t lds_blocks_per_cu = 8;             // LDS-staged decode grid (2 resident per CU at 64 KB)
     BatchSummary *h_summary = nullptr;          // pinned
     SlotRT *h_slots = nullptr;                  // pinned, NGZ_MAX_SLOTS
+    unsigned long long *h_proc = nullptr;       // pinned, NGZ_MAX_SLOTS: processed_count increments
     float t_decode = 0, t_pipeline = 0;
     bool plans_dirty = true;
     uint32_t n_template_dgrams = 0;
     uint64_t tmpl_gen = 1, uploaded_gen = 0;  // template-state generation vs the device tables
+    // steady-state decode launches (run_pipeline): the slots of the last batch
+    bool pred_valid = false;
+    std::vector<int32_t> pred_versions;
+    std::vector<uint8_t> pred_active;
 };
 
 namespace {
@@ -911,48 +916,115 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
     if (ngz_launch_scan(ctx->d_scan_tmp.p, scan_tmp, ctx->d_counts.p, ctx->d_scan.p, n_items, st))
         return fail(ctx, NGZ_E_DEVICE, "scan launch");
     if (ngz_launch_layout_emit(&B, hf_flag, hf_first, st)) return fail(ctx, NGZ_E_DEVICE, "layout/emit launch");
-    // per-slot chunk ranges and capacities decide which decode kernels run
-    HIPCHK(hipMemcpyAsync(ctx->h_summary, ctx->d_summary.p, sizeof(BatchSummary), hipMemcpyDeviceToHost, st));
-    if (S) HIPCHK(hipMemcpyAsync(ctx->h_slots, ctx->d_slots.p, S * sizeof(SlotRT), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    ctx->summary = *ctx->h_summary;
-    if (ctx->summary.overflow) {
-        if (ctx->summary.overflow & 1) ctx->d_arena.ensure(ctx->summary.arena_used + 4096);
-        if (ctx->summary.overflow & 2) ctx->d_chunks.ensure(ctx->summary.n_chunks + 1024);
-        if (ctx->summary.overflow & 4) ctx->d_sets.ensure(ctx->summary.n_sets + 1024);
-        return 1;  // retry
-    }
+    // Decode launches.  The record counts per slot are known on the device
+    // only; reading them back costs a host round trip in the middle of the
+    // pipeline.  In steady state (same slots as the previous batch) the
+    // decode kernels of the slots that had records last time are launched
+    // right away, with grid-strided geometry that needs no counts, and the
+    // counts are checked after the final synchronisation: a slot that gained
+    // records is decoded then, and processed counts / statuses are redone.
     const uint32_t grid = (uint32_t)ctx->n_cus * ctx->blocks_per_cu;  // 256-thread blocks
-    bool generic = false;
-    HIPCHK(hipEventRecord(ctx->ev[1], st));
-    for (uint32_t s = 0; s < S; ++s) {
-        const SlotRT &rt = ctx->h_slots[s];
-        if (!rt.total || (rt.mode == NGZ_MODE_CHUNK && !rt.nchunks)) continue;
+    const bool predict = ctx->pred_valid && ctx->pred_versions == ctx->slot_version && !hf;
+    // launch the decode of slot s (rt: its counts when known)
+    auto launch_slot = [&](uint32_t s, const SlotRT *rt, bool &generic) -> int {
         const Version &v = ctx->versions[ctx->slot_version[s]];
-        if (!v.plan.rpl) continue;
+        if (!v.plan.rpl) return 0;
         if (ctx->specialize && v.rtc_state == 1 && !v.plan.has_vlen) {
             // one specialised kernel per active template, over that slot's chunks only
             uint32_t g, block = 256;
             if (v.plan.lds_waves) {
                 // one workgroup per window of 256*lds_waves rows (grid-strided)
                 const uint32_t rows = NGZ_REG_WINDOW * v.plan.lds_waves;
-                g = std::min<uint32_t>((uint32_t)ctx->n_cus * ctx->lds_blocks_per_cu, (rt.total + rows - 1) / rows);
+                g = (uint32_t)ctx->n_cus * ctx->lds_blocks_per_cu;
+                if (rt) g = std::min<uint32_t>(g, (rt->total + rows - 1) / rows);
                 block = 64 * v.plan.lds_waves;
             } else {
-                const uint32_t units =
-                    rt.mode == NGZ_MODE_ROW ? (rt.total + NGZ_REG_WINDOW - 1) / NGZ_REG_WINDOW : rt.nchunks;
-                g = std::min<uint32_t>(grid, (units + 3) / 4);
+                g = grid;
+                if (rt) {
+                    const uint32_t units =
+                        rt->mode == NGZ_MODE_ROW ? (rt->total + NGZ_REG_WINDOW - 1) / NGZ_REG_WINDOW : rt->nchunks;
+                    g = std::min<uint32_t>(grid, (units + 3) / 4);
+                }
             }
-            if (ngz_rtc_launch(v.rtc_fn, &B, s, g, block, st)) return fail(ctx, NGZ_E_DEVICE, "specialised decode launch");
+            if (g && ngz_rtc_launch(v.rtc_fn, &B, s, g, block, st)) return fail(ctx, NGZ_E_DEVICE, "specialised decode launch");
         } else {
             generic = true;
         }
+        return 0;
+    };
+    auto read_back = [&]() -> int {
+        HIPCHK(hipMemcpyAsync(ctx->h_summary, ctx->d_summary.p, sizeof(BatchSummary), hipMemcpyDeviceToHost, st));
+        if (S) HIPCHK(hipMemcpyAsync(ctx->h_slots, ctx->d_slots.p, S * sizeof(SlotRT), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        ctx->summary = *ctx->h_summary;
+        if (ctx->summary.overflow) {
+            if (ctx->summary.overflow & 1) ctx->d_arena.ensure(ctx->summary.arena_used + 4096);
+            if (ctx->summary.overflow & 2) ctx->d_chunks.ensure(ctx->summary.n_chunks + 1024);
+            if (ctx->summary.overflow & 4) ctx->d_sets.ensure(ctx->summary.n_sets + 1024);
+            ctx->pred_valid = false;
+            return 1;  // retry
+        }
+        return 0;
+    };
+    std::vector<uint8_t> launched(S, 0);
+    bool generic = false;
+    if (!predict) {
+        // the kernels that run depend on the per-slot counts: read them first
+        const int r = read_back();
+        if (r) return r;
+    }
+    HIPCHK(hipEventRecord(ctx->ev[1], st));
+    for (uint32_t s = 0; s < S; ++s) {
+        if (predict) {
+            if (!ctx->pred_active[s]) continue;
+            if (launch_slot(s, nullptr, generic)) return -1;
+        } else {
+            const SlotRT &rt = ctx->h_slots[s];
+            if (!rt.total || (rt.mode == NGZ_MODE_CHUNK && !rt.nchunks)) continue;
+            if (launch_slot(s, &rt, generic)) return -1;
+        }
+        launched[s] = 1;
     }
     if (generic && ngz_launch_decode_generic(&B, grid, st)) return fail(ctx, NGZ_E_DEVICE, "decode launch");
     HIPCHK(hipEventRecord(ctx->ev[2], st));
     if (ngz_launch_counts(&B, ctx->d_sets.cap, st)) return fail(ctx, NGZ_E_DEVICE, "counts launch");
     HIPCHK(hipEventRecord(ctx->ev[3], st));
+    if (predict) {
+        const int r = read_back();
+        if (r) return r;
+        // slots that gained records since the last batch
+        bool missed = false, generic2 = false;
+        for (uint32_t s = 0; s < S; ++s) {
+            const SlotRT &rt = ctx->h_slots[s];
+            if (launched[s] || !rt.total || (rt.mode == NGZ_MODE_CHUNK && !rt.nchunks)) continue;
+            missed = true;
+            const Version &v = ctx->versions[ctx->slot_version[s]];
+            const bool spec = ctx->specialize && v.rtc_state == 1 && !v.plan.has_vlen;
+            if (!spec && generic) continue;  // the generic kernel walked every non-specialised slot
+            if (launch_slot(s, &rt, generic2)) return -1;
+            launched[s] = 1;
+        }
+        if (missed) {
+            if (generic2 && ngz_launch_decode_generic(&B, grid, st)) return fail(ctx, NGZ_E_DEVICE, "decode launch");
+            HIPCHK(hipMemsetAsync(ctx->d_proc.p, 0, std::max<uint32_t>(S, 1) * 8, st));
+            if (ngz_launch_counts(&B, ctx->d_sets.cap, st)) return fail(ctx, NGZ_E_DEVICE, "counts launch");
+            HIPCHK(hipEventRecord(ctx->ev[3], st));
+        }
+    }
+    // slot counts and processed_count increments for finish_batch, with the same synchronisation
+    if (S) {
+        HIPCHK(hipMemcpyAsync(ctx->h_slots, ctx->d_slots.p, S * sizeof(SlotRT), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(ctx->h_proc, ctx->d_proc.p, S * 8, hipMemcpyDeviceToHost, st));
+    }
     HIPCHK(hipStreamSynchronize(st));
+    // slots with records this batch: launched without a round trip next time
+    ctx->pred_versions = ctx->slot_version;
+    ctx->pred_active.assign(S, 0);
+    for (uint32_t s = 0; s < S; ++s) {
+        const SlotRT &rt = ctx->h_slots[s];
+        ctx->pred_active[s] = rt.total && !(rt.mode == NGZ_MODE_CHUNK && !rt.nchunks);
+    }
+    ctx->pred_valid = !hf;
     hipEventElapsedTime(&ctx->t_decode, ctx->ev[1], ctx->ev[2]);
     hipEventElapsedTime(&ctx->t_pipeline, ctx->ev[0], ctx->ev[3]);
     return 0;
@@ -960,13 +1032,10 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
 
 int finish_batch(ngz_ctx *ctx, const ngz_batch_in *in, ngz_batch_out *out, hipStream_t st) {
     const uint32_t S = (uint32_t)ctx->slot_version.size();
-    ctx->slot_rt.resize(S);
-    std::vector<unsigned long long> proc(S);
-    if (S) {
-        HIPCHK(hipMemcpyAsync(ctx->slot_rt.data(), ctx->d_slots.p, S * sizeof(SlotRT), hipMemcpyDeviceToHost, st));
-        HIPCHK(hipMemcpyAsync(proc.data(), ctx->d_proc.p, S * 8, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
-    }
+    (void)st;
+    // run_pipeline left the slot table and the processed_count increments in pinned memory
+    ctx->slot_rt.assign(ctx->h_slots, ctx->h_slots + S);
+    std::vector<unsigned long long> proc(ctx->h_proc, ctx->h_proc + S);
     ctx->slot_infos.resize(S);
     for (uint32_t s = 0; s < S; ++s) {
         Version &v = ctx->versions[ctx->slot_version[s]];
@@ -1016,7 +1085,8 @@ int ngz_ctx_create(int device, ngz_ctx **out) {
     for (auto &e : ctx->ev) hipEventCreate(&e);
     hipDeviceGetAttribute(&ctx->n_cus, hipDeviceAttributeMultiprocessorCount, device);
     if (hipHostMalloc((void **)&ctx->h_summary, sizeof(BatchSummary), 0) != hipSuccess ||
-        hipHostMalloc((void **)&ctx->h_slots, NGZ_MAX_SLOTS * sizeof(SlotRT), 0) != hipSuccess) {
+        hipHostMalloc((void **)&ctx->h_slots, NGZ_MAX_SLOTS * sizeof(SlotRT), 0) != hipSuccess ||
+        hipHostMalloc((void **)&ctx->h_proc, NGZ_MAX_SLOTS * sizeof(unsigned long long), 0) != hipSuccess) {
         ngz_ctx_destroy(ctx);
         return NGZ_E_NOMEM;
     }
@@ -1040,6 +1110,7 @@ void ngz_ctx_destroy(ngz_ctx *ctx) {
     for (auto &e : ctx->ev) hipEventDestroy(e);
     if (ctx->h_summary) hipHostFree(ctx->h_summary);
     if (ctx->h_slots) hipHostFree(ctx->h_slots);
+    if (ctx->h_proc) hipHostFree(ctx->h_proc);
     hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -1227,6 +1298,23 @@ int ngz_decode_batch_host(ngz_ctx *ctx, const uint8_t *bytes, uint64_t bytes_siz
     HIPCHK(hipMemcpyAsync(ctx->d_in_len.p, lengths, n * 4ull, hipMemcpyHostToDevice, ctx->stream));
     ngz_batch_in in{ctx->d_in_bytes.p, bytes_size, ctx->d_in_off.p, ctx->d_in_len.p, n};
     return ngz_decode_batch(ctx, &in, out, nullptr);
+}
+
+int64_t ngz_columns_to_host(ngz_ctx *ctx, void *dst, uint64_t cap) {
+    if (!ctx || (!dst && cap)) return NGZ_E_INVALID;
+    HIPCHK(hipSetDevice(ctx->device));
+    uint64_t at = 0;
+    for (size_t s = 0; s < ctx->slot_infos.size(); ++s) {
+        const ngz_slot_info &si = ctx->slot_infos[s];
+        if (!si.n_records) continue;
+        const uint64_t bytes = (uint64_t)si.capacity * ctx->versions[si.version_id].plan.row_bytes;
+        at = (at + 255) & ~255ull;
+        if (at + bytes > cap) return fail(ctx, NGZ_E_INVALID, "ngz_columns_to_host: destination too small");
+        HIPCHK(hipMemcpyAsync((uint8_t *)dst + at, si.columns, bytes, hipMemcpyDeviceToHost, ctx->stream));
+        at += bytes;
+    }
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return (int64_t)at;
 }
 
 int ngz_slot_fields(ngz_ctx *ctx, uint32_t slot, ngz_field_info *fields, uint32_t cap) {

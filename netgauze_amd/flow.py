@@ -172,6 +172,14 @@ class FlowInfoCodec:
                                                 ctypes.byref(out)))
         return DecodedBatch(self, out)
 
+    def columns_to_host(self, host_ptr, cap):
+        """D2H of the last batch's column blocks (slot order, 256-byte aligned)
+        on the context's stream; returns the bytes written."""
+        n = lib().ngz_columns_to_host(self._ctx, host_ptr, cap)
+        if n < 0:
+            self._check(int(n))
+        return int(n)
+
     def templates(self, proto):
         n = lib().ngz_templates_json(self._ctx, proto, None, 0)
         buf = ctypes.create_string_buffer(n + 1)

@@ -89,6 +89,39 @@ def test_t20_steady_state_batches(dev):
     assert codec.template_counts(10) == {256: oc.ipfix_templates[256].processed_count}
 
 
+def test_steady_state_active_templates_change(dev):
+    """Batches after the first launch the decode kernels of the templates
+    that had records in the previous batch without a host round trip; a
+    template that gains records (or loses them) in a later batch must still
+    decode bit-exact, with processed counts and statuses redone."""
+    from netgauze_amd import synth
+    tpls = synth.CFG3_TEMPLATES[:3]
+    codec = new_codec()
+    oc = O.FlowInfoCodec()
+    tm = synth.templates_message(tpls)
+    codec.decode_datagrams([tm])
+    oc.decode(bytearray(tm))
+
+    def stream(ids, n, seed):
+        dgrams = []
+        for i, tid in enumerate(ids):
+            fields = dict(tpls)[tid]
+            rec = synth.template_records(fields, n, seed + i)
+            _, rl = synth.field_offsets(fields)
+            buf, offs, lens = synth.ipfix_data_stream(rec, rl, tid=tid, rec_per_msg=max(1, 60000 // rl))
+            b = bytes(buf.numpy())
+            dgrams += [b[o:o + ln] for o, ln in zip(offs.tolist(), lens.tolist())]
+        return dgrams
+
+    for ids, seed in (([256], 11), ([256], 12), ([256, 347], 13), ([348], 14), ([256, 347, 348], 15)):
+        data = stream(ids, 3000, seed)
+        batch = codec.decode_datagrams(data)
+        oracle, _ = parity.oracle_datagrams(data, oc)
+        stats = parity.check_batch(batch, oracle)
+        assert stats["records"] == 3000 * len(ids), (ids, stats)
+        assert codec.template_counts(10) == {t: oc.ipfix_templates[t].processed_count for t, _ in tpls}
+
+
 def test_t20_device_resident_large(dev):
     """Full-column check at 10^6 records against big-endian numpy views."""
     from netgauze_amd import synth
