@@ -169,6 +169,28 @@ int ngz_slot_fields(ngz_ctx *ctx, uint32_t slot, ngz_field_info *fields, uint32_
  * Returns the string length (excluding NUL) or <0. */
 int ngz_dgram_error_json(ngz_ctx *ctx, uint32_t dgram, char *buf, size_t cap);
 
+/* serde_json text of the datagram's decoded FlowInfo (status OK) or of its
+ * FlowInfoCodecDecoderError (status ERROR), rendered from the last batch's
+ * columns: the reference's `serde_json::to_string(&flow_info)` for the same
+ * bytes (FlowInfo / IpfixPacket / NetFlowV9Packet Serialize, ipfix.rs:99-108,
+ * 212-221, 419-424; crates/pcap-decoder/src/handlers/mod.rs:64-80).  The whole
+ * batch is copied to the host on the first call after a decode.  Returns the
+ * length (excluding NUL; buf is truncated to cap) or <0 (NGZ_E_INVALID for
+ * NEED_MORE / UNSUPPORTED datagrams). */
+int64_t ngz_dgram_json(ngz_ctx *ctx, uint32_t dgram, char *buf, size_t cap);
+
+/* Line callback of ngz_batch_json: datagram index, NGZ_DG_OK / NGZ_DG_ERROR,
+ * the JSON text (not NUL-terminated), and the bytes FlowInfoCodec::decode
+ * consumed from the datagram (codec.rs:151-183).  Non-zero return stops. */
+typedef int (*ngz_json_line_fn)(void *user, uint32_t dgram, int status, const char *json, size_t len,
+                                uint32_t consumed);
+
+/* Render every datagram of the last batch that produced a FlowInfo or an
+ * error, in datagram order (one D2H of headers, sets and columns).
+ * host_bytes: the batch bytes in host memory (for variable-length values), or
+ * NULL to copy them from the device.  Returns the lines emitted or <0. */
+int64_t ngz_batch_json(ngz_ctx *ctx, const uint8_t *host_bytes, ngz_json_line_fn fn, void *user);
+
 /* Template introspection: serde_json text of the current template map for one
  * protocol (10 or 9): [{"id":..,"scope_field_specifiers":[..],"field_specifiers":[..]},..]. */
 int ngz_templates_json(ngz_ctx *ctx, int proto, char *buf, size_t cap);

@@ -1,4 +1,4 @@
-"""ctypes binding of the C ABI in include/ngz/flow_decode.h (libngz.so).
+"""ctypes binding of the C ABI in include/ngz/flow_decode.h and flow_ingest.h (libngz.so).
 
 The library is built in-tree by __graft_entry__.build() (hipcc, gfx950).  If
 it is missing this module raises at import: there is no CPU fallback.
@@ -20,8 +20,34 @@ ABI_FUNCTIONS = [
     "ngz_ctx_create", "ngz_ctx_destroy", "ngz_last_error", "ngz_decode_batch",
     "ngz_decode_batch_host", "ngz_slot_fields", "ngz_dgram_error_json",
     "ngz_templates_json", "ngz_template_counts", "ngz_last_timing", "ngz_ctx_set_option",
-    "ngz_template_kernel", "ngz_columns_to_host",
+    "ngz_template_kernel", "ngz_columns_to_host", "ngz_dgram_json", "ngz_batch_json",
 ]
+# include/ngz/flow_ingest.h
+INGEST_FUNCTIONS = [
+    "ngz_pcap_open", "ngz_pcap_next", "ngz_pcap_close", "ngz_collector_create", "ngz_collector_destroy",
+    "ngz_collector_last_error", "ngz_collector_push", "ngz_collector_flush", "ngz_collector_peers",
+    "ngz_udp_recv", "ngz_pcap_to_jsonl",
+]
+NGZ_COLLECT_PCAP_DECODER, NGZ_COLLECT_FLOW_INFO = 0, 1
+NGZ_PROTO_TCP, NGZ_PROTO_UDP = 6, 17
+
+# ngz_json_line_fn(user, dgram, status, json, len, consumed)
+JSON_LINE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int,
+                                ctypes.POINTER(ctypes.c_char), ctypes.c_size_t, ctypes.c_uint32)
+# ngz_collect_line_fn(user, tag, line, len)
+COLLECT_LINE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_char),
+                                   ctypes.c_size_t)
+
+
+class PeerKey(ctypes.Structure):
+    _fields_ = [("family", ctypes.c_uint8), ("reserved", ctypes.c_uint8 * 3), ("src", ctypes.c_uint8 * 16),
+                ("dst", ctypes.c_uint8 * 16), ("src_port", ctypes.c_uint16), ("dst_port", ctypes.c_uint16)]
+
+
+class Packet(ctypes.Structure):
+    _fields_ = [("key", PeerKey), ("proto", ctypes.c_uint8), ("reserved", ctypes.c_uint8 * 7),
+                ("frame", ctypes.c_uint64), ("payload", ctypes.POINTER(ctypes.c_uint8)), ("len", ctypes.c_uint32),
+                ("reserved2", ctypes.c_uint32)]
 
 
 class BatchIn(ctypes.Structure):
@@ -87,6 +113,34 @@ def load():
     lib.ngz_template_kernel.restype = I
     lib.ngz_ctx_set_option.argtypes = [P, I, ctypes.c_int64]
     lib.ngz_ctx_set_option.restype = I
+    lib.ngz_dgram_json.argtypes = [P, U32, ctypes.c_char_p, ctypes.c_size_t]
+    lib.ngz_dgram_json.restype = ctypes.c_int64
+    lib.ngz_batch_json.argtypes = [P, P, JSON_LINE_FN, P]
+    lib.ngz_batch_json.restype = ctypes.c_int64
+    # ingest (flow_ingest.h)
+    lib.ngz_pcap_open.argtypes = [ctypes.c_char_p, ctypes.POINTER(P)]
+    lib.ngz_pcap_open.restype = I
+    lib.ngz_pcap_next.argtypes = [P, ctypes.POINTER(Packet)]
+    lib.ngz_pcap_next.restype = I
+    lib.ngz_pcap_close.argtypes = [P]
+    lib.ngz_pcap_close.restype = None
+    lib.ngz_collector_create.argtypes = [I, I, ctypes.POINTER(P)]
+    lib.ngz_collector_create.restype = I
+    lib.ngz_collector_destroy.argtypes = [P]
+    lib.ngz_collector_destroy.restype = None
+    lib.ngz_collector_last_error.argtypes = [P]
+    lib.ngz_collector_last_error.restype = ctypes.c_char_p
+    lib.ngz_collector_push.argtypes = [P, ctypes.POINTER(PeerKey), P, U32, U64]
+    lib.ngz_collector_push.restype = I
+    lib.ngz_collector_flush.argtypes = [P, COLLECT_LINE_FN, P]
+    lib.ngz_collector_flush.restype = ctypes.c_int64
+    lib.ngz_collector_peers.argtypes = [P]
+    lib.ngz_collector_peers.restype = U32
+    lib.ngz_udp_recv.argtypes = [I, P, U64, ctypes.POINTER(PeerKey), P, P, U32, I]
+    lib.ngz_udp_recv.restype = I
+    lib.ngz_pcap_to_jsonl.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_uint16), U32, ctypes.c_char_p, I,
+                                      ctypes.c_int64, I]
+    lib.ngz_pcap_to_jsonl.restype = ctypes.c_int64
     return lib
 
 

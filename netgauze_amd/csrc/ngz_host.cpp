@@ -24,6 +24,9 @@
 
 #include "ngz/flow_decode.h"
 #include "ngz_internal.h"
+#include "ngz_host.h"
+
+using namespace ngzh;
 
 extern "C" int ngz_launch_frame(const BatchDev *B, const uint32_t *hf_flag, const uint32_t *hf_first, hipStream_t st);
 extern "C" int ngz_scan_temp_bytes(uint64_t n_items, size_t *bytes);
@@ -43,25 +46,6 @@ namespace {
 // ------------------------------------------------------------------------
 // IE registry (generated from the reference XML, tools/gen_ie_registry.py)
 // ------------------------------------------------------------------------
-enum DataType : uint8_t {
-    DT_octetArray = 0, DT_unsigned8, DT_unsigned16, DT_unsigned32, DT_unsigned64, DT_signed8, DT_signed16,
-    DT_signed32, DT_signed64, DT_float32, DT_float64, DT_boolean, DT_macAddress, DT_string, DT_dateTimeSeconds,
-    DT_dateTimeMilliseconds, DT_dateTimeMicroseconds, DT_dateTimeNanoseconds, DT_ipv4Address, DT_ipv6Address,
-    DT_basicList, DT_subTemplateList, DT_subTemplateMultiList, DT_unsigned256,
-};
-
-struct IeRow {
-    uint32_t pen;
-    uint16_t id;
-    uint8_t dtype;
-    uint8_t flags;  // 1 mpls, 2 tcpControlBits, 4 sub-registry
-    const char *name;
-};
-struct VendorRow {
-    uint32_t pen;
-    const char *name;
-};
-
 #define NGZ_IE(pen, id, dt, fl, nm) {pen, (uint16_t)(id), (uint8_t)(dt), (uint8_t)(fl), nm},
 #define NGZ_VENDOR(pen, nm)
 const IeRow kIes[] = {
@@ -109,31 +93,9 @@ void length_range(uint8_t dt, int &lo, int &hi) {
 // ------------------------------------------------------------------------
 // Template model
 // ------------------------------------------------------------------------
-enum IeKind : uint8_t { IK_IANA, IK_VENDOR, IK_VENDOR_UNKNOWN, IK_UNKNOWN, IK_SCOPE };
+}  // namespace
 
-struct Spec {
-    IeKind kind;
-    uint8_t dtype;
-    uint8_t flags;
-    bool scope;
-    uint32_t pen;
-    uint16_t id;  // scope: raw code
-    uint16_t length;
-    const char *name;    // IANA/vendor IE name
-    const char *vendor;  // vendor display name
-};
-
-struct Version {
-    uint8_t proto;  // 10 / 9
-    uint16_t tid;
-    std::vector<Spec> specs;  // scope first
-    uint32_t n_scope;
-    DevPlan plan;
-    std::vector<uint8_t> fail_sub;  // per field: 1 InvalidLength, 2 InvalidPaddingLength, 3 scope InvalidLength
-    uint64_t processed = 0;
-    int rtc_state = 0;              // specialised kernel: 0 not looked up, 1 ready, 2 unavailable
-    void *rtc_fn = nullptr;
-};
+namespace ngzh {
 
 std::string json_str(const char *s) {
     std::string o = "\"";
@@ -180,6 +142,14 @@ std::string spec_json(const Spec &s) {
     snprintf(b, sizeof b, ",\"length\":%u}", s.length);
     return "{\"element_id\":" + ie_json(s) + b;
 }
+
+std::string wrap(const char *tag, const std::string &inner) { return std::string("{\"") + tag + "\":" + inner + "}"; }
+
+const IeRow *ie_find(uint32_t pen, uint16_t id) { return ies().find(pen, id); }
+
+}  // namespace ngzh
+
+namespace {
 
 // Decode rule of one field (generator.rs:1439-1807 by data type;
 // netflow.rs:443-475 for NFv9 scope fields) -> device kind and column width.
@@ -295,94 +265,6 @@ void build_plan(Version &v) {
     P.lds_waves = (P.rpl && !vlen && lds_on) ? ngz_lds_waves(P.row_bytes) : 0;
 }
 
-struct ErrInfo {  // host-side framing error
-    std::string json;
-};
-
-// ------------------------------------------------------------------------
-// Context
-// ------------------------------------------------------------------------
-template <class T>
-struct DevBuf {
-    T *p = nullptr;
-    size_t cap = 0;
-    int ensure(size_t n) {
-        if (n <= cap) return 0;
-        if (p) hipFree(p);
-        p = nullptr;
-        size_t c = std::max(n, cap + cap / 2);
-        if (hipMalloc((void **)&p, c * sizeof(T) + 64) != hipSuccess) {
-            cap = 0;
-            return -1;
-        }
-        cap = c;
-        return 0;
-    }
-    void release() {
-        if (p) hipFree(p);
-        p = nullptr;
-        cap = 0;
-    }
-};
-
-}  // namespace
-
-struct ngz_ctx {
-    int device = 0;
-    hipStream_t stream = nullptr;
-    std::string last_error;
-    std::vector<Version> versions;              // append-only
-    std::vector<int32_t> cur[2];                // [proto idx][template id] -> version or -1
-    // batch
-    std::vector<int32_t> slot_version;          // slot -> version
-    std::vector<int32_t> version_slot;          // version -> slot (this batch) or -1
-    DevBuf<DevPlan> d_plans;
-    DevBuf<uint16_t> d_cur_slot;
-    DevBuf<uint32_t> d_tl_key, d_tl_dgram;
-    DevBuf<uint16_t> d_tl_slot;
-    DevBuf<uint32_t> d_hf_flag;
-    DevBuf<ngz_dgram_hdr> d_hf_hdr;
-    DevBuf<uint32_t> d_hf_first;
-    DevBuf<HostSet> d_hf_sets;
-    DevBuf<ngz_dgram_hdr> d_hdr;
-    DevBuf<uint32_t> d_counts, d_scan;
-    DevBuf<uint8_t> d_scan_tmp;
-    DevBuf<SlotRT> d_slots;
-    DevBuf<Chunk> d_chunks;
-    DevBuf<ngz_set_info> d_sets;
-    DevBuf<uint8_t> d_arena;
-    DevBuf<unsigned long long> d_proc;
-    DevBuf<BatchSummary> d_summary;
-    // host staging for ngz_decode_batch_host
-    DevBuf<uint8_t> d_in_bytes;
-    DevBuf<uint64_t> d_in_off;
-    DevBuf<uint32_t> d_in_len;
-    // results of the last batch
-    std::vector<ngz_slot_info> slot_infos;
-    std::vector<SlotRT> slot_rt;
-    std::vector<ErrInfo> host_errors;
-    BatchSummary summary{};
-    ngz_batch_in last_in{};
-    hipEvent_t ev[4]{};
-    int n_cus = 256;
-    int specialize = 1;                         // NGZ_OPT_SPECIALIZE
-    uint32_t blocks_per_cu = 4;                 // decode grid: 4 x 256 threads per CU
-    uint32_t lds_blocks_per_cu = 8;             // LDS-staged decode grid (2 resident per CU at 64 KB)
-    BatchSummary *h_summary = nullptr;          // pinned
-    SlotRT *h_slots = nullptr;                  // pinned, NGZ_MAX_SLOTS
-    unsigned long long *h_proc = nullptr;       // pinned, NGZ_MAX_SLOTS: processed_count increments
-    float t_decode = 0, t_pipeline = 0;
-    bool plans_dirty = true;
-    uint32_t n_template_dgrams = 0;
-    uint64_t tmpl_gen = 1, uploaded_gen = 0;  // template-state generation vs the device tables
-    // steady-state decode launches (run_pipeline): the slots of the last batch
-    bool pred_valid = false;
-    std::vector<int32_t> pred_versions;
-    std::vector<uint8_t> pred_active;
-};
-
-namespace {
-
 int fail(ngz_ctx *c, int code, const char *msg) {
     if (c) c->last_error = msg;
     return code;
@@ -397,8 +279,6 @@ int fail(ngz_ctx *c, int code, const char *msg) {
         }                                                                           \
     } while (0)
 
-uint32_t rd16(const uint8_t *p) { return ((uint32_t)p[0] << 8) | p[1]; }
-uint32_t rd32(const uint8_t *p) { return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3]; }
 
 // ------------------------------------------------------------------------
 // Host framing of a template-bearing datagram (stream order).  Restates
@@ -409,7 +289,22 @@ struct HostFrameOut {
     ngz_dgram_hdr hdr{};
     std::vector<HostSet> sets;
     std::vector<std::pair<uint32_t, int32_t>> defs;  // (set position, version) defined here
+    std::vector<std::pair<uint32_t, std::string>> tsets;  // (set position, serde JSON) of template sets
 };
+
+// serde JSON of a parsed (options) template record (ipfix.rs:384-413 /
+// :276-327, netflow.rs:265-353; TemplateRecord has no scope key)
+std::string template_record_json(uint32_t tid, const std::vector<Spec> *scope, const std::vector<Spec> &fields) {
+    std::string j = "{\"id\":" + std::to_string(tid);
+    if (scope) {
+        j += ",\"scope_field_specifiers\":[";
+        for (size_t i = 0; i < scope->size(); ++i) j += (i ? "," : "") + spec_json((*scope)[i]);
+        j += "]";
+    }
+    j += ",\"field_specifiers\":[";
+    for (size_t i = 0; i < fields.size(); ++i) j += (i ? "," : "") + spec_json(fields[i]);
+    return j + "]}";
+}
 
 struct Eof {
     uint32_t offset, needed, available;
@@ -505,7 +400,6 @@ bool parse_scope_spec(Cur &c, Spec &out, std::string &err) {
     return true;
 }
 
-std::string wrap(const char *tag, const std::string &inner) { return std::string("{\"") + tag + "\":" + inner + "}"; }
 
 int32_t define_template(ngz_ctx *ctx, uint8_t proto, uint16_t tid, std::vector<Spec> &&scope, std::vector<Spec> &&fields) {
     Version v;
@@ -567,6 +461,7 @@ void host_frame(ngz_ctx *ctx, const uint8_t *p, uint32_t dl, uint32_t limit, Hos
             h.n_sets++;
             Cur c{p, pos + 4, pos + sl};
             if (id == 2) {  // ipfix.rs:162-168, TemplateRecord::parse :384-413
+                std::string recs;
                 while (c.pos < c.end) {
                     const uint32_t toff = c.pos;
                     Eof e;
@@ -586,9 +481,12 @@ void host_frame(ngz_ctx *ctx, const uint8_t *p, uint32_t dl, uint32_t limit, Hos
                         if (!parse_field_spec(c, s, err)) { terr(wrap("FieldSpecifierError", err)); return; }
                         fields.push_back(s);
                     }
+                    recs += (recs.empty() ? "" : ",") + template_record_json(tid, nullptr, fields);
                     o.defs.push_back({toff, define_template(ctx, 10, (uint16_t)tid, {}, std::move(fields))});
                 }
+                o.tsets.push_back({pos, "{\"Template\":[" + recs + "]}"});
             } else if (id == 3) {  // ipfix.rs:169-181, OptionsTemplateRecord::parse :276-327
+                std::string recs;
                 while (c.end - c.pos > 3) {
                     const uint32_t toff = c.pos;
                     Eof e;
@@ -617,6 +515,7 @@ void host_frame(ngz_ctx *ctx, const uint8_t *p, uint32_t dl, uint32_t limit, Hos
                         if (!parse_field_spec(c, s, err)) { terr(wrap("FieldError", err)); return; }
                         (i < scount ? scope : fields).push_back(s);
                     }
+                    recs += (recs.empty() ? "" : ",") + template_record_json(tid, &scope, fields);
                     o.defs.push_back({toff, define_template(ctx, 10, (uint16_t)tid, std::move(scope), std::move(fields))});
                 }
                 for (uint32_t q = c.pos; q < c.end; ++q)  // check_padding_value (ipfix.rs:240-251)
@@ -624,6 +523,7 @@ void host_frame(ngz_ctx *ctx, const uint8_t *p, uint32_t dl, uint32_t limit, Hos
                         snprintf(b, sizeof b, "{\"InvalidPaddingValue\":{\"offset\":%u,\"value\":%u}}", q, p[q]);
                         serr(q, b); return;
                     }
+                o.tsets.push_back({pos, "{\"OptionsTemplate\":[" + recs + "]}"});
             } else {
                 const int32_t vid = ctx->cur[0][id];
                 if (vid < 0) {
@@ -672,6 +572,7 @@ void host_frame(ngz_ctx *ctx, const uint8_t *p, uint32_t dl, uint32_t limit, Hos
             h.n_sets++;
             Cur c{p, pos + 4, pos + sl};
             if (id == 0) {  // netflow.rs:172-178, TemplateRecord :324-353
+                std::string recs;
                 while (c.pos < c.end) {
                     const uint32_t toff = c.pos;
                     Eof e;
@@ -691,10 +592,13 @@ void host_frame(ngz_ctx *ctx, const uint8_t *p, uint32_t dl, uint32_t limit, Hos
                         if (!parse_field_spec(c, s, err)) { terr(wrap("FieldSpecifierError", err)); return; }
                         fields.push_back(s);
                     }
+                    recs += (recs.empty() ? "" : ",") + template_record_json(tid, nullptr, fields);
                     o.defs.push_back({toff, define_template(ctx, 9, (uint16_t)tid, {}, std::move(fields))});
                 }
+                o.tsets.push_back({pos, "{\"Template\":[" + recs + "]}"});
                 i -= 1;
             } else if (id == 1) {  // netflow.rs:179-190, OptionsTemplateRecord :265-310
+                std::string recs;
                 while (c.end - c.pos > 3) {
                     const uint32_t toff = c.pos;
                     Eof e;
@@ -726,6 +630,7 @@ void host_frame(ngz_ctx *ctx, const uint8_t *p, uint32_t dl, uint32_t limit, Hos
                         if (!parse_field_spec(oc, s, err)) { serr(oc.pos, wrap("OptionsTemplateRecordError", wrap("FieldSpecifierError", err))); return; }
                         fields.push_back(s);
                     }
+                    recs += (recs.empty() ? "" : ",") + template_record_json(tid, &scope, fields);
                     o.defs.push_back({toff, define_template(ctx, 9, (uint16_t)tid, std::move(scope), std::move(fields))});
                 }
                 for (uint32_t q = c.pos; q < c.end; ++q)
@@ -733,6 +638,7 @@ void host_frame(ngz_ctx *ctx, const uint8_t *p, uint32_t dl, uint32_t limit, Hos
                         snprintf(b, sizeof b, "{\"InvalidPaddingValue\":{\"offset\":%u,\"value\":%u}}", q, p[q]);
                         serr(q, b); return;
                     }
+                o.tsets.push_back({pos, "{\"OptionsTemplate\":[" + recs + "]}"});
                 i -= 1;
             } else {
                 const int32_t vid = ctx->cur[1][id];
@@ -1139,6 +1045,9 @@ int ngz_decode_batch(ngz_ctx *ctx, const ngz_batch_in *in, ngz_batch_out *out, v
     HIPCHK(hipSetDevice(ctx->device));
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : ctx->stream;
     ctx->host_errors.clear();
+    ctx->tmpl_sets.clear();
+    ctx->batch_serial++;
+    ctx->json_view.reset();
     memset(out, 0, sizeof *out);
     // snapshot of the template state at batch start (for the slow path)
     const size_t nver0 = ctx->versions.size();
@@ -1177,7 +1086,9 @@ int ngz_decode_batch(ngz_ctx *ctx, const ngz_batch_in *in, ngz_batch_out *out, v
     }
     ctx->n_template_dgrams = (uint32_t)host_idx.size();
     std::vector<uint32_t> limit(host_idx.size(), 0xFFFFFFFFu);
+    std::vector<TemplateSetJson> tsets;
     for (int round = 0; round < 16; ++round) {
+        tsets.clear();
         // roll the template state back to the batch start
         ctx->uploaded_gen = 0;  // device tables will describe the batch start, not the end state
         ctx->versions.resize(nver0);
@@ -1199,6 +1110,7 @@ int ngz_decode_batch(ngz_ctx *ctx, const ngz_batch_in *in, ngz_batch_out *out, v
             per.push_back({d, std::move(o.sets)});
             defs[i] = o.defs;
             for (auto &df : o.defs) tl_entries.push_back({(uint32_t)df.second, d});
+            for (auto &ts : o.tsets) tsets.push_back({d, ts.first, std::move(ts.second)});
         }
         std::vector<int32_t> extra;
         for (auto &t : tl_entries) extra.push_back((int32_t)t.first);
@@ -1284,6 +1196,7 @@ int ngz_decode_batch(ngz_ctx *ctx, const ngz_batch_in *in, ngz_batch_out *out, v
         }
         if (!redo) break;
     }
+    ctx->tmpl_sets = std::move(tsets);
     return finish_batch(ctx, in, out, st);
 }
 
@@ -1577,3 +1490,22 @@ extern "C" int ngz_template_kernel(const uint8_t *tmpl, size_t len, int compile,
     }
     return rc;
 }
+
+namespace ngzh {
+
+void state_save(ngz_ctx *ctx, TemplateState &s) {
+    s.versions = ctx->versions;
+    s.cur[0] = ctx->cur[0];
+    s.cur[1] = ctx->cur[1];
+}
+
+void state_restore(ngz_ctx *ctx, const TemplateState &s) {
+    ctx->versions = s.versions;
+    ctx->cur[0] = s.cur[0];
+    ctx->cur[1] = s.cur[1];
+    ctx->tmpl_gen++;  // device plan tables are re-uploaded by the next batch
+    ctx->plans_dirty = true;
+    ctx->pred_valid = false;
+}
+
+}  // namespace ngzh

@@ -1,0 +1,211 @@
+// Host-side internals shared by ngz_host.cpp (C ABI, template registry,
+// batch pipeline), ngz_json.cpp (serde-JSON rendering of decoded datagrams)
+// and ngz_collector.cpp (per-peer stream framing, pcap/UDP ingest).  Not part
+// of the C ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "ngz/flow_decode.h"
+#include "ngz_internal.h"
+
+namespace ngzh {
+
+// ------------------------------------------------------------------------
+// IE registry rows (generated from the reference XML, tools/gen_ie_registry.py)
+// ------------------------------------------------------------------------
+enum DataType : uint8_t {
+    DT_octetArray = 0, DT_unsigned8, DT_unsigned16, DT_unsigned32, DT_unsigned64, DT_signed8, DT_signed16,
+    DT_signed32, DT_signed64, DT_float32, DT_float64, DT_boolean, DT_macAddress, DT_string, DT_dateTimeSeconds,
+    DT_dateTimeMilliseconds, DT_dateTimeMicroseconds, DT_dateTimeNanoseconds, DT_ipv4Address, DT_ipv6Address,
+    DT_basicList, DT_subTemplateList, DT_subTemplateMultiList, DT_unsigned256,
+};
+
+struct IeRow {
+    uint32_t pen;
+    uint16_t id;
+    uint8_t dtype;
+    uint8_t flags;  // 1 mpls, 2 tcpControlBits, 4 sub-registry
+    const char *name;
+};
+struct VendorRow {
+    uint32_t pen;
+    const char *name;
+};
+
+// (pen, id) -> registry row, or null
+const IeRow *ie_find(uint32_t pen, uint16_t id);
+
+// ------------------------------------------------------------------------
+// Template model
+// ------------------------------------------------------------------------
+enum IeKind : uint8_t { IK_IANA, IK_VENDOR, IK_VENDOR_UNKNOWN, IK_UNKNOWN, IK_SCOPE };
+
+struct Spec {
+    IeKind kind;
+    uint8_t dtype;
+    uint8_t flags;
+    bool scope;
+    uint32_t pen;
+    uint16_t id;  // scope: raw code
+    uint16_t length;
+    const char *name;    // IANA/vendor IE name
+    const char *vendor;  // vendor display name
+};
+
+struct Version {
+    uint8_t proto;  // 10 / 9
+    uint16_t tid;
+    std::vector<Spec> specs;  // scope first
+    uint32_t n_scope;
+    DevPlan plan;
+    std::vector<uint8_t> fail_sub;  // per field: 1 InvalidLength, 2 InvalidPaddingLength, 3 scope InvalidLength
+    uint64_t processed = 0;
+    int rtc_state = 0;              // specialised kernel: 0 not looked up, 1 ready, 2 unavailable
+    void *rtc_fn = nullptr;
+};
+
+// serde_json helpers (ngz_host.cpp)
+std::string json_str(const char *s);
+std::string ie_json(const Spec &s);    // IE / ScopeIE element_id value
+std::string spec_json(const Spec &s);  // FieldSpecifier / ScopeFieldSpecifier
+std::string wrap(const char *tag, const std::string &inner);
+
+inline uint32_t rd16(const uint8_t *p) { return ((uint32_t)p[0] << 8) | p[1]; }
+inline uint32_t rd32(const uint8_t *p) {
+    return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+
+struct ErrInfo {  // host-side framing error
+    std::string json;
+};
+
+// ------------------------------------------------------------------------
+// Context
+// ------------------------------------------------------------------------
+template <class T>
+struct DevBuf {
+    T *p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t n) {
+        if (n <= cap) return 0;
+        if (p) hipFree(p);
+        p = nullptr;
+        size_t c = std::max(n, cap + cap / 2);
+        if (hipMalloc((void **)&p, c * sizeof(T) + 64) != hipSuccess) {
+            cap = 0;
+            return -1;
+        }
+        cap = c;
+        return 0;
+    }
+    void release() {
+        if (p) hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+// serde JSON of one (options) template set of a host-framed datagram
+// ({"Template":[..]} / {"OptionsTemplate":[..]}), kept for the JSON renderer
+struct TemplateSetJson {
+    uint32_t dgram;
+    uint32_t set_pos;
+    std::string json;
+};
+
+// Host copies of one decoded batch for the JSON renderer (ngz_json.cpp)
+struct JsonView {
+    uint64_t serial = 0;                     // ngz_ctx::batch_serial it was loaded from
+    std::vector<ngz_dgram_hdr> hdr;
+    std::vector<ngz_set_info> sets;
+    std::vector<uint32_t> set_first;         // CSR: data sets of datagram d
+    std::vector<uint32_t> tset_first;        // CSR: ngz_ctx::tmpl_sets of datagram d
+    std::vector<std::vector<uint8_t>> cols;  // per slot: its column block (slots with records)
+    std::vector<uint8_t> own_bytes;          // D2H copy of the batch bytes when no host copy is given
+    const uint8_t *bytes = nullptr;          // batch bytes (host)
+    std::vector<uint64_t> offs;
+    std::vector<uint32_t> lens;
+};
+
+}  // namespace ngzh
+
+struct ngz_ctx;
+namespace ngzh {
+// Host template state of a context (both TemplatesMaps): saved before a
+// speculative batch and restored when its framing guess was wrong (ngz_collector.cpp)
+struct TemplateState {
+    std::vector<Version> versions;
+    std::vector<int32_t> cur[2];
+};
+void state_save(ngz_ctx *ctx, TemplateState &s);
+void state_restore(ngz_ctx *ctx, const TemplateState &s);
+// D2H of the last batch (host_bytes: the batch bytes already in host memory, or null)
+int json_view_load(ngz_ctx *ctx, const uint8_t *host_bytes, JsonView &v);
+// serde JSON of datagram d (FlowInfo, or the error) appended to `out`; returns its
+// NGZ_DG_* status and the bytes FlowInfoCodec::decode consumed from it
+// (codec.rs:151-183: IPFIX length, NFv9 end of the last parsed set, errors per the codec)
+int json_render(ngz_ctx *ctx, const JsonView &v, uint32_t d, std::string &out, uint32_t *consumed);
+}  // namespace ngzh
+
+struct ngz_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string last_error;
+    std::vector<ngzh::Version> versions;              // append-only
+    std::vector<int32_t> cur[2];                // [proto idx][template id] -> version or -1
+    // batch
+    std::vector<int32_t> slot_version;          // slot -> version
+    std::vector<int32_t> version_slot;          // version -> slot (this batch) or -1
+    ngzh::DevBuf<DevPlan> d_plans;
+    ngzh::DevBuf<uint16_t> d_cur_slot;
+    ngzh::DevBuf<uint32_t> d_tl_key, d_tl_dgram;
+    ngzh::DevBuf<uint16_t> d_tl_slot;
+    ngzh::DevBuf<uint32_t> d_hf_flag;
+    ngzh::DevBuf<ngz_dgram_hdr> d_hf_hdr;
+    ngzh::DevBuf<uint32_t> d_hf_first;
+    ngzh::DevBuf<HostSet> d_hf_sets;
+    ngzh::DevBuf<ngz_dgram_hdr> d_hdr;
+    ngzh::DevBuf<uint32_t> d_counts, d_scan;
+    ngzh::DevBuf<uint8_t> d_scan_tmp;
+    ngzh::DevBuf<SlotRT> d_slots;
+    ngzh::DevBuf<Chunk> d_chunks;
+    ngzh::DevBuf<ngz_set_info> d_sets;
+    ngzh::DevBuf<uint8_t> d_arena;
+    ngzh::DevBuf<unsigned long long> d_proc;
+    ngzh::DevBuf<BatchSummary> d_summary;
+    // host staging for ngz_decode_batch_host
+    ngzh::DevBuf<uint8_t> d_in_bytes;
+    ngzh::DevBuf<uint64_t> d_in_off;
+    ngzh::DevBuf<uint32_t> d_in_len;
+    // results of the last batch
+    std::vector<ngz_slot_info> slot_infos;
+    std::vector<SlotRT> slot_rt;
+    std::vector<ngzh::ErrInfo> host_errors;
+    BatchSummary summary{};
+    ngz_batch_in last_in{};
+    hipEvent_t ev[4]{};
+    int n_cus = 256;
+    int specialize = 1;                         // NGZ_OPT_SPECIALIZE
+    uint32_t blocks_per_cu = 4;                 // decode grid: 4 x 256 threads per CU
+    uint32_t lds_blocks_per_cu = 8;             // LDS-staged decode grid (2 resident per CU at 64 KB)
+    BatchSummary *h_summary = nullptr;          // pinned
+    SlotRT *h_slots = nullptr;                  // pinned, NGZ_MAX_SLOTS
+    unsigned long long *h_proc = nullptr;       // pinned, NGZ_MAX_SLOTS: processed_count increments
+    float t_decode = 0, t_pipeline = 0;
+    bool plans_dirty = true;
+    uint32_t n_template_dgrams = 0;
+    uint64_t tmpl_gen = 1, uploaded_gen = 0;  // template-state generation vs the device tables
+    // steady-state decode launches (run_pipeline): the slots of the last batch
+    bool pred_valid = false;
+    std::vector<int32_t> pred_versions;
+    std::vector<uint8_t> pred_active;
+    std::vector<ngzh::TemplateSetJson> tmpl_sets;  // template sets of the last batch, (dgram, set_pos) order
+    uint64_t batch_serial = 0;                      // bumped by every ngz_decode_batch
+    std::shared_ptr<ngzh::JsonView> json_view;      // ngz_dgram_json cache of the last batch
+};

@@ -110,6 +110,33 @@ class DecodedBatch:
         s = self.error_json(d)
         return None if s is None else json.loads(s)
 
+    def json(self, d):
+        """serde_json text of datagram d's FlowInfo (or of its error), rendered
+        from the decoded columns (ngz_dgram_json); None for Ok(None)."""
+        n = lib().ngz_dgram_json(self._codec._ctx, d, None, 0)
+        if n < 0:
+            return None
+        buf = ctypes.create_string_buffer(n + 1)
+        lib().ngz_dgram_json(self._codec._ctx, d, buf, n + 1)
+        return buf.raw[:n].decode("utf-8")
+
+    def json_lines(self):
+        """[(dgram, status, json, consumed)] for every datagram with a FlowInfo
+        or an error (ngz_batch_json: one host copy of the whole batch)."""
+        from netgauze_amd import _lib
+        out = []
+
+        def cb(_user, d, status, text, n, consumed):
+            out.append((int(d), int(status), ctypes.string_at(text, n).decode("utf-8"), int(consumed)))
+            return 0
+
+        fn = _lib.JSON_LINE_FN(cb)
+        host = self._source if isinstance(self._source, np.ndarray) else None
+        n = lib().ngz_batch_json(self._codec._ctx, host.ctypes.data if host is not None else None, fn, None)
+        if n < 0:
+            raise NgzError("ngz_batch_json failed: %d" % n)
+        return out
+
 
 OPT_SPECIALIZE = 1
 OPT_BLOCKS_PER_CU = 2

@@ -13,6 +13,8 @@ flow pcap the reference's pcap_tests.rs walks (assets/pcaps/pmacct-tests/*/
                  u8 ip-version, 16 B src ip, u16 src port, 16 B dst ip,
                  u16 dst port, u32 payload length, payload
   <name>.jsonl.gz the reference's expected output lines, verbatim (gzip)
+  <name>.pcap     (--pcaps) the capture itself, for captures up to 50 kB and the
+                 pcap-decoder golden: input of the product's pcap reader
 
 Extraction uses oracle/pcap.py; the goldens then pin both the extraction and
 the decoder (a wrong datagram would produce a mismatching line).
@@ -54,7 +56,29 @@ def write_case(name, pcap_path, ports, json_path):
     return n
 
 
+PCAP_FIXTURE_MAX = 50_000  # copy the small captures themselves (the product's pcap reader reads them)
+
+
+def copy_pcaps():
+    """<name>.pcap: the reference's own capture files (data its tests hold),
+    for the captures up to PCAP_FIXTURE_MAX bytes and the pcap-decoder golden."""
+    import shutil
+    n = 0
+    for p in sorted(glob.glob(REF + "/assets/pcaps/pmacct-tests/*/*.pcap") + glob.glob(REF + "/assets/pcaps/flow/*/*.pcap")):
+        j = p[:-len(".pcap")] + "-flow.json"
+        if not os.path.exists(j) or os.path.getsize(j) == 0 or os.path.getsize(p) > PCAP_FIXTURE_MAX:
+            continue
+        name = os.path.basename(os.path.dirname(p)) + "__" + os.path.basename(p)[:-5]
+        shutil.copyfile(p, os.path.join(HERE, name + ".pcap"))
+        n += 1
+    shutil.copyfile(REF + "/crates/pcap-decoder/tests/data/502-IPFIXv10-BGP-IPv6-CISCO-SRv6-lcomms.pcap",
+                    os.path.join(HERE, "pcap_decoder__502.pcap"))
+    print("copied %d captures + pcap_decoder__502.pcap" % n)
+
+
 def main():
+    if "--pcaps" in sys.argv:
+        return copy_pcaps()
     cases = []
     for p in sorted(glob.glob(REF + "/assets/pcaps/pmacct-tests/*/*.pcap") + glob.glob(REF + "/assets/pcaps/flow/*/*.pcap")):
         j = p[:-len(".pcap")] + "-flow.json"

@@ -7,17 +7,21 @@ import re
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADER = os.path.join(ROOT, "include", "ngz", "flow_decode.h")
+HEADERS = [os.path.join(ROOT, "include", "ngz", h) for h in ("flow_decode.h", "flow_ingest.h")]
 
 
-def declared_functions():
-    text = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(ngz_[a-z_0-9]+)\s*\(", text, re.M)))
+def declared_functions(headers=HEADERS):
+    names = set()
+    for h in headers:
+        text = open(h).read()
+        names |= set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(ngz_[a-z_0-9]+)\s*\(", text, re.M))
+    return sorted(names)
 
 
 def test_header_declares_abi():
     from netgauze_amd import _lib
-    assert declared_functions() == sorted(_lib.ABI_FUNCTIONS)
+    assert declared_functions(HEADERS[:1]) == sorted(_lib.ABI_FUNCTIONS)
+    assert declared_functions(HEADERS[1:]) == sorted(_lib.INGEST_FUNCTIONS)
 
 
 def test_library_exports_every_declared_symbol():
