@@ -148,6 +148,9 @@ const char *ngz_last_error(ngz_ctx *ctx);
                                    compiled at run time (hiprtc) and cached by layout; 0: the generic
                                    field-table kernel for every template */
 #define NGZ_OPT_BLOCKS_PER_CU 2 /* decode grid size: 256-thread blocks per CU (default 4) */
+#define NGZ_OPT_CAP_PAD 4       /* extra row windows of column capacity per template slot (column spacing) */
+#define NGZ_OPT_ARENA_SHIFT 3   /* bytes (multiple of 256) the column blocks start into the context's
+                                   device arena: moves the output onto other HBM pages */
 int ngz_ctx_set_option(ngz_ctx *ctx, int opt, int64_t value);
 
 /* --- decode ------------------------------------------------------------- */

@@ -40,6 +40,10 @@ std::string ngz_rtc_source(const DevPlan &P);
 int ngz_rtc_compile_only(const DevPlan &P, std::string *log_out);
 int ngz_rtc_launch(void *fn, const BatchDev *B, uint32_t slot, uint32_t grid, uint32_t block, hipStream_t st);
 extern "C" int ngz_launch_counts(const BatchDev *B, uint64_t set_cap, hipStream_t st);
+extern "C" int ngz_launch_export(const BatchDev *B, BatchSummary *h_summary, SlotRT *h_slots,
+                                 unsigned long long *h_proc, BatchSummary *next_summary,
+                                 unsigned long long *next_proc, unsigned long long *h_done, unsigned long long seq,
+                                 hipStream_t st);
 
 namespace {
 
@@ -696,6 +700,7 @@ int assign_slots(ngz_ctx *ctx, const std::vector<int32_t> &extra) {
     }
     ctx->version_slot.assign(ctx->versions.size(), -1);
     for (size_t s = 0; s < sv.size(); ++s) ctx->version_slot[sv[s]] = (int32_t)s;
+    ctx->assigned_gen = extra.empty() ? ctx->tmpl_gen : 0;  // reused until the template state changes
     return 0;
 }
 
@@ -753,13 +758,17 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
         if (P.rec_len) ratio = std::max(ratio, (double)(P.row_bytes + 12) / (double)P.rec_len);
         maxwin_row = std::max<uint32_t>(maxwin_row, P.window * std::max<uint32_t>(P.lds_waves, 1) * P.row_bytes);
     }
-    uint64_t arena_cap = (uint64_t)(ratio * (double)in->bytes_size) + (uint64_t)S * (maxwin_row + 256) + 4096;
-    arena_cap = std::max<uint64_t>(arena_cap, ctx->d_arena.cap);
+    uint64_t arena_cap = (uint64_t)(ratio * (double)in->bytes_size) +
+                         (uint64_t)S * (1 + ctx->cap_pad_windows) * (maxwin_row + 256) + 4096;
+    arena_cap = std::max<uint64_t>(arena_cap + ctx->arena_shift, ctx->d_arena.cap);
     if (ctx->d_hdr.ensure(std::max<uint32_t>(N, 1)) || ctx->d_counts.ensure(n_items) || ctx->d_scan.ensure(n_items) ||
         ctx->d_scan_tmp.ensure(scan_tmp + 1) || ctx->d_slots.ensure(std::max<uint32_t>(S, 1)) ||
         ctx->d_chunks.ensure(chunk_cap) || ctx->d_sets.ensure(set_cap) || ctx->d_arena.ensure(arena_cap) ||
-        ctx->d_proc.ensure(std::max<uint32_t>(S, 1)) || ctx->d_summary.ensure(1))
+        ctx->d_proc.ensure(2 * NGZ_MAX_SLOTS) || ctx->d_summary.ensure(2))
         return fail(ctx, NGZ_E_NOMEM, "device alloc (batch)");
+    const int par = ctx->parity;
+    BatchSummary *d_sum = ctx->d_summary.p + par;
+    unsigned long long *d_proc = ctx->d_proc.p + (size_t)par * NGZ_MAX_SLOTS;
     // host-framed inputs
     const uint32_t *hf_flag = nullptr;
     const uint32_t *hf_first = nullptr;
@@ -809,15 +818,43 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
     B.chunk_cap = ctx->d_chunks.cap;
     B.sets = ctx->d_sets.p;
     B.set_cap = ctx->d_sets.cap;
-    B.arena = ctx->d_arena.p;
-    B.arena_cap = ctx->d_arena.cap;
-    B.proc_counts = ctx->d_proc.p;
-    B.summary = ctx->d_summary.p;
+    B.arena = ctx->d_arena.p + ctx->arena_shift;
+    B.arena_cap = ctx->d_arena.cap - ctx->arena_shift;
+    B.proc_counts = d_proc;
+    B.cap_pad_windows = ctx->cap_pad_windows;
+    B.summary = d_sum;
 
     HIPCHK(hipEventRecord(ctx->ev[0], st));
-    HIPCHK(hipMemsetAsync(ctx->d_counts.p, 0, n_items * 4, st));
-    HIPCHK(hipMemsetAsync(ctx->d_summary.p, 0, sizeof(BatchSummary), st));
-    HIPCHK(hipMemsetAsync(ctx->d_proc.p, 0, std::max<uint32_t>(S, 1) * 8, st));
+    // k_frame zeroes the count matrix itself; the summary and increments of
+    // this parity were zeroed by the previous batch's k_export
+    if (!N) HIPCHK(hipMemsetAsync(ctx->d_counts.p, 0, n_items * 4, st));
+    if (!ctx->clean[par]) {
+        HIPCHK(hipMemsetAsync(d_sum, 0, sizeof(BatchSummary), st));
+        HIPCHK(hipMemsetAsync(d_proc, 0, NGZ_MAX_SLOTS * 8, st));
+    }
+    ctx->clean[par] = false;
+    BatchSummary *next_sum = ctx->d_summary.p + (par ^ 1);
+    unsigned long long *next_proc = ctx->d_proc.p + (size_t)(par ^ 1) * NGZ_MAX_SLOTS;
+    auto export_results = [&]() -> int {
+        const unsigned long long seq = ++ctx->export_seq;
+        if (ngz_launch_export(&B, ctx->dh_summary, ctx->dh_slots, ctx->dh_proc, next_sum, next_proc, ctx->dh_done,
+                              seq, st))
+            return fail(ctx, NGZ_E_DEVICE, "export launch");
+        // spin on the completion word (the export is the stream's last command);
+        // a stream synchronisation covers errors and very long batches
+        bool done = false;
+        if (ctx->spin_wait) {
+            const auto t0 = std::chrono::steady_clock::now();
+            for (uint32_t k = 0;; ++k) {
+                if (__atomic_load_n(ctx->h_done, __ATOMIC_ACQUIRE) == seq) { done = true; break; }
+                if ((k & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200)) break;
+                __builtin_ia32_pause();
+            }
+        }
+        if (!done) HIPCHK(hipStreamSynchronize(st));
+        ctx->clean[par ^ 1] = true;
+        return 0;
+    };
     if (ngz_launch_frame(&B, hf_flag, hf_first, st)) return fail(ctx, NGZ_E_DEVICE, "k_frame launch");
     if (ngz_launch_scan(ctx->d_scan_tmp.p, scan_tmp, ctx->d_counts.p, ctx->d_scan.p, n_items, st))
         return fail(ctx, NGZ_E_DEVICE, "scan launch");
@@ -858,10 +895,7 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
         }
         return 0;
     };
-    auto read_back = [&]() -> int {
-        HIPCHK(hipMemcpyAsync(ctx->h_summary, ctx->d_summary.p, sizeof(BatchSummary), hipMemcpyDeviceToHost, st));
-        if (S) HIPCHK(hipMemcpyAsync(ctx->h_slots, ctx->d_slots.p, S * sizeof(SlotRT), hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
+    auto check_summary = [&]() -> int {
         ctx->summary = *ctx->h_summary;
         if (ctx->summary.overflow) {
             if (ctx->summary.overflow & 1) ctx->d_arena.ensure(ctx->summary.arena_used + 4096);
@@ -876,7 +910,10 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
     bool generic = false;
     if (!predict) {
         // the kernels that run depend on the per-slot counts: read them first
-        const int r = read_back();
+        HIPCHK(hipMemcpyAsync(ctx->h_summary, d_sum, sizeof(BatchSummary), hipMemcpyDeviceToHost, st));
+        if (S) HIPCHK(hipMemcpyAsync(ctx->h_slots, ctx->d_slots.p, S * sizeof(SlotRT), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        const int r = check_summary();
         if (r) return r;
     }
     HIPCHK(hipEventRecord(ctx->ev[1], st));
@@ -895,8 +932,11 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
     HIPCHK(hipEventRecord(ctx->ev[2], st));
     if (ngz_launch_counts(&B, ctx->d_sets.cap, st)) return fail(ctx, NGZ_E_DEVICE, "counts launch");
     HIPCHK(hipEventRecord(ctx->ev[3], st));
+    // summary, slot table and processed_count increments straight into pinned memory, one synchronisation
+    int rc = export_results();
+    if (rc) return rc;
     if (predict) {
-        const int r = read_back();
+        const int r = check_summary();
         if (r) return r;
         // slots that gained records since the last batch
         bool missed = false, generic2 = false;
@@ -912,17 +952,14 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
         }
         if (missed) {
             if (generic2 && ngz_launch_decode_generic(&B, grid, st)) return fail(ctx, NGZ_E_DEVICE, "decode launch");
-            HIPCHK(hipMemsetAsync(ctx->d_proc.p, 0, std::max<uint32_t>(S, 1) * 8, st));
+            HIPCHK(hipMemsetAsync(d_proc, 0, NGZ_MAX_SLOTS * 8, st));
             if (ngz_launch_counts(&B, ctx->d_sets.cap, st)) return fail(ctx, NGZ_E_DEVICE, "counts launch");
             HIPCHK(hipEventRecord(ctx->ev[3], st));
+            rc = export_results();
+            if (rc) return rc;
         }
     }
-    // slot counts and processed_count increments for finish_batch, with the same synchronisation
-    if (S) {
-        HIPCHK(hipMemcpyAsync(ctx->h_slots, ctx->d_slots.p, S * sizeof(SlotRT), hipMemcpyDeviceToHost, st));
-        HIPCHK(hipMemcpyAsync(ctx->h_proc, ctx->d_proc.p, S * 8, hipMemcpyDeviceToHost, st));
-    }
-    HIPCHK(hipStreamSynchronize(st));
+    ctx->parity ^= 1;
     // slots with records this batch: launched without a round trip next time
     ctx->pred_versions = ctx->slot_version;
     ctx->pred_active.assign(S, 0);
@@ -933,6 +970,55 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
     ctx->pred_valid = !hf;
     hipEventElapsedTime(&ctx->t_decode, ctx->ev[1], ctx->ev[2]);
     hipEventElapsedTime(&ctx->t_pipeline, ctx->ev[0], ctx->ev[3]);
+    return 0;
+}
+
+// Arena placement.  The decode kernel's speed depends on where in HBM the
+// column arena was allocated: on MI355X some allocations run the same decode
+// up to 15 % slower than others, stably for the allocation's lifetime and
+// independent of offsets inside it (tools/arena_shift.py, tools/cap_pad.py,
+// tools/alloc_var3.py).  The first large device batch of a
+// context is therefore decoded on up to NGZ_PLACE_TRIALS fresh arenas (each
+// kept while the next is allocated, so every trial gets other memory); the
+// fastest is kept and the batch's results are the ones decoded on it.
+int place_arena(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st) {
+    if (ctx->placed || ctx->place_trials <= 1) return 0;
+    if (ctx->t_decode < 0.25f) return 0;  // small batches: launch-bound, placement does not show; try the next
+    ctx->placed = true;
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return 0;
+    const size_t cap = ctx->d_arena.cap;
+    const int trials = (int)std::min<size_t>((size_t)ctx->place_trials, free_b / std::max<size_t>(cap, 1) / 2 + 1);
+    std::vector<DevBuf<uint8_t>> arenas{ctx->d_arena};
+    std::vector<float> ms{ctx->t_decode};
+    for (int k = 1; k < trials; ++k) {
+        DevBuf<uint8_t> a;
+        if (a.ensure(cap)) break;  // out of room: keep what was tried
+        ctx->d_arena = a;
+        int rc;
+        for (int tries = 0; (rc = run_pipeline(ctx, in, st, nullptr)) == 1 && tries < 4; ++tries) {}
+        arenas.push_back(ctx->d_arena);  // (a retry may have regrown it)
+        if (rc) {
+            ctx->d_arena = arenas[0];
+            for (size_t i = 1; i < arenas.size(); ++i) arenas[i].release();
+            return rc < 0 ? rc : fail(ctx, NGZ_E_NOMEM, "batch buffers kept overflowing");
+        }
+        ms.push_back(ctx->t_decode);
+    }
+    const size_t best = (size_t)(std::min_element(ms.begin(), ms.end()) - ms.begin());
+    if (getenv("NGZ_DEBUG")) {
+        fprintf(stderr, "[ngz] arena placement:");
+        for (float m : ms) fprintf(stderr, " %.3f", m);
+        fprintf(stderr, " ms -> %zu\n", best);
+    }
+    ctx->d_arena = arenas[best];
+    for (size_t i = 0; i < arenas.size(); ++i)
+        if (i != best) arenas[i].release();
+    if (best != arenas.size() - 1) {  // leave this batch's results in the kept arena
+        int rc;
+        for (int tries = 0; (rc = run_pipeline(ctx, in, st, nullptr)) == 1 && tries < 4; ++tries) {}
+        if (rc) return rc < 0 ? rc : fail(ctx, NGZ_E_NOMEM, "batch buffers kept overflowing");
+    }
     return 0;
 }
 
@@ -953,7 +1039,7 @@ int finish_batch(ngz_ctx *ctx, const ngz_batch_in *in, ngz_batch_out *out, hipSt
         si.n_fields = (uint8_t)std::min<size_t>(v.specs.size(), 255);
         si.n_records = ctx->slot_rt[s].total;
         si.capacity = ctx->slot_rt[s].cap;
-        si.columns = ctx->d_arena.p + ctx->slot_rt[s].block;
+        si.columns = ctx->d_arena.p + ctx->arena_shift + ctx->slot_rt[s].block;
     }
     out->n_dgrams = in->n;
     out->n_sets = ctx->summary.n_sets;
@@ -990,13 +1076,24 @@ int ngz_ctx_create(int device, ngz_ctx **out) {
     }
     for (auto &e : ctx->ev) hipEventCreate(&e);
     hipDeviceGetAttribute(&ctx->n_cus, hipDeviceAttributeMultiprocessorCount, device);
-    if (hipHostMalloc((void **)&ctx->h_summary, sizeof(BatchSummary), 0) != hipSuccess ||
-        hipHostMalloc((void **)&ctx->h_slots, NGZ_MAX_SLOTS * sizeof(SlotRT), 0) != hipSuccess ||
-        hipHostMalloc((void **)&ctx->h_proc, NGZ_MAX_SLOTS * sizeof(unsigned long long), 0) != hipSuccess) {
+    // fine-grained (coherent) pinned memory: k_export writes it directly
+    const unsigned hf = hipHostMallocCoherent | hipHostMallocMapped;
+    if (hipHostMalloc((void **)&ctx->h_summary, sizeof(BatchSummary), hf) != hipSuccess ||
+        hipHostMalloc((void **)&ctx->h_slots, NGZ_MAX_SLOTS * sizeof(SlotRT), hf) != hipSuccess ||
+        hipHostMalloc((void **)&ctx->h_proc, NGZ_MAX_SLOTS * sizeof(unsigned long long), hf) != hipSuccess ||
+        hipHostGetDevicePointer((void **)&ctx->dh_summary, ctx->h_summary, 0) != hipSuccess ||
+        hipHostGetDevicePointer((void **)&ctx->dh_slots, ctx->h_slots, 0) != hipSuccess ||
+        hipHostGetDevicePointer((void **)&ctx->dh_proc, ctx->h_proc, 0) != hipSuccess ||
+        hipHostMalloc((void **)&ctx->h_done, 64, hf) != hipSuccess ||
+        hipHostGetDevicePointer((void **)&ctx->dh_done, ctx->h_done, 0) != hipSuccess) {
         ngz_ctx_destroy(ctx);
         return NGZ_E_NOMEM;
     }
     if (const char *e = getenv("NGZ_SPECIALIZE")) ctx->specialize = atoi(e);
+    if (const char *e = getenv("NGZ_SPIN")) ctx->spin_wait = atoi(e) != 0;
+    if (const char *e = getenv("NGZ_ARENA_CONTIG")) ctx->d_arena.contiguous = atoi(e) != 0;
+    if (const char *e = getenv("NGZ_PLACE_TRIALS")) ctx->place_trials = atoi(e);
+    *ctx->h_done = 0;
     if (const char *e = getenv("NGZ_BLOCKS_PER_CU")) ctx->blocks_per_cu = std::max(1, std::min(32, atoi(e)));
     if (const char *e = getenv("NGZ_LDS_BLOCKS_PER_CU")) ctx->lds_blocks_per_cu = std::max(1, std::min(512, atoi(e)));
     *out = ctx;
@@ -1017,6 +1114,7 @@ void ngz_ctx_destroy(ngz_ctx *ctx) {
     if (ctx->h_summary) hipHostFree(ctx->h_summary);
     if (ctx->h_slots) hipHostFree(ctx->h_slots);
     if (ctx->h_proc) hipHostFree(ctx->h_proc);
+    if (ctx->h_done) hipHostFree(ctx->h_done);
     hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -1030,6 +1128,14 @@ int ngz_ctx_set_option(ngz_ctx *ctx, int opt, int64_t value) {
         if (value != 0 && value != 1) return fail(ctx, NGZ_E_INVALID, "NGZ_OPT_SPECIALIZE takes 0 or 1");
         if (ctx->specialize != (int)value) ctx->plans_dirty = true;  // device plans carry the spec flag
         ctx->specialize = (int)value;
+        return NGZ_OK;
+    case NGZ_OPT_ARENA_SHIFT:
+        if (value < 0 || value > (1ll << 32) || value % 256) return fail(ctx, NGZ_E_INVALID, "NGZ_OPT_ARENA_SHIFT: 0..4 GiB, 256-byte multiple");
+        ctx->arena_shift = (uint64_t)value;
+        return NGZ_OK;
+    case NGZ_OPT_CAP_PAD:
+        if (value < 0 || value > 4096) return fail(ctx, NGZ_E_INVALID, "NGZ_OPT_CAP_PAD takes 0..4096");
+        ctx->cap_pad_windows = (uint32_t)value;
         return NGZ_OK;
     case NGZ_OPT_BLOCKS_PER_CU:
         if (value < 1 || value > 32) return fail(ctx, NGZ_E_INVALID, "NGZ_OPT_BLOCKS_PER_CU takes 1..32");
@@ -1049,13 +1155,10 @@ int ngz_decode_batch(ngz_ctx *ctx, const ngz_batch_in *in, ngz_batch_out *out, v
     ctx->batch_serial++;
     ctx->json_view.reset();
     memset(out, 0, sizeof *out);
-    // snapshot of the template state at batch start (for the slow path)
-    const size_t nver0 = ctx->versions.size();
-    std::vector<int32_t> cur0[2] = {ctx->cur[0], ctx->cur[1]};
-    int rc = assign_slots(ctx, {});
+    int rc = ctx->assigned_gen == ctx->tmpl_gen ? 0 : assign_slots(ctx, {});
     if (rc) return rc;
     if (ctx->plans_dirty || ctx->uploaded_gen != ctx->tmpl_gen) {
-        rc = upload_slots(ctx, cur0, st);
+        rc = upload_slots(ctx, ctx->cur, st);
         if (rc) return rc;
         ctx->uploaded_gen = ctx->tmpl_gen;
     }
@@ -1064,9 +1167,16 @@ int ngz_decode_batch(ngz_ctx *ctx, const ngz_batch_in *in, ngz_batch_out *out, v
     if (rc < 0) return rc;
     if (rc == 1) return fail(ctx, NGZ_E_NOMEM, "batch buffers kept overflowing");
     ctx->n_template_dgrams = ctx->summary.n_host;
-    if (ctx->summary.n_host == 0) return finish_batch(ctx, in, out, st);
+    if (ctx->summary.n_host == 0) {
+        rc = place_arena(ctx, in, st);
+        if (rc) return rc;
+        return finish_batch(ctx, in, out, st);
+    }
 
-    // slow path: frame template-bearing datagrams on the host, in stream order
+    // slow path: frame template-bearing datagrams on the host, in stream order.
+    // The fast pass left the template state untouched: it is the batch-start state.
+    const size_t nver0 = ctx->versions.size();
+    const std::vector<int32_t> cur0[2] = {ctx->cur[0], ctx->cur[1]};
     const uint32_t N = in->n;
     std::vector<ngz_dgram_hdr> hdr(N);
     std::vector<uint64_t> offs(N);

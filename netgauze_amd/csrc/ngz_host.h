@@ -92,11 +92,17 @@ template <class T>
 struct DevBuf {
     T *p = nullptr;
     size_t cap = 0;
+    bool contiguous = false;  // ask for physically contiguous memory (falls back to hipMalloc)
     int ensure(size_t n) {
         if (n <= cap) return 0;
         if (p) hipFree(p);
         p = nullptr;
         size_t c = std::max(n, cap + cap / 2);
+        if (contiguous && hipExtMallocWithFlags((void **)&p, c * sizeof(T) + 64, hipDeviceMallocContiguous) == hipSuccess) {
+            cap = c;
+            return 0;
+        }
+        p = nullptr;
         if (hipMalloc((void **)&p, c * sizeof(T) + 64) != hipSuccess) {
             cap = 0;
             return -1;
@@ -194,9 +200,24 @@ struct ngz_ctx {
     int specialize = 1;                         // NGZ_OPT_SPECIALIZE
     uint32_t blocks_per_cu = 4;                 // decode grid: 4 x 256 threads per CU
     uint32_t lds_blocks_per_cu = 8;             // LDS-staged decode grid (2 resident per CU at 64 KB)
+    // device summary / processed_count increments alternate between two
+    // parities: a batch's k_export zeroes the other parity for the next one
+    int parity = 0;
+    bool clean[2] = {false, false};
+    uint64_t assigned_gen = 0;                  // tmpl_gen the slot assignment was computed for
     BatchSummary *h_summary = nullptr;          // pinned
     SlotRT *h_slots = nullptr;                  // pinned, NGZ_MAX_SLOTS
     unsigned long long *h_proc = nullptr;       // pinned, NGZ_MAX_SLOTS: processed_count increments
+    BatchSummary *dh_summary = nullptr;         // device aliases of the three pinned export buffers
+    SlotRT *dh_slots = nullptr;
+    unsigned long long *dh_proc = nullptr;
+    unsigned long long *h_done = nullptr, *dh_done = nullptr;  // k_export completion word (pinned)
+    unsigned long long export_seq = 0;
+    uint32_t cap_pad_windows = 0;               // NGZ_OPT_CAP_PAD
+    int place_trials = 6;                       // arena placement trials on the first large batch (NGZ_PLACE_TRIALS)
+    bool placed = false;
+    uint64_t arena_shift = 0;                   // NGZ_OPT_ARENA_SHIFT: columns start this far into the arena
+    bool spin_wait = true;                      // wait for a batch by spinning on h_done (NGZ_SPIN=0: stream sync)
     float t_decode = 0, t_pipeline = 0;
     bool plans_dirty = true;
     uint32_t n_template_dgrams = 0;

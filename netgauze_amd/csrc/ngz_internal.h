@@ -226,4 +226,6 @@ struct BatchDev {        // device pointers of one batch
     uint64_t arena_cap;
     unsigned long long *proc_counts; // [n_slots] processed_count increments
     BatchSummary *summary;
+    uint32_t cap_pad_windows;  // extra workgroup windows of capacity per slot (column placement tuning)
+    uint32_t reserved_b;
 };

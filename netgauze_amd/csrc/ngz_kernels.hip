@@ -14,6 +14,8 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
+
 #include "ngz/flow_decode.h"
 #include "ngz_dev.h"
 #include "ngz_internal.h"
@@ -220,6 +222,9 @@ struct CountVis {
 __global__ void k_frame(BatchDev B, const uint32_t *hf_flag, const uint32_t *hf_first) {
     const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
     if (d >= B.n) return;
+    // this datagram's column of the count matrix starts at zero (no memset pass)
+    for (uint32_t r = 0; r < 2 * B.n_slots; ++r) B.counts[(uint64_t)r * B.n + d] = 0;
+    if (d == 0) B.counts[(uint64_t)(2 * B.n_slots + 1) * B.n] = 0;  // the scan's trailing element
     CountVis vis{B.counts, B.n, B.n_slots, d, 0, B.plans};
     WalkOut o;
     walk_datagram(B, hf_flag, hf_first, d, o, vis);
@@ -258,7 +263,7 @@ __global__ void k_layout(BatchDev B) {
         const uint32_t w = B.plans[s].window ? B.plans[s].window : 64;
         // LDS-staged kernels store whole workgroup windows: capacity in those
         const uint32_t wa = B.plans[s].lds_waves ? w * B.plans[s].lds_waves : w;
-        const uint32_t cap = total ? ((total + wa - 1) / wa) * wa : 0;
+        const uint32_t cap = total ? ((total + wa - 1) / wa + B.cap_pad_windows) * wa : 0;
         SlotRT rt;
         rt.block = off;
         rt.cap = cap;
@@ -514,56 +519,97 @@ __device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
 }
 
 __global__ void __launch_bounds__(256) k_counts(BatchDev B) {
-    const uint32_t nsets = B.summary->n_sets;
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    __shared__ unsigned long long acc[NGZ_MAX_SLOTS];  // this block's processed_count increments
     if (B.summary->overflow) return;
-    uint32_t slot = 0;
-    uint64_t inc = 0;
-    if (i < nsets) {
-        const ngz_set_info s = ((const ngz_set_info *)B.sets)[i];
-        const ngz_dgram_hdr h = ((const ngz_dgram_hdr *)B.hdr)[s.dgram];
-        slot = s.slot;
-        if (h.status != NGZ_FR_NEED_MORE && h.status != NGZ_FR_UNSUPPORTED) {
-            const uint32_t stop = h.err_key == NGZ_NO_ERR ? 0x10000u : (uint32_t)(h.err_key >> 48);
+    const uint32_t nsets = B.summary->n_sets;
+    const uint32_t S = B.n_slots;
+    for (uint32_t k = threadIdx.x; k < S; k += blockDim.x) acc[k] = 0;
+    __syncthreads();
+    const uint32_t lim = max(nsets, B.n);
+    // grid-stride over sets and datagrams; the loop bound is uniform per block
+    for (uint32_t base = blockIdx.x * blockDim.x; base < lim; base += gridDim.x * blockDim.x) {
+        const uint32_t i = base + threadIdx.x;
+        // final datagram status.  The status byte only moves OK -> ERROR, which
+        // the count rule below treats alike, so threads reading this header
+        // concurrently are unaffected.  NGZ_FR_HOST survives only in the
+        // speculative pass, whose results the host discards and redoes with
+        // the template-bearing datagrams host-framed.
+        if (i < B.n) {
+            ngz_dgram_hdr *h = &((ngz_dgram_hdr *)B.hdr)[i];
+            if (h->err_key != NGZ_NO_ERR && h->status != NGZ_FR_UNSUPPORTED && h->status != NGZ_FR_HOST)
+                h->status = NGZ_DG_ERROR;
+        }
+        uint32_t slot = 0;
+        uint64_t inc = 0;
+        if (i < nsets) {
+            const ngz_set_info s = ((const ngz_set_info *)B.sets)[i];
+            const ngz_dgram_hdr h = ((const ngz_dgram_hdr *)B.hdr)[s.dgram];
+            slot = s.slot;
             const DevPlan &pl = B.plans[s.slot];
-            const uint8_t *p = B.bytes + B.offsets[s.dgram];
-            const uint32_t set_len = be16(p + s.set_pos + 2);
-            if (pl.proto == 10) {
-                // the set's records all parsed (ipfix.rs:219-223); an UnexpectedEof at
-                // exactly the set end (available 0) is this set's failing record
-                const uint32_t code = h.err_key == NGZ_NO_ERR ? 0 : (uint32_t)(h.err_key >> 40) & 0xFF;
-                const uint32_t end = s.set_pos + set_len;
-                inc = (stop > end || (stop == end && code != E_REC_EOF)) ? 1 : 0;
+            if (h.status == NGZ_FR_NEED_MORE || h.status == NGZ_FR_UNSUPPORTED) {
+                inc = 0;
+            } else if (h.err_key == NGZ_NO_ERR) {
+                // the whole message parsed: +1 per IPFIX set (ipfix.rs:223), +1 per NFv9 record (netflow.rs:218)
+                inc = pl.proto == 10 ? 1 : s.n;
             } else {
-                // records fully parsed before the stop position
-                const uint32_t first = s.set_pos + 4, rl = pl.rec_len;
-                if (rl && stop > first) {
-                    inc = (stop - first) / rl;
-                    if (inc > s.n) inc = s.n;
+                const uint32_t stop = (uint32_t)(h.err_key >> 48);
+                const uint8_t *p = B.bytes + B.offsets[s.dgram];
+                const uint32_t set_len = be16(p + s.set_pos + 2);
+                if (pl.proto == 10) {
+                    // the set's records all parsed (ipfix.rs:219-223); an UnexpectedEof at
+                    // exactly the set end (available 0) is this set's failing record
+                    const uint32_t code = (uint32_t)(h.err_key >> 40) & 0xFF;
+                    const uint32_t end = s.set_pos + set_len;
+                    inc = (stop > end || (stop == end && code != E_REC_EOF)) ? 1 : 0;
+                } else {
+                    // records fully parsed before the stop position
+                    const uint32_t first = s.set_pos + 4, rl = pl.rec_len;
+                    if (rl && stop > first) {
+                        inc = (stop - first) / rl;
+                        if (inc > s.n) inc = s.n;
+                    }
                 }
             }
         }
+        // one LDS atomic per (wave, slot): consecutive sets mostly share a template
+        uint64_t pending = __ballot(inc != 0);
+        while (pending) {
+            const uint32_t leader = (uint32_t)__ffsll((unsigned long long)pending) - 1;
+            const uint32_t s0 = __builtin_amdgcn_readlane(slot, leader);
+            const bool mine = inc != 0 && slot == s0;
+            const uint64_t sum = wave_sum(mine ? inc : 0);
+            if ((threadIdx.x & 63) == leader) atomicAdd(&acc[s0], (unsigned long long)sum);
+            pending &= ~__ballot(mine);
+        }
     }
-    // one atomic per (wave, slot): consecutive sets mostly share a template
-    uint64_t pending = __ballot(inc != 0);
-    while (pending) {
-        const uint32_t leader = (uint32_t)__ffsll((unsigned long long)pending) - 1;
-        const uint32_t s0 = __builtin_amdgcn_readlane(slot, leader);
-        const bool mine = inc != 0 && slot == s0;
-        const uint64_t sum = wave_sum(mine ? inc : 0);
-        if ((threadIdx.x & 63) == leader) atomicAdd(&B.proc_counts[s0], (unsigned long long)sum);
-        pending &= ~__ballot(mine);
-    }
+    __syncthreads();
+    // one global atomic per (block, slot with increments)
+    for (uint32_t k = threadIdx.x; k < S; k += blockDim.x)
+        if (acc[k]) atomicAdd(&B.proc_counts[k], acc[k]);
 }
 
-__global__ void k_finalize(BatchDev B) {
-    const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
-    if (d >= B.n) return;
-    ngz_dgram_hdr *h = &((ngz_dgram_hdr *)B.hdr)[d];
-    // NGZ_FR_HOST survives only in the speculative pass, whose results the
-    // host discards and redoes with the template-bearing datagrams host-framed
-    if (h->err_key != NGZ_NO_ERR && h->status != NGZ_FR_UNSUPPORTED && h->status != NGZ_FR_HOST)
-        h->status = NGZ_DG_ERROR;
+// End of a batch: the summary, the slot table and the processed_count
+// increments go straight into the context's pinned host export buffers
+// (device writes over the fabric, no copy commands), and the other parity's
+// summary / increments are zeroed for the next batch.
+__global__ void __launch_bounds__(256) k_export(BatchDev B, BatchSummary *h_summary, SlotRT *h_slots,
+                                                unsigned long long *h_proc, BatchSummary *next_summary,
+                                                unsigned long long *next_proc, unsigned long long *h_done,
+                                                unsigned long long seq) {
+    const uint32_t t = threadIdx.x, S = B.n_slots;
+    if (t == 0) {
+        *h_summary = *B.summary;
+        *next_summary = BatchSummary{};
+    }
+    for (uint32_t i = t; i < S; i += blockDim.x) {
+        h_slots[i] = B.slots[i];
+        h_proc[i] = B.proc_counts[i];
+    }
+    for (uint32_t i = t; i < NGZ_MAX_SLOTS; i += blockDim.x) next_proc[i] = 0;  // the next batch may have more slots
+    __threadfence_system();
+    __syncthreads();
+    // completion word last: the host may spin on it instead of a stream synchronisation
+    if (t == 0) __hip_atomic_store(h_done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 }  // namespace
@@ -604,9 +650,17 @@ extern "C" int ngz_launch_decode_generic(const BatchDev *B, uint32_t grid, hipSt
 }
 
 extern "C" int ngz_launch_counts(const BatchDev *B, uint64_t set_cap, hipStream_t st) {
-    const uint64_t nb = (set_cap + 255) / 256;  // n_sets is known on device only
+    // n_sets is known on device only; the grid also covers every datagram (finalize)
+    const uint64_t nb = std::min<uint64_t>((std::max<uint64_t>(set_cap, B->n) + 255) / 256, 256);
     if (nb) hipLaunchKernelGGL(k_counts, dim3((uint32_t)nb), dim3(256), 0, st, *B);
-    const uint32_t nd = (B->n + 255) / 256;
-    if (nd) hipLaunchKernelGGL(k_finalize, dim3(nd), dim3(256), 0, st, *B);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int ngz_launch_export(const BatchDev *B, BatchSummary *h_summary, SlotRT *h_slots,
+                                 unsigned long long *h_proc, BatchSummary *next_summary,
+                                 unsigned long long *next_proc, unsigned long long *h_done, unsigned long long seq,
+                                 hipStream_t st) {
+    hipLaunchKernelGGL(k_export, dim3(1), dim3(256), 0, st, *B, h_summary, h_slots, h_proc, next_summary, next_proc,
+                       h_done, seq);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }

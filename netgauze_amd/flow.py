@@ -79,7 +79,14 @@ class DecodedBatch:
         self.n_sets = out.n_sets
         self.n_records = out.n_records
         self.n_template_dgrams = out.n_template_dgrams
-        self.slots = [Slot(codec, i, out.slots[i]) for i in range(out.n_slots)]
+        self._slots = None
+
+    @property
+    def slots(self):
+        """Per template version: where its records landed (built on first use)."""
+        if self._slots is None:
+            self._slots = [Slot(self._codec, i, self.out.slots[i]) for i in range(self.out.n_slots)]
+        return self._slots
 
     def input_bytes(self, offset, n):
         """Bytes [offset, offset+n) of this batch's input: variable-length
