@@ -146,7 +146,9 @@ const char *ngz_last_error(ngz_ctx *ctx);
 /* Context options (ngz_ctx_set_option). */
 #define NGZ_OPT_SPECIALIZE 1    /* 1 (default): decode each template with its own kernel, generated and
                                    compiled at run time (hiprtc) and cached by layout; 0: the generic
-                                   field-table kernel for every template */
+                                   field-table kernel for every template; 2: generic kernel until a
+                                   template has decoded 65536 records, then its own kernel (short
+                                   captures skip the 0.1-0.3 s compile per template) */
 #define NGZ_OPT_BLOCKS_PER_CU 2 /* decode grid size: 256-thread blocks per CU (default 4) */
 #define NGZ_OPT_CAP_PAD 4       /* extra row windows of column capacity per template slot (column spacing) */
 #define NGZ_OPT_ARENA_SHIFT 3   /* bytes (multiple of 256) the column blocks start into the context's

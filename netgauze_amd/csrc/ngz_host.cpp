@@ -714,7 +714,9 @@ int upload_slots(ngz_ctx *ctx, const std::vector<int32_t> cur_start[2], hipStrea
         plans[s] = v.plan;
         plans[s].spec = 0;
         if (ctx->specialize && v.plan.rpl && !v.plan.has_vlen) {  // vlen templates: generic kernel
-            if (v.rtc_state == 0) {
+            // NGZ_OPT_SPECIALIZE 2: compile once the template has seen enough records to pay for it
+            const bool want = ctx->specialize == 1 || v.seen_records >= NGZ_SPECIALIZE_MIN_RECORDS;
+            if (v.rtc_state == 0 && want) {
                 v.rtc_fn = ngz_rtc_kernel(ctx->device, v.plan);
                 v.rtc_state = v.rtc_fn ? 1 : 2;
             }
@@ -1032,6 +1034,9 @@ int finish_batch(ngz_ctx *ctx, const ngz_batch_in *in, ngz_batch_out *out, hipSt
     for (uint32_t s = 0; s < S; ++s) {
         Version &v = ctx->versions[ctx->slot_version[s]];
         v.processed += proc[s];
+        v.seen_records += ctx->slot_rt[s].total;
+        if (ctx->specialize == 2 && v.rtc_state == 0 && v.seen_records >= NGZ_SPECIALIZE_MIN_RECORDS)
+            ctx->plans_dirty = true;  // the next batch compiles its kernel
         ngz_slot_info &si = ctx->slot_infos[s];
         si.version_id = (uint32_t)ctx->slot_version[s];
         si.template_id = v.tid;
@@ -1125,7 +1130,7 @@ int ngz_ctx_set_option(ngz_ctx *ctx, int opt, int64_t value) {
     if (!ctx) return NGZ_E_INVALID;
     switch (opt) {
     case NGZ_OPT_SPECIALIZE:
-        if (value != 0 && value != 1) return fail(ctx, NGZ_E_INVALID, "NGZ_OPT_SPECIALIZE takes 0 or 1");
+        if (value < 0 || value > 2) return fail(ctx, NGZ_E_INVALID, "NGZ_OPT_SPECIALIZE takes 0, 1 or 2");
         if (ctx->specialize != (int)value) ctx->plans_dirty = true;  // device plans carry the spec flag
         ctx->specialize = (int)value;
         return NGZ_OK;

@@ -14,6 +14,9 @@
 #include "ngz/flow_decode.h"
 #include "ngz_internal.h"
 
+// NGZ_OPT_SPECIALIZE 2: a template's kernel is compiled once it has decoded this many records
+#define NGZ_SPECIALIZE_MIN_RECORDS 65536
+
 namespace ngzh {
 
 // ------------------------------------------------------------------------
@@ -66,6 +69,7 @@ struct Version {
     DevPlan plan;
     std::vector<uint8_t> fail_sub;  // per field: 1 InvalidLength, 2 InvalidPaddingLength, 3 scope InvalidLength
     uint64_t processed = 0;
+    uint64_t seen_records = 0;      // records decoded with this version (NGZ_OPT_SPECIALIZE 2)
     int rtc_state = 0;              // specialised kernel: 0 not looked up, 1 ready, 2 unavailable
     void *rtc_fn = nullptr;
 };
