@@ -74,17 +74,21 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--records", type=int, default=100_000_000, help="records per GPU")
-    ap.add_argument("--workload", choices=["t20", "mixed8", "cfg4"], default="t20",
+    ap.add_argument("--records", type=int, default=None,
+                    help="records per GPU (default 10^8; cfg5: 1.25*10^8, i.e. 10^9 over 8 GPUs)")
+    ap.add_argument("--workload", choices=["t20", "mixed8", "cfg4", "cfg5"], default="t20",
                     help="t20 (headline): one 20-field 64-B template; mixed8: config 3, 8 reference-shaped "
                          "templates (40-153 B) in interleaved messages; cfg4: config 4, NetFlow v9 + IPFIX "
-                         "variable-length/enterprise IEs")
+                         "variable-length/enterprise IEs; cfg5: config 5, 16 templates (config 3 + 8 width "
+                         "permutations), one shard per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e-contexts", type=int, default=3, help="--e2e: contexts (host threads) in flight")
     ap.add_argument("--e2e-ranges", type=int, default=12, help="--e2e: message ranges per batch")
     ap.add_argument("--e2e", action="store_true",
                     help="host-to-host rate instead: pinned host datagrams -> H2D -> decode -> D2H of all columns")
     args = ap.parse_args()
+    if args.records is None:
+        args.records = 125_000_000 if args.workload == "cfg5" else 100_000_000
     if args.e2e:
         return main_e2e(args)
 
@@ -110,9 +114,11 @@ def main():
         buf, offs, lens = synth.ipfix_data_stream(rec, 64)
         del rec
         rec_bytes = {256: 64}
-    elif args.workload == "mixed8":
-        codec.decode_datagrams([synth.templates_message(synth.CFG3_TEMPLATES)])
-        buf, offs, lens, recs = synth.mixed_stream(n, seed=synth.SEED_CFG3 + 16 * rank, device=dev)
+    elif args.workload in ("mixed8", "cfg5"):
+        tpls = synth.CFG3_TEMPLATES if args.workload == "mixed8" else synth.CFG5_TEMPLATES
+        seed = synth.SEED_CFG3 if args.workload == "mixed8" else synth.SEED_CFG5
+        codec.decode_datagrams([synth.templates_message(tpls)])
+        buf, offs, lens, recs = synth.mixed_stream(n, templates=tpls, seed=seed + 64 * rank, device=dev)
         rec_bytes = {tid: r.shape[1] for tid, r in recs.items()}
         del recs
     else:
@@ -165,6 +171,7 @@ def main():
     out = {
         "metric": {"t20": "IPFIX flow records/sec + GB/s (device-resident), 20-field fixed template",
                    "mixed8": "IPFIX flow records/sec (device-resident), config 3: 8 templates",
+                   "cfg5": "IPFIX flow records/sec (device-resident), config 5: 16 templates, sharded per GPU",
                    "cfg4": "flow records/sec (device-resident), config 4: NetFlow v9 + IPFIX variable-length"}
                   [args.workload],
         "value": value,
@@ -178,10 +185,12 @@ def main():
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (splitmix64 records, seed 0x4E475A450000000%d+rank)"
-                % {"t20": 2, "mixed8": 3, "cfg4": 4}[args.workload],
+                % {"t20": 2, "mixed8": 3, "cfg4": 4, "cfg5": 5}[args.workload],
         "config": {"workload": {"t20": "T20 x %d records/GPU, 1023 records per 65,492-byte IPFIX message" % n,
                                 "mixed8": "config 3: %d records/GPU over templates %s, interleaved messages"
                                 % (n, ",".join(str(t) for t, _ in synth.CFG3_TEMPLATES)),
+                                "cfg5": "config 5: %d records/GPU (10^9 at 8 GPUs) over 16 templates %s"
+                                % (n, ",".join(str(t) for t, _ in synth.CFG5_TEMPLATES)),
                                 "cfg4": "config 4: %d records/GPU, NFv9 template 313 (130 B, 10/packet) + IPFIX "
                                         "template 900 (vlen strings/octets, VMware/Huawei IEs)" % n}[args.workload],
                    "records_per_gpu": n, "messages_per_gpu": int(offs.numel()),

@@ -182,6 +182,37 @@ __device__ __forceinline__ uint8_t *pass_col(const Pass &P, uint32_t col_off, ui
     return P.blk + (uint64_t)P.cap * col_off + (uint64_t)P.prow * width;
 }
 
+// Direct column stores (buffer resource on the column's pass address)
+struct ColGlb {
+    __amdgpu_buffer_rsrc_t r;
+    __device__ __forceinline__ ColGlb(const Pass &P, uint32_t col_off, uint32_t width)
+        : r(__builtin_amdgcn_make_buffer_rsrc(pass_col(P, col_off, width), (short)0, 0x7FFFFFF0, 0x00020000)) {}
+    __device__ __forceinline__ void b8(uint32_t off, uint32_t v) const {
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, r, off, 0, 0);
+    }
+    __device__ __forceinline__ void b16(uint32_t off, uint32_t v) const {
+        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)v, r, off, 0, 0);
+    }
+    __device__ __forceinline__ void b32(uint32_t off, uint32_t v) const {
+        __builtin_amdgcn_raw_buffer_store_b32(v, r, off, 0, 0);
+    }
+    __device__ __forceinline__ void b64(uint32_t off, uint32_t lo, uint32_t hi) const {
+        v2u x = {lo, hi};
+        __builtin_amdgcn_raw_buffer_store_b64(x, r, off, 0, 0);
+    }
+    __device__ __forceinline__ void b128(uint32_t off, uint32_t a, uint32_t b, uint32_t c, uint32_t d) const {
+        v4u x = {a, b, c, d};
+        __builtin_amdgcn_raw_buffer_store_b128(x, r, off, 0, 0);
+    }
+    // one value of `width` bytes (1/2/4/8) at row lrow
+    __device__ __forceinline__ void w(uint32_t lrow, uint32_t width, uint64_t v) const {
+        if (width == 1) b8(lrow, (uint32_t)v);
+        else if (width == 2) b16(2 * lrow, (uint32_t)v);
+        else if (width == 4) b32(4 * lrow, (uint32_t)v);
+        else b64(8 * lrow, (uint32_t)v, (uint32_t)(v >> 32));
+    }
+};
+
 #ifdef NGZ_LDS_WAVES
 // LDS-staged per-template kernels (generated with NGZ_LDS_WAVES / NGZ_LDS_ROWB
 // defined): the decode writes a workgroup window of LDS_ROWS rows into LDS,
@@ -226,35 +257,7 @@ __device__ __forceinline__ void lds_flush(uint8_t *dst, uint32_t at, uint32_t ld
     }
 }
 #else
-struct ColSt {
-    __amdgpu_buffer_rsrc_t r;
-    __device__ __forceinline__ ColSt(const Pass &P, uint32_t col_off, uint32_t width)
-        : r(__builtin_amdgcn_make_buffer_rsrc(pass_col(P, col_off, width), (short)0, 0x7FFFFFF0, 0x00020000)) {}
-    __device__ __forceinline__ void b8(uint32_t off, uint32_t v) const {
-        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, r, off, 0, 0);
-    }
-    __device__ __forceinline__ void b16(uint32_t off, uint32_t v) const {
-        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)v, r, off, 0, 0);
-    }
-    __device__ __forceinline__ void b32(uint32_t off, uint32_t v) const {
-        __builtin_amdgcn_raw_buffer_store_b32(v, r, off, 0, 0);
-    }
-    __device__ __forceinline__ void b64(uint32_t off, uint32_t lo, uint32_t hi) const {
-        v2u x = {lo, hi};
-        __builtin_amdgcn_raw_buffer_store_b64(x, r, off, 0, 0);
-    }
-    __device__ __forceinline__ void b128(uint32_t off, uint32_t a, uint32_t b, uint32_t c, uint32_t d) const {
-        v4u x = {a, b, c, d};
-        __builtin_amdgcn_raw_buffer_store_b128(x, r, off, 0, 0);
-    }
-    // one value of `width` bytes (1/2/4/8) at row lrow
-    __device__ __forceinline__ void w(uint32_t lrow, uint32_t width, uint64_t v) const {
-        if (width == 1) b8(lrow, (uint32_t)v);
-        else if (width == 2) b16(2 * lrow, (uint32_t)v);
-        else if (width == 4) b32(4 * lrow, (uint32_t)v);
-        else b64(8 * lrow, (uint32_t)v, (uint32_t)(v >> 32));
-    }
-};
+typedef ColGlb ColSt;
 #endif
 
 // Value of a numeric field (UINT/SCOPE32/TCPFLAGS/SINT/BOOL/DTMS/DTFRAC) at
@@ -286,11 +289,14 @@ __device__ __forceinline__ uint64_t num_value(const uint32_t (&R)[WIN_DW], const
     return v;
 }
 
-// Numeric field of one record per lane: one store of `width` bytes per lane.
+// Numeric field of one record per lane: one store of `width` bytes per lane
+// (Col = ColSt: the kernel's column store, LDS in staged kernels; ColGlb: a
+// direct HBM store, for the wide columns of a staged kernel).
+template <class Col = ColSt>
 __device__ __forceinline__ void dec_num(const uint32_t (&R)[WIN_DW], const Pass &P, uint32_t o, uint32_t off,
                                         uint32_t f, uint32_t len, uint32_t width, uint32_t kind, uint32_t col_off) {
     const uint64_t v = num_value(R, P, o, off, f, len, kind);
-    if (P.valid) ColSt(P, col_off, width).w(P.lrow, width, v);
+    if (P.valid) Col(P, col_off, width).w(P.lrow, width, v);
 }
 
 // Numeric field of C consecutive rows per lane (run_chunks<C, true>): the C
@@ -389,10 +395,11 @@ __device__ __forceinline__ void check_str(const uint32_t (&R)[WIN_DW], const Pas
 // Copy `piece` (<= 64) raw wire bytes at window offset o to column bytes
 // [j, j+piece) of this lane's row; `pad_to` > 0 zero-fills [j+piece, pad_to)
 // (u256: left-aligned, zero padded).
+template <class Col = ColSt>
 __device__ __forceinline__ void dec_raw(const uint32_t (&R)[WIN_DW], const Pass &P, uint32_t o, uint32_t j,
                                         uint32_t piece, uint32_t width, uint32_t col_off, uint32_t pad_to) {
     if (!P.valid) return;
-    const ColSt cs(P, col_off, width);
+    const Col cs(P, col_off, width);
     const uint32_t at = P.lrow * width + j;
     const bool dw = (width & 3) == 0 && (j & 3) == 0;
     uint32_t t = 0;

@@ -266,7 +266,25 @@ void build_plan(Version &v) {
     // per-template kernels stage the columns of 256*lds_waves rows in LDS
     // (NGZ_LDS=0: direct column stores, for A/B measurements)
     static const bool lds_on = !getenv("NGZ_LDS") || atoi(getenv("NGZ_LDS")) != 0;
-    P.lds_waves = (P.rpl && !vlen && lds_on) ? ngz_lds_waves(P.row_bytes) : 0;
+    // LDS budget per workgroup (gfx950 allows up to 160 KiB) and waves per window
+    static const uint32_t lds_budget = getenv("NGZ_LDS_BUDGET") ? (uint32_t)atoi(getenv("NGZ_LDS_BUDGET")) : NGZ_LDS_BUDGET;
+    static const uint32_t lds_maxw = getenv("NGZ_LDS_MAXW") ? (uint32_t)atoi(getenv("NGZ_LDS_MAXW")) : 4u;
+    // columns at least lds_direct bytes wide skip LDS (stored directly; 0 = stage every column).
+    // Default: rows too wide for 4 staged waves in the budget send their 8- and 16-byte columns
+    // direct (config 5: 4.35 -> 4.12 ms per 10^8 records); narrower rows stage everything
+    // (T20 stays at its 1024-row windows).
+    static const int lds_direct_env = getenv("NGZ_LDS_DIRECT_MIN") ? atoi(getenv("NGZ_LDS_DIRECT_MIN")) : -1;
+    const uint32_t lds_direct = lds_direct_env >= 0 ? (uint32_t)lds_direct_env
+                                : (NGZ_REG_WINDOW * 4 * P.row_bytes > lds_budget ? 8u : 0u);
+    uint32_t staged = 0;
+    for (uint32_t i = 0; i < P.n_fields; ++i) {
+        bool seen = false;
+        for (uint32_t g = 0; g < i; ++g) seen = seen || (P.f[g].width && P.f[g].col_off == P.f[i].col_off);
+        if (!seen && !(lds_direct && P.f[i].width >= lds_direct)) staged += P.f[i].width;
+    }
+    P.reserved0 = (uint8_t)std::min<uint32_t>(lds_direct, 255);
+    P.lds_waves = (P.rpl && !vlen && lds_on && staged) ? ngz_lds_waves(staged, lds_budget, lds_maxw) : 0;
+    if (!P.lds_waves) P.reserved0 = 0;
 }
 
 int fail(ngz_ctx *c, int code, const char *msg) {
@@ -871,7 +889,7 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
     const uint32_t grid = (uint32_t)ctx->n_cus * ctx->blocks_per_cu;  // 256-thread blocks
     const bool predict = ctx->pred_valid && ctx->pred_versions == ctx->slot_version && !hf;
     // launch the decode of slot s (rt: its counts when known)
-    auto launch_slot = [&](uint32_t s, const SlotRT *rt, bool &generic) -> int {
+    auto launch_slot = [&](uint32_t s, const SlotRT *rt, bool &generic, hipStream_t ls) -> int {
         const Version &v = ctx->versions[ctx->slot_version[s]];
         if (!v.plan.rpl) return 0;
         if (ctx->specialize && v.rtc_state == 1 && !v.plan.has_vlen) {
@@ -891,7 +909,7 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
                     g = std::min<uint32_t>(grid, (units + 3) / 4);
                 }
             }
-            if (g && ngz_rtc_launch(v.rtc_fn, &B, s, g, block, st)) return fail(ctx, NGZ_E_DEVICE, "specialised decode launch");
+            if (g && ngz_rtc_launch(v.rtc_fn, &B, s, g, block, ls)) return fail(ctx, NGZ_E_DEVICE, "specialised decode launch");
         } else {
             generic = true;
         }
@@ -919,18 +937,35 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
         if (r) return r;
     }
     HIPCHK(hipEventRecord(ctx->ev[1], st));
+    std::vector<std::pair<uint32_t, const SlotRT *>> todo;
     for (uint32_t s = 0; s < S; ++s) {
         if (predict) {
             if (!ctx->pred_active[s]) continue;
-            if (launch_slot(s, nullptr, generic)) return -1;
+            todo.push_back({s, nullptr});
         } else {
             const SlotRT &rt = ctx->h_slots[s];
             if (!rt.total || (rt.mode == NGZ_MODE_CHUNK && !rt.nchunks)) continue;
-            if (launch_slot(s, &rt, generic)) return -1;
+            todo.push_back({s, &rt});
         }
         launched[s] = 1;
     }
+    // several active templates: their kernels run side by side on the context's
+    // auxiliary streams (fork/join with events), so one kernel's tail overlaps
+    // the next one's start instead of draining the GPU between templates
+    const uint32_t n_aux = todo.size() >= 2 ? std::min<uint32_t>(ctx->n_aux, (uint32_t)todo.size() - 1) : 0;
+    if (n_aux) {
+        HIPCHK(hipEventRecord(ctx->fork_ev, st));
+        for (uint32_t i = 0; i < n_aux; ++i) HIPCHK(hipStreamWaitEvent(ctx->aux[i], ctx->fork_ev, 0));
+    }
+    for (size_t k = 0; k < todo.size(); ++k) {
+        const hipStream_t ls = (n_aux && k > 0) ? ctx->aux[(k - 1) % n_aux] : st;
+        if (launch_slot(todo[k].first, todo[k].second, generic, ls)) return -1;
+    }
     if (generic && ngz_launch_decode_generic(&B, grid, st)) return fail(ctx, NGZ_E_DEVICE, "decode launch");
+    for (uint32_t i = 0; i < n_aux; ++i) {
+        HIPCHK(hipEventRecord(ctx->join_ev[i], ctx->aux[i]));
+        HIPCHK(hipStreamWaitEvent(st, ctx->join_ev[i], 0));
+    }
     HIPCHK(hipEventRecord(ctx->ev[2], st));
     if (ngz_launch_counts(&B, ctx->d_sets.cap, st)) return fail(ctx, NGZ_E_DEVICE, "counts launch");
     HIPCHK(hipEventRecord(ctx->ev[3], st));
@@ -949,7 +984,7 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
             const Version &v = ctx->versions[ctx->slot_version[s]];
             const bool spec = ctx->specialize && v.rtc_state == 1 && !v.plan.has_vlen;
             if (!spec && generic) continue;  // the generic kernel walked every non-specialised slot
-            if (launch_slot(s, &rt, generic2)) return -1;
+            if (launch_slot(s, &rt, generic2, st)) return -1;
             launched[s] = 1;
         }
         if (missed) {
@@ -1080,6 +1115,15 @@ int ngz_ctx_create(int device, ngz_ctx **out) {
         return NGZ_E_DEVICE;
     }
     for (auto &e : ctx->ev) hipEventCreate(&e);
+    if (const char *e = getenv("NGZ_DECODE_STREAMS")) ctx->n_aux = (uint32_t)std::max(0, std::min(NGZ_MAX_AUX, atoi(e) - 1));
+    for (uint32_t i = 0; i < ctx->n_aux; ++i) {
+        if (hipStreamCreateWithFlags(&ctx->aux[i], hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&ctx->join_ev[i], hipEventDisableTiming) != hipSuccess) {
+            ctx->n_aux = i;
+            break;
+        }
+    }
+    hipEventCreateWithFlags(&ctx->fork_ev, hipEventDisableTiming);
     hipDeviceGetAttribute(&ctx->n_cus, hipDeviceAttributeMultiprocessorCount, device);
     // fine-grained (coherent) pinned memory: k_export writes it directly
     const unsigned hf = hipHostMallocCoherent | hipHostMallocMapped;
@@ -1116,6 +1160,12 @@ void ngz_ctx_destroy(ngz_ctx *ctx) {
     ctx->d_proc.release(); ctx->d_summary.release(); ctx->d_in_bytes.release(); ctx->d_in_off.release();
     ctx->d_in_len.release();
     for (auto &e : ctx->ev) hipEventDestroy(e);
+    for (uint32_t i = 0; i < ctx->n_aux; ++i) {
+        hipStreamSynchronize(ctx->aux[i]);
+        hipStreamDestroy(ctx->aux[i]);
+        hipEventDestroy(ctx->join_ev[i]);
+    }
+    if (ctx->fork_ev) hipEventDestroy(ctx->fork_ev);
     if (ctx->h_summary) hipHostFree(ctx->h_summary);
     if (ctx->h_slots) hipHostFree(ctx->h_slots);
     if (ctx->h_proc) hipHostFree(ctx->h_proc);

@@ -16,6 +16,7 @@
 
 // NGZ_OPT_SPECIALIZE 2: a template's kernel is compiled once it has decoded this many records
 #define NGZ_SPECIALIZE_MIN_RECORDS 65536
+#define NGZ_MAX_AUX 7  // auxiliary decode streams per context
 
 namespace ngzh {
 
@@ -200,6 +201,11 @@ struct ngz_ctx {
     BatchSummary summary{};
     ngz_batch_in last_in{};
     hipEvent_t ev[4]{};
+    // auxiliary decode streams: per-template kernels of one batch run side by side
+    uint32_t n_aux = 3;                         // NGZ_DECODE_STREAMS - 1
+    hipStream_t aux[NGZ_MAX_AUX]{};
+    hipEvent_t join_ev[NGZ_MAX_AUX]{};
+    hipEvent_t fork_ev = nullptr;
     int n_cus = 256;
     int specialize = 1;                         // NGZ_OPT_SPECIALIZE
     uint32_t blocks_per_cu = 4;                 // decode grid: 4 x 256 threads per CU

@@ -18,10 +18,11 @@
 // column-major, then writes every column's 256*lds_waves rows as one
 // contiguous run of 16-byte stores.  As many waves as the budget allows, at
 // most 4; 0 (rows too wide) = direct stores.
-static inline __host__ __device__ uint32_t ngz_lds_waves(uint32_t row_bytes) {
+static inline __host__ __device__ uint32_t ngz_lds_waves(uint32_t row_bytes, uint32_t budget = NGZ_LDS_BUDGET,
+                                                         uint32_t max_waves = 4) {
     if (!row_bytes) return 0;
-    const uint32_t w = NGZ_LDS_BUDGET / (NGZ_REG_WINDOW * row_bytes);
-    return w > 4 ? 4 : w;
+    const uint32_t w = budget / (NGZ_REG_WINDOW * row_bytes);
+    return w > max_waves ? max_waves : w;
 }
 
 // datagram frame state (k_frame -> host)

@@ -43,7 +43,8 @@ struct Item {           // one extraction step of the generated pass body
 };
 
 std::string signature(const DevPlan &P) {
-    std::string s = "rl" + std::to_string(P.rec_len) + "lw" + std::to_string(P.lds_waves);
+    std::string s = "rl" + std::to_string(P.rec_len) + "lw" + std::to_string(P.lds_waves) + "dm" +
+                    std::to_string(P.reserved0);
     char b[96];
     for (uint32_t f = 0; f < P.n_fields; ++f) {
         const DevField &d = P.f[f];
@@ -143,18 +144,38 @@ std::string generate(const DevPlan &P) {
         }
         if (rpl != 1 && rpl != 2 && rpl != 4) rpl = 4;
     }
+    // LDS-staged kernels stage the columns narrower than P.reserved0 bytes (all
+    // of them when 0) in LDS; wider columns (64 lanes x 8-16 B = 0.5-1 KB per
+    // store instruction already) are stored to HBM directly, so the LDS window
+    // holds more rows and more waves fit a CU.  lds_col[f]: the field's column
+    // offset factor inside the staged (LDS) row.
+    const uint32_t lw0 = P.lds_waves;
+    std::vector<uint32_t> lds_col(P.n_fields, 0);
+    std::vector<uint8_t> direct(P.n_fields, 0);
+    uint32_t staged_rowb = 0;
+    for (uint32_t f = 0; f < P.n_fields; ++f) {
+        const DevField &d = P.f[f];
+        uint32_t same = f;  // pieces of one raw field share a column
+        for (uint32_t g = 0; g < f; ++g)
+            if (P.f[g].width && P.f[g].col_off == d.col_off) { same = g; break; }
+        if (same != f) { lds_col[f] = lds_col[same]; direct[f] = direct[same]; continue; }
+        direct[f] = lw0 && P.reserved0 && d.width >= P.reserved0;
+        if (!direct[f]) { lds_col[f] = staged_rowb; staged_rowb += d.width; }
+    }
     std::string body;
     char b[512];
     auto emit_item = [&](const Item &it, uint32_t wb, int k) {
         const std::string R = "R[" + std::to_string(k) + "]", P = "P[" + std::to_string(k) + "]";
+        const bool dir = direct[it.f];
+        const uint32_t co = (lw0 && !dir) ? lds_col[it.f] : it.col_off;
         switch (it.type) {
         case 0:
-            snprintf(b, sizeof b, "        dec_num(%s, %s, %uu, %uu, %uu, %uu, %uu, %uu, %uu);\n", R.c_str(), P.c_str(),
-                     it.off - wb, it.off, it.f, it.len, it.width, it.kind, it.col_off);
+            snprintf(b, sizeof b, "        dec_num%s(%s, %s, %uu, %uu, %uu, %uu, %uu, %uu, %uu);\n", dir ? "<ColGlb>" : "",
+                     R.c_str(), P.c_str(), it.off - wb, it.off, it.f, it.len, it.width, it.kind, co);
             break;
         case 1:
-            snprintf(b, sizeof b, "        dec_raw(%s, %s, %uu, %uu, %uu, %uu, %uu, %uu);\n", R.c_str(), P.c_str(),
-                     it.off + it.j - wb, it.j, it.piece, it.width, it.col_off, it.pad_to);
+            snprintf(b, sizeof b, "        dec_raw%s(%s, %s, %uu, %uu, %uu, %uu, %uu, %uu);\n", dir ? "<ColGlb>" : "",
+                     R.c_str(), P.c_str(), it.off + it.j - wb, it.j, it.piece, it.width, co, it.pad_to);
             break;
         case 2:
             snprintf(b, sizeof b, "        check_str(%s, %s, %uu, %uu, %uu, %uu, true);\n", R.c_str(), P.c_str(),
@@ -186,14 +207,16 @@ std::string generate(const DevPlan &P) {
         if (consec) {
             for (size_t t = i; t < e; ++t) {
                 const Item &it = items[t];
-                if (it.type == 0) {
+                const uint32_t co = lw0 ? lds_col[it.f] : it.col_off;
+                if (direct[it.f]) {
+                    for (int k = 0; k < rpl; ++k) emit_item(it, wb, k);
+                } else if (it.type == 0) {
                     snprintf(b, sizeof b, "        dec_num_c<%d>(R, P, %uu, %uu, %uu, %uu, %uu, %uu, %uu);\n", rpl,
-                             it.off - wb, it.off, it.f, it.len, it.width, it.kind, it.col_off);
+                             it.off - wb, it.off, it.f, it.len, it.width, it.kind, co);
                     body += b;
                 } else if (it.type == 1 && it.j == 0 && it.piece == it.len && it.len == it.width && it.width <= 16) {
                     // whole short raw field: packed C-row store
-                    snprintf(b, sizeof b, "        dec_raw_c<%d>(R, P, %uu, %uu, %uu);\n", rpl, it.off - wb, it.width,
-                             it.col_off);
+                    snprintf(b, sizeof b, "        dec_raw_c<%d>(R, P, %uu, %uu, %uu);\n", rpl, it.off - wb, it.width, co);
                     body += b;
                 } else {
                     for (int k = 0; k < rpl; ++k) emit_item(it, wb, k);
@@ -211,7 +234,7 @@ std::string generate(const DevPlan &P) {
     src += "// generated by ngz_rtc.cpp for plan " + signature(P) + "\n";
     if (lw) {
         src += "#define NGZ_LDS_WAVES " + std::to_string(lw) + "\n";
-        src += "#define NGZ_LDS_ROWB " + std::to_string(P.row_bytes) + "\n";
+        src += "#define NGZ_LDS_ROWB " + std::to_string(staged_rowb) + "\n";
     }
     src += "#include \"ngz_dev.h\"\nusing namespace ngzdev;\n";
     src += "extern \"C\" __global__ void __launch_bounds__(" + std::to_string(lw ? 64 * lw : 256) +
@@ -235,7 +258,7 @@ std::string generate(const DevPlan &P) {
         uint32_t u = 0;
         for (uint32_t f = 0; f < P.n_fields; ++f) {
             const DevField &d = P.f[f];
-            if (!d.width) continue;
+            if (!d.width || direct[f]) continue;
             // pieces of one raw field share its column: one run per column
             bool seen = false;
             for (uint32_t g = 0; g < f; ++g) seen = seen || (P.f[g].width && P.f[g].col_off == d.col_off);
@@ -245,7 +268,7 @@ std::string generate(const DevPlan &P) {
                 const uint32_t lanes = std::min<uint32_t>(1024, run - at) / 16;
                 snprintf(b, sizeof b,
                          "            lds_flush(blk + (uint64_t)cap * %uu + (uint64_t)W * %uu, %uu, %uu, %uu);\n",
-                         d.col_off, run, at, rows * d.col_off + at, lanes);
+                         d.col_off, run, at, rows * lds_col[f] + at, lanes);
                 per_wave[u % lw] += b;
             }
         }

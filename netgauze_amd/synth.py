@@ -156,6 +156,11 @@ _F313R = [(f, {1: 4, 2: 4, 198: 4, 89: 1, 234: 2, 235: 2}.get(f, ln)) for f, ln 
 CFG3_TEMPLATES = [(256, T20), (347, _F347), (348, _F348), (342, _F342), (313, _F313), (307, _F307), (1024, _F1024),
                   (2313, _F313R)]
 
+# Config 5: the 8 config-3 templates plus 8 width permutations (the same IEs
+# in reverse order: other field offsets, another per-template kernel each)
+SEED_CFG5 = 0x4E475A4500000005
+CFG5_TEMPLATES = CFG3_TEMPLATES + [(tid + 4000, list(reversed(f))) for tid, f in CFG3_TEMPLATES]
+
 _DT_MS = {152, 153, 154, 155, 156, 157, 158, 159}  # dateTime{Milli,Micro,Nano}seconds IEs used here (152/153 ms)
 
 

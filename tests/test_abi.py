@@ -55,14 +55,15 @@ def test_product_does_not_import_oracle():
                 assert "ngz_oracle" not in text and "oracle/" not in text, f
 
 
-@pytest.mark.parametrize("tid", [t for t, _ in __import__("netgauze_amd.synth", fromlist=["x"]).CFG3_TEMPLATES])
+@pytest.mark.parametrize("tid", [t for t, _ in __import__("netgauze_amd.synth", fromlist=["x"]).CFG5_TEMPLATES])
 def test_template_kernels_compile_for_gfx950(tid):
-    """The per-template decode kernel of every config-3 template is generated
+    """The per-template decode kernel of every config-5 template (config 3 and
+    its width permutations) is generated
     and compiled for gfx950 by hiprtc (no device needed): LDS-staged where the
     rows fit the workgroup budget, direct column stores otherwise."""
     import struct
     from netgauze_amd import _lib, synth
-    fields = dict(synth.CFG3_TEMPLATES)[tid]
+    fields = dict(synth.CFG5_TEMPLATES)[tid]
     rec = struct.pack(">HH", tid, len(fields)) + b"".join(struct.pack(">HH", i, ln) for i, ln in fields)
     lib = ctypes.CDLL(_lib.LIB_PATH)
     buf = ctypes.create_string_buffer(1 << 20)

@@ -69,3 +69,41 @@ def test_shard_range_partitions():
             parts = [shard_range(n, r, w) for r in range(w)]
             assert parts[0][0] == 0 and parts[-1][1] == n
             assert all(parts[i][1] == parts[i + 1][0] for i in range(w - 1))
+
+
+def _worker_many(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from netgauze_amd import dist as ndist
+    # rank 0 sees 20 templates (more than the default table), rank 1 three of them
+    counts = {256 + t: 10 * t + 1 for t in range(20)} if rank == 0 else {256: 5, 260: 7, 5000: 9}
+    total, tables = ndist.gather_template_counts(counts)
+    q.put((rank, total, [tuple(t.shape) for t in tables]))
+    dist.destroy_process_group()
+
+
+def test_count_allgather_more_templates_than_default_table():
+    """Config 5 has 16 templates per rank; a rank with more must not have any
+    dropped: ranks agree on the table size before the all-gather."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_many, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    exp = {256 + t: 10 * t + 1 for t in range(20)}
+    exp[256] += 5
+    exp[260] += 7
+    exp[5000] = 9
+    for _, total, shapes in res:
+        assert total == exp
+        assert shapes == [(20, 3), (20, 3)]

@@ -220,6 +220,32 @@ def test_cfg3_mixed_templates_oracle(dev):
     assert codec.template_counts(10) == {t: oc.ipfix_templates[t].processed_count for t, _ in synth.CFG3_TEMPLATES}
 
 
+def test_cfg5_sixteen_templates_sharded(dev):
+    """Config 5 shape (16 templates: config 3 + width permutations) against
+    the oracle, decoded as two shards on two contexts (ranks) as bench.py
+    --gpus N does; the shards' processed counts add up to the oracle's."""
+    from netgauze_amd import dist, synth
+    b, o, ln, _ = synth.mixed_stream(32_000, templates=synth.CFG5_TEMPLATES, seed=synth.SEED_CFG5)
+    bb = bytes(b.numpy())
+    data = [bb[x:x + y] for x, y in zip(o.tolist(), ln.tolist())]
+    tm = synth.templates_message(synth.CFG5_TEMPLATES)
+    oc = O.FlowInfoCodec()
+    oc.decode(bytearray(tm))
+    total = {}
+    for rank in range(2):
+        lo, hi = dist.shard_range(len(data), rank, 2)
+        codec = new_codec()
+        codec.decode_datagrams([tm])
+        shard = data[lo:hi]
+        batch = codec.decode_datagrams(shard)
+        oracle, _ = parity.oracle_datagrams(shard, oc)
+        stats = parity.check_batch(batch, oracle)
+        assert stats["unsupported"] == 0 and stats["err"] == 0
+        for t, c in codec.template_counts(10).items():
+            total[t] = total.get(t, 0) + c
+    assert total == {t: oc.ipfix_templates[t].processed_count for t, _ in synth.CFG5_TEMPLATES}
+
+
 def test_cfg3_mixed_templates_1e7(dev):
     """Config 3 at 10^7 records (1.25e6 per template): every column of every
     template compared on the GPU with the wire bytes re-laid."""
