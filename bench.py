@@ -96,16 +96,22 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; on a box with fewer GPUs than ranks (a rehearsal of
+    # the multi-rank path) ranks share devices round robin
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", init_method="env://")
+        # "nccl" is RCCL on ROCm (over xGMI between the GPUs of a node); NGZ_DIST_BACKEND=gloo
+        # rehearses the multi-rank path where ranks share one GPU
+        dist.init_process_group(os.environ.get("NGZ_DIST_BACKEND", "nccl"), init_method="env://")
 
     from netgauze_amd import synth
     from netgauze_amd.flow import FlowInfoCodec
 
     dev = torch.device("cuda", local)
+    cdev = dev if dist is None or dist.get_backend() == "nccl" else torch.device("cpu")  # collective tensors
     codec = FlowInfoCodec(local)
     n = args.records
     if args.workload == "t20":
@@ -134,7 +140,7 @@ def main():
     def step():
         batch = codec.decode_batch(buf, offs, lens, stream=stream)
         if dist is not None:  # templates.usage: RCCL all-gather of per-template counts
-            ndist.gather_template_counts(codec.template_counts(10, reset=True), device=dev)
+            ndist.gather_template_counts(codec.template_counts(10, reset=True), device=cdev)
         return batch
 
     for _ in range(args.warmup):
@@ -159,7 +165,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_per_step = elapsed / args.steps * 1e3
