@@ -383,12 +383,37 @@ __device__ bool utf8_valid_prefix(const F &byte_at, uint32_t len, bool stop_at_n
     return true;
 }
 
+// UTF-8 check of bytes [base, base+len) of a buffer resource: an ASCII fast
+// path reads the bytes 16 at a time (any byte >= 0x80 in them -> the exact
+// byte-wise check).  Strings made of ASCII are valid with or without the
+// stop-at-NUL rule, so the fast path answers for both.
+__device__ __forceinline__ bool utf8_valid_global(__amdgpu_buffer_rsrc_t r, uint32_t base, uint32_t len,
+                                                  bool stop_at_nul) {
+    const uint32_t end = base + len;
+    uint32_t acc = 0;
+    for (uint32_t a = base & ~3u; a < end; a += 16) {
+        const v4u x = __builtin_amdgcn_raw_buffer_load_b128(r, a, 0, 0);
+        const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int lo = (int)base - (int)(a + 4 * j), hi = (int)end - (int)(a + 4 * j);
+            if (hi <= 0) break;
+            uint32_t m = 0xFFFFFFFFu;
+            if (lo > 0) m = lo >= 4 ? 0u : (m << (8 * lo));
+            if (hi < 4) m &= 0xFFFFFFFFu >> (8 * (4 - hi));
+            acc |= w[j] & m;
+        }
+    }
+    if (!(acc & 0x80808080u)) return true;
+    return utf8_valid_prefix(GlobalBytes{r, base}, len, stop_at_nul);
+}
+
 // UTF-8 check of a fixed string field (errors only; the bytes go through dec_raw)
 __device__ __forceinline__ void check_str(const uint32_t (&R)[WIN_DW], const Pass &P, uint32_t o, uint32_t off,
                                           uint32_t f, uint32_t len, bool in_window) {
     if (!P.valid) return;
     const bool ok = in_window ? utf8_valid_prefix(WindowBytes{R, o}, len)
-                              : utf8_valid_prefix(GlobalBytes{P.rsrc, P.rbase + P.sh + off}, len);
+                              : utf8_valid_global(P.rsrc, P.rbase + P.sh + off, len, true);
     if (!ok) rec_error(P, off, E_REC_UTF8, f);
 }
 

@@ -219,6 +219,15 @@ void field_rule(const Spec &s, uint8_t &kind, uint16_t &width, uint8_t &fail) {
     failk(1);
 }
 
+// A plan gets a generated kernel when the device decodes it at all and no
+// raw field is huge (IE::Unknown of length 65535 never yields a record).
+bool rtc_eligible(const DevPlan &P) {
+    if (!P.rpl) return false;
+    for (uint32_t i = 0; i < P.n_fields; ++i)
+        if (P.f[i].kind != NGZ_K_VLEN && P.f[i].len > 4096) return false;
+    return true;
+}
+
 void build_plan(Version &v) {
     DevPlan &P = v.plan;
     memset(&P, 0, sizeof P);
@@ -731,7 +740,7 @@ int upload_slots(ngz_ctx *ctx, const std::vector<int32_t> cur_start[2], hipStrea
         Version &v = ctx->versions[ctx->slot_version[s]];
         plans[s] = v.plan;
         plans[s].spec = 0;
-        if (ctx->specialize && v.plan.rpl && !v.plan.has_vlen) {  // vlen templates: generic kernel
+        if (ctx->specialize && rtc_eligible(v.plan)) {
             // NGZ_OPT_SPECIALIZE 2: compile once the template has seen enough records to pay for it
             const bool want = ctx->specialize == 1 || v.seen_records >= NGZ_SPECIALIZE_MIN_RECORDS;
             if (v.rtc_state == 0 && want) {
@@ -892,7 +901,7 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
     auto launch_slot = [&](uint32_t s, const SlotRT *rt, bool &generic, hipStream_t ls) -> int {
         const Version &v = ctx->versions[ctx->slot_version[s]];
         if (!v.plan.rpl) return 0;
-        if (ctx->specialize && v.rtc_state == 1 && !v.plan.has_vlen) {
+        if (ctx->specialize && v.rtc_state == 1) {
             // one specialised kernel per active template, over that slot's chunks only
             uint32_t g, block = 256;
             if (v.plan.lds_waves) {
@@ -982,7 +991,7 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
             if (launched[s] || !rt.total || (rt.mode == NGZ_MODE_CHUNK && !rt.nchunks)) continue;
             missed = true;
             const Version &v = ctx->versions[ctx->slot_version[s]];
-            const bool spec = ctx->specialize && v.rtc_state == 1 && !v.plan.has_vlen;
+            const bool spec = ctx->specialize && v.rtc_state == 1;
             if (!spec && generic) continue;  // the generic kernel walked every non-specialised slot
             if (launch_slot(s, &rt, generic2, st)) return -1;
             launched[s] = 1;
@@ -1638,7 +1647,7 @@ extern "C" int ngz_template_kernel(const uint8_t *tmpl, size_t len, int compile,
         v.specs.push_back(s);
     }
     build_plan(v);
-    if (!v.plan.rpl || v.plan.has_vlen) return NGZ_E_INVALID;
+    if (!rtc_eligible(v.plan)) return NGZ_E_INVALID;
     std::string out = ngz_rtc_source(v.plan);
     int rc = NGZ_OK;
     if (compile) {

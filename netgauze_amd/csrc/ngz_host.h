@@ -202,7 +202,8 @@ struct ngz_ctx {
     ngz_batch_in last_in{};
     hipEvent_t ev[4]{};
     // auxiliary decode streams: per-template kernels of one batch run side by side
-    uint32_t n_aux = 3;                         // NGZ_DECODE_STREAMS - 1
+    uint32_t n_aux = 0;                         // NGZ_DECODE_STREAMS - 1 (side-by-side decode measured no better:
+                                                //  config 3 4.34 vs 4.42 ms, config 4 1.95 vs 2.40 ms serial vs 4 streams)
     hipStream_t aux[NGZ_MAX_AUX]{};
     hipEvent_t join_ev[NGZ_MAX_AUX]{};
     hipEvent_t fork_ev = nullptr;

@@ -468,7 +468,7 @@ __global__ void __launch_bounds__(256) k_decode_generic(BatchDev B) {
                 if (P.valid) {
                     const uint64_t at = P0.a0 + rel0 + data;
                     ColSt(P, col_off, 16).b128(P.lrow * 16, (uint32_t)at, (uint32_t)(at >> 32), L, 0);
-                    if ((dy >> 31) && !utf8_valid_prefix(GlobalBytes{P.rsrc, rel0 + data}, L, false))  // vlen string
+                    if ((dy >> 31) && !utf8_valid_global(P.rsrc, rel0 + data, L, false))  // vlen string
                         rec_error(P0, data, E_REC_UTF8, f, L);
                 }
                 seg = data + L;  // the next segment starts after the value

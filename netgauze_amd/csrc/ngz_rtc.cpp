@@ -48,13 +48,16 @@ std::string signature(const DevPlan &P) {
     char b[96];
     for (uint32_t f = 0; f < P.n_fields; ++f) {
         const DevField &d = P.f[f];
-        snprintf(b, sizeof b, ";%u,%u,%u,%u,%u", d.off, d.len, d.width, d.kind, d.col_off);
+        snprintf(b, sizeof b, ";%u,%u,%u,%u,%u,%u", d.off, d.len, d.width, d.kind, d.col_off, d.flags);
         s += b;
     }
     return s;
 }
 
+std::string generate_vlen(const DevPlan &P);
+
 std::string generate(const DevPlan &P) {
+    if (P.has_vlen) return generate_vlen(P);
     std::vector<Item> items;
     for (uint32_t f = 0; f < P.n_fields; ++f) {
         const DevField &d = P.f[f];
@@ -288,6 +291,194 @@ std::string generate(const DevPlan &P) {
     }
     src += "    if (rt.mode == NGZ_MODE_ROW) run_windows<" + L + ">(B, slot, shape, pass);\n";
     src += "    else run_chunks<" + L + ">(B, c0, c0 + nc, [](uint32_t) { return true; }, shape, pass);\n}\n";
+    return src;
+}
+
+// Templates with variable-length fields (IPFIX length 65535, RFC 7011 s7):
+// records are found by the framing walk (ngz_vlen_walk, per-row record
+// offsets) and decoded one record per lane in row mode.  The fields between
+// two variable-length fields form a segment whose offsets relative to the
+// segment start are constants, so each segment is decoded like a small fixed
+// template: statically planned register windows at the lane's segment start
+// (16-byte aligned loads re-aligned per lane, as for unaligned fixed records),
+// constant extraction offsets.  A variable-length field reads its u8 / 255 +
+// 3-byte length (generator.rs:1775-1793) from the window, stores
+// {u64 batch offset, u32 length, 0}, checks UTF-8 for strings (no NUL
+// truncation, generator.rs:1635-1672) and moves the lane's segment start past
+// its value.  Replaces the generic kernel's field-table walk with run-time
+// register indexing for these templates.
+std::string generate_vlen(const DevPlan &P) {
+    struct Seg {
+        std::vector<Item> items;   // fixed fields, offsets relative to the segment start
+        int vf = -1;               // variable-length field ending the segment
+        uint32_t vpos = 0;         // its length prefix, relative to the segment start
+    };
+    std::vector<Seg> segs(1);
+    uint32_t so = 0;
+    for (uint32_t f = 0; f < P.n_fields; ++f) {
+        const DevField &d = P.f[f];
+        Seg &sg = segs.back();
+        Item it{};
+        it.f = f;
+        it.off = so;
+        it.len = d.len;
+        it.width = d.width;
+        it.kind = d.kind;
+        it.col_off = d.col_off;
+        switch (d.kind) {
+        case NGZ_K_VLEN:
+            sg.vf = (int)f;
+            sg.vpos = so;
+            segs.emplace_back();
+            so = 0;
+            continue;
+        case NGZ_K_FAIL:
+            it.type = 4;
+            sg.items.push_back(it);
+            break;
+        case NGZ_K_UINT: case NGZ_K_SCOPE32: case NGZ_K_TCPFLAGS: case NGZ_K_SINT:
+        case NGZ_K_BOOL: case NGZ_K_DTMS: case NGZ_K_DTFRAC: {
+            uint32_t L = d.len;
+            if (d.kind == NGZ_K_DTMS || d.kind == NGZ_K_DTFRAC) L = 8;
+            if (d.kind == NGZ_K_BOOL) L = 1;
+            if (L == 0) L = 1;
+            it.type = 0;
+            it.d0 = so >> 2;
+            it.d1 = (so + L - 1) >> 2;
+            sg.items.push_back(it);
+            break;
+        }
+        case NGZ_K_STR: case NGZ_K_BYTES: case NGZ_K_U256: {
+            if (d.kind == NGZ_K_STR) {
+                Item c = it;
+                c.type = d.len <= 64 ? 2 : 3;
+                c.d0 = so >> 2;
+                c.d1 = d.len ? (so + d.len - 1) >> 2 : c.d0;
+                sg.items.push_back(c);
+            }
+            for (uint32_t j = 0;; j += 64) {
+                Item r = it;
+                r.type = 1;
+                r.j = j;
+                r.piece = std::min<uint32_t>(64, d.len - j);
+                const bool last = j + 64 >= d.len;
+                r.pad_to = last ? d.width : 0;
+                r.d0 = (so + j) >> 2;
+                r.d1 = r.piece ? (so + j + r.piece - 1) >> 2 : r.d0;
+                sg.items.push_back(r);
+                if (last) break;
+            }
+            break;
+        }
+        default:
+            break;
+        }
+        so += d.len;
+    }
+    std::string body;
+    char b[640];
+    body += "        const Pass &P0 = P[0];\n";
+    body += "        Pass Q = P0;                              // window loads relative to the segment start\n";
+    body += "        const uint32_t rel0 = P0.rbase + P0.sh;   // record start, relative to the resource\n";
+    body += "        uint32_t seg = 0;                         // per lane: record offset of the segment\n";
+    body += "        (void)rel0; (void)seg;\n";
+    for (size_t si = 0; si < segs.size(); ++si) {
+        Seg &sg = segs[si];
+        // the length prefix of the closing vlen field is read from the segment's windows too
+        std::vector<Item> items = sg.items;
+        if (sg.vf >= 0) {
+            Item v{};
+            v.type = 5;
+            v.f = (uint32_t)sg.vf;
+            v.off = sg.vpos;
+            v.d0 = sg.vpos >> 2;
+            v.d1 = (sg.vpos + 3) >> 2;
+            items.push_back(v);
+        }
+        // windows: greedy in segment order
+        std::vector<std::pair<uint32_t, uint32_t>> wins;
+        std::vector<int> item_win(items.size(), -1);
+        for (size_t i = 0; i < items.size(); ++i) {
+            const Item &it = items[i];
+            if (it.type == 3 || it.type == 4) continue;
+            if (wins.empty() || it.d0 < wins.back().first || it.d1 >= wins.back().first + kWinDw) wins.push_back({it.d0, 1});
+            auto &w = wins.back();
+            w.second = std::max(w.second, it.d1 - w.first + 1);
+            item_win[i] = (int)wins.size() - 1;
+        }
+        int cur = -1;
+        for (size_t i = 0; i < items.size(); ++i) {
+            const Item &it = items[i];
+            const int w = item_win[i];
+            if (w >= 0 && w != cur) {
+                snprintf(b, sizeof b, "        win_load<%u>(R[0], Q, %uu);\n", wins[w].second, 4 * wins[w].first);
+                body += b;
+                cur = w;
+            }
+            const uint32_t wb = w >= 0 ? 4 * wins[w].first : 0;
+            switch (it.type) {
+            case 0:
+                snprintf(b, sizeof b, "        dec_num(R[0], P0, %uu, seg + %uu, %uu, %uu, %uu, %uu, %uu);\n", it.off - wb,
+                         it.off, it.f, it.len, it.width, it.kind, it.col_off);
+                break;
+            case 1:
+                snprintf(b, sizeof b, "        dec_raw(R[0], P0, %uu, %uu, %uu, %uu, %uu, %uu);\n", it.off + it.j - wb, it.j,
+                         it.piece, it.width, it.col_off, it.pad_to);
+                break;
+            case 2:
+                snprintf(b, sizeof b, "        check_str(R[0], P0, %uu, seg + %uu, %uu, %uu, true);\n", it.off - wb, it.off,
+                         it.f, it.len);
+                break;
+            case 3:
+                snprintf(b, sizeof b,
+                         "        if (P0.valid && !utf8_valid_global(P0.rsrc, rel0 + seg + %uu, %uu, true))"
+                         " rec_error(P0, seg + %uu, E_REC_UTF8, %uu);\n",
+                         it.off, it.len, it.off, it.f);
+                break;
+            case 4:
+                snprintf(b, sizeof b, "        fail_field(P0, seg + %uu, %uu);\n", it.off, it.f);
+                break;
+            case 5: {
+                const DevField &d = P.f[it.f];
+                const std::string F = std::to_string(it.f);
+                body += "        {  // variable-length field " + F + "\n";
+                snprintf(b, sizeof b,
+                         "            uint32_t L = rbyte(R[0], %uu), hdr = 1;\n"
+                         "            if (L == 255) { L = (uint32_t)rbe(R[0], %uu, 3); hdr = 4; }\n"
+                         "            const uint32_t data = seg + %uu + hdr;\n"
+                         "            if (P0.valid) {\n"
+                         "                const uint64_t at = P0.a0 + rel0 + data;\n"
+                         "                ColSt(P0, %uu, 16).b128(P0.lrow * 16, (uint32_t)at, (uint32_t)(at >> 32), L, 0);\n",
+                         it.off - wb, it.off + 1 - wb, it.off, d.col_off);
+                body += b;
+                if (d.flags & 0x80)  // string: every byte UTF-8 checked
+                    body += "                if (!utf8_valid_global(P0.rsrc, rel0 + data, L, false))\n"
+                            "                    rec_error(P0, data, E_REC_UTF8, " + F + "u, L);\n";
+                body += "            }\n"
+                        "            seg = data + L;\n"
+                        "            Q.rbase = (rel0 + seg) & ~3u;\n"
+                        "            Q.sh = (rel0 + seg) & 3u;\n"
+                        "            Q.any_sh = __builtin_amdgcn_ballot_w64(Q.sh != 0) != 0;\n"
+                        "        }\n";
+                cur = -1;  // the next segment needs its own windows
+                break;
+            }
+            }
+            if (it.type != 5) body += b;
+        }
+    }
+    std::string src;
+    src += "// generated by ngz_rtc.cpp for plan " + signature(P) + "\n";
+    src += "#include \"ngz_dev.h\"\nusing namespace ngzdev;\n";
+    src += "extern \"C\" __global__ void __launch_bounds__(256) ngz_tpl(BatchDev B, uint32_t slot) {\n";
+    src += "    if (sload(&B.summary->overflow)) return;\n";
+    src += "    auto shape = [](uint32_t) { return RecShape{" + std::to_string(P.rec_len) + "u, " +
+           std::to_string(P.row_bytes) + "u, true}; };\n";
+    src += "    auto pass = [&](const Pass (&P)[1]) {\n";
+    src += "        uint32_t R[1][WIN_DW];\n";
+    src += body;
+    src += "    };\n";
+    src += "    run_windows<1, false>(B, slot, shape, pass);\n}\n";
     return src;
 }
 
