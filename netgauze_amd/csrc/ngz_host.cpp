@@ -851,12 +851,23 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
     B.arena_cap = ctx->d_arena.cap - ctx->arena_shift;
     B.proc_counts = d_proc;
     B.cap_pad_windows = ctx->cap_pad_windows;
+    B.recmap = nullptr;
+    bool any_vlen = false;
+    for (uint32_t s = 0; s < S; ++s) {
+        const DevPlan &P = ctx->versions[ctx->slot_version[s]].plan;
+        any_vlen = any_vlen || (P.has_vlen && P.rpl);
+    }
+    if (any_vlen && getenv("NGZ_RECMAP") == nullptr) {  // NGZ_RECMAP set: walk twice (A/B)
+        if (ctx->d_recmap.ensure(in->bytes_size / 32 + 2)) return fail(ctx, NGZ_E_NOMEM, "device alloc (record map)");
+        B.recmap = ctx->d_recmap.p;
+    }
     B.summary = d_sum;
 
     HIPCHK(hipEventRecord(ctx->ev[0], st));
     // k_frame zeroes the count matrix itself; the summary and increments of
     // this parity were zeroed by the previous batch's k_export
     if (!N) HIPCHK(hipMemsetAsync(ctx->d_counts.p, 0, n_items * 4, st));
+    if (B.recmap) HIPCHK(hipMemsetAsync(B.recmap, 0, (in->bytes_size / 32 + 2) * 4, st));
     if (!ctx->clean[par]) {
         HIPCHK(hipMemsetAsync(d_sum, 0, sizeof(BatchSummary), st));
         HIPCHK(hipMemsetAsync(d_proc, 0, NGZ_MAX_SLOTS * 8, st));
@@ -1166,7 +1177,7 @@ void ngz_ctx_destroy(ngz_ctx *ctx) {
     ctx->d_tl_slot.release(); ctx->d_hf_flag.release(); ctx->d_hf_hdr.release(); ctx->d_hf_first.release(); ctx->d_hf_sets.release();
     ctx->d_hdr.release(); ctx->d_counts.release(); ctx->d_scan.release(); ctx->d_scan_tmp.release();
     ctx->d_slots.release(); ctx->d_chunks.release(); ctx->d_sets.release(); ctx->d_arena.release();
-    ctx->d_proc.release(); ctx->d_summary.release(); ctx->d_in_bytes.release(); ctx->d_in_off.release();
+    ctx->d_proc.release(); ctx->d_summary.release(); ctx->d_recmap.release(); ctx->d_in_bytes.release(); ctx->d_in_off.release();
     ctx->d_in_len.release();
     for (auto &e : ctx->ev) hipEventDestroy(e);
     for (uint32_t i = 0; i < ctx->n_aux; ++i) {

@@ -190,6 +190,7 @@ struct ngz_ctx {
     ngzh::DevBuf<uint8_t> d_arena;
     ngzh::DevBuf<unsigned long long> d_proc;
     ngzh::DevBuf<BatchSummary> d_summary;
+    ngzh::DevBuf<uint32_t> d_recmap;            // record-start bitmap of variable-length sets
     // host staging for ngz_decode_batch_host
     ngzh::DevBuf<uint8_t> d_in_bytes;
     ngzh::DevBuf<uint64_t> d_in_off;

@@ -209,8 +209,17 @@ struct CountVis {
     uint32_t N, S, d;
     uint32_t sets;
     const DevPlan *plans;
+    uint32_t *recmap;
+    uint64_t dg_off;
     __device__ uint32_t vlen(const uint8_t *p, uint32_t pos, uint32_t end, uint32_t, const DevPlan &pl, uint64_t *err) {
-        return ngz_vlen_walk(p, pos, end, pl, err, [](uint32_t, uint32_t) {});
+        uint32_t *rm = recmap;
+        const uint64_t g = dg_off;
+        return ngz_vlen_walk(p, pos, end, pl, err, [rm, g](uint32_t, uint32_t at) {
+            if (rm) {
+                const uint64_t b = g + at;
+                atomicOr(&rm[b >> 5], 1u << (b & 31));
+            }
+        });
     }
     __device__ void on_set(uint32_t, uint32_t slot, uint32_t n, uint32_t, uint32_t) {
         counts[(uint64_t)slot * N + d] += n;
@@ -225,7 +234,7 @@ __global__ void k_frame(BatchDev B, const uint32_t *hf_flag, const uint32_t *hf_
     // this datagram's column of the count matrix starts at zero (no memset pass)
     for (uint32_t r = 0; r < 2 * B.n_slots; ++r) B.counts[(uint64_t)r * B.n + d] = 0;
     if (d == 0) B.counts[(uint64_t)(2 * B.n_slots + 1) * B.n] = 0;  // the scan's trailing element
-    CountVis vis{B.counts, B.n, B.n_slots, d, 0, B.plans};
+    CountVis vis{B.counts, B.n, B.n_slots, d, 0, B.plans, B.recmap, B.offsets[d]};
     WalkOut o;
     walk_datagram(B, hf_flag, hf_first, d, o, vis);
     if (o.status != NGZ_FR_HOST && !(hf_flag && hf_flag[d]) && has_template_sets(B, d)) o.status = NGZ_FR_HOST;
@@ -315,6 +324,31 @@ struct EmitVis {
         const uint32_t rec0 = B->scan[(uint64_t)slot * B->n + d] - B->slots[slot].base;
         uint64_t *rs = rowsrc(slot) + rec0;
         uint32_t *rd = rowdg(slot) + rec0;
+        if (B->recmap) {
+            // k_frame's walk marked every complete record start: read the marks
+            // instead of walking the records again (independent loads, no
+            // dependent length-prefix chain)
+            const uint64_t g0 = dg_off + pos, g1 = dg_off + end;
+            uint32_t k = 0;
+            for (uint64_t w = g0 >> 5; g0 < g1 && w <= (g1 - 1) >> 5; ++w) {
+                uint32_t bits = B->recmap[w];
+                if ((w << 5) < g0) bits &= 0xFFFFFFFFu << (g0 & 31);
+                if (((w + 1) << 5) > g1) bits &= 0xFFFFFFFFu >> (32 - (g1 & 31));
+                while (bits) {
+                    const uint32_t bit = (uint32_t)__builtin_ctz(bits);
+                    rs[k] = (w << 5) + bit;
+                    rd[k] = d;
+                    ++k;
+                    bits &= bits - 1;
+                }
+            }
+            // the walk stopped inside (or right at the end of) this set: k_frame
+            // recorded that framing error in the datagram header
+            const uint64_t ek = ((const ngz_dgram_hdr *)B->hdr)[d].err_key;
+            const uint32_t stop = (uint32_t)(ek >> 48);
+            if (ek != NGZ_NO_ERR && stop >= pos && stop <= end) *err = ek;
+            return k;
+        }
         return ngz_vlen_walk(p, pos, end, pl, err, [&](uint32_t k, uint32_t at) {
             rs[k] = dg_off + at;
             rd[k] = d;
