@@ -28,6 +28,13 @@ INGEST_FUNCTIONS = [
     "ngz_collector_last_error", "ngz_collector_push", "ngz_collector_flush", "ngz_collector_peers",
     "ngz_udp_recv", "ngz_pcap_to_jsonl",
 ]
+# include/ngz/flow_aggregate.h
+AGG_FUNCTIONS = [
+    "ngz_agg_create", "ngz_agg_destroy", "ngz_agg_last_error", "ngz_agg_push", "ngz_agg_layout",
+    "ngz_agg_groups", "ngz_agg_flush", "ngz_agg_sets", "ngz_agg_last_timing",
+]
+NGZ_AGG_KEY, NGZ_AGG_ADD, NGZ_AGG_MIN, NGZ_AGG_MAX, NGZ_AGG_OR = range(5)
+NGZ_AGG_E_OVERFLOW, NGZ_AGG_E_COLLISION = -10, -11
 NGZ_COLLECT_PCAP_DECODER, NGZ_COLLECT_FLOW_INFO = 0, 1
 NGZ_PROTO_TCP, NGZ_PROTO_UDP = 6, 17
 
@@ -74,6 +81,19 @@ class FieldInfo(ctypes.Structure):
                 ("pen", ctypes.c_uint32), ("ie_id", ctypes.c_uint16), ("reserved", ctypes.c_uint16)]
 
 
+class AggField(ctypes.Structure):
+    _fields_ = [("pen", ctypes.c_uint32), ("ie_id", ctypes.c_uint16), ("index", ctypes.c_uint16),
+                ("op", ctypes.c_uint8), ("reserved", ctypes.c_uint8 * 7)]
+
+
+AGG_ROW_DTYPE = np.dtype([("window_start", "<u4"), ("flow_type", "u1"), ("reserved0", "u1", 3),
+                          ("key_present", "<u4"), ("val_present", "<u4"), ("record_count", "<u8"),
+                          ("min_export_time", "<u4"), ("max_export_time", "<u4"), ("max_sys_up_time", "<u4"),
+                          ("reserved1", "<u4"), ("min_collection_ms", "<i8"), ("max_collection_ms", "<i8"),
+                          ("template_bits", "<u8"), ("port_bits", "<u8"), ("domain_bits", "<u8", 2)])
+assert AGG_ROW_DTYPE.itemsize == 88
+
+
 DGRAM_HDR_DTYPE = np.dtype([("status", "u1"), ("version", "u1"), ("length", "<u2"), ("time", "<u4"),
                             ("sequence", "<u4"), ("domain", "<u4"), ("sys_up_time", "<u4"),
                             ("n_sets", "<u4"), ("err_key", "<u8")])
@@ -117,6 +137,28 @@ def load():
     lib.ngz_dgram_json.restype = ctypes.c_int64
     lib.ngz_batch_json.argtypes = [P, P, JSON_LINE_FN, P]
     lib.ngz_batch_json.restype = ctypes.c_int64
+    # aggregation (flow_aggregate.h)
+    lib.ngz_agg_create.argtypes = [I, ctypes.POINTER(AggField), U32, U64, U64, U64, ctypes.POINTER(P)]
+    lib.ngz_agg_create.restype = I
+    lib.ngz_agg_destroy.argtypes = [P]
+    lib.ngz_agg_destroy.restype = None
+    lib.ngz_agg_last_error.argtypes = [P]
+    lib.ngz_agg_last_error.restype = ctypes.c_char_p
+    lib.ngz_agg_push.argtypes = [P, P, ctypes.POINTER(BatchOut), ctypes.c_uint16, ctypes.c_int64,
+                                 ctypes.POINTER(ctypes.c_uint64), P]
+    lib.ngz_agg_push.restype = I
+    lib.ngz_agg_layout.argtypes = [P, ctypes.POINTER(U32), ctypes.POINTER(U32), ctypes.POINTER(ctypes.c_uint16),
+                                   ctypes.POINTER(U32), ctypes.POINTER(ctypes.c_uint16)]
+    lib.ngz_agg_layout.restype = I
+    lib.ngz_agg_groups.argtypes = [P]
+    lib.ngz_agg_groups.restype = ctypes.c_int64
+    lib.ngz_agg_flush.argtypes = [P, P, U64]
+    lib.ngz_agg_flush.restype = ctypes.c_int64
+    lib.ngz_agg_sets.argtypes = [P, ctypes.POINTER(U32), ctypes.POINTER(U32), ctypes.POINTER(ctypes.c_uint16),
+                                 ctypes.POINTER(U32), ctypes.POINTER(U32), ctypes.POINTER(U32), U32]
+    lib.ngz_agg_sets.restype = I
+    lib.ngz_agg_last_timing.argtypes = [P, ctypes.POINTER(ctypes.c_float)]
+    lib.ngz_agg_last_timing.restype = I
     # ingest (flow_ingest.h)
     lib.ngz_pcap_open.argtypes = [ctypes.c_char_p, ctypes.POINTER(P)]
     lib.ngz_pcap_open.restype = I

@@ -1,0 +1,841 @@
+// Flow aggregation on the device: the collector's windowed FlowAggregator
+// (crates/collector/src/flow/aggregation/aggregator.rs) over the columns the
+// decode path leaves in HBM.  C ABI: include/ngz/flow_aggregate.h.
+//
+// Pipeline of one ngz_agg_push (all on one stream):
+//   k_agg_dgram   per datagram: event time it contributes (OK status and >= 1
+//                 data record, aggregator.rs:308 yields one item per record),
+//                 observation-domain dictionary bit (device CAS table)
+//   hipcub max-scan over event times -> k_agg_late: lateness flag per datagram
+//                 (aggregation.rs:139-141: ts < current_time - lateness, with
+//                 current_time the running max of earlier non-late items)
+//   hipcub sum-scan over set record counts -> k_agg_setidx: set of every record
+//   k_agg_insert  one lane per record: key hash over the key columns, open
+//                 addressing insert into the HBM group table (64-bit CAS on the
+//                 tag), then the reductions of FlowCacheRecord::reduce
+//                 (aggregator.rs:159-198) as atomics on the group row
+//   k_agg_verify  (after all inserts) re-hashes every record and compares its
+//                 key bytes with the stored key of the group it landed in; a
+//                 mismatch is a 64-bit hash collision -> NGZ_AGG_E_COLLISION
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "ngz/flow_aggregate.h"
+#include "ngz/flow_decode.h"
+#include "ngz_host.h"
+
+namespace {
+
+constexpr uint32_t ROW_HDR = 88;  // sizeof(ngz_agg_row)
+static_assert(sizeof(ngz_agg_row) == ROW_HDR, "ngz_agg_row layout");
+constexpr uint32_t DOM_SLOTS = 128;
+
+// value classes (how a column value becomes the 64-bit accumulator operand)
+enum : uint8_t { VC_UINT = 0, VC_SINT = 1, VC_DTFRAC = 2, VC_BYTES = 3 };
+
+struct AggSlotPlan {            // per batch slot, built on the host every push
+    const uint8_t *key_col[NGZ_AGG_MAX_KEYS];   // null: the record has no such field (None)
+    const uint8_t *val_col[NGZ_AGG_MAX_VALUES];
+    uint16_t key_w[NGZ_AGG_MAX_KEYS];
+    uint16_t val_w[NGZ_AGG_MAX_VALUES];
+    uint8_t key_str[NGZ_AGG_MAX_KEYS];          // fixed string: bytes after the first NUL do not count
+    uint8_t val_vc[NGZ_AGG_MAX_VALUES];
+    uint64_t tpl_bit;
+    uint32_t proto;
+    uint32_t usable;                            // 0: slot not aggregated (no records / not device-decoded)
+};
+
+struct AggParams {
+    uint32_t n_keys, n_vals;
+    uint32_t key_off[NGZ_AGG_MAX_KEYS];
+    uint32_t val_off[NGZ_AGG_MAX_VALUES];
+    uint8_t val_op[NGZ_AGG_MAX_VALUES];
+    uint32_t row_bytes;
+    uint64_t mask;              // capacity - 1
+    uint32_t push_id;
+    uint32_t port_bit;
+    uint64_t coll_flip;         // collection time ms, sign bit flipped (unsigned order == signed order)
+};
+
+// dginfo: bit 0 usable (OK + has records + not late), bits 1..7 domain bit
+__device__ __forceinline__ uint64_t mix64(uint64_t h, uint64_t v) {
+    h ^= v + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
+    h *= 0xBF58476D1CE4E5B9ull;
+    return h ^ (h >> 31);
+}
+
+__device__ __forceinline__ uint32_t load_word(const uint8_t *p, uint32_t w, uint32_t j, bool str, bool &nul) {
+    // word j (4 bytes, zero padded past w) of a w-byte value at p
+    if ((w & 3) == 0 && !str) return *(const uint32_t *)(p + 4 * j);
+    uint32_t r = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < 4; ++b) {
+        const uint32_t i = 4 * j + b;
+        uint32_t c = i < w ? p[i] : 0u;
+        if (str) {
+            if (nul) c = 0;
+            else if (c == 0) nul = true;
+        }
+        r |= c << (8 * b);
+    }
+    return r;
+}
+
+__device__ __forceinline__ uint64_t key_hash(const AggSlotPlan &sp, const AggParams &P, uint64_t row, uint32_t win,
+                                             uint32_t &present) {
+    uint64_t h = mix64(0x4E475A41474731ull, ((uint64_t)win << 8) | sp.proto);
+    present = 0;
+    for (uint32_t k = 0; k < P.n_keys; ++k) {
+        const uint8_t *c = sp.key_col[k];
+        const uint32_t w = sp.key_w[k];
+        h = mix64(h, c ? (0x10000u | w) : 0u);
+        if (!c) continue;
+        present |= 1u << k;
+        const uint8_t *p = c + row * w;
+        bool nul = false;
+        for (uint32_t j = 0; j < (w + 3) / 4; ++j) h = mix64(h, load_word(p, w, j, sp.key_str[k], nul));
+    }
+    return h ? h : 1;
+}
+
+__device__ __forceinline__ uint64_t load_value(const uint8_t *p, uint32_t w, uint8_t vc) {
+    uint64_t v = 0;
+    if (vc == VC_DTFRAC) {  // {u32 secs, u32 nanos} -> ordered (secs, nanos)
+        const uint32_t s = *(const uint32_t *)p, ns = *(const uint32_t *)(p + 4);
+        return ((uint64_t)s << 32) | ns;
+    }
+    if (w == 8) v = *(const uint64_t *)p;
+    else if (w == 4) v = *(const uint32_t *)p;
+    else if (w == 2) v = *(const uint16_t *)p;
+    else v = *p;
+    if (vc == VC_SINT && w < 8) {  // sign-extend to 64 bits
+        const uint32_t sh = 64 - 8 * w;
+        v = (uint64_t)(((int64_t)(v << sh)) >> sh);
+    }
+    return v;
+}
+
+__global__ void k_agg_dgram(const ngz_dgram_hdr *__restrict__ hdr, const ngz_set_info *__restrict__ sets,
+                            uint32_t n_sets, uint32_t *__restrict__ has_rec) {
+    // has_rec[d] = 1 if the datagram carries >= 1 data record (in any set)
+    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < n_sets; s += gridDim.x * blockDim.x)
+        if (sets[s].n) has_rec[sets[s].dgram] = 1;
+}
+
+__global__ void k_agg_ts(const ngz_dgram_hdr *__restrict__ hdr, const uint32_t *__restrict__ has_rec, uint32_t n,
+                         uint32_t *__restrict__ ts) {
+    for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d < n; d += gridDim.x * blockDim.x)
+        ts[d] = (hdr[d].status == NGZ_DG_OK && has_rec[d]) ? hdr[d].time : 0u;
+}
+
+__global__ void k_agg_late(const ngz_dgram_hdr *__restrict__ hdr, const uint32_t *__restrict__ has_rec,
+                           const uint32_t *__restrict__ pmax, uint32_t n, uint32_t state_ct, uint64_t lateness_ms,
+                           unsigned long long *__restrict__ dom_tab, uint8_t *__restrict__ dginfo,
+                           unsigned int *__restrict__ err) {
+    for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d < n; d += gridDim.x * blockDim.x) {
+        uint8_t info = 0;
+        if (hdr[d].status == NGZ_DG_OK && has_rec[d]) {
+            uint32_t ct = state_ct;
+            if (d > 0 && pmax[d - 1] > ct) ct = pmax[d - 1];
+            const bool late = ct != 0 && (int64_t)hdr[d].time * 1000 < (int64_t)ct * 1000 - (int64_t)lateness_ms;
+            if (!late) {
+                // observation domain dictionary: linear probing over DOM_SLOTS entries (1<<32 | id)
+                const unsigned long long key = (1ull << 32) | hdr[d].domain;
+                uint32_t i = (hdr[d].domain * 2654435761u) % DOM_SLOTS, probes = 0;
+                for (;;) {
+                    unsigned long long cur = dom_tab[i];
+                    if (cur == 0) {
+                        cur = atomicCAS(&dom_tab[i], 0ull, key);
+                        if (cur == 0) break;
+                    }
+                    if (cur == key) break;
+                    i = (i + 1) % DOM_SLOTS;
+                    if (++probes == DOM_SLOTS) { atomicOr(err, 1u); i = 0xFF; break; }
+                }
+                if (i != 0xFF) info = (uint8_t)(1u | (i << 1));
+            } else {
+                info = 0x80;  // late marker (bit 0 clear)
+            }
+        }
+        dginfo[d] = info;
+    }
+}
+
+__global__ void k_agg_setidx(const ngz_set_info *__restrict__ sets, const uint32_t *__restrict__ rstart,
+                             uint32_t n_sets, uint32_t *__restrict__ setidx) {
+    // one wave per set writes the set index of each of its records
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t n_waves = (gridDim.x * blockDim.x) >> 6;
+    for (uint32_t s = wave; s < n_sets; s += n_waves) {
+        const uint32_t n = sets[s].n, r0 = rstart[s];
+        for (uint32_t i = lane; i < n; i += 64) setidx[r0 + i] = s;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_agg_insert(const ngz_dgram_hdr *__restrict__ hdr,
+                                                    const ngz_set_info *__restrict__ sets,
+                                                    const uint32_t *__restrict__ rstart,
+                                                    const uint32_t *__restrict__ setidx, uint64_t n_rec,
+                                                    const uint8_t *__restrict__ dginfo,
+                                                    const AggSlotPlan *__restrict__ plans, const AggParams P,
+                                                    unsigned long long *__restrict__ tags, uint8_t *__restrict__ rows,
+                                                    unsigned long long *__restrict__ late_count,
+                                                    unsigned int *__restrict__ err) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n_rec) return;
+    const uint32_t s = setidx[t];
+    const ngz_set_info si = sets[s];
+    const uint8_t info = dginfo[si.dgram];
+    if (!(info & 1)) {
+        if (info == 0x80) atomicAdd(late_count, 1ull);
+        return;
+    }
+    const AggSlotPlan &sp = plans[si.slot];
+    if (!sp.usable) return;
+    const uint64_t row = si.rec0 + (uint32_t)(t - rstart[s]);
+    const uint32_t ts = hdr[si.dgram].time;
+    const uint32_t win = ts - ts % 60;  // get_window_start: minute floor
+    uint32_t kp;
+    const uint64_t h = key_hash(sp, P, row, win, kp);
+    uint64_t g = h & P.mask;
+    bool won = false;
+    for (uint64_t probes = 0;; ++probes) {
+        unsigned long long cur = tags[g];
+        if (cur == 0) {
+            cur = atomicCAS(&tags[g], 0ull, (unsigned long long)h);
+            if (cur == 0) { won = true; break; }
+        }
+        if (cur == h) break;
+        g = (g + 1) & P.mask;
+        if (probes > P.mask) { atomicOr(err, 2u); return; }
+    }
+    uint8_t *R = rows + g * P.row_bytes;
+    if (won) {  // the group's first record writes its key (plain stores; read by later kernels only)
+        *(uint32_t *)(R + 0) = win;
+        *(uint32_t *)(R + 4) = sp.proto;
+        *(uint32_t *)(R + 8) = kp;
+        for (uint32_t k = 0; k < P.n_keys; ++k) {
+            const uint8_t *c = sp.key_col[k];
+            const uint32_t w = sp.key_w[k];
+            uint32_t *dst = (uint32_t *)(R + P.key_off[k]);
+            bool nul = false;
+            if (c)
+                for (uint32_t j = 0; j < (w + 3) / 4; ++j) dst[j] = load_word(c + row * w, w, j, sp.key_str[k], nul);
+        }
+    }
+    atomicAdd((unsigned long long *)(R + 16), 1ull);
+    atomicMin((unsigned int *)(R + 24), ts);
+    atomicMax((unsigned int *)(R + 28), ts);
+    const uint32_t sysup = hdr[si.dgram].version == 9 ? hdr[si.dgram].sys_up_time : 0u;
+    atomicMax((unsigned int *)(R + 32), sysup);
+    atomicOr((unsigned long long *)(R + 56), (unsigned long long)sp.tpl_bit);
+    const uint32_t db = info >> 1;
+    atomicOr((unsigned long long *)(R + 72 + 8 * (db >> 6)), 1ull << (db & 63));
+    // per-push constants once per (group, push): collection time, peer port
+    if (atomicExch((unsigned int *)(R + 36), P.push_id) != P.push_id) {
+        atomicMin((unsigned long long *)(R + 40), (unsigned long long)P.coll_flip);
+        atomicMax((unsigned long long *)(R + 48), (unsigned long long)P.coll_flip);
+        atomicOr((unsigned long long *)(R + 64), 1ull << P.port_bit);
+    }
+    uint32_t vp = 0;
+    for (uint32_t v = 0; v < P.n_vals; ++v) {
+        const uint8_t *c = sp.val_col[v];
+        if (!c) continue;
+        vp |= 1u << v;
+        const uint32_t w = sp.val_w[v];
+        const uint8_t vc = sp.val_vc[v];
+        uint8_t *dst = R + P.val_off[v];
+        if (vc == VC_BYTES) {  // BoolMapOr over bytes (mac, mpls label, octetArray, u256)
+            bool nul = false;
+            for (uint32_t j = 0; j < (w + 3) / 4; ++j) {
+                const uint32_t x = load_word(c + row * w, w, j, false, nul);
+                if (x) atomicOr((unsigned int *)dst + j, x);
+            }
+            continue;
+        }
+        uint64_t x = load_value(c + row * w, w, vc);
+        switch (P.val_op[v]) {
+        case NGZ_AGG_ADD: atomicAdd((unsigned long long *)dst, (unsigned long long)x); break;
+        case NGZ_AGG_MIN:
+            if (vc == VC_SINT) x ^= 1ull << 63;
+            atomicMin((unsigned long long *)dst, (unsigned long long)x);
+            break;
+        case NGZ_AGG_MAX:
+            if (vc == VC_SINT) x ^= 1ull << 63;
+            atomicMax((unsigned long long *)dst, (unsigned long long)x);
+            break;
+        default:
+            if (x) atomicOr((unsigned long long *)dst, (unsigned long long)x);
+            break;
+        }
+    }
+    if (vp) atomicOr((unsigned int *)(R + 12), vp);
+}
+
+__global__ __launch_bounds__(256) void k_agg_verify(const ngz_dgram_hdr *__restrict__ hdr,
+                                                    const ngz_set_info *__restrict__ sets,
+                                                    const uint32_t *__restrict__ rstart,
+                                                    const uint32_t *__restrict__ setidx, uint64_t n_rec,
+                                                    const uint8_t *__restrict__ dginfo,
+                                                    const AggSlotPlan *__restrict__ plans, const AggParams P,
+                                                    const unsigned long long *__restrict__ tags,
+                                                    const uint8_t *__restrict__ rows, unsigned int *__restrict__ err) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n_rec) return;
+    const uint32_t s = setidx[t];
+    const ngz_set_info si = sets[s];
+    if (!(dginfo[si.dgram] & 1)) return;
+    const AggSlotPlan &sp = plans[si.slot];
+    if (!sp.usable) return;
+    const uint64_t row = si.rec0 + (uint32_t)(t - rstart[s]);
+    const uint32_t ts = hdr[si.dgram].time;
+    const uint32_t win = ts - ts % 60;
+    uint32_t kp;
+    const uint64_t h = key_hash(sp, P, row, win, kp);
+    uint64_t g = h & P.mask;
+    for (uint64_t probes = 0; tags[g] != h; ++probes) {
+        g = (g + 1) & P.mask;
+        if (probes > P.mask) { atomicOr(err, 4u); return; }
+    }
+    const uint8_t *R = rows + g * P.row_bytes;
+    bool same = *(const uint32_t *)(R + 0) == win && *(const uint32_t *)(R + 4) == sp.proto &&
+                *(const uint32_t *)(R + 8) == kp;
+    for (uint32_t k = 0; k < P.n_keys && same; ++k) {
+        const uint8_t *c = sp.key_col[k];
+        if (!c) continue;
+        const uint32_t w = sp.key_w[k];
+        bool nul = false;
+        for (uint32_t j = 0; j < (w + 3) / 4; ++j)
+            same = same && ((const uint32_t *)(R + P.key_off[k]))[j] == load_word(c + row * w, w, j, sp.key_str[k], nul);
+    }
+    if (!same) atomicOr(err, 8u);
+}
+
+__global__ void k_agg_init(uint8_t *__restrict__ rows, uint64_t n_groups, uint32_t row_bytes,
+                           const uint32_t *__restrict__ ident, uint32_t ident_words) {
+    // every row <- the identity row (min fields at their maximum)
+    const uint64_t n_words = n_groups * (row_bytes / 4);
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_words;
+         i += (uint64_t)gridDim.x * blockDim.x)
+        ((uint32_t *)rows)[i] = ident[i % ident_words];
+}
+
+__global__ void k_agg_count(const unsigned long long *__restrict__ tags, uint64_t n_groups,
+                            unsigned long long *__restrict__ cursor) {
+    uint32_t c = 0;
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n_groups;
+         g += (uint64_t)gridDim.x * blockDim.x)
+        c += tags[g] != 0;
+    if (c) atomicAdd(cursor, (unsigned long long)c);
+}
+
+__global__ void k_agg_compact(const unsigned long long *__restrict__ tags, const uint8_t *__restrict__ rows,
+                              uint64_t n_groups, uint32_t row_bytes, uint8_t *__restrict__ out,
+                              unsigned long long *__restrict__ cursor) {
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n_groups;
+         g += (uint64_t)gridDim.x * blockDim.x) {
+        if (!tags[g]) continue;
+        const uint64_t o = atomicAdd(cursor, 1ull);
+        const uint32_t *src = (const uint32_t *)(rows + g * row_bytes);
+        uint32_t *dst = (uint32_t *)(out + o * row_bytes);
+        for (uint32_t i = 0; i < row_bytes / 4; ++i) dst[i] = src[i];
+    }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------
+struct ngz_agg {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    std::string last_error;
+    std::vector<ngz_agg_field> keys, vals;
+    uint64_t window_ms = 0, lateness_ms = 0;
+    uint64_t cap = 0;
+    AggParams P{};
+    // per-value state fixed at first sight: column width and value class
+    std::vector<int> val_w, val_vc, key_w;
+    std::vector<uint8_t> val_dtype;
+    // dictionaries (host) for template ids and peer ports
+    std::vector<uint32_t> templates;
+    std::vector<uint16_t> ports;
+    uint32_t current_time = 0;  // the peer's event time (seconds), 0 = none yet
+    uint32_t push_id = 0;
+    float t_push = 0;
+    // device
+    unsigned long long *tags = nullptr;
+    uint8_t *rows = nullptr;
+    uint32_t *ident = nullptr;
+    unsigned long long *dom_tab = nullptr;
+    unsigned int *err = nullptr;
+    unsigned long long *late = nullptr;
+    unsigned long long *cursor = nullptr;
+    AggSlotPlan *plans = nullptr;
+    uint32_t plans_cap = 0;
+    // scratch, grown on demand
+    void *scratch = nullptr;
+    size_t scratch_cap = 0;
+};
+
+namespace {
+
+int fail(ngz_agg *a, int rc, const std::string &msg) {
+    if (a) a->last_error = msg;
+    return rc;
+}
+
+#define AGG_HIP(a, x)                                                                     \
+    do {                                                                                  \
+        hipError_t e_ = (x);                                                              \
+        if (e_ != hipSuccess) return fail(a, NGZ_E_DEVICE, std::string(#x ": ") + hipGetErrorString(e_)); \
+    } while (0)
+
+uint32_t grid_for(uint64_t n, uint32_t block = 256, uint32_t max_blocks = 8192) {
+    uint64_t g = (n + block - 1) / block;
+    if (g == 0) g = 1;
+    return (uint32_t)std::min<uint64_t>(g, max_blocks);
+}
+
+int reset_table(ngz_agg *a) {
+    AGG_HIP(a, hipMemsetAsync(a->tags, 0, a->cap * 8, a->stream));
+    hipLaunchKernelGGL(k_agg_init, dim3(8192), dim3(256), 0, a->stream, a->rows, a->cap, a->P.row_bytes, a->ident,
+                       a->P.row_bytes / 4);
+    AGG_HIP(a, hipGetLastError());
+    return NGZ_OK;
+}
+
+// Which reductions the device runs for an IE data type (generator.rs:580-629,
+// config.rs:212-250).  Returns the value class or -1 with a reason.
+int value_class(const ngzh::IeRow *r, uint8_t op, std::string &why) {
+    using namespace ngzh;
+    const uint8_t dt = r ? r->dtype : DT_octetArray;
+    const bool subreg = r && (r->flags & 4);
+    const bool tcp = r && (r->flags & 2);
+    const bool integer = dt == DT_unsigned8 || dt == DT_unsigned16 || dt == DT_unsigned32 || dt == DT_unsigned64 ||
+                         dt == DT_signed8 || dt == DT_signed16 || dt == DT_signed32 || dt == DT_signed64;
+    const bool sgn = dt == DT_signed8 || dt == DT_signed16 || dt == DT_signed32 || dt == DT_signed64;
+    switch (op) {
+    case NGZ_AGG_ADD:
+        if (dt == DT_float32 || dt == DT_float64) { why = "float addition is order dependent (not on device)"; return -1; }
+        if (!integer || subreg || tcp) { why = "field does not support arithmetic operations"; return -1; }
+        return sgn ? VC_SINT : VC_UINT;
+    case NGZ_AGG_MIN:
+    case NGZ_AGG_MAX:
+        if (dt == DT_float32 || dt == DT_float64 || dt == DT_macAddress || dt == DT_ipv6Address || subreg || tcp ||
+            dt == DT_boolean) {
+            why = "comparison of this type is not on the device yet";
+            return -1;
+        }
+        if (integer || dt == DT_ipv4Address || dt == DT_dateTimeSeconds) return sgn ? VC_SINT : VC_UINT;
+        if (dt == DT_dateTimeMilliseconds) return VC_SINT;
+        if (dt == DT_dateTimeMicroseconds || dt == DT_dateTimeNanoseconds) return VC_DTFRAC;
+        why = "field does not support comparison operations";
+        return -1;
+    case NGZ_AGG_OR:
+        if (dt == DT_float32 || dt == DT_float64 || dt == DT_string || dt == DT_basicList ||
+            dt == DT_subTemplateList || dt == DT_subTemplateMultiList || dt == DT_dateTimeSeconds ||
+            dt == DT_dateTimeMilliseconds || dt == DT_dateTimeMicroseconds || dt == DT_dateTimeNanoseconds) {
+            why = "field does not support bitwise operations";
+            return -1;
+        }
+        if (subreg && !tcp) { why = "bitwise OR of sub-registry values is not on the device yet"; return -1; }
+        if (integer || dt == DT_boolean || dt == DT_ipv4Address) return VC_UINT;
+        return VC_BYTES;  // octetArray, macAddress, ipv6Address, unsigned256
+    }
+    why = "unknown op";
+    return -1;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ngz_agg_create(int device, const ngz_agg_field *fields, uint32_t n_fields, uint64_t window_ms,
+                   uint64_t lateness_ms, uint64_t capacity, ngz_agg **out) {
+    if (!out || (n_fields && !fields)) return NGZ_E_INVALID;
+    *out = nullptr;
+    if (window_ms == 0 || lateness_ms > window_ms) return NGZ_E_INVALID;  // AggregationConfig::validate
+    ngz_agg *a = new ngz_agg();
+    a->device = device;
+    a->window_ms = window_ms;
+    a->lateness_ms = lateness_ms;
+    for (uint32_t i = 0; i < n_fields; ++i) {
+        const ngz_agg_field &f = fields[i];
+        if (f.op > NGZ_AGG_OR) { delete a; return NGZ_E_INVALID; }
+        if (f.op == NGZ_AGG_KEY) a->keys.push_back(f);
+        else {
+            std::string why;
+            if (value_class(ngzh::ie_find(f.pen, f.ie_id), f.op, why) < 0) { delete a; return NGZ_E_INVALID; }
+            a->vals.push_back(f);
+        }
+    }
+    if (a->keys.size() > NGZ_AGG_MAX_KEYS || a->vals.size() > NGZ_AGG_MAX_VALUES) { delete a; return NGZ_E_LIMIT; }
+    a->key_w.assign(a->keys.size(), -1);
+    a->val_w.assign(a->vals.size(), -1);
+    a->val_vc.assign(a->vals.size(), -1);
+    // row layout: header, keys (IE width rounded to 4; the width is fixed by the IE's Rust type except
+    // for octet arrays, whose width is fixed at first sight), values (8 B; byte ORs up to 32 B)
+    uint32_t off = ROW_HDR;
+    AggParams &P = a->P;
+    P.n_keys = (uint32_t)a->keys.size();
+    P.n_vals = (uint32_t)a->vals.size();
+    for (uint32_t k = 0; k < P.n_keys; ++k) {
+        const ngzh::IeRow *r = ngzh::ie_find(a->keys[k].pen, a->keys[k].ie_id);
+        uint32_t w = 32;  // octetArray / string keys: up to 32 bytes on the device
+        if (r) {
+            switch (r->dtype) {
+            case ngzh::DT_unsigned8: case ngzh::DT_signed8: case ngzh::DT_boolean: w = 4; break;
+            case ngzh::DT_unsigned16: case ngzh::DT_signed16: w = 4; break;
+            case ngzh::DT_unsigned32: case ngzh::DT_signed32: case ngzh::DT_float32: case ngzh::DT_ipv4Address:
+            case ngzh::DT_dateTimeSeconds: w = 4; break;
+            case ngzh::DT_unsigned64: case ngzh::DT_signed64: case ngzh::DT_float64:
+            case ngzh::DT_dateTimeMilliseconds: case ngzh::DT_dateTimeMicroseconds:
+            case ngzh::DT_dateTimeNanoseconds: w = 8; break;
+            case ngzh::DT_macAddress: w = 8; break;
+            case ngzh::DT_ipv6Address: w = 16; break;
+            default: w = 32; break;
+            }
+        }
+        P.key_off[k] = off;
+        off += w;
+    }
+    if (off - ROW_HDR > NGZ_AGG_MAX_KEY_BYTES + 64) { delete a; return NGZ_E_LIMIT; }
+    off = (off + 7) & ~7u;
+    for (uint32_t v = 0; v < P.n_vals; ++v) {
+        std::string why;
+        const int vc = value_class(ngzh::ie_find(a->vals[v].pen, a->vals[v].ie_id), a->vals[v].op, why);
+        P.val_off[v] = off;
+        P.val_op[v] = a->vals[v].op;
+        off += vc == VC_BYTES ? 32 : 8;
+    }
+    P.row_bytes = (off + 7) & ~7u;
+    uint64_t cap = 1024;
+    while (cap < 2 * std::max<uint64_t>(capacity, 1)) cap <<= 1;
+    a->cap = cap;
+    P.mask = cap - 1;
+    // identity row: min fields at their maximum
+    std::vector<uint32_t> ident(P.row_bytes / 4, 0);
+    ident[24 / 4] = 0xFFFFFFFFu;                      // min_export_time
+    ident[40 / 4] = ident[44 / 4] = 0xFFFFFFFFu;      // min_collection (flipped order)
+    for (uint32_t v = 0; v < P.n_vals; ++v)
+        if (P.val_op[v] == NGZ_AGG_MIN) ident[P.val_off[v] / 4] = ident[P.val_off[v] / 4 + 1] = 0xFFFFFFFFu;
+    int rc = NGZ_OK;
+    auto bail = [&](int r, const char *what) {
+        a->last_error = what;
+        ngz_agg_destroy(a);
+        return r;
+    };
+    if (hipSetDevice(device) != hipSuccess) return bail(NGZ_E_DEVICE, "hipSetDevice");
+    if (hipStreamCreateWithFlags(&a->stream, hipStreamNonBlocking) != hipSuccess) return bail(NGZ_E_DEVICE, "stream");
+    hipEventCreate(&a->ev0);
+    hipEventCreate(&a->ev1);
+    if (hipMalloc(&a->tags, cap * 8) != hipSuccess || hipMalloc(&a->rows, cap * P.row_bytes) != hipSuccess ||
+        hipMalloc(&a->ident, P.row_bytes) != hipSuccess || hipMalloc(&a->dom_tab, DOM_SLOTS * 8) != hipSuccess ||
+        hipMalloc(&a->err, 4) != hipSuccess || hipMalloc(&a->late, 8) != hipSuccess ||
+        hipMalloc(&a->cursor, 8) != hipSuccess)
+        return bail(NGZ_E_NOMEM, "hipMalloc (group table)");
+    hipMemcpy(a->ident, ident.data(), P.row_bytes, hipMemcpyHostToDevice);
+    hipMemset(a->dom_tab, 0, DOM_SLOTS * 8);
+    hipMemset(a->err, 0, 4);
+    rc = reset_table(a);
+    if (rc == NGZ_OK && hipStreamSynchronize(a->stream) != hipSuccess) rc = NGZ_E_DEVICE;
+    if (rc != NGZ_OK) return bail(rc, "table init");
+    *out = a;
+    return NGZ_OK;
+}
+
+void ngz_agg_destroy(ngz_agg *a) {
+    if (!a) return;
+    if (a->stream) hipStreamSynchronize(a->stream);
+    hipFree(a->tags);
+    hipFree(a->rows);
+    hipFree(a->ident);
+    hipFree(a->dom_tab);
+    hipFree(a->err);
+    hipFree(a->late);
+    hipFree(a->cursor);
+    hipFree(a->plans);
+    hipFree(a->scratch);
+    if (a->ev0) hipEventDestroy(a->ev0);
+    if (a->ev1) hipEventDestroy(a->ev1);
+    if (a->stream) hipStreamDestroy(a->stream);
+    delete a;
+}
+
+const char *ngz_agg_last_error(ngz_agg *a) { return a ? a->last_error.c_str() : "null aggregator"; }
+
+int ngz_agg_layout(ngz_agg *a, uint32_t *row_bytes, uint32_t *key_off, uint16_t *key_width, uint32_t *val_off,
+                   uint16_t *val_width) {
+    if (!a) return NGZ_E_INVALID;
+    if (row_bytes) *row_bytes = a->P.row_bytes;
+    for (uint32_t k = 0; k < a->P.n_keys; ++k) {
+        if (key_off) key_off[k] = a->P.key_off[k];
+        if (key_width) key_width[k] = (uint16_t)std::max(a->key_w[k], 0);
+    }
+    for (uint32_t v = 0; v < a->P.n_vals; ++v) {
+        if (val_off) val_off[v] = a->P.val_off[v];
+        if (val_width) val_width[v] = (uint16_t)std::max(a->val_w[v], 0);
+    }
+    return NGZ_OK;
+}
+
+int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, uint16_t peer_port, int64_t collection_time_ms,
+                 uint64_t *late_records, void *hip_stream) {
+    if (!a || !ctx || !out) return NGZ_E_INVALID;
+    if (late_records) *late_records = 0;
+    AGG_HIP(a, hipSetDevice(a->device));
+    if (hip_stream) AGG_HIP(a, hipStreamSynchronize((hipStream_t)hip_stream));
+    // port dictionary
+    uint32_t port_bit = 0;
+    {
+        auto it = std::find(a->ports.begin(), a->ports.end(), peer_port);
+        if (it == a->ports.end()) {
+            if (a->ports.size() >= NGZ_AGG_SET_BITS) return fail(a, NGZ_AGG_E_OVERFLOW, "more than 64 peer ports");
+            a->ports.push_back(peer_port);
+            it = a->ports.end() - 1;
+        }
+        port_bit = (uint32_t)(it - a->ports.begin());
+    }
+    // per-slot plans: FieldRef lookup (IE, occurrence among non-scope fields), types fixed at first sight
+    const uint32_t S = out->n_slots;
+    std::vector<AggSlotPlan> plans(std::max<uint32_t>(S, 1));
+    std::vector<ngz_field_info> fi;
+    for (uint32_t s = 0; s < S; ++s) {
+        AggSlotPlan &sp = plans[s];
+        memset(&sp, 0, sizeof sp);
+        const ngz_slot_info &si = out->slots[s];
+        sp.proto = si.proto;
+        if (!si.n_records || !si.columns) continue;
+        const int nf = ngz_slot_fields(ctx, s, nullptr, 0);
+        if (nf < 0) return fail(a, NGZ_E_INVALID, "ngz_slot_fields");
+        fi.resize(std::max(nf, 1));
+        ngz_slot_fields(ctx, s, fi.data(), (uint32_t)nf);
+        const uint32_t tkey = ((uint32_t)si.proto << 16) | si.template_id;
+        auto it = std::find(a->templates.begin(), a->templates.end(), tkey);
+        if (it == a->templates.end()) {
+            if (a->templates.size() >= NGZ_AGG_SET_BITS) return fail(a, NGZ_AGG_E_OVERFLOW, "more than 64 template ids");
+            a->templates.push_back(tkey);
+            it = a->templates.end() - 1;
+        }
+        sp.tpl_bit = 1ull << (it - a->templates.begin());
+        auto find_field = [&](const ngz_agg_field &f) -> int {
+            uint32_t seen = 0;
+            for (int i = 0; i < nf; ++i) {
+                if (fi[i].is_scope) continue;
+                if (fi[i].pen == f.pen && fi[i].ie_id == f.ie_id) {
+                    if (seen == f.index) return i;
+                    ++seen;
+                }
+            }
+            return -1;
+        };
+        for (uint32_t k = 0; k < a->P.n_keys; ++k) {
+            const int i = find_field(a->keys[k]);
+            if (i < 0) continue;
+            const ngz_field_info &f = fi[i];
+            if (f.kind == NGZ_K_VLEN || f.kind == NGZ_K_FAIL)
+                return fail(a, NGZ_E_LIMIT, "variable-length key field (not on the device yet)");
+            const uint32_t room = (k + 1 < a->P.n_keys ? a->P.key_off[k + 1] : ((a->P.n_vals ? a->P.val_off[0] : a->P.row_bytes))) - a->P.key_off[k];
+            if (f.width > room) return fail(a, NGZ_E_LIMIT, "key field wider than its row slot");
+            sp.key_col[k] = si.columns + (uint64_t)si.capacity * f.col_off;
+            sp.key_w[k] = f.width;
+            sp.key_str[k] = f.kind == NGZ_K_STR;
+            if (a->key_w[k] < 0) a->key_w[k] = f.width;
+        }
+        for (uint32_t v = 0; v < a->P.n_vals; ++v) {
+            const int i = find_field(a->vals[v]);
+            if (i < 0) continue;
+            const ngz_field_info &f = fi[i];
+            std::string why;
+            const int vc = value_class(ngzh::ie_find(a->vals[v].pen, a->vals[v].ie_id), a->vals[v].op, why);
+            if (f.kind == NGZ_K_VLEN || f.kind == NGZ_K_FAIL || (vc == VC_BYTES && f.width > 32))
+                return fail(a, NGZ_E_LIMIT, "aggregated field is variable-length or wider than 32 bytes");
+            if (vc != VC_BYTES && vc != VC_DTFRAC && f.width != 1 && f.width != 2 && f.width != 4 && f.width != 8)
+                return fail(a, NGZ_E_LIMIT, "aggregated integer field of odd width");
+            if (a->val_w[v] >= 0 && a->val_w[v] != f.width)
+                return fail(a, NGZ_E_LIMIT, "aggregated field width differs between templates");
+            a->val_w[v] = f.width;
+            a->val_vc[v] = vc;
+            sp.val_col[v] = si.columns + (uint64_t)si.capacity * f.col_off;
+            sp.val_w[v] = f.width;
+            sp.val_vc[v] = (uint8_t)vc;
+        }
+        sp.usable = 1;
+    }
+    const uint32_t D = out->n_dgrams, NS = out->n_sets;
+    if (!D || !NS) return NGZ_OK;
+    // scratch: has_rec[D], ts[D], pmax[D], dginfo[D], rstart[NS+1], setidx[R], cub temp
+    uint64_t n_rec = 0;
+    for (uint32_t s = 0; s < S; ++s) n_rec += out->slots[s].n_records;
+    size_t cub_max = 0, cub_sum = 0;
+    hipcub::DeviceScan::InclusiveScan(nullptr, cub_max, (uint32_t *)nullptr, (uint32_t *)nullptr, hipcub::Max(), D,
+                                      a->stream);
+    hipcub::DeviceScan::ExclusiveSum(nullptr, cub_sum, (uint32_t *)nullptr, (uint32_t *)nullptr, NS + 1, a->stream);
+    auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+    const size_t o_has = 0, o_ts = o_has + al(4ull * D), o_pm = o_ts + al(4ull * D), o_dg = o_pm + al(4ull * D),
+                 o_cnt = o_dg + al(D), o_rs = o_cnt + al(4ull * (NS + 1)), o_si = o_rs + al(4ull * (NS + 1)),
+                 o_cub = o_si + al(4ull * std::max<uint64_t>(n_rec, 1)), need = o_cub + al(std::max(cub_max, cub_sum));
+    if (need > a->scratch_cap) {
+        hipFree(a->scratch);
+        a->scratch = nullptr;
+        if (hipMalloc(&a->scratch, need) != hipSuccess) { a->scratch_cap = 0; return fail(a, NGZ_E_NOMEM, "scratch"); }
+        a->scratch_cap = need;
+    }
+    uint8_t *sc = (uint8_t *)a->scratch;
+    uint32_t *has_rec = (uint32_t *)(sc + o_has), *ts = (uint32_t *)(sc + o_ts), *pm = (uint32_t *)(sc + o_pm);
+    uint8_t *dginfo = sc + o_dg;
+    uint32_t *cnt = (uint32_t *)(sc + o_cnt), *rstart = (uint32_t *)(sc + o_rs), *setidx = (uint32_t *)(sc + o_si);
+    void *cub_tmp = sc + o_cub;
+    if (S > a->plans_cap) {
+        hipFree(a->plans);
+        a->plans = nullptr;
+        if (hipMalloc(&a->plans, sizeof(AggSlotPlan) * S) != hipSuccess) { a->plans_cap = 0; return fail(a, NGZ_E_NOMEM, "plans"); }
+        a->plans_cap = S;
+    }
+    hipStream_t st = a->stream;
+    AGG_HIP(a, hipMemcpyAsync(a->plans, plans.data(), sizeof(AggSlotPlan) * S, hipMemcpyHostToDevice, st));
+    AggParams P = a->P;
+    P.push_id = ++a->push_id;
+    P.port_bit = port_bit;
+    P.coll_flip = (uint64_t)collection_time_ms ^ (1ull << 63);
+    AGG_HIP(a, hipEventRecord(a->ev0, st));
+    AGG_HIP(a, hipMemsetAsync(has_rec, 0, 4ull * D, st));
+    AGG_HIP(a, hipMemsetAsync(a->late, 0, 8, st));
+    AGG_HIP(a, hipMemsetAsync(a->err, 0, 4, st));
+    const ngz_dgram_hdr *hdr = out->dgrams;
+    const ngz_set_info *sets = out->sets;
+    hipLaunchKernelGGL(k_agg_dgram, dim3(grid_for(NS)), dim3(256), 0, st, hdr, sets, NS, has_rec);
+    hipLaunchKernelGGL(k_agg_ts, dim3(grid_for(D)), dim3(256), 0, st, hdr, has_rec, D, ts);
+    size_t tmp = cub_max;
+    AGG_HIP(a, hipcub::DeviceScan::InclusiveScan(cub_tmp, tmp, ts, pm, hipcub::Max(), D, st));
+    hipLaunchKernelGGL(k_agg_late, dim3(grid_for(D)), dim3(256), 0, st, hdr, has_rec, pm, D, a->current_time,
+                       a->lateness_ms, a->dom_tab, dginfo, a->err);
+    // record starts of every set: n copied out of the set table (stride 16 B) then scanned
+    AGG_HIP(a, hipMemsetAsync(cnt + NS, 0, 4, st));
+    AGG_HIP(a, hipMemcpy2DAsync(cnt, 4, (const uint8_t *)sets + offsetof(ngz_set_info, n), sizeof(ngz_set_info), 4, NS,
+                                hipMemcpyDeviceToDevice, st));
+    tmp = cub_sum;
+    AGG_HIP(a, hipcub::DeviceScan::ExclusiveSum(cub_tmp, tmp, cnt, rstart, NS + 1, st));
+    hipLaunchKernelGGL(k_agg_setidx, dim3(grid_for(64ull * NS, 256, 4096)), dim3(256), 0, st, sets, rstart, NS, setidx);
+    AGG_HIP(a, hipGetLastError());
+    const uint32_t blocks = (uint32_t)((n_rec + 255) / 256);
+    if (n_rec) {
+        hipLaunchKernelGGL(k_agg_insert, dim3(blocks), dim3(256), 0, st, hdr, sets, rstart, setidx, n_rec, dginfo,
+                           a->plans, P, a->tags, a->rows, a->late, a->err);
+        hipLaunchKernelGGL(k_agg_verify, dim3(blocks), dim3(256), 0, st, hdr, sets, rstart, setidx, n_rec, dginfo,
+                           a->plans, P, a->tags, a->rows, a->err);
+    }
+    AGG_HIP(a, hipGetLastError());
+    AGG_HIP(a, hipEventRecord(a->ev1, st));
+    uint32_t last_pm = 0, errv = 0;
+    unsigned long long late = 0;
+    AGG_HIP(a, hipMemcpyAsync(&last_pm, pm + (D - 1), 4, hipMemcpyDeviceToHost, st));
+    AGG_HIP(a, hipMemcpyAsync(&errv, a->err, 4, hipMemcpyDeviceToHost, st));
+    AGG_HIP(a, hipMemcpyAsync(&late, a->late, 8, hipMemcpyDeviceToHost, st));
+    AGG_HIP(a, hipStreamSynchronize(st));
+    hipEventElapsedTime(&a->t_push, a->ev0, a->ev1);
+    if (last_pm > a->current_time) a->current_time = last_pm;
+    if (late_records) *late_records = late;
+    if (errv & 1) return fail(a, NGZ_AGG_E_OVERFLOW, "more than 128 observation domains");
+    if (errv & 6) return fail(a, NGZ_AGG_E_OVERFLOW, "group table full");
+    if (errv & 8) return fail(a, NGZ_AGG_E_COLLISION, "64-bit key hash collision");
+    return NGZ_OK;
+}
+
+int64_t ngz_agg_groups(ngz_agg *a) {
+    if (!a) return NGZ_E_INVALID;
+    AGG_HIP(a, hipSetDevice(a->device));
+    unsigned long long n = 0;
+    AGG_HIP(a, hipMemsetAsync(a->cursor, 0, 8, a->stream));
+    hipLaunchKernelGGL(k_agg_count, dim3(grid_for(a->cap)), dim3(256), 0, a->stream, a->tags, a->cap, a->cursor);
+    AGG_HIP(a, hipMemcpyAsync(&n, a->cursor, 8, hipMemcpyDeviceToHost, a->stream));
+    AGG_HIP(a, hipStreamSynchronize(a->stream));
+    return (int64_t)n;
+}
+
+int64_t ngz_agg_flush(ngz_agg *a, void *dst, uint64_t cap) {
+    if (!a) return NGZ_E_INVALID;
+    const int64_t n = ngz_agg_groups(a);
+    if (n < 0) return n;
+    const uint32_t RB = a->P.row_bytes;
+    if ((uint64_t)n * RB > cap || (n && !dst)) return fail(a, NGZ_E_INVALID, "flush buffer too small");
+    if (n) {
+        uint8_t *tmp = nullptr;
+        if (hipMalloc(&tmp, (uint64_t)n * RB) != hipSuccess) return fail(a, NGZ_E_NOMEM, "flush staging");
+        AGG_HIP(a, hipMemsetAsync(a->cursor, 0, 8, a->stream));
+        hipLaunchKernelGGL(k_agg_compact, dim3(grid_for(a->cap)), dim3(256), 0, a->stream, a->tags, a->rows, a->cap, RB,
+                           tmp, a->cursor);
+        hipError_t e = hipMemcpyAsync(dst, tmp, (uint64_t)n * RB, hipMemcpyDeviceToHost, a->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(a->stream);
+        hipFree(tmp);
+        if (e != hipSuccess) return fail(a, NGZ_E_DEVICE, hipGetErrorString(e));
+        // host finish: collection times back to signed, per-push marker cleared, values at the IE width
+        for (int64_t g = 0; g < n; ++g) {
+            uint8_t *R = (uint8_t *)dst + (uint64_t)g * RB;
+            uint64_t c;
+            memcpy(&c, R + 40, 8); c ^= 1ull << 63; memcpy(R + 40, &c, 8);
+            memcpy(&c, R + 48, 8); c ^= 1ull << 63; memcpy(R + 48, &c, 8);
+            memset(R + 36, 0, 4);
+            uint32_t vp;
+            memcpy(&vp, R + 12, 4);
+            for (uint32_t v = 0; v < a->P.n_vals; ++v) {
+                if (a->val_vc[v] == VC_BYTES || a->val_vc[v] < 0) continue;
+                uint8_t *p = R + a->P.val_off[v];
+                uint64_t x;
+                memcpy(&x, p, 8);
+                if (!(vp >> v & 1)) x = 0;
+                else {
+                    const int vc = a->val_vc[v];
+                    const uint8_t op = a->P.val_op[v];
+                    if (vc == VC_SINT && (op == NGZ_AGG_MIN || op == NGZ_AGG_MAX)) x ^= 1ull << 63;
+                    const int w = a->val_w[v];
+                    if (vc != VC_DTFRAC && w < 8) {  // wrap at the Rust width (release-mode +=), then extend
+                        const uint32_t sh = 64 - 8 * w;
+                        x = vc == VC_SINT ? (uint64_t)(((int64_t)(x << sh)) >> sh) : (x << sh) >> sh;
+                    }
+                }
+                memcpy(p, &x, 8);
+            }
+        }
+    }
+    a->current_time = 0;  // WindowAggregator::flush clears current_time
+    int rc = reset_table(a);
+    if (rc != NGZ_OK) return rc;
+    AGG_HIP(a, hipStreamSynchronize(a->stream));
+    return n;
+}
+
+int ngz_agg_sets(ngz_agg *a, uint32_t *templates, uint32_t *n_templates, uint16_t *ports, uint32_t *n_ports,
+                 uint32_t *domains, uint32_t *n_domains, uint32_t cap) {
+    if (!a) return NGZ_E_INVALID;
+    if (n_templates) *n_templates = (uint32_t)a->templates.size();
+    if (n_ports) *n_ports = (uint32_t)a->ports.size();
+    for (uint32_t i = 0; i < a->templates.size() && i < cap; ++i)
+        if (templates) templates[i] = a->templates[i];
+    for (uint32_t i = 0; i < a->ports.size() && i < cap; ++i)
+        if (ports) ports[i] = a->ports[i];
+    unsigned long long tab[DOM_SLOTS];
+    AGG_HIP(a, hipMemcpy(tab, a->dom_tab, sizeof tab, hipMemcpyDeviceToHost));
+    if (n_domains) *n_domains = DOM_SLOTS;
+    for (uint32_t i = 0; i < DOM_SLOTS && i < cap; ++i)  // bit i <-> slot i; absent slots read 0xFFFFFFFF
+        if (domains) domains[i] = tab[i] ? (uint32_t)tab[i] : 0xFFFFFFFFu;
+    return NGZ_OK;
+}
+
+int ngz_agg_last_timing(ngz_agg *a, float *push_ms) {
+    if (!a) return NGZ_E_INVALID;
+    if (push_ms) *push_ms = a->t_push;
+    return NGZ_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,172 @@
+"""CPU restatement of the collector's windowed flow aggregation (TEST INFRASTRUCTURE ONLY).
+
+This module is the checker for the device aggregation (include/ngz/flow_aggregate.h,
+netgauze_amd/csrc/ngz_agg.hip).  Only tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg may use it; the product path never imports it.
+
+It restates, over the packets of ngz_oracle.FlowInfoCodec:
+  - explode                      crates/collector/src/flow/aggregation/aggregator.rs:286-354
+  - FieldRef::map_fields         crates/collector/src/flow/types.rs:82-100
+  - FlowAggregator::push         aggregator.rs:78-90
+  - FlowCacheRecord::reduce      aggregator.rs:159-198
+  - Field add/min/max/or         ipfix-code-generator/src/generator.rs:896-1080 (`*lhs += *rhs`,
+                                 release-mode wrapping at the Rust width; `min`/`max`; `|=`,
+                                 byte-wise zip for arrays)
+  - WindowAggregator::process_item crates/analytics/src/aggregation.rs:124-172 (lateness drop,
+                                 window start = get_window_start :79-89, minute floor)
+Pinned by the reference's own unit tests (aggregator/tests.rs: test_reduce_add_operations
+:244-337, test_explode_ipfix_repeating_ie_fields :755-827, test_explode_ipfix_missing_fields
+:830-893), restated as vectors in tests/kats_agg.py.
+
+Values are canonical Python values: ints for integer / ipv4 / tcpControlBits / bool / date-time
+seconds, bytes for byte-like fields, str for strings.
+"""
+import ngz_oracle as O
+
+OP_KEY, OP_ADD, OP_MIN, OP_MAX, OP_OR = 0, 1, 2, 3, 4
+
+RUST_WIDTH = {"unsigned8": 1, "unsigned16": 2, "unsigned32": 4, "unsigned64": 8, "signed8": 1, "signed16": 2,
+              "signed32": 4, "signed64": 8}
+
+
+def canon(field):
+    """Field value -> canonical value (see module doc)."""
+    v = field.value
+    if isinstance(v, tuple) and v and v[0] in ("v4", "v6"):
+        return v[1] if v[0] == "v4" else v[1].to_bytes(16, "big")
+    if isinstance(v, bool):
+        return int(v)
+    if isinstance(v, O.DateTime):
+        return (v.secs, v.nanos)
+    return v
+
+
+def _wrap(ie, x):
+    w = RUST_WIDTH.get(ie.dtype)
+    if w is None:
+        return x
+    x &= (1 << (8 * w)) - 1
+    if ie.dtype.startswith("signed") and x >> (8 * w - 1):
+        x -= 1 << (8 * w)
+    return x
+
+
+def reduce_value(ie, op, lhs, rhs):
+    """Field::{add,min,max,bitwise_or}_assign_field on canonical values (generator.rs:896-1080)."""
+    if op == OP_ADD:
+        return _wrap(ie, lhs + rhs)
+    if op == OP_MIN:
+        return min(lhs, rhs)
+    if op == OP_MAX:
+        return max(lhs, rhs)
+    if isinstance(lhs, (bytes, bytearray)):  # lhs.iter_mut().zip(rhs): lhs keeps its length
+        out = bytearray(lhs)
+        for i, b in enumerate(rhs[:len(out)]):
+            out[i] |= b
+        return bytes(out)
+    return lhs | rhs
+
+
+def map_fields(fields):
+    """FieldRef::map_fields (types.rs:82-100): (IE key, occurrence index) -> Field."""
+    seen, out = {}, {}
+    for f in fields:
+        k = (f.ie.pen, f.ie.id)
+        i = seen.get(k, 0)
+        seen[k] = i + 1
+        out[(k, i)] = f
+    return out
+
+
+class FlowAggregatorOracle:
+    """One peer's WindowAggregator<IpAddr, UnifiedConfig, FlowAggregator> (aggregation.rs:96-186).
+
+    fields: [(pen, ie_id, index, op)] in transform order; keys and aggregated fields keep
+    their relative order (config.rs:252-335)."""
+
+    def __init__(self, fields, window_s=60, lateness_s=10):
+        self.keys = [(pen, ie, idx) for pen, ie, idx, op in fields if op == OP_KEY]
+        self.vals = [((pen, ie, idx), op) for pen, ie, idx, op in fields if op != OP_KEY]
+        self.window_s, self.lateness_s = window_s, lateness_s
+        self.current_time = None
+        self.groups = {}   # (window_start, flow_type, key tuple) -> record dict
+        self.late = 0
+
+    def explode(self, pkt, peer_port, collection_ms):
+        """aggregator.rs:286-354: one item per data record (non-scope fields)."""
+        if isinstance(pkt, O.IpfixPacket):
+            flow_type, ts, sysup, domain = 10, pkt.export_time.secs, 0, pkt.observation_domain_id
+        else:
+            flow_type, ts, sysup, domain = 9, pkt.unix_time.secs, pkt.sys_up_time, pkt.source_id
+        for sid, rec in pkt.data_records():
+            fields = rec[1] if isinstance(rec, tuple) else rec.fields
+            m = map_fields(fields)
+            key = tuple(canon(m[((p, i), x)]) if ((p, i), x) in m else None for p, i, x in self.keys)
+            vals = [(m[((p, i), x)].ie, canon(m[((p, i), x)])) if ((p, i), x) in m else None
+                    for (p, i, x), _op in self.vals]
+            yield flow_type, ts, key, dict(ports={peer_port}, domains={domain}, templates={(flow_type, sid)},
+                                           min_export=ts, max_export=ts, min_coll=collection_ms,
+                                           max_coll=collection_ms, max_sysup=sysup, vals=vals, count=1)
+
+    def push_packet(self, pkt, peer_port, collection_ms):
+        for flow_type, ts, key, rec in self.explode(pkt, peer_port, collection_ms):
+            # WindowAggregator::process_item (aggregation.rs:135-150), times in seconds (lateness in s)
+            if self.current_time is None:
+                self.current_time = ts
+            if ts < self.current_time - self.lateness_s:
+                self.late += 1
+                continue
+            self.current_time = max(self.current_time, ts)
+            g = (ts - ts % 60, flow_type, key)
+            cur = self.groups.get(g)
+            if cur is None:
+                self.groups[g] = rec
+            else:
+                self.reduce(cur, rec)
+
+    def reduce(self, lhs, rhs):
+        """FlowCacheRecord::reduce (aggregator.rs:159-198)."""
+        lhs["ports"] |= rhs["ports"]
+        lhs["domains"] |= rhs["domains"]
+        lhs["templates"] |= rhs["templates"]
+        lhs["min_export"] = min(lhs["min_export"], rhs["min_export"])
+        lhs["max_export"] = max(lhs["max_export"], rhs["max_export"])
+        lhs["min_coll"] = min(lhs["min_coll"], rhs["min_coll"])
+        lhs["max_coll"] = max(lhs["max_coll"], rhs["max_coll"])
+        lhs["max_sysup"] = max(lhs["max_sysup"], rhs["max_sysup"])
+        lhs["count"] += rhs["count"]
+        for i, (_ref, op) in enumerate(self.vals):
+            a, b = lhs["vals"][i], rhs["vals"][i]
+            if a is not None and b is not None:
+                lhs["vals"][i] = (a[0], reduce_value(a[0], op, a[1], b[1]))
+            elif a is None and b is not None:
+                lhs["vals"][i] = b
+
+    def flush(self):
+        """WindowAggregator::flush: every group, then forget the event time."""
+        out = []
+        for (win, ft, key), r in self.groups.items():
+            out.append(dict(window_start=win, flow_type=ft, key=key,
+                            vals=tuple(None if v is None else v[1] for v in r["vals"]),
+                            record_count=r["count"], min_export=r["min_export"], max_export=r["max_export"],
+                            max_sysup=r["max_sysup"], min_coll=r["min_coll"], max_coll=r["max_coll"],
+                            templates=set(r["templates"]), ports=set(r["ports"]), domains=set(r["domains"])))
+        self.groups = {}
+        self.current_time = None
+        return out
+
+
+def aggregate_datagrams(fields, datagrams, peer_port=4739, collection_ms=0, window_s=60, lateness_s=10):
+    """Decode `datagrams` in order with one codec (FlowInfoCodec::decode per datagram) and
+    aggregate every decoded packet; failed datagrams yield nothing."""
+    codec = O.FlowInfoCodec()
+    agg = FlowAggregatorOracle(fields, window_s, lateness_s)
+    for d in datagrams:
+        buf = bytearray(d)
+        try:
+            pkt = codec.decode(buf)
+        except O.ParseFail:
+            continue
+        if pkt is not None:
+            agg.push_packet(pkt, peer_port, collection_ms)
+    return agg

@@ -7,7 +7,8 @@ import re
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADERS = [os.path.join(ROOT, "include", "ngz", h) for h in ("flow_decode.h", "flow_ingest.h")]
+HEADERS = [os.path.join(ROOT, "include", "ngz", h) for h in ("flow_decode.h", "flow_ingest.h",
+                                                                        "flow_aggregate.h")]
 
 
 def declared_functions(headers=HEADERS):
@@ -21,7 +22,30 @@ def declared_functions(headers=HEADERS):
 def test_header_declares_abi():
     from netgauze_amd import _lib
     assert declared_functions(HEADERS[:1]) == sorted(_lib.ABI_FUNCTIONS)
-    assert declared_functions(HEADERS[1:]) == sorted(_lib.INGEST_FUNCTIONS)
+    assert declared_functions(HEADERS[1:2]) == sorted(_lib.INGEST_FUNCTIONS)
+    assert declared_functions(HEADERS[2:]) == sorted(_lib.AGG_FUNCTIONS)
+
+
+def test_agg_config_validation_without_device():
+    """AggregationConfig::validate / validate_operation_compatibility are checked before any
+    device call (config.rs:107-119, 212-250): zero window, lateness > window, Add on a
+    non-numeric IE, Min on a float all fail; the row layout matches ngz_agg_row."""
+    from netgauze_amd import _lib
+    lib = _lib.load()
+    A = _lib.AggField
+
+    def create(fields, window=60000, lateness=10000):
+        arr = (A * max(len(fields), 1))(*[A(p, i, x, o) for p, i, x, o in fields])
+        h = ctypes.c_void_p()
+        return lib.ngz_agg_create(0, arr, len(fields), window, lateness, 1024, ctypes.byref(h))
+    ok = [(0, 8, 0, _lib.NGZ_AGG_KEY), (0, 1, 0, _lib.NGZ_AGG_ADD)]
+    assert create(ok, window=0) == -1
+    assert create(ok, window=1000, lateness=2000) == -1
+    assert create([(0, 8, 0, _lib.NGZ_AGG_ADD)]) == -1        # sourceIPv4Address: not arithmetic
+    assert create([(0, 4, 0, _lib.NGZ_AGG_ADD)]) == -1        # protocolIdentifier: sub-registry
+    assert create([(0, 6, 0, _lib.NGZ_AGG_OR)]) in (-2, -3)   # tcpControlBits OR: valid, needs the device
+    assert create([(0, 56, 0, _lib.NGZ_AGG_ADD)]) == -1       # sourceMacAddress
+    assert create([(0, 1, 0, 9)]) == -1                       # unknown op
 
 
 def test_library_exports_every_declared_symbol():

@@ -1,0 +1,70 @@
+"""CPU: the aggregation oracle reproduces the reference's aggregation unit tests
+(tests/kats_agg.py, from aggregator/tests.rs) and the window/lateness rules of
+analytics/src/aggregation.rs:124-172."""
+import os
+import struct
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import kats_agg as K  # noqa: E402
+import ngz_agg_oracle as A  # noqa: E402
+
+
+def ipfix_msg(sets, export_time, seq=1, domain=7):
+    body = b"".join(sets)
+    return struct.pack(">HHIII", 10, 16 + len(body), export_time, seq, domain) + body
+
+
+def tset(tid, fields):
+    body = struct.pack(">HH", tid, len(fields)) + b"".join(struct.pack(">HH", i, n) for i, n in fields)
+    return struct.pack(">HH", 2, 4 + len(body)) + body
+
+
+def dset(tid, recs):
+    body = b"".join(recs)
+    return struct.pack(">HH", tid, 4 + len(body)) + body
+
+
+def test_repeating_ie_fields():
+    d = [ipfix_msg([tset(400, K.REPEAT_TEMPLATE), dset(400, [K.REPEAT_RECORD])], K.T_2025_01_01_16, domain=300)]
+    (g,) = A.aggregate_datagrams(K.REPEAT_FIELDS, d, peer_port=4739).flush()
+    for k, v in K.REPEAT_EXPECTED.items():
+        assert g[k] == v, k
+
+
+def test_missing_fields():
+    d = [ipfix_msg([tset(300, K.MISSING_TEMPLATE), dset(300, [K.MISSING_RECORD])], 1_700_000_000)]
+    (g,) = A.aggregate_datagrams(K.MISSING_FIELDS, d).flush()
+    for k, v in K.MISSING_EXPECTED.items():
+        assert g[k] == v, k
+
+
+def test_reduce_add_operations():
+    d = [ipfix_msg([tset(256, K.REDUCE_TEMPLATE_1), tset(257, K.REDUCE_TEMPLATE_2),
+                    dset(256, [K.REDUCE_WIRE_1]), dset(257, [K.REDUCE_WIRE_2])], 1_700_000_000)]
+    (g,) = A.aggregate_datagrams(K.REDUCE_FIELDS, d).flush()
+    assert g["vals"] == K.REDUCE_EXPECTED
+    assert g["record_count"] == 2 and g["templates"] == {(10, 256), (10, 257)}
+
+
+def test_add_wraps_at_rust_width():
+    # release-mode `*lhs += *rhs` on u8 / i8 wraps
+    ie_u8 = type("IE", (), {"dtype": "unsigned8"})()
+    ie_i8 = type("IE", (), {"dtype": "signed8"})()
+    assert A.reduce_value(ie_u8, A.OP_ADD, 200, 100) == 44
+    assert A.reduce_value(ie_i8, A.OP_ADD, 100, 100) == -56
+    assert A.reduce_value(ie_u8, A.OP_OR, b"\x01\x02", b"\x10\x20\x30") == b"\x11\x22"
+
+
+def test_lateness_and_minute_windows():
+    t = [tset(256, K.MISSING_TEMPLATE)]
+    rec = [dset(256, [K.MISSING_RECORD])]
+    times = [1_700_000_150, 1_700_000_180, 1_700_000_165, 1_700_000_169, 1_700_000_171]
+    d = [ipfix_msg(t + rec, times[0])] + [ipfix_msg(rec, x) for x in times[1:]]
+    agg = A.aggregate_datagrams(K.MISSING_FIELDS, d, lateness_s=10)
+    assert agg.late == 2  # 165 and 169 are more than 10 s behind 180
+    got = sorted((g["window_start"], g["record_count"]) for g in agg.flush())
+    assert got == [(1_700_000_100, 1), (1_700_000_160, 2)]  # minute floors
