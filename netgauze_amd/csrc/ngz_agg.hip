@@ -122,10 +122,10 @@ __device__ __forceinline__ uint64_t load_value(const uint8_t *p, uint32_t w, uin
 }
 
 __global__ void k_agg_dgram(const ngz_dgram_hdr *__restrict__ hdr, const ngz_set_info *__restrict__ sets,
-                            uint32_t n_sets, uint32_t *__restrict__ has_rec) {
+                            uint32_t n_sets, uint32_t n_dgrams, uint32_t *__restrict__ has_rec) {
     // has_rec[d] = 1 if the datagram carries >= 1 data record (in any set)
     for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < n_sets; s += gridDim.x * blockDim.x)
-        if (sets[s].n) has_rec[sets[s].dgram] = 1;
+        if (sets[s].n && sets[s].dgram < n_dgrams) has_rec[sets[s].dgram] = 1;
 }
 
 __global__ void k_agg_ts(const ngz_dgram_hdr *__restrict__ hdr, const uint32_t *__restrict__ has_rec, uint32_t n,
@@ -179,31 +179,30 @@ __global__ void k_agg_setidx(const ngz_set_info *__restrict__ sets, const uint32
     }
 }
 
-__global__ __launch_bounds__(256) void k_agg_insert(const ngz_dgram_hdr *__restrict__ hdr,
-                                                    const ngz_set_info *__restrict__ sets,
-                                                    const uint32_t *__restrict__ rstart,
-                                                    const uint32_t *__restrict__ setidx, uint64_t n_rec,
-                                                    const uint8_t *__restrict__ dginfo,
-                                                    const AggSlotPlan *__restrict__ plans, const AggParams P,
-                                                    unsigned long long *__restrict__ tags, uint8_t *__restrict__ rows,
-                                                    unsigned long long *__restrict__ late_count,
-                                                    unsigned int *__restrict__ err) {
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n_rec) return;
-    const uint32_t s = setidx[t];
-    const ngz_set_info si = sets[s];
-    const uint8_t info = dginfo[si.dgram];
-    if (!(info & 1)) {
-        if (info == 0x80) atomicAdd(late_count, 1ull);
-        return;
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
+    const int lo = __shfl_xor((int)(uint32_t)v, m), hi = __shfl_xor((int)(uint32_t)(v >> 32), m);
+    return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int lane) {
+    const int lo = __shfl((int)(uint32_t)v, lane), hi = __shfl((int)(uint32_t)(v >> 32), lane);
+    return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+enum { R_ADD, R_MIN, R_MAX, R_OR };
+template <int OP>
+__device__ __forceinline__ uint64_t wave_reduce(uint64_t v) {  // butterfly over the 64 lanes
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        const uint64_t o = shfl_xor64(v, m);
+        v = OP == R_ADD ? v + o : OP == R_MIN ? (o < v ? o : v) : OP == R_MAX ? (o > v ? o : v) : (v | o);
     }
-    const AggSlotPlan &sp = plans[si.slot];
-    if (!sp.usable) return;
-    const uint64_t row = si.rec0 + (uint32_t)(t - rstart[s]);
-    const uint32_t ts = hdr[si.dgram].time;
-    const uint32_t win = ts - ts % 60;  // get_window_start: minute floor
-    uint32_t kp;
-    const uint64_t h = key_hash(sp, P, row, win, kp);
+    return v;
+}
+
+// Open-addressing insert of hash h: returns the group's row, the key written by the
+// record that claimed the slot (64-bit CAS on the tag).
+__device__ __forceinline__ uint8_t *group_row(const AggSlotPlan &sp, const AggParams &P, uint64_t row, uint32_t win,
+                                              uint32_t kp, uint64_t h, unsigned long long *__restrict__ tags,
+                                              uint8_t *__restrict__ rows, unsigned int *__restrict__ err) {
     uint64_t g = h & P.mask;
     bool won = false;
     for (uint64_t probes = 0;; ++probes) {
@@ -214,10 +213,10 @@ __global__ __launch_bounds__(256) void k_agg_insert(const ngz_dgram_hdr *__restr
         }
         if (cur == h) break;
         g = (g + 1) & P.mask;
-        if (probes > P.mask) { atomicOr(err, 2u); return; }
+        if (probes > P.mask) { atomicOr(err, 2u); return nullptr; }
     }
     uint8_t *R = rows + g * P.row_bytes;
-    if (won) {  // the group's first record writes its key (plain stores; read by later kernels only)
+    if (won) {  // plain stores; read by later kernels only (flush, verify)
         *(uint32_t *)(R + 0) = win;
         *(uint32_t *)(R + 4) = sp.proto;
         *(uint32_t *)(R + 8) = kp;
@@ -230,59 +229,201 @@ __global__ __launch_bounds__(256) void k_agg_insert(const ngz_dgram_hdr *__restr
                 for (uint32_t j = 0; j < (w + 3) / 4; ++j) dst[j] = load_word(c + row * w, w, j, sp.key_str[k], nul);
         }
     }
-    atomicAdd((unsigned long long *)(R + 16), 1ull);
-    atomicMin((unsigned int *)(R + 24), ts);
-    atomicMax((unsigned int *)(R + 28), ts);
-    const uint32_t sysup = hdr[si.dgram].version == 9 ? hdr[si.dgram].sys_up_time : 0u;
-    atomicMax((unsigned int *)(R + 32), sysup);
-    atomicOr((unsigned long long *)(R + 56), (unsigned long long)sp.tpl_bit);
-    const uint32_t db = info >> 1;
-    atomicOr((unsigned long long *)(R + 72 + 8 * (db >> 6)), 1ull << (db & 63));
-    // per-push constants once per (group, push): collection time, peer port
-    if (atomicExch((unsigned int *)(R + 36), P.push_id) != P.push_id) {
+    return R;
+}
+
+// Operand of value v for the accumulator (signed min/max: sign bit flipped so unsigned order holds).
+__device__ __forceinline__ uint64_t value_operand(const AggSlotPlan &sp, const AggParams &P, uint32_t v, uint64_t row) {
+    const uint8_t vc = sp.val_vc[v];
+    uint64_t x = load_value(sp.val_col[v] + row * sp.val_w[v], sp.val_w[v], vc);
+    if (vc == VC_SINT && (P.val_op[v] == NGZ_AGG_MIN || P.val_op[v] == NGZ_AGG_MAX)) x ^= 1ull << 63;
+    return x;
+}
+
+// Conditional atomics: a plain load of the accumulator first.  Min / max / OR only ever
+// move one way between table resets, so a stale value can only cause an unneeded atomic,
+// never a skipped one; after a group's first few records most of them are skipped.
+__device__ __forceinline__ uint32_t peek32(const uint8_t *p) { return *(const volatile uint32_t *)p; }
+__device__ __forceinline__ uint64_t peek64(const uint8_t *p) { return *(const volatile uint64_t *)p; }
+__device__ __forceinline__ void min32(uint8_t *p, uint32_t v) { if (v < peek32(p)) atomicMin((unsigned int *)p, v); }
+__device__ __forceinline__ void max32(uint8_t *p, uint32_t v) { if (v > peek32(p)) atomicMax((unsigned int *)p, v); }
+__device__ __forceinline__ void or32(uint8_t *p, uint32_t v) {
+    if (v & ~peek32(p)) atomicOr((unsigned int *)p, v);
+}
+__device__ __forceinline__ void or64(uint8_t *p, uint64_t v) {
+    if (v & ~peek64(p)) atomicOr((unsigned long long *)p, (unsigned long long)v);
+}
+
+__device__ __forceinline__ void apply_value(uint8_t *dst, uint8_t op, uint64_t x) {
+    switch (op) {
+    case NGZ_AGG_ADD: if (x) atomicAdd((unsigned long long *)dst, (unsigned long long)x); break;
+    case NGZ_AGG_MIN: if (x < peek64(dst)) atomicMin((unsigned long long *)dst, (unsigned long long)x); break;
+    case NGZ_AGG_MAX: if (x > peek64(dst)) atomicMax((unsigned long long *)dst, (unsigned long long)x); break;
+    default: or64(dst, x); break;
+    }
+}
+
+__device__ __forceinline__ void apply_value_hot(uint8_t *dst, uint8_t op, uint64_t x) {
+    switch (op) {
+    case NGZ_AGG_ADD: atomicAdd((unsigned long long *)dst, (unsigned long long)x); break;
+    case NGZ_AGG_MIN: atomicMin((unsigned long long *)dst, (unsigned long long)x); break;
+    case NGZ_AGG_MAX: atomicMax((unsigned long long *)dst, (unsigned long long)x); break;
+    default: if (x) atomicOr((unsigned long long *)dst, (unsigned long long)x); break;
+    }
+}
+
+template <bool HOT = false>
+__device__ __forceinline__ void apply_push_constants(uint8_t *R, const AggParams &P) {
+    // per-push constants once per (group, push): collection time bounds, peer port
+    if ((HOT || peek32(R + 36) != P.push_id) && atomicExch((unsigned int *)(R + 36), P.push_id) != P.push_id) {
         atomicMin((unsigned long long *)(R + 40), (unsigned long long)P.coll_flip);
         atomicMax((unsigned long long *)(R + 48), (unsigned long long)P.coll_flip);
         atomicOr((unsigned long long *)(R + 64), 1ull << P.port_bit);
     }
+}
+
+// One lane per record.  Lanes of a wave that share a group (same key hash) are first
+// reduced across the wave and applied by one lane (wave pre-aggregation: low-cardinality
+// keys would otherwise serialise on a few hot rows); once the largest remaining group of
+// the wave has fewer than 4 records, every remaining lane applies its own record.
+__global__ __launch_bounds__(256) void k_agg_insert(const ngz_dgram_hdr *__restrict__ hdr,
+                                                    const ngz_set_info *__restrict__ sets,
+                                                    const uint32_t *__restrict__ rstart,
+                                                    const uint32_t *__restrict__ setidx, uint64_t n_rec,
+                                                    uint32_t n_dgrams, uint32_t n_slots,
+                                                    const uint8_t *__restrict__ dginfo,
+                                                    const AggSlotPlan *__restrict__ plans, const AggParams P,
+                                                    unsigned long long *__restrict__ tags, uint8_t *__restrict__ rows,
+                                                    unsigned long long *__restrict__ late_count,
+                                                    unsigned int *__restrict__ err) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    bool valid = false, late = false;
+    ngz_set_info si{};
+    uint8_t info = 0;
+    if (t < n_rec) {
+        const uint32_t s = setidx[t];
+        si = sets[s];
+        if (si.dgram >= n_dgrams || si.slot >= n_slots) atomicOr(err, 16u);
+        else {
+            info = dginfo[si.dgram];
+            late = info == 0x80;
+            valid = (info & 1) && plans[si.slot].usable;
+            if (valid) si.rec0 += (uint32_t)(t - rstart[s]);  // the record's row
+        }
+    }
+    const uint64_t late_mask = __ballot(late);
+    if (lane == 0 && late_mask) atomicAdd(late_count, (unsigned long long)__popcll(late_mask));
+    const AggSlotPlan &sp = plans[valid ? si.slot : 0];
+    const uint64_t row = si.rec0;
+    uint32_t ts = 0, win = 0, kp = 0, sysup = 0;
+    uint64_t h = 0, tpl = 0, dom0 = 0, dom1 = 0;
+    if (valid) {
+        ts = hdr[si.dgram].time;
+        win = ts - ts % 60;  // get_window_start: minute floor
+        h = key_hash(sp, P, row, win, kp);
+        sysup = hdr[si.dgram].version == 9 ? hdr[si.dgram].sys_up_time : 0u;
+        tpl = sp.tpl_bit;
+        const uint32_t db = info >> 1;
+        (db < 64 ? dom0 : dom1) = 1ull << (db & 63);
+    }
+    uint64_t todo = __ballot(valid);
+    while (todo) {
+        const int leader = __ffsll((unsigned long long)todo) - 1;
+        const uint64_t lh = readlane64(h, leader);
+        const bool mine = valid && ((todo >> lane) & 1) && h == lh;
+        const uint64_t match = __ballot(mine);
+        if (__popcll(match) < 4) break;
+        todo &= ~match;
+        const uint64_t cnt = __popcll(match);
+        const uint64_t tmin = wave_reduce<R_MIN>(mine ? ts : 0xFFFFFFFFull);
+        const uint64_t tmax = wave_reduce<R_MAX>(mine ? ts : 0ull);
+        const uint64_t smax = wave_reduce<R_MAX>(mine ? sysup : 0ull);
+        const uint64_t tpls = wave_reduce<R_OR>(mine ? tpl : 0ull);
+        const uint64_t d0 = wave_reduce<R_OR>(mine ? dom0 : 0ull), d1 = wave_reduce<R_OR>(mine ? dom1 : 0ull);
+        uint8_t *R = nullptr;
+        if (lane == leader) {
+            R = group_row(sp, P, row, win, kp, h, tags, rows, err);
+            if (R) {
+                atomicAdd((unsigned long long *)(R + 16), (unsigned long long)cnt);
+                // hot rows: fire-and-forget atomics (a load of a contended line costs more)
+                atomicMin((unsigned int *)(R + 24), (uint32_t)tmin);
+                atomicMax((unsigned int *)(R + 28), (uint32_t)tmax);
+                if (smax) atomicMax((unsigned int *)(R + 32), (uint32_t)smax);
+                atomicOr((unsigned long long *)(R + 56), (unsigned long long)tpls);
+                if (d0) atomicOr((unsigned long long *)(R + 72), (unsigned long long)d0);
+                if (d1) atomicOr((unsigned long long *)(R + 80), (unsigned long long)d1);
+                apply_push_constants<true>(R, P);
+            }
+        }
+        uint32_t vp = 0;
+        for (uint32_t v = 0; v < P.n_vals; ++v) {
+            const bool has = mine && sp.val_col[v] != nullptr;
+            if (!__ballot(has)) continue;
+            vp |= 1u << v;
+            const uint8_t op = P.val_op[v];
+            const bool bytes = has && sp.val_vc[v] == VC_BYTES;
+            const uint64_t x = (has && !bytes) ? value_operand(sp, P, v, row)
+                                               : (op == NGZ_AGG_MIN ? ~0ull : 0ull);
+            uint64_t r;
+            switch (op) {
+            case NGZ_AGG_ADD: r = wave_reduce<R_ADD>(x); break;
+            case NGZ_AGG_MIN: r = wave_reduce<R_MIN>(x); break;
+            case NGZ_AGG_MAX: r = wave_reduce<R_MAX>(x); break;
+            default: r = wave_reduce<R_OR>(x); break;
+            }
+            const bool any_num = __ballot(has && !bytes) != 0;  // (ballot outside lane-divergent code)
+            if (lane == leader && R && any_num) apply_value_hot(R + P.val_off[v], op, r);
+            if (__ballot(bytes)) {  // byte ORs: each matching lane ORs its words into the leader's row
+                const uint64_t Rl = readlane64((uint64_t)R, leader);
+                if (bytes && Rl) {
+                    const uint32_t w = sp.val_w[v];
+                    bool nul = false;
+                    for (uint32_t j = 0; j < (w + 3) / 4; ++j) {
+                        const uint32_t y = load_word(sp.val_col[v] + row * w, w, j, false, nul);
+                        or32((uint8_t *)Rl + P.val_off[v] + 4 * j, y);
+                    }
+                }
+            }
+        }
+        if (lane == leader && R && vp) atomicOr((unsigned int *)(R + 12), vp);
+    }
+    if (!(valid && ((todo >> lane) & 1))) return;
+    // per-record path
+    uint8_t *R = group_row(sp, P, row, win, kp, h, tags, rows, err);
+    if (!R) return;
+    atomicAdd((unsigned long long *)(R + 16), 1ull);
+    min32(R + 24, ts);
+    max32(R + 28, ts);
+    max32(R + 32, sysup);
+    or64(R + 56, tpl);
+    or64(R + (dom0 ? 72 : 80), dom0 | dom1);
+    apply_push_constants(R, P);
     uint32_t vp = 0;
     for (uint32_t v = 0; v < P.n_vals; ++v) {
         const uint8_t *c = sp.val_col[v];
         if (!c) continue;
         vp |= 1u << v;
         const uint32_t w = sp.val_w[v];
-        const uint8_t vc = sp.val_vc[v];
         uint8_t *dst = R + P.val_off[v];
-        if (vc == VC_BYTES) {  // BoolMapOr over bytes (mac, mpls label, octetArray, u256)
+        if (sp.val_vc[v] == VC_BYTES) {  // BoolMapOr over bytes (mac, mpls label, octetArray, u256)
             bool nul = false;
             for (uint32_t j = 0; j < (w + 3) / 4; ++j) {
                 const uint32_t x = load_word(c + row * w, w, j, false, nul);
-                if (x) atomicOr((unsigned int *)dst + j, x);
+                or32(dst + 4 * j, x);
             }
             continue;
         }
-        uint64_t x = load_value(c + row * w, w, vc);
-        switch (P.val_op[v]) {
-        case NGZ_AGG_ADD: atomicAdd((unsigned long long *)dst, (unsigned long long)x); break;
-        case NGZ_AGG_MIN:
-            if (vc == VC_SINT) x ^= 1ull << 63;
-            atomicMin((unsigned long long *)dst, (unsigned long long)x);
-            break;
-        case NGZ_AGG_MAX:
-            if (vc == VC_SINT) x ^= 1ull << 63;
-            atomicMax((unsigned long long *)dst, (unsigned long long)x);
-            break;
-        default:
-            if (x) atomicOr((unsigned long long *)dst, (unsigned long long)x);
-            break;
-        }
+        apply_value(dst, P.val_op[v], value_operand(sp, P, v, row));
     }
-    if (vp) atomicOr((unsigned int *)(R + 12), vp);
+    or32(R + 12, vp);
 }
 
 __global__ __launch_bounds__(256) void k_agg_verify(const ngz_dgram_hdr *__restrict__ hdr,
                                                     const ngz_set_info *__restrict__ sets,
                                                     const uint32_t *__restrict__ rstart,
                                                     const uint32_t *__restrict__ setidx, uint64_t n_rec,
+                                                    uint32_t n_dgrams, uint32_t n_slots,
                                                     const uint8_t *__restrict__ dginfo,
                                                     const AggSlotPlan *__restrict__ plans, const AggParams P,
                                                     const unsigned long long *__restrict__ tags,
@@ -291,6 +432,7 @@ __global__ __launch_bounds__(256) void k_agg_verify(const ngz_dgram_hdr *__restr
     if (t >= n_rec) return;
     const uint32_t s = setidx[t];
     const ngz_set_info si = sets[s];
+    if (si.dgram >= n_dgrams || si.slot >= n_slots) return;
     if (!(dginfo[si.dgram] & 1)) return;
     const AggSlotPlan &sp = plans[si.slot];
     if (!sp.usable) return;
@@ -385,6 +527,8 @@ struct ngz_agg {
     // scratch, grown on demand
     void *scratch = nullptr;
     size_t scratch_cap = 0;
+    uint32_t *setidx = nullptr;
+    uint64_t setidx_cap = 0;
 };
 
 namespace {
@@ -566,6 +710,7 @@ void ngz_agg_destroy(ngz_agg *a) {
     hipFree(a->cursor);
     hipFree(a->plans);
     hipFree(a->scratch);
+    hipFree(a->setidx);
     if (a->ev0) hipEventDestroy(a->ev0);
     if (a->ev1) hipEventDestroy(a->ev1);
     if (a->stream) hipStreamDestroy(a->stream);
@@ -674,17 +819,15 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, uint16_t pe
     }
     const uint32_t D = out->n_dgrams, NS = out->n_sets;
     if (!D || !NS) return NGZ_OK;
-    // scratch: has_rec[D], ts[D], pmax[D], dginfo[D], rstart[NS+1], setidx[R], cub temp
-    uint64_t n_rec = 0;
-    for (uint32_t s = 0; s < S; ++s) n_rec += out->slots[s].n_records;
+    // scratch: has_rec[D], ts[D], pm[D], dginfo[D], cnt/rstart[NS+1], cub temp; then setidx[R]
     size_t cub_max = 0, cub_sum = 0;
     hipcub::DeviceScan::InclusiveScan(nullptr, cub_max, (uint32_t *)nullptr, (uint32_t *)nullptr, hipcub::Max(), D,
                                       a->stream);
     hipcub::DeviceScan::ExclusiveSum(nullptr, cub_sum, (uint32_t *)nullptr, (uint32_t *)nullptr, NS + 1, a->stream);
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t o_has = 0, o_ts = o_has + al(4ull * D), o_pm = o_ts + al(4ull * D), o_dg = o_pm + al(4ull * D),
-                 o_cnt = o_dg + al(D), o_rs = o_cnt + al(4ull * (NS + 1)), o_si = o_rs + al(4ull * (NS + 1)),
-                 o_cub = o_si + al(4ull * std::max<uint64_t>(n_rec, 1)), need = o_cub + al(std::max(cub_max, cub_sum));
+                 o_cnt = o_dg + al(D), o_rs = o_cnt + al(4ull * (NS + 1)), o_cub = o_rs + al(4ull * (NS + 1)),
+                 need = o_cub + al(std::max(cub_max, cub_sum));
     if (need > a->scratch_cap) {
         hipFree(a->scratch);
         a->scratch = nullptr;
@@ -694,7 +837,7 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, uint16_t pe
     uint8_t *sc = (uint8_t *)a->scratch;
     uint32_t *has_rec = (uint32_t *)(sc + o_has), *ts = (uint32_t *)(sc + o_ts), *pm = (uint32_t *)(sc + o_pm);
     uint8_t *dginfo = sc + o_dg;
-    uint32_t *cnt = (uint32_t *)(sc + o_cnt), *rstart = (uint32_t *)(sc + o_rs), *setidx = (uint32_t *)(sc + o_si);
+    uint32_t *cnt = (uint32_t *)(sc + o_cnt), *rstart = (uint32_t *)(sc + o_rs);
     void *cub_tmp = sc + o_cub;
     if (S > a->plans_cap) {
         hipFree(a->plans);
@@ -714,7 +857,7 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, uint16_t pe
     AGG_HIP(a, hipMemsetAsync(a->err, 0, 4, st));
     const ngz_dgram_hdr *hdr = out->dgrams;
     const ngz_set_info *sets = out->sets;
-    hipLaunchKernelGGL(k_agg_dgram, dim3(grid_for(NS)), dim3(256), 0, st, hdr, sets, NS, has_rec);
+    hipLaunchKernelGGL(k_agg_dgram, dim3(grid_for(NS)), dim3(256), 0, st, hdr, sets, NS, D, has_rec);
     hipLaunchKernelGGL(k_agg_ts, dim3(grid_for(D)), dim3(256), 0, st, hdr, has_rec, D, ts);
     size_t tmp = cub_max;
     AGG_HIP(a, hipcub::DeviceScan::InclusiveScan(cub_tmp, tmp, ts, pm, hipcub::Max(), D, st));
@@ -726,14 +869,26 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, uint16_t pe
                                 hipMemcpyDeviceToDevice, st));
     tmp = cub_sum;
     AGG_HIP(a, hipcub::DeviceScan::ExclusiveSum(cub_tmp, tmp, cnt, rstart, NS + 1, st));
+    // records of the set table (synchronises once: the grid of the record kernels depends on it)
+    uint32_t n_rec = 0;
+    AGG_HIP(a, hipMemcpyAsync(&n_rec, rstart + NS, 4, hipMemcpyDeviceToHost, st));
+    AGG_HIP(a, hipStreamSynchronize(st));
+    if ((uint64_t)n_rec * 4 > a->setidx_cap) {
+        hipFree(a->setidx);
+        a->setidx = nullptr;
+        a->setidx_cap = 0;
+        if (hipMalloc(&a->setidx, std::max<uint64_t>(n_rec, 1) * 4) != hipSuccess) return fail(a, NGZ_E_NOMEM, "setidx");
+        a->setidx_cap = std::max<uint64_t>(n_rec, 1) * 4;
+    }
+    uint32_t *setidx = a->setidx;
     hipLaunchKernelGGL(k_agg_setidx, dim3(grid_for(64ull * NS, 256, 4096)), dim3(256), 0, st, sets, rstart, NS, setidx);
     AGG_HIP(a, hipGetLastError());
     const uint32_t blocks = (uint32_t)((n_rec + 255) / 256);
     if (n_rec) {
-        hipLaunchKernelGGL(k_agg_insert, dim3(blocks), dim3(256), 0, st, hdr, sets, rstart, setidx, n_rec, dginfo,
-                           a->plans, P, a->tags, a->rows, a->late, a->err);
-        hipLaunchKernelGGL(k_agg_verify, dim3(blocks), dim3(256), 0, st, hdr, sets, rstart, setidx, n_rec, dginfo,
-                           a->plans, P, a->tags, a->rows, a->err);
+        hipLaunchKernelGGL(k_agg_insert, dim3(blocks), dim3(256), 0, st, hdr, sets, rstart, setidx, (uint64_t)n_rec,
+                           D, S, dginfo, a->plans, P, a->tags, a->rows, a->late, a->err);
+        hipLaunchKernelGGL(k_agg_verify, dim3(blocks), dim3(256), 0, st, hdr, sets, rstart, setidx, (uint64_t)n_rec,
+                           D, S, dginfo, a->plans, P, a->tags, a->rows, a->err);
     }
     AGG_HIP(a, hipGetLastError());
     AGG_HIP(a, hipEventRecord(a->ev1, st));
@@ -749,6 +904,7 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, uint16_t pe
     if (errv & 1) return fail(a, NGZ_AGG_E_OVERFLOW, "more than 128 observation domains");
     if (errv & 6) return fail(a, NGZ_AGG_E_OVERFLOW, "group table full");
     if (errv & 8) return fail(a, NGZ_AGG_E_COLLISION, "64-bit key hash collision");
+    if (errv & 16) return fail(a, NGZ_E_INVALID, "set table entry out of range");
     return NGZ_OK;
 }
 

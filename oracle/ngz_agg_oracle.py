@@ -32,6 +32,8 @@ RUST_WIDTH = {"unsigned8": 1, "unsigned16": 2, "unsigned32": 4, "unsigned64": 8,
 def canon(field):
     """Field value -> canonical value (see module doc)."""
     v = field.value
+    if field.ie.kind == "iana" and field.ie.id == 6:  # tcpControlBits -> TCPHeaderFlags::from(u16) keeps the
+        return v & 0xFF                                # low 8 bits (iana/src/tcp.rs:165-168)
     if isinstance(v, tuple) and v and v[0] in ("v4", "v6"):
         return v[1] if v[0] == "v4" else v[1].to_bytes(16, "big")
     if isinstance(v, bool):

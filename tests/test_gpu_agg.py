@@ -212,3 +212,30 @@ def test_reference_captures(dev, name):
         except AggError as e:
             # selected fields that are variable-length in some template are not on the device yet
             assert "variable-length" in str(e), e
+
+
+def test_wave_preaggregation_bytes_and_presence(dev):
+    """Low-cardinality keys (wave pre-aggregation path) with a byte-wise OR (mac), a
+    signed min and fields present in only one of two templates."""
+    import random
+    rnd = random.Random(7)
+    t1 = [(8, 4), (56, 6), (1, 8), (434, 4)]
+    t2 = [(8, 4), (2, 8)]
+    r1 = [struct.pack(">I6sQi", rnd.choice([1, 2]), bytes(rnd.getrandbits(8) for _ in range(6)),
+                      rnd.getrandbits(64), rnd.randint(-2**31, 2**31 - 1)) for _ in range(700)]
+    r2 = [struct.pack(">IQ", rnd.choice([1, 2, 3]), rnd.getrandbits(64)) for _ in range(500)]
+    d = [ipfix_msg([tset(600, t1), tset(601, t2)], 1_700_000_000)]
+    for i in range(0, 700, 100):
+        d.append(ipfix_msg([dset(600, r1[i:i + 100]), dset(601, r2[i:i + 100] if i < 500 else [])]
+                           if i < 500 else [dset(600, r1[i:i + 100])], 1_700_000_000 + i // 100))
+    fields = [(0, 8, 0, OK), (0, 56, 0, OR), (0, 1, 0, ADD), (0, 2, 0, MX), (0, 434, 0, MN)]
+    from netgauze_amd.aggregate import FlowAggregator
+    from netgauze_amd.flow import FlowInfoCodec
+    codec = FlowInfoCodec()
+    agg = FlowAggregator(fields, kinds={**KINDS, (0, 434): "sint"})
+    agg.push(codec.decode_datagrams(d))
+    got = norm(agg.flush())
+    ref = norm(A.aggregate_datagrams(fields, d, collection_ms=0).flush())
+    assert set(got) == set(ref) and len(got) == 3
+    for k in ref:
+        assert got[k] == ref[k], (k, got[k], ref[k])
