@@ -61,6 +61,7 @@ struct AggParams {
     uint32_t push_id;
     uint32_t port_bit;
     uint64_t coll_flip;         // collection time ms, sign bit flipped (unsigned order == signed order)
+    uint32_t lds_ok;            // 1: no byte-wise OR values (wave results may be combined in LDS)
 };
 
 // dginfo: bit 0 usable (OK + has records + not late), bits 1..7 domain bit
@@ -285,7 +286,11 @@ __device__ __forceinline__ void apply_push_constants(uint8_t *R, const AggParams
 // One lane per record.  Lanes of a wave that share a group (same key hash) are first
 // reduced across the wave and applied by one lane (wave pre-aggregation: low-cardinality
 // keys would otherwise serialise on a few hot rows); once the largest remaining group of
-// the wave has fewer than 4 records, every remaining lane applies its own record.
+// the wave has fewer than 4 records, every remaining lane applies its own record.  Wave
+// results are combined further in a per-workgroup LDS table (CN entries) across all the
+// tiles the workgroup walks, and applied to HBM once per workgroup: hot rows then see one
+// set of atomics per workgroup instead of one per wave.
+constexpr int CN = 64;
 __global__ __launch_bounds__(256) void k_agg_insert(const ngz_dgram_hdr *__restrict__ hdr,
                                                     const ngz_set_info *__restrict__ sets,
                                                     const uint32_t *__restrict__ rstart,
@@ -296,8 +301,19 @@ __global__ __launch_bounds__(256) void k_agg_insert(const ngz_dgram_hdr *__restr
                                                     unsigned long long *__restrict__ tags, uint8_t *__restrict__ rows,
                                                     unsigned long long *__restrict__ late_count,
                                                     unsigned int *__restrict__ err) {
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    __shared__ unsigned long long c_tag[CN], c_cnt[CN], c_tpl[CN], c_d0[CN], c_d1[CN];
+    __shared__ unsigned long long c_val[CN][NGZ_AGG_MAX_VALUES];
+    __shared__ uint32_t c_slot[CN], c_row[CN], c_win[CN], c_kp[CN], c_tmin[CN], c_tmax[CN], c_smax[CN], c_vp[CN];
+    for (int e = threadIdx.x; e < CN; e += blockDim.x) {
+        c_tag[e] = c_cnt[e] = c_tpl[e] = c_d0[e] = c_d1[e] = 0;
+        c_tmin[e] = 0xFFFFFFFFu;
+        c_tmax[e] = c_smax[e] = c_vp[e] = 0;
+        for (uint32_t v = 0; v < P.n_vals; ++v) c_val[e][v] = P.val_op[v] == NGZ_AGG_MIN ? ~0ull : 0ull;
+    }
+    __syncthreads();
     const int lane = threadIdx.x & 63;
+    for (uint64_t tile = blockIdx.x; tile * blockDim.x < n_rec; tile += gridDim.x) {
+    const uint64_t t = tile * blockDim.x + threadIdx.x;
     bool valid = false, late = false;
     ngz_set_info si{};
     uint8_t info = 0;
@@ -328,6 +344,17 @@ __global__ __launch_bounds__(256) void k_agg_insert(const ngz_dgram_hdr *__restr
         (db < 64 ? dom0 : dom1) = 1ull << (db & 63);
     }
     uint64_t todo = __ballot(valid);
+    // records of one datagram share export time, sys-up time, template and domain: when the
+    // whole wave does, the wave reductions of those are skipped
+    bool hdr_uniform = false;
+    if (todo) {
+        const int l0 = __ffsll((unsigned long long)todo) - 1;
+        const uint64_t u0 = readlane64(((uint64_t)ts << 32) | sysup, l0), u1 = readlane64(tpl, l0),
+                       u2 = readlane64(dom0 | (dom1 ? (1ull << 63) | dom1 : 0ull), l0);
+        const bool same = !valid || ((((uint64_t)ts << 32) | sysup) == u0 && tpl == u1 &&
+                                     (dom0 | (dom1 ? (1ull << 63) | dom1 : 0ull)) == u2);
+        hdr_uniform = __ballot(!same) == 0;
+    }
     while (todo) {
         const int leader = __ffsll((unsigned long long)todo) - 1;
         const uint64_t lh = readlane64(h, leader);
@@ -336,13 +363,45 @@ __global__ __launch_bounds__(256) void k_agg_insert(const ngz_dgram_hdr *__restr
         if (__popcll(match) < 4) break;
         todo &= ~match;
         const uint64_t cnt = __popcll(match);
-        const uint64_t tmin = wave_reduce<R_MIN>(mine ? ts : 0xFFFFFFFFull);
-        const uint64_t tmax = wave_reduce<R_MAX>(mine ? ts : 0ull);
-        const uint64_t smax = wave_reduce<R_MAX>(mine ? sysup : 0ull);
-        const uint64_t tpls = wave_reduce<R_OR>(mine ? tpl : 0ull);
-        const uint64_t d0 = wave_reduce<R_OR>(mine ? dom0 : 0ull), d1 = wave_reduce<R_OR>(mine ? dom1 : 0ull);
+        uint64_t tmin = ts, tmax = ts, smax = sysup, tpls = tpl, d0 = dom0, d1 = dom1;  // (leader's own)
+        if (!hdr_uniform) {
+            tmin = wave_reduce<R_MIN>(mine ? ts : 0xFFFFFFFFull);
+            tmax = wave_reduce<R_MAX>(mine ? ts : 0ull);
+            smax = wave_reduce<R_MAX>(mine ? sysup : 0ull);
+            tpls = wave_reduce<R_OR>(mine ? tpl : 0ull);
+            d0 = wave_reduce<R_OR>(mine ? dom0 : 0ull);
+            d1 = wave_reduce<R_OR>(mine ? dom1 : 0ull);
+        }
         uint8_t *R = nullptr;
-        if (lane == leader) {
+        int e = -1;
+        if (lane == leader && P.lds_ok) {  // workgroup combine table (linear probing, CAS on the tag)
+            int i = (int)(h & (CN - 1));
+            for (int probes = 0; probes < CN; ++probes, i = (i + 1) & (CN - 1)) {
+                unsigned long long cur = c_tag[i];
+                if (cur == 0) {
+                    cur = atomicCAS(&c_tag[i], 0ull, (unsigned long long)h);
+                    if (cur == 0) {
+                        c_slot[i] = si.slot;
+                        c_row[i] = (uint32_t)row;
+                        c_win[i] = win;
+                        c_kp[i] = kp;
+                        e = i;
+                        break;
+                    }
+                }
+                if (cur == h) { e = i; break; }
+            }
+            if (e >= 0) {
+                atomicAdd(&c_cnt[e], (unsigned long long)cnt);
+                atomicMin(&c_tmin[e], (uint32_t)tmin);
+                atomicMax(&c_tmax[e], (uint32_t)tmax);
+                atomicMax(&c_smax[e], (uint32_t)smax);
+                atomicOr(&c_tpl[e], (unsigned long long)tpls);
+                atomicOr(&c_d0[e], (unsigned long long)d0);
+                atomicOr(&c_d1[e], (unsigned long long)d1);
+            }
+        }
+        if (lane == leader && e < 0) {
             R = group_row(sp, P, row, win, kp, h, tags, rows, err);
             if (R) {
                 atomicAdd((unsigned long long *)(R + 16), (unsigned long long)cnt);
@@ -373,7 +432,19 @@ __global__ __launch_bounds__(256) void k_agg_insert(const ngz_dgram_hdr *__restr
             default: r = wave_reduce<R_OR>(x); break;
             }
             const bool any_num = __ballot(has && !bytes) != 0;  // (ballot outside lane-divergent code)
-            if (lane == leader && R && any_num) apply_value_hot(R + P.val_off[v], op, r);
+            if (lane == leader && any_num) {
+                if (e >= 0) {
+                    unsigned long long *c = &c_val[e][v];
+                    switch (op) {
+                    case NGZ_AGG_ADD: atomicAdd(c, (unsigned long long)r); break;
+                    case NGZ_AGG_MIN: atomicMin(c, (unsigned long long)r); break;
+                    case NGZ_AGG_MAX: atomicMax(c, (unsigned long long)r); break;
+                    default: atomicOr(c, (unsigned long long)r); break;
+                    }
+                } else if (R) {
+                    apply_value_hot(R + P.val_off[v], op, r);
+                }
+            }
             if (__ballot(bytes)) {  // byte ORs: each matching lane ORs its words into the leader's row
                 const uint64_t Rl = readlane64((uint64_t)R, leader);
                 if (bytes && Rl) {
@@ -386,12 +457,13 @@ __global__ __launch_bounds__(256) void k_agg_insert(const ngz_dgram_hdr *__restr
                 }
             }
         }
+        if (lane == leader && e >= 0 && vp) atomicOr(&c_vp[e], vp);
         if (lane == leader && R && vp) atomicOr((unsigned int *)(R + 12), vp);
     }
-    if (!(valid && ((todo >> lane) & 1))) return;
+    if (!(valid && ((todo >> lane) & 1))) continue;
     // per-record path
     uint8_t *R = group_row(sp, P, row, win, kp, h, tags, rows, err);
-    if (!R) return;
+    if (!R) continue;
     atomicAdd((unsigned long long *)(R + 16), 1ull);
     min32(R + 24, ts);
     max32(R + 28, ts);
@@ -417,6 +489,26 @@ __global__ __launch_bounds__(256) void k_agg_insert(const ngz_dgram_hdr *__restr
         apply_value(dst, P.val_op[v], value_operand(sp, P, v, row));
     }
     or32(R + 12, vp);
+    }  // tiles
+    __syncthreads();
+    for (int e = threadIdx.x; e < CN; e += blockDim.x) {  // the workgroup's combined groups -> HBM
+        const unsigned long long h = c_tag[e];
+        if (!h) continue;
+        uint8_t *R = group_row(plans[c_slot[e]], P, c_row[e], c_win[e], c_kp[e], h, tags, rows, err);
+        if (!R) continue;
+        atomicAdd((unsigned long long *)(R + 16), c_cnt[e]);
+        min32(R + 24, c_tmin[e]);
+        max32(R + 28, c_tmax[e]);
+        max32(R + 32, c_smax[e]);
+        or64(R + 56, c_tpl[e]);
+        or64(R + 72, c_d0[e]);
+        or64(R + 80, c_d1[e]);
+        apply_push_constants(R, P);
+        const uint32_t vp = c_vp[e];
+        for (uint32_t v = 0; v < P.n_vals; ++v)
+            if ((vp >> v) & 1) apply_value(R + P.val_off[v], P.val_op[v], c_val[e][v]);
+        or32(R + 12, vp);
+    }
 }
 
 __global__ __launch_bounds__(256) void k_agg_verify(const ngz_dgram_hdr *__restrict__ hdr,
@@ -663,6 +755,11 @@ int ngz_agg_create(int device, const ngz_agg_field *fields, uint32_t n_fields, u
         off += vc == VC_BYTES ? 32 : 8;
     }
     P.row_bytes = (off + 7) & ~7u;
+    P.lds_ok = 1;
+    for (uint32_t v = 0; v < P.n_vals; ++v) {
+        std::string why;
+        if (value_class(ngzh::ie_find(a->vals[v].pen, a->vals[v].ie_id), a->vals[v].op, why) == VC_BYTES) P.lds_ok = 0;
+    }
     uint64_t cap = 1024;
     while (cap < 2 * std::max<uint64_t>(capacity, 1)) cap <<= 1;
     a->cap = cap;
@@ -885,7 +982,7 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, uint16_t pe
     AGG_HIP(a, hipGetLastError());
     const uint32_t blocks = (uint32_t)((n_rec + 255) / 256);
     if (n_rec) {
-        hipLaunchKernelGGL(k_agg_insert, dim3(blocks), dim3(256), 0, st, hdr, sets, rstart, setidx, (uint64_t)n_rec,
+        hipLaunchKernelGGL(k_agg_insert, dim3(std::min<uint32_t>(blocks, 4096)), dim3(256), 0, st, hdr, sets, rstart, setidx, (uint64_t)n_rec,
                            D, S, dginfo, a->plans, P, a->tags, a->rows, a->late, a->err);
         hipLaunchKernelGGL(k_agg_verify, dim3(blocks), dim3(256), 0, st, hdr, sets, rstart, setidx, (uint64_t)n_rec,
                            D, S, dginfo, a->plans, P, a->tags, a->rows, a->err);
