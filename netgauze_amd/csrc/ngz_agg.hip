@@ -22,6 +22,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -54,6 +55,7 @@ struct AggSlotPlan {            // per batch slot, built on the host every push
 struct AggParams {
     uint32_t n_keys, n_vals;
     uint32_t key_off[NGZ_AGG_MAX_KEYS];
+    uint32_t key_w[NGZ_AGG_MAX_KEYS];   // packed mode: the IE's fixed column width
     uint32_t val_off[NGZ_AGG_MAX_VALUES];
     uint8_t val_op[NGZ_AGG_MAX_VALUES];
     uint32_t row_bytes;
@@ -62,6 +64,7 @@ struct AggParams {
     uint32_t port_bit;
     uint64_t coll_flip;         // collection time ms, sign bit flipped (unsigned order == signed order)
     uint32_t lds_ok;            // 1: no byte-wise OR values (wave results may be combined in LDS)
+    uint32_t packed;            // 1: the whole group key packs into 63 bits (exact tag, no verify pass)
 };
 
 // dginfo: bit 0 usable (OK + has records + not late), bits 1..7 domain bit
@@ -69,6 +72,12 @@ __device__ __forceinline__ uint64_t mix64(uint64_t h, uint64_t v) {
     h ^= v + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
     h *= 0xBF58476D1CE4E5B9ull;
     return h ^ (h >> 31);
+}
+
+__device__ __forceinline__ uint64_t slot_of(uint64_t h) {  // table position of a tag (tags may be packed keys)
+    h ^= h >> 33;
+    h *= 0xFF51AFD7ED558CCDull;
+    return h ^ (h >> 33);
 }
 
 __device__ __forceinline__ uint32_t load_word(const uint8_t *p, uint32_t w, uint32_t j, bool str, bool &nul) {
@@ -90,6 +99,22 @@ __device__ __forceinline__ uint32_t load_word(const uint8_t *p, uint32_t w, uint
 
 __device__ __forceinline__ uint64_t key_hash(const AggSlotPlan &sp, const AggParams &P, uint64_t row, uint32_t win,
                                              uint32_t &present) {
+    if (P.packed) {  // exact tag: bit 63 | window/60 (27 bits) | flow type | presence bits | key bits
+        uint64_t x = ((uint64_t)(win / 60) << 1) | (sp.proto == 9);
+        present = 0;
+        for (uint32_t k = 0; k < P.n_keys; ++k) {
+            const uint8_t *c = sp.key_col[k];
+            const uint32_t w = sp.key_w[k];
+            uint64_t v = 0;
+            if (c) {
+                present |= 1u << k;
+                const uint8_t *q = c + row * w;
+                v = w == 4 ? *(const uint32_t *)q : w == 2 ? *(const uint16_t *)q : w == 8 ? *(const uint64_t *)q : *q;
+            }
+            x = (((x << 1) | (c != nullptr)) << (8 * P.key_w[k])) | v;
+        }
+        return x | (1ull << 63);
+    }
     uint64_t h = mix64(0x4E475A41474731ull, ((uint64_t)win << 8) | sp.proto);
     present = 0;
     for (uint32_t k = 0; k < P.n_keys; ++k) {
@@ -204,7 +229,7 @@ __device__ __forceinline__ uint64_t wave_reduce(uint64_t v) {  // butterfly over
 __device__ __forceinline__ uint8_t *group_row(const AggSlotPlan &sp, const AggParams &P, uint64_t row, uint32_t win,
                                               uint32_t kp, uint64_t h, unsigned long long *__restrict__ tags,
                                               uint8_t *__restrict__ rows, unsigned int *__restrict__ err) {
-    uint64_t g = h & P.mask;
+    uint64_t g = slot_of(h) & P.mask;
     bool won = false;
     for (uint64_t probes = 0;; ++probes) {
         unsigned long long cur = tags[g];
@@ -291,6 +316,7 @@ __device__ __forceinline__ void apply_push_constants(uint8_t *R, const AggParams
 // tiles the workgroup walks, and applied to HBM once per workgroup: hot rows then see one
 // set of atomics per workgroup instead of one per wave.
 constexpr int CN = 64;
+template <int MAXV>  // aggregated fields held in registers (value loads issued together, before any atomic)
 __global__ __launch_bounds__(256) void k_agg_insert(const ngz_dgram_hdr *__restrict__ hdr,
                                                     const ngz_set_info *__restrict__ sets,
                                                     const uint32_t *__restrict__ rstart,
@@ -343,6 +369,16 @@ __global__ __launch_bounds__(256) void k_agg_insert(const ngz_dgram_hdr *__restr
         const uint32_t db = info >> 1;
         (db < 64 ? dom0 : dom1) = 1ull << (db & 63);
     }
+    uint64_t xv[MAXV];
+    uint32_t hv = 0, hb = 0;  // aggregated fields present: numeric (in xv) / byte-wise OR
+#pragma unroll
+    for (int v = 0; v < MAXV; ++v) {
+        xv[v] = 0;
+        if (valid && v < (int)P.n_vals && sp.val_col[v]) {
+            if (sp.val_vc[v] == VC_BYTES) hb |= 1u << v;
+            else { xv[v] = value_operand(sp, P, v, row); hv |= 1u << v; }
+        }
+    }
     uint64_t todo = __ballot(valid);
     // records of one datagram share export time, sys-up time, template and domain: when the
     // whole wave does, the wave reductions of those are skipped
@@ -375,7 +411,7 @@ __global__ __launch_bounds__(256) void k_agg_insert(const ngz_dgram_hdr *__restr
         uint8_t *R = nullptr;
         int e = -1;
         if (lane == leader && P.lds_ok) {  // workgroup combine table (linear probing, CAS on the tag)
-            int i = (int)(h & (CN - 1));
+            int i = (int)(slot_of(h) & (CN - 1));
             for (int probes = 0; probes < CN; ++probes, i = (i + 1) & (CN - 1)) {
                 unsigned long long cur = c_tag[i];
                 if (cur == 0) {
@@ -416,22 +452,22 @@ __global__ __launch_bounds__(256) void k_agg_insert(const ngz_dgram_hdr *__restr
             }
         }
         uint32_t vp = 0;
-        for (uint32_t v = 0; v < P.n_vals; ++v) {
-            const bool has = mine && sp.val_col[v] != nullptr;
-            if (!__ballot(has)) continue;
+#pragma unroll
+        for (int v = 0; v < MAXV; ++v) {
+            if (v >= (int)P.n_vals) break;
+            const bool hasn = mine && ((hv >> v) & 1), bytes = mine && ((hb >> v) & 1);
+            const bool any_num = __ballot(hasn) != 0, any_bytes = __ballot(bytes) != 0;
+            if (!any_num && !any_bytes) continue;
             vp |= 1u << v;
             const uint8_t op = P.val_op[v];
-            const bool bytes = has && sp.val_vc[v] == VC_BYTES;
-            const uint64_t x = (has && !bytes) ? value_operand(sp, P, v, row)
-                                               : (op == NGZ_AGG_MIN ? ~0ull : 0ull);
-            uint64_t r;
-            switch (op) {
+            const uint64_t x = hasn ? xv[v] : (op == NGZ_AGG_MIN ? ~0ull : 0ull);
+            uint64_t r = 0;
+            if (any_num) switch (op) {
             case NGZ_AGG_ADD: r = wave_reduce<R_ADD>(x); break;
             case NGZ_AGG_MIN: r = wave_reduce<R_MIN>(x); break;
             case NGZ_AGG_MAX: r = wave_reduce<R_MAX>(x); break;
             default: r = wave_reduce<R_OR>(x); break;
             }
-            const bool any_num = __ballot(has && !bytes) != 0;  // (ballot outside lane-divergent code)
             if (lane == leader && any_num) {
                 if (e >= 0) {
                     unsigned long long *c = &c_val[e][v];
@@ -445,7 +481,7 @@ __global__ __launch_bounds__(256) void k_agg_insert(const ngz_dgram_hdr *__restr
                     apply_value_hot(R + P.val_off[v], op, r);
                 }
             }
-            if (__ballot(bytes)) {  // byte ORs: each matching lane ORs its words into the leader's row
+            if (any_bytes) {  // byte ORs: each matching lane ORs its words into the leader's row
                 const uint64_t Rl = readlane64((uint64_t)R, leader);
                 if (bytes && Rl) {
                     const uint32_t w = sp.val_w[v];
@@ -471,24 +507,19 @@ __global__ __launch_bounds__(256) void k_agg_insert(const ngz_dgram_hdr *__restr
     or64(R + 56, tpl);
     or64(R + (dom0 ? 72 : 80), dom0 | dom1);
     apply_push_constants(R, P);
-    uint32_t vp = 0;
-    for (uint32_t v = 0; v < P.n_vals; ++v) {
-        const uint8_t *c = sp.val_col[v];
-        if (!c) continue;
-        vp |= 1u << v;
-        const uint32_t w = sp.val_w[v];
+#pragma unroll
+    for (int v = 0; v < MAXV; ++v) {
+        if (v >= (int)P.n_vals) break;
         uint8_t *dst = R + P.val_off[v];
-        if (sp.val_vc[v] == VC_BYTES) {  // BoolMapOr over bytes (mac, mpls label, octetArray, u256)
+        if ((hv >> v) & 1) {
+            apply_value(dst, P.val_op[v], xv[v]);
+        } else if ((hb >> v) & 1) {  // BoolMapOr over bytes (mac, mpls label, octetArray, u256)
+            const uint32_t w = sp.val_w[v];
             bool nul = false;
-            for (uint32_t j = 0; j < (w + 3) / 4; ++j) {
-                const uint32_t x = load_word(c + row * w, w, j, false, nul);
-                or32(dst + 4 * j, x);
-            }
-            continue;
+            for (uint32_t j = 0; j < (w + 3) / 4; ++j) or32(dst + 4 * j, load_word(sp.val_col[v] + row * w, w, j, false, nul));
         }
-        apply_value(dst, P.val_op[v], value_operand(sp, P, v, row));
     }
-    or32(R + 12, vp);
+    or32(R + 12, hv | hb);
     }  // tiles
     __syncthreads();
     for (int e = threadIdx.x; e < CN; e += blockDim.x) {  // the workgroup's combined groups -> HBM
@@ -533,7 +564,7 @@ __global__ __launch_bounds__(256) void k_agg_verify(const ngz_dgram_hdr *__restr
     const uint32_t win = ts - ts % 60;
     uint32_t kp;
     const uint64_t h = key_hash(sp, P, row, win, kp);
-    uint64_t g = h & P.mask;
+    uint64_t g = slot_of(h) & P.mask;
     for (uint64_t probes = 0; tags[g] != h; ++probes) {
         g = (g + 1) & P.mask;
         if (probes > P.mask) { atomicOr(err, 4u); return; }
@@ -744,6 +775,17 @@ int ngz_agg_create(int device, const ngz_agg_field *fields, uint32_t n_fields, u
         }
         P.key_off[k] = off;
         off += w;
+        // packed-key eligibility: IEs whose column width is fixed by the Rust type (1/2/4/8 bytes)
+        int fw = 0;
+        if (r) switch (r->dtype) {
+            case ngzh::DT_unsigned8: case ngzh::DT_signed8: case ngzh::DT_boolean: fw = 1; break;
+            case ngzh::DT_unsigned16: fw = (r->flags & 2) ? 1 : 2; break;  // tcpControlBits column is u8
+            case ngzh::DT_signed16: fw = 2; break;
+            case ngzh::DT_unsigned32: case ngzh::DT_signed32: case ngzh::DT_ipv4Address:
+            case ngzh::DT_dateTimeSeconds: case ngzh::DT_float32: fw = 4; break;
+            default: fw = 0; break;
+        }
+        P.key_w[k] = (uint32_t)fw;
     }
     if (off - ROW_HDR > NGZ_AGG_MAX_KEY_BYTES + 64) { delete a; return NGZ_E_LIMIT; }
     off = (off + 7) & ~7u;
@@ -755,6 +797,15 @@ int ngz_agg_create(int device, const ngz_agg_field *fields, uint32_t n_fields, u
         off += vc == VC_BYTES ? 32 : 8;
     }
     P.row_bytes = (off + 7) & ~7u;
+    {
+        uint32_t bits = 28;  // window/60 + flow type
+        bool ok = true;
+        for (uint32_t k = 0; k < P.n_keys; ++k) {
+            ok = ok && P.key_w[k] != 0;
+            bits += 1 + 8 * P.key_w[k];
+        }
+        P.packed = ok && bits <= 63 && getenv("NGZ_AGG_NO_PACK") == nullptr;
+    }
     P.lds_ok = 1;
     for (uint32_t v = 0; v < P.n_vals; ++v) {
         std::string why;
@@ -889,6 +940,8 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, uint16_t pe
                 return fail(a, NGZ_E_LIMIT, "variable-length key field (not on the device yet)");
             const uint32_t room = (k + 1 < a->P.n_keys ? a->P.key_off[k + 1] : ((a->P.n_vals ? a->P.val_off[0] : a->P.row_bytes))) - a->P.key_off[k];
             if (f.width > room) return fail(a, NGZ_E_LIMIT, "key field wider than its row slot");
+            if (a->P.packed && f.width != a->P.key_w[k])
+                return fail(a, NGZ_E_LIMIT, "key column width differs from the IE's width");
             sp.key_col[k] = si.columns + (uint64_t)si.capacity * f.col_off;
             sp.key_w[k] = f.width;
             sp.key_str[k] = f.kind == NGZ_K_STR;
@@ -982,9 +1035,15 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, uint16_t pe
     AGG_HIP(a, hipGetLastError());
     const uint32_t blocks = (uint32_t)((n_rec + 255) / 256);
     if (n_rec) {
-        hipLaunchKernelGGL(k_agg_insert, dim3(std::min<uint32_t>(blocks, 4096)), dim3(256), 0, st, hdr, sets, rstart, setidx, (uint64_t)n_rec,
-                           D, S, dginfo, a->plans, P, a->tags, a->rows, a->late, a->err);
-        hipLaunchKernelGGL(k_agg_verify, dim3(blocks), dim3(256), 0, st, hdr, sets, rstart, setidx, (uint64_t)n_rec,
+        if (P.n_vals <= 8)
+            hipLaunchKernelGGL(k_agg_insert<8>, dim3(std::min<uint32_t>(blocks, 4096)), dim3(256), 0, st, hdr, sets,
+                               rstart, setidx, (uint64_t)n_rec, D, S, dginfo, a->plans, P, a->tags, a->rows, a->late,
+                               a->err);
+        else
+            hipLaunchKernelGGL(k_agg_insert<NGZ_AGG_MAX_VALUES>, dim3(std::min<uint32_t>(blocks, 4096)), dim3(256), 0,
+                               st, hdr, sets, rstart, setidx, (uint64_t)n_rec, D, S, dginfo, a->plans, P, a->tags,
+                               a->rows, a->late, a->err);
+        if (!P.packed) hipLaunchKernelGGL(k_agg_verify, dim3(blocks), dim3(256), 0, st, hdr, sets, rstart, setidx, (uint64_t)n_rec,
                            D, S, dginfo, a->plans, P, a->tags, a->rows, a->err);
     }
     AGG_HIP(a, hipGetLastError());
