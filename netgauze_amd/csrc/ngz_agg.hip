@@ -399,6 +399,59 @@ __global__ __launch_bounds__(256) void k_agg_insert(const ngz_dgram_hdr *__restr
         if (__popcll(match) < 4) break;
         todo &= ~match;
         const uint64_t cnt = __popcll(match);
+        if (P.lds_ok) {
+            // combine-table path: the leader claims the group's LDS entry and every matching
+            // lane applies its own record with LDS atomics (no cross-lane reductions)
+            int e0 = -1;
+            if (lane == leader) {
+                int i = (int)(slot_of(h) & (CN - 1));
+                for (int probes = 0; probes < CN; ++probes, i = (i + 1) & (CN - 1)) {
+                    unsigned long long cur = c_tag[i];
+                    if (cur == 0) {
+                        cur = atomicCAS(&c_tag[i], 0ull, (unsigned long long)h);
+                        if (cur == 0) {
+                            c_slot[i] = si.slot;
+                            c_row[i] = (uint32_t)row;
+                            c_win[i] = win;
+                            c_kp[i] = kp;
+                            e0 = i;
+                            break;
+                        }
+                    }
+                    if (cur == h) { e0 = i; break; }
+                }
+            }
+            const int e = __shfl(e0, leader);
+            if (e >= 0) {
+                if (lane == leader) atomicAdd(&c_cnt[e], (unsigned long long)cnt);
+                if (hdr_uniform ? lane == leader : mine) {
+                    atomicMin(&c_tmin[e], ts);
+                    atomicMax(&c_tmax[e], ts);
+                    if (sysup) atomicMax(&c_smax[e], sysup);
+                    atomicOr(&c_tpl[e], (unsigned long long)tpl);
+                    if (dom0) atomicOr(&c_d0[e], (unsigned long long)dom0);
+                    if (dom1) atomicOr(&c_d1[e], (unsigned long long)dom1);
+                }
+                uint32_t vp = 0;
+#pragma unroll
+                for (int v = 0; v < MAXV; ++v) {
+                    if (v >= (int)P.n_vals) break;
+                    const bool hasn = mine && ((hv >> v) & 1);
+                    if (__ballot(hasn)) vp |= 1u << v;
+                    if (hasn) {
+                        unsigned long long *c = &c_val[e][v];
+                        switch (P.val_op[v]) {
+                        case NGZ_AGG_ADD: atomicAdd(c, (unsigned long long)xv[v]); break;
+                        case NGZ_AGG_MIN: atomicMin(c, (unsigned long long)xv[v]); break;
+                        case NGZ_AGG_MAX: atomicMax(c, (unsigned long long)xv[v]); break;
+                        default: atomicOr(c, (unsigned long long)xv[v]); break;
+                        }
+                    }
+                }
+                if (lane == leader && vp) atomicOr(&c_vp[e], vp);
+                continue;  // the wave's next group
+            }
+        }
         uint64_t tmin = ts, tmax = ts, smax = sysup, tpls = tpl, d0 = dom0, d1 = dom1;  // (leader's own)
         if (!hdr_uniform) {
             tmin = wave_reduce<R_MIN>(mine ? ts : 0xFFFFFFFFull);
