@@ -316,8 +316,9 @@ __device__ __forceinline__ void apply_push_constants(uint8_t *R, const AggParams
 // tiles the workgroup walks, and applied to HBM once per workgroup: hot rows then see one
 // set of atomics per workgroup instead of one per wave.
 constexpr int CN = 64;
+// (256, 4): 4 waves per SIMD (<= 128 VGPRs, no spills); the kernel is latency-bound
 template <int MAXV>  // aggregated fields held in registers (value loads issued together, before any atomic)
-__global__ __launch_bounds__(256) void k_agg_insert(const ngz_dgram_hdr *__restrict__ hdr,
+__global__ __launch_bounds__(256, 4) void k_agg_insert(const ngz_dgram_hdr *__restrict__ hdr,
                                                     const ngz_set_info *__restrict__ sets,
                                                     const uint32_t *__restrict__ rstart,
                                                     const uint32_t *__restrict__ setidx, uint64_t n_rec,
