@@ -1088,13 +1088,16 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, uint16_t pe
     hipLaunchKernelGGL(k_agg_setidx, dim3(grid_for(64ull * NS, 256, 4096)), dim3(256), 0, st, sets, rstart, NS, setidx);
     AGG_HIP(a, hipGetLastError());
     const uint32_t blocks = (uint32_t)((n_rec + 255) / 256);
+    // insert grid: workgroups walk tiles of 256 records (NGZ_AGG_GRID overrides the default 4096)
+    static const uint32_t grid_cap = getenv("NGZ_AGG_GRID") ? (uint32_t)std::max(1, atoi(getenv("NGZ_AGG_GRID"))) : 4096u;
+    const uint32_t ig = std::min<uint32_t>(blocks, grid_cap);
     if (n_rec) {
         if (P.n_vals <= 8)
-            hipLaunchKernelGGL(k_agg_insert<8>, dim3(std::min<uint32_t>(blocks, 4096)), dim3(256), 0, st, hdr, sets,
+            hipLaunchKernelGGL(k_agg_insert<8>, dim3(ig), dim3(256), 0, st, hdr, sets,
                                rstart, setidx, (uint64_t)n_rec, D, S, dginfo, a->plans, P, a->tags, a->rows, a->late,
                                a->err);
         else
-            hipLaunchKernelGGL(k_agg_insert<NGZ_AGG_MAX_VALUES>, dim3(std::min<uint32_t>(blocks, 4096)), dim3(256), 0,
+            hipLaunchKernelGGL(k_agg_insert<NGZ_AGG_MAX_VALUES>, dim3(ig), dim3(256), 0,
                                st, hdr, sets, rstart, setidx, (uint64_t)n_rec, D, S, dginfo, a->plans, P, a->tags,
                                a->rows, a->late, a->err);
         if (!P.packed) hipLaunchKernelGGL(k_agg_verify, dim3(blocks), dim3(256), 0, st, hdr, sets, rstart, setidx, (uint64_t)n_rec,
