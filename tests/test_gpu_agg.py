@@ -246,3 +246,26 @@ def test_wave_preaggregation_bytes_and_presence(dev):
     assert set(got) == set(ref) and len(got) == 3
     for k in ref:
         assert got[k] == ref[k], (k, got[k], ref[k])
+
+
+def test_table_full_and_flush_buffer_errors(dev):
+    """A group table that fills up reports NGZ_AGG_E_OVERFLOW (no hang); a flush buffer that is
+    too small is refused without emptying the table."""
+    import numpy as np
+    from netgauze_amd import _lib
+    from netgauze_amd.aggregate import AggError, FlowAggregator, lib
+    from netgauze_amd.flow import FlowInfoCodec
+    d = t20_datagrams(5000, 500, [1_700_000_000])
+    codec = FlowInfoCodec()
+    agg = FlowAggregator([(0, 8, 0, OK), (0, 12, 0, OK)] + T20_AGG, capacity=16)  # 2048 slots
+    with pytest.raises(AggError, match="group table full"):
+        agg.push(codec.decode_datagrams(d))
+    agg2 = FlowAggregator([(0, 4, 0, OK)] + T20_AGG)
+    agg2.push(codec.decode_datagrams(d[:3]))
+    n = agg2.n_groups()
+    assert n == 6  # 3 protocols x 2 minute windows (the two data messages are 60 s apart)
+    rb = agg2.layout()[0]
+    buf = np.zeros(rb * n - 1, dtype=np.uint8)
+    assert lib().ngz_agg_flush(agg2._h, buf.ctypes.data, buf.nbytes) == -1  # NGZ_E_INVALID
+    assert agg2.n_groups() == n
+    assert len(agg2.flush()) == n and agg2.n_groups() == 0
