@@ -228,9 +228,11 @@ __device__ __forceinline__ uint64_t wave_reduce(uint64_t v) {  // butterfly over
 // record that claimed the slot (64-bit CAS on the tag).
 __device__ __forceinline__ uint8_t *group_row(const AggSlotPlan &sp, const AggParams &P, uint64_t row, uint32_t win,
                                               uint32_t kp, uint64_t h, unsigned long long *__restrict__ tags,
-                                              uint8_t *__restrict__ rows, unsigned int *__restrict__ err) {
+                                              uint8_t *__restrict__ rows, unsigned int *__restrict__ err,
+                                              bool *claimed = nullptr) {
     uint64_t g = slot_of(h) & P.mask;
     bool won = false;
+    if (claimed) *claimed = false;
     for (uint64_t probes = 0;; ++probes) {
         unsigned long long cur = tags[g];
         if (cur == 0) {
@@ -242,6 +244,7 @@ __device__ __forceinline__ uint8_t *group_row(const AggSlotPlan &sp, const AggPa
         if (probes > P.mask) { atomicOr(err, 2u); return nullptr; }
     }
     uint8_t *R = rows + g * P.row_bytes;
+    if (claimed) *claimed = won;
     if (won) {  // plain stores; read by later kernels only (flush, verify)
         *(uint32_t *)(R + 0) = win;
         *(uint32_t *)(R + 4) = sp.proto;
@@ -552,28 +555,40 @@ __global__ __launch_bounds__(256, 4) void k_agg_insert(const ngz_dgram_hdr *__re
     }
     if (!(valid && ((todo >> lane) & 1))) continue;
     // per-record path
-    uint8_t *R = group_row(sp, P, row, win, kp, h, tags, rows, err);
+    bool claimed;
+    uint8_t *R = group_row(sp, P, row, win, kp, h, tags, rows, err, &claimed);
     if (!R) continue;
     atomicAdd((unsigned long long *)(R + 16), 1ull);
-    min32(R + 24, ts);
-    max32(R + 28, ts);
-    max32(R + 32, sysup);
-    or64(R + 56, tpl);
-    or64(R + (dom0 ? 72 : 80), dom0 | dom1);
-    apply_push_constants(R, P);
+    if (claimed) {  // a row this record just claimed: a pre-load would only read the identities back
+        atomicMin((unsigned int *)(R + 24), ts);
+        atomicMax((unsigned int *)(R + 28), ts);
+        if (sysup) atomicMax((unsigned int *)(R + 32), sysup);
+        atomicOr((unsigned long long *)(R + 56), (unsigned long long)tpl);
+        atomicOr((unsigned long long *)(R + (dom0 ? 72 : 80)), (unsigned long long)(dom0 | dom1));
+        apply_push_constants<true>(R, P);
+    } else {
+        min32(R + 24, ts);
+        max32(R + 28, ts);
+        max32(R + 32, sysup);
+        or64(R + 56, tpl);
+        or64(R + (dom0 ? 72 : 80), dom0 | dom1);
+        apply_push_constants(R, P);
+    }
 #pragma unroll
     for (int v = 0; v < MAXV; ++v) {
         if (v >= (int)P.n_vals) break;
         uint8_t *dst = R + P.val_off[v];
         if ((hv >> v) & 1) {
-            apply_value(dst, P.val_op[v], xv[v]);
+            if (claimed) apply_value_hot(dst, P.val_op[v], xv[v]);
+            else apply_value(dst, P.val_op[v], xv[v]);
         } else if ((hb >> v) & 1) {  // BoolMapOr over bytes (mac, mpls label, octetArray, u256)
             const uint32_t w = sp.val_w[v];
             bool nul = false;
             for (uint32_t j = 0; j < (w + 3) / 4; ++j) or32(dst + 4 * j, load_word(sp.val_col[v] + row * w, w, j, false, nul));
         }
     }
-    or32(R + 12, hv | hb);
+    if (claimed) atomicOr((unsigned int *)(R + 12), hv | hb);
+    else or32(R + 12, hv | hb);
     }  // tiles
     __syncthreads();
     for (int e = threadIdx.x; e < CN; e += blockDim.x) {  // the workgroup's combined groups -> HBM
