@@ -42,3 +42,25 @@ REDUCE_TEMPLATE_1 = [(1, 8), (2, 8), (52, 1), (53, 1), (7, 2), (6, 2)]
 REDUCE_TEMPLATE_2 = [(1, 8), (2, 8), (52, 1), (53, 1), (11, 2), (6, 2)]
 REDUCE_WIRE_1 = struct.pack(">QQBBHH", 1000, 10, 64, 128, 80, 0x03)
 REDUCE_WIRE_2 = struct.pack(">QQBBHH", 2000, 20, 32, 255, 22, 0xC0)
+
+# test_explode_simple_netflowv9_packet (tests.rs:946-1017): NetFlowV9Packet::new(sys_up_time 1000,
+# 2025-01-01 12:00:00, seq 1, source_id 100), data set 256, peer 192.168.1.1:9995, collection
+# time 2025-01-01 10:00:00
+T_2025_01_01_12 = 1735732800
+T_2025_01_01_10_MS = 1735725600000
+NF_TEMPLATE = [(8, 4), (12, 4), (7, 2), (11, 2), (1, 8), (2, 8)]
+NF_RECORD = struct.pack(">IIHHQQ", 0x0A000001, 0x0A000002, 80, 443, 1000, 10)
+NF_FIELDS = [(0, 8, 0, OP_KEY), (0, 12, 0, OP_KEY), (0, 7, 0, OP_KEY), (0, 11, 0, OP_KEY),
+             (0, 1, 0, OP_ADD), (0, 2, 0, OP_ADD)]
+NF_EXPECTED = dict(flow_type=9, key=(0x0A000001, 0x0A000002, 80, 443), vals=(1000, 10), record_count=1,
+                   ports={9995}, domains={100}, templates={(9, 256)}, min_export=T_2025_01_01_12,
+                   max_export=T_2025_01_01_12, max_sysup=1000, min_coll=T_2025_01_01_10_MS,
+                   max_coll=T_2025_01_01_10_MS)
+
+
+def nf_packet():
+    """The test's packet as NetFlow v9 wire bytes: template flowset + data flowset, count 2."""
+    tpl = struct.pack(">HH", 256, len(NF_TEMPLATE)) + b"".join(struct.pack(">HH", i, n) for i, n in NF_TEMPLATE)
+    tset = struct.pack(">HH", 0, 4 + len(tpl)) + tpl
+    dset = struct.pack(">HH", 256, 4 + len(NF_RECORD)) + NF_RECORD
+    return struct.pack(">HHIIII", 9, 2, 1000, T_2025_01_01_12, 1, 100) + tset + dset

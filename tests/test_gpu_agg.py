@@ -269,3 +269,9 @@ def test_table_full_and_flush_buffer_errors(dev):
     assert lib().ngz_agg_flush(agg2._h, buf.ctypes.data, buf.nbytes) == -1  # NGZ_E_INVALID
     assert agg2.n_groups() == n
     assert len(agg2.flush()) == n and agg2.n_groups() == 0
+
+
+def test_kat_netflowv9_explode(dev):
+    (g,) = check(K.NF_FIELDS, [[K.nf_packet()]], port=9995, coll=K.T_2025_01_01_10_MS)
+    for k, v in K.NF_EXPECTED.items():
+        assert g[k] == v, k

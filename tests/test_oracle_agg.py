@@ -68,3 +68,10 @@ def test_lateness_and_minute_windows():
     assert agg.late == 2  # 165 and 169 are more than 10 s behind 180
     got = sorted((g["window_start"], g["record_count"]) for g in agg.flush())
     assert got == [(1_700_000_100, 1), (1_700_000_160, 2)]  # minute floors
+
+
+def test_netflowv9_explode():
+    agg = A.aggregate_datagrams(K.NF_FIELDS, [K.nf_packet()], peer_port=9995, collection_ms=K.T_2025_01_01_10_MS)
+    (g,) = agg.flush()
+    for k, v in K.NF_EXPECTED.items():
+        assert g[k] == v, k
