@@ -16,7 +16,7 @@ It restates, over the packets of ngz_oracle.FlowInfoCodec:
                                  window start = get_window_start :79-89, minute floor)
 Pinned by the reference's own unit tests (aggregator/tests.rs: test_reduce_add_operations
 :244-337, test_explode_ipfix_repeating_ie_fields :755-827, test_explode_ipfix_missing_fields
-:830-893), restated as vectors in tests/kats_agg.py.
+:830-893, test_explode_simple_netflowv9_packet :946-1017), restated as vectors in tests/kats_agg.py.
 
 Values are canonical Python values: ints for integer / ipv4 / tcpControlBits / bool / date-time
 seconds, bytes for byte-like fields, str for strings.

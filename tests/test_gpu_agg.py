@@ -275,3 +275,14 @@ def test_kat_netflowv9_explode(dev):
     (g,) = check(K.NF_FIELDS, [[K.nf_packet()]], port=9995, coll=K.T_2025_01_01_10_MS)
     for k, v in K.NF_EXPECTED.items():
         assert g[k] == v, k
+
+
+def test_flow_type_separates_groups(dev):
+    """The same key exported over NetFlow v9 and IPFIX by one peer makes two groups
+    (FlowCacheKey.flow_type; reference test_aggregator_push_netflowv9_and_ipfix_different_flow_types,
+    aggregator/tests.rs:1179-1262)."""
+    ipfix = ipfix_msg([tset(256, K.NF_TEMPLATE), dset(256, [K.NF_RECORD, K.NF_RECORD])], K.T_2025_01_01_12,
+                      domain=100)
+    g = check(K.NF_FIELDS, [[K.nf_packet(), ipfix]], port=9995, coll=K.T_2025_01_01_10_MS)
+    assert sorted((x["flow_type"], x["record_count"], x["vals"]) for x in g) == [(9, 1, (1000, 10)),
+                                                                                 (10, 2, (2000, 20))]
