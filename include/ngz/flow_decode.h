@@ -40,7 +40,8 @@
 extern "C" {
 #endif
 
-#define NGZ_ABI_VERSION 1
+#define NGZ_ABI_VERSION 2  /* 2: ngz_slot_info.n_fields is 32-bit (no field cap), ngz_dgram_error,
+                              ngz_template_counts_device */
 
 /* return codes */
 #define NGZ_OK 0
@@ -53,7 +54,8 @@ extern "C" {
 #define NGZ_DG_OK 0            /* Ok(Some(FlowInfo)) */
 #define NGZ_DG_NEED_MORE 1     /* Ok(None): shorter than 16 B or than the header length */
 #define NGZ_DG_ERROR 2         /* Err(FlowInfoCodecDecoderError), see ngz_dgram_error_json */
-#define NGZ_DG_UNSUPPORTED 3   /* needs a path not built yet (variable-length data records) */
+#define NGZ_DG_UNSUPPORTED 3   /* a data set of a template whose fixed record is longer than 65535 bytes
+                                  (NGZ_MAX_REC_LEN; every other template is decoded on the device) */
 
 /* field decode kinds (ngz_field_info.kind); column encodings in DESIGN.md */
 #define NGZ_K_UINT 1      /* big-endian unsigned, reduced size, zero-extended to width */
@@ -66,7 +68,8 @@ extern "C" {
 #define NGZ_K_DTFRAC 8    /* dateTimeMicro/Nanoseconds -> {u32 secs, u32 nanos} */
 #define NGZ_K_STR 9       /* fixed string: raw bytes, NUL-truncated prefix UTF-8 checked */
 #define NGZ_K_SCOPE32 10  /* NFv9 System/Interface/LineCard scope: reduced u32 (len<=4) */
-#define NGZ_K_VLEN 11     /* variable-length field (not decodable on device yet) */
+#define NGZ_K_VLEN 11     /* variable-length field (65535): column = {u64 offset into the batch bytes,
+                             u32 value length, u32 0}; strings UTF-8 checked */
 #define NGZ_K_FAIL 12     /* always fails with a template-constant error */
 
 typedef struct ngz_ctx ngz_ctx;
@@ -109,10 +112,12 @@ typedef struct {
     uint32_t version_id;  /* context-unique template version id */
     uint16_t template_id;
     uint8_t proto;        /* 10 or 9 */
-    uint8_t n_fields;     /* scope + non-scope fields (columns) */
+    uint8_t reserved;
     uint32_t n_records;   /* rows filled in this batch */
     uint32_t capacity;    /* rows allocated (column stride is capacity*width) */
     uint8_t *columns;     /* device base; column f at columns + capacity*col_off[f] */
+    uint32_t n_fields;    /* scope + non-scope fields (columns); no cap */
+    uint32_t reserved2;
 } ngz_slot_info;
 
 typedef struct {
@@ -174,6 +179,64 @@ int ngz_slot_fields(ngz_ctx *ctx, uint32_t slot, ngz_field_info *fields, uint32_
  * Returns the string length (excluding NUL) or <0. */
 int ngz_dgram_error_json(ngz_ctx *ctx, uint32_t dgram, char *buf, size_t cap);
 
+/* Structured FlowInfoCodecDecoderError of a datagram (status ERROR): the
+ * innermost reference error variant and its fields, the layer it was raised
+ * in, and the IE it concerns.  It carries the same information as the serde
+ * text of ngz_dgram_error_json (which it is derived from), so a host binding
+ * can rebuild the reference's nested error enums without parsing JSON:
+ *   layer CODEC    FlowInfoCodecDecoderError::UnsupportedVersion (codec.rs:214-217)
+ *         MESSAGE  IpfixPacketParsingError / NetFlowV9PacketParsingError (ipfix.rs:54-104, netflow.rs:56-114)
+ *         SET      SetParsingError / SetError (ipfix.rs:133-251, netflow.rs:143-248)
+ *         TEMPLATE (Options)TemplateRecordError, FieldSpecifierError, ScopeFieldSpecifierError
+ *                  (ipfix.rs:276-327,384-413, netflow.rs:265-388, deserializer/mod.rs:50-67)
+ *         RECORD   DataRecordError -> FieldError / ScopeFieldError (ipfix.rs:335-370, netflow.rs:399-475)
+ * Field meaning per kind (offset is always the absolute message offset the
+ * reference reports; NGZ_ERR_INVALID_LENGTH's length is the bad length):
+ *   UNSUPPORTED_VERSION value=version | UNEXPECTED_EOF length=needed, available |
+ *   INVALID_PADDING_LENGTH length=requested, value=ret_len | INVALID_SET_ID value=id |
+ *   NO_TEMPLATE value=template id | INVALID_PADDING_VALUE value | INVALID_COUNT value=count |
+ *   INVALID_TEMPLATE_ID value=template id | INVALID_SCOPE_FIELDS_COUNT value=scope count, length=total |
+ *   UNDEFINED_IANA_IE ie_id | INVALID_TIMESTAMP value=seconds | INVALID_TIMESTAMP_MILLIS value=millis |
+ *   INVALID_TIMESTAMP_FRACTION value=seconds, length=fraction | UTF8 offset of the string. */
+#define NGZ_ERR_NONE 0
+#define NGZ_ERR_UNSUPPORTED_VERSION 1
+#define NGZ_ERR_INVALID_LENGTH 2
+#define NGZ_ERR_UNEXPECTED_EOF 3
+#define NGZ_ERR_INVALID_PADDING_LENGTH 4
+#define NGZ_ERR_INVALID_SET_ID 5
+#define NGZ_ERR_NO_TEMPLATE 6
+#define NGZ_ERR_INVALID_PADDING_VALUE 7
+#define NGZ_ERR_INVALID_COUNT 8
+#define NGZ_ERR_INVALID_TEMPLATE_ID 9
+#define NGZ_ERR_INVALID_SCOPE_FIELDS_COUNT 10
+#define NGZ_ERR_UNDEFINED_IANA_IE 11
+#define NGZ_ERR_INVALID_TIMESTAMP 12
+#define NGZ_ERR_INVALID_TIMESTAMP_MILLIS 13
+#define NGZ_ERR_INVALID_TIMESTAMP_FRACTION 14
+#define NGZ_ERR_UTF8 15
+
+#define NGZ_ERRL_CODEC 0
+#define NGZ_ERRL_MESSAGE 1
+#define NGZ_ERRL_SET 2
+#define NGZ_ERRL_TEMPLATE 3
+#define NGZ_ERRL_RECORD 4
+
+typedef struct {
+    uint16_t kind;       /* NGZ_ERR_* */
+    uint8_t layer;       /* NGZ_ERRL_* */
+    uint8_t vendor;      /* 1: wrapped in the IE vendor's error ({Vendor}Error, generator.rs:2875-2895) */
+    uint32_t offset;     /* absolute byte offset in the message */
+    uint64_t value;      /* per kind, above */
+    uint32_t length;     /* per kind, above */
+    uint32_t available;  /* UNEXPECTED_EOF */
+    uint32_t ie_pen;     /* IE the error concerns (field / specifier errors), else 0 */
+    uint16_t ie_id;
+    uint16_t field;      /* RECORD layer: field index in the template (scope first), else 0xFFFF */
+} ngz_error;
+
+/* Returns 0 and fills *err for a datagram with status ERROR; NGZ_E_INVALID otherwise. */
+int ngz_dgram_error(ngz_ctx *ctx, uint32_t dgram, ngz_error *err);
+
 /* serde_json text of the datagram's decoded FlowInfo (status OK) or of its
  * FlowInfoCodecDecoderError (status ERROR), rendered from the last batch's
  * columns: the reference's `serde_json::to_string(&flow_info)` for the same
@@ -204,6 +267,17 @@ int ngz_templates_json(ngz_ctx *ctx, int proto, char *buf, size_t cap);
  * fills ids[i], counts[i] for up to cap templates; reset != 0 zeroes them
  * afterwards (reset_processed_count).  Returns the number of templates. */
 int ngz_template_counts(ngz_ctx *ctx, int proto, uint16_t *ids, uint64_t *counts, uint32_t cap, int reset);
+
+/* The same table written to DEVICE memory, ready for a collective (the
+ * per-template count exchange behind templates.usage, flow_actor.rs:362-381):
+ * dev_table[2*i] = template id, dev_table[2*i+1] = processed_count, ids
+ * ascending, entries [n, cap) zeroed.  One host-to-device copy queued on
+ * hip_stream (NULL = the context's stream): an ncclAllGather / ncclAllReduce
+ * queued after it on that stream sees the table, with no host synchronisation.
+ * reset as ngz_template_counts.  Returns the number of templates n (> cap:
+ * only the first cap were written; re-agree the table size and call again). */
+int ngz_template_counts_device(ngz_ctx *ctx, int proto, uint64_t *dev_table, uint32_t cap, int reset,
+                               void *hip_stream);
 
 /* Timing of the last ngz_decode_batch: device milliseconds of the record
  * decode kernel and of the whole device pipeline (HIP events). */

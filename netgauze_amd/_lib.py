@@ -21,7 +21,15 @@ ABI_FUNCTIONS = [
     "ngz_decode_batch_host", "ngz_slot_fields", "ngz_dgram_error_json",
     "ngz_templates_json", "ngz_template_counts", "ngz_last_timing", "ngz_ctx_set_option",
     "ngz_template_kernel", "ngz_columns_to_host", "ngz_dgram_json", "ngz_batch_json",
+    "ngz_dgram_error", "ngz_template_counts_device",
 ]
+NGZ_ABI_VERSION = 2
+# ngz_error.kind / .layer (flow_decode.h)
+ERR_KINDS = ["NONE", "UNSUPPORTED_VERSION", "INVALID_LENGTH", "UNEXPECTED_EOF", "INVALID_PADDING_LENGTH",
+             "INVALID_SET_ID", "NO_TEMPLATE", "INVALID_PADDING_VALUE", "INVALID_COUNT", "INVALID_TEMPLATE_ID",
+             "INVALID_SCOPE_FIELDS_COUNT", "UNDEFINED_IANA_IE", "INVALID_TIMESTAMP", "INVALID_TIMESTAMP_MILLIS",
+             "INVALID_TIMESTAMP_FRACTION", "UTF8"]
+ERR_LAYERS = ["CODEC", "MESSAGE", "SET", "TEMPLATE", "RECORD"]
 # include/ngz/flow_ingest.h
 INGEST_FUNCTIONS = [
     "ngz_pcap_open", "ngz_pcap_next", "ngz_pcap_close", "ngz_collector_create", "ngz_collector_destroy",
@@ -64,15 +72,25 @@ class BatchIn(ctypes.Structure):
 
 class SlotInfo(ctypes.Structure):
     _fields_ = [("version_id", ctypes.c_uint32), ("template_id", ctypes.c_uint16),
-                ("proto", ctypes.c_uint8), ("n_fields", ctypes.c_uint8),
+                ("proto", ctypes.c_uint8), ("reserved", ctypes.c_uint8),
                 ("n_records", ctypes.c_uint32), ("capacity", ctypes.c_uint32),
-                ("columns", ctypes.c_void_p)]
+                ("columns", ctypes.c_void_p), ("n_fields", ctypes.c_uint32), ("reserved2", ctypes.c_uint32)]
 
 
 class BatchOut(ctypes.Structure):
     _fields_ = [("n_dgrams", ctypes.c_uint32), ("n_sets", ctypes.c_uint32), ("n_slots", ctypes.c_uint32),
                 ("n_records", ctypes.c_uint64), ("dgrams", ctypes.c_void_p), ("sets", ctypes.c_void_p),
                 ("slots", ctypes.POINTER(SlotInfo)), ("n_template_dgrams", ctypes.c_uint32)]
+
+
+class Error(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_uint16), ("layer", ctypes.c_uint8), ("vendor", ctypes.c_uint8),
+                ("offset", ctypes.c_uint32), ("value", ctypes.c_uint64), ("length", ctypes.c_uint32),
+                ("available", ctypes.c_uint32), ("ie_pen", ctypes.c_uint32), ("ie_id", ctypes.c_uint16),
+                ("field", ctypes.c_uint16)]
+
+
+assert ctypes.sizeof(Error) == 32
 
 
 class FieldInfo(ctypes.Structure):
@@ -137,6 +155,10 @@ def load():
     lib.ngz_dgram_json.restype = ctypes.c_int64
     lib.ngz_batch_json.argtypes = [P, P, JSON_LINE_FN, P]
     lib.ngz_batch_json.restype = ctypes.c_int64
+    lib.ngz_dgram_error.argtypes = [P, U32, ctypes.POINTER(Error)]
+    lib.ngz_dgram_error.restype = I
+    lib.ngz_template_counts_device.argtypes = [P, I, P, U32, I, P]
+    lib.ngz_template_counts_device.restype = I
     # aggregation (flow_aggregate.h)
     lib.ngz_agg_create.argtypes = [I, ctypes.POINTER(AggField), U32, U64, U64, U64, ctypes.POINTER(P)]
     lib.ngz_agg_create.restype = I

@@ -151,6 +151,20 @@ std::string wrap(const char *tag, const std::string &inner) { return std::string
 
 const IeRow *ie_find(uint32_t pen, uint16_t id) { return ies().find(pen, id); }
 
+const IeRow *ie_find_name(const char *vendor, const std::string &name) {
+    const uint32_t pen = vendor ? vendor_pen(vendor) : 0;
+    if (vendor && !pen) return nullptr;
+    for (const auto &r : kIes)
+        if (r.pen == pen && name == r.name) return &r;
+    return nullptr;
+}
+
+uint32_t vendor_pen(const std::string &vendor) {
+    for (const auto &v : kVendors)
+        if (vendor == v.name) return v.pen;
+    return 0;
+}
+
 }  // namespace ngzh
 
 namespace {
@@ -222,7 +236,7 @@ void field_rule(const Spec &s, uint8_t &kind, uint16_t &width, uint8_t &fail) {
 // A plan gets a generated kernel when the device decodes it at all and no
 // raw field is huge (IE::Unknown of length 65535 never yields a record).
 bool rtc_eligible(const DevPlan &P) {
-    if (!P.rpl) return false;
+    if (!P.rpl || P.n_fields > NGZ_RTC_MAX_FIELDS) return false;
     for (uint32_t i = 0; i < P.n_fields; ++i)
         if (P.f[i].kind != NGZ_K_VLEN && P.f[i].len > 4096) return false;
     return true;
@@ -234,8 +248,9 @@ void build_plan(Version &v) {
     P.proto = v.proto;
     P.template_id = v.tid;
     v.fail_sub.assign(v.specs.size(), 0);
+    v.fields.assign(v.specs.size(), DevField{});
     uint32_t off = 0, col = 0, rl = 0;
-    bool vlen = false, devok = v.specs.size() <= NGZ_MAXF;
+    bool vlen = false;
     for (size_t i = 0; i < v.specs.size(); ++i) {
         const Spec &s = v.specs[i];
         uint8_t kind, fail;
@@ -246,20 +261,19 @@ void build_plan(Version &v) {
         if (v.proto == 10 && s.length == 0xFFFF) vlen = true;
         // min_record_length counts a vlen field as 1 (ipfix.rs:193-214); NFv9 literal (netflow.rs:201-210)
         rl += (v.proto == 10 && s.length == 0xFFFF) ? 1 : s.length;
-        if (i < NGZ_MAXF) {
-            DevField &fd = P.f[i];
-            fd.off = (uint16_t)(vlen ? 0xFFFF : off);
-            fd.len = s.length;
-            fd.width = width;
-            fd.kind = kind;
-            fd.flags = fail;
-            fd.col_off = col;
-        }
+        DevField &fd = v.fields[i];
+        fd.off = (uint16_t)(vlen ? 0xFFFF : off);
+        fd.len = s.length;
+        fd.width = width;
+        fd.kind = kind;
+        fd.flags = fail;
+        fd.col_off = col;
         v.fail_sub[i] = fail;
         off += s.length;
         col += width;
     }
-    P.n_fields = (uint16_t)std::min<size_t>(v.specs.size(), NGZ_MAXF);
+    P.f = v.fields.data();
+    P.n_fields = (uint16_t)v.specs.size();
     P.rec_len = rl;
     P.row_bytes = col;
     P.has_vlen = vlen;
@@ -271,7 +285,7 @@ void build_plan(Version &v) {
     // variable-length fields through the framing walk + record-offset arrays)
     P.rpl = 0;
     P.window = NGZ_REG_WINDOW;
-    if (devok && rl <= NGZ_MAX_REC_LEN) P.rpl = 1;
+    if (rl <= NGZ_MAX_REC_LEN) P.rpl = 1;
     // per-template kernels stage the columns of 256*lds_waves rows in LDS
     // (NGZ_LDS=0: direct column stores, for A/B measurements)
     static const bool lds_on = !getenv("NGZ_LDS") || atoi(getenv("NGZ_LDS")) != 0;
@@ -735,10 +749,17 @@ int upload_slots(ngz_ctx *ctx, const std::vector<int32_t> cur_start[2], hipStrea
     const size_t S = ctx->slot_version.size();
     if (ctx->d_plans.ensure(std::max<size_t>(S, 1)) || ctx->d_cur_slot.ensure(2 * 65536))
         return fail(ctx, NGZ_E_NOMEM, "device alloc (plans)");
+    size_t nf_total = 0;
+    for (size_t s = 0; s < S; ++s) nf_total += ctx->versions[ctx->slot_version[s]].fields.size();
+    if (ctx->d_fields.ensure(std::max<size_t>(nf_total, 1))) return fail(ctx, NGZ_E_NOMEM, "device alloc (field tables)");
     std::vector<DevPlan> plans(S);
+    std::vector<DevField> ftab;
+    ftab.reserve(nf_total);
     for (size_t s = 0; s < S; ++s) {
         Version &v = ctx->versions[ctx->slot_version[s]];
         plans[s] = v.plan;
+        plans[s].f = ctx->d_fields.p + ftab.size();  // the slot's descriptors in the device field table
+        ftab.insert(ftab.end(), v.fields.begin(), v.fields.end());
         plans[s].spec = 0;
         if (ctx->specialize && rtc_eligible(v.plan)) {
             // NGZ_OPT_SPECIALIZE 2: compile once the template has seen enough records to pay for it
@@ -755,6 +776,8 @@ int upload_slots(ngz_ctx *ctx, const std::vector<int32_t> cur_start[2], hipStrea
         for (uint32_t id = 0; id < 65536; ++id)
             if (cur_start[pi][id] >= 0) cs[pi * 65536 + id] = (uint16_t)ctx->version_slot[cur_start[pi][id]];
     HIPCHK(hipMemcpyAsync(ctx->d_plans.p, plans.data(), S * sizeof(DevPlan), hipMemcpyHostToDevice, st));
+    if (!ftab.empty())
+        HIPCHK(hipMemcpyAsync(ctx->d_fields.p, ftab.data(), ftab.size() * sizeof(DevField), hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(ctx->d_cur_slot.p, cs.data(), cs.size() * 2, hipMemcpyHostToDevice, st));
     HIPCHK(hipStreamSynchronize(st));  // host vectors go out of scope
     ctx->plans_dirty = false;
@@ -1096,7 +1119,9 @@ int finish_batch(ngz_ctx *ctx, const ngz_batch_in *in, ngz_batch_out *out, hipSt
         si.version_id = (uint32_t)ctx->slot_version[s];
         si.template_id = v.tid;
         si.proto = v.proto;
-        si.n_fields = (uint8_t)std::min<size_t>(v.specs.size(), 255);
+        si.n_fields = (uint32_t)v.specs.size();
+        si.reserved = 0;
+        si.reserved2 = 0;
         si.n_records = ctx->slot_rt[s].total;
         si.capacity = ctx->slot_rt[s].cap;
         si.columns = ctx->d_arena.p + ctx->arena_shift + ctx->slot_rt[s].block;
@@ -1173,7 +1198,7 @@ void ngz_ctx_destroy(ngz_ctx *ctx) {
     if (!ctx) return;
     hipSetDevice(ctx->device);
     hipStreamSynchronize(ctx->stream);
-    ctx->d_plans.release(); ctx->d_cur_slot.release(); ctx->d_tl_key.release(); ctx->d_tl_dgram.release();
+    ctx->d_plans.release(); ctx->d_fields.release(); ctx->d_cur_slot.release(); ctx->d_tl_key.release(); ctx->d_tl_dgram.release();
     ctx->d_tl_slot.release(); ctx->d_hf_flag.release(); ctx->d_hf_hdr.release(); ctx->d_hf_first.release(); ctx->d_hf_sets.release();
     ctx->d_hdr.release(); ctx->d_counts.release(); ctx->d_scan.release(); ctx->d_scan_tmp.release();
     ctx->d_slots.release(); ctx->d_chunks.release(); ctx->d_sets.release(); ctx->d_arena.release();
@@ -1190,6 +1215,8 @@ void ngz_ctx_destroy(ngz_ctx *ctx) {
     if (ctx->h_slots) hipHostFree(ctx->h_slots);
     if (ctx->h_proc) hipHostFree(ctx->h_proc);
     if (ctx->h_done) hipHostFree(ctx->h_done);
+    if (ctx->counts_ev) { hipEventSynchronize(ctx->counts_ev); hipEventDestroy(ctx->counts_ev); }
+    if (ctx->h_counts_stage) hipHostFree(ctx->h_counts_stage);
     hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -1427,12 +1454,10 @@ int ngz_slot_fields(ngz_ctx *ctx, uint32_t slot, ngz_field_info *fields, uint32_
         f.is_scope = i < v.n_scope;
         f.pen = s.pen;
         f.ie_id = s.id;
-        if (i < NGZ_MAXF) {
-            f.wire_offset = v.plan.f[i].off;
-            f.width = v.plan.f[i].width;
-            f.kind = v.plan.f[i].kind;
-            f.col_off = v.plan.f[i].col_off;
-        }
+        f.wire_offset = v.fields[i].off;
+        f.width = v.fields[i].width;
+        f.kind = v.fields[i].kind;
+        f.col_off = v.fields[i].col_off;
     }
     return (int)n;
 }
@@ -1459,6 +1484,36 @@ int ngz_template_counts(ngz_ctx *ctx, int proto, uint16_t *ids, uint64_t *counts
         ++n;
     }
     return (int)n;
+}
+
+int ngz_template_counts_device(ngz_ctx *ctx, int proto, uint64_t *dev_table, uint32_t cap, int reset,
+                               void *hip_stream) {
+    if (!ctx || (proto != 9 && proto != 10) || (cap && !dev_table)) return NGZ_E_INVALID;
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : ctx->stream;
+    // the staging buffer is reused: the previous table's copy must have left it
+    if (ctx->counts_ev) HIPCHK(hipEventSynchronize(ctx->counts_ev));
+    else HIPCHK(hipEventCreateWithFlags(&ctx->counts_ev, hipEventDisableTiming));
+    if (cap > ctx->h_counts_cap) {
+        if (ctx->h_counts_stage) hipHostFree(ctx->h_counts_stage);
+        ctx->h_counts_stage = nullptr;
+        ctx->h_counts_cap = 0;
+        HIPCHK(hipHostMalloc((void **)&ctx->h_counts_stage, 16ull * cap, hipHostMallocDefault));
+        ctx->h_counts_cap = cap;
+    }
+    const int n = ngz_template_counts(ctx, proto, nullptr, nullptr, 0, 0);
+    std::vector<uint16_t> ids(std::max(n, 1));
+    std::vector<uint64_t> cnt(std::max(n, 1));
+    ngz_template_counts(ctx, proto, ids.data(), cnt.data(), (uint32_t)n, reset);
+    for (uint32_t i = 0; i < cap; ++i) {
+        ctx->h_counts_stage[2 * i] = (int)i < n ? ids[i] : 0;
+        ctx->h_counts_stage[2 * i + 1] = (int)i < n ? cnt[i] : 0;
+    }
+    if (cap) {
+        HIPCHK(hipMemcpyAsync(dev_table, ctx->h_counts_stage, 16ull * cap, hipMemcpyHostToDevice, st));
+        HIPCHK(hipEventRecord(ctx->counts_ev, st));
+    }
+    return n;
 }
 
 int ngz_templates_json(ngz_ctx *ctx, int proto, char *buf, size_t cap) {

@@ -44,6 +44,10 @@ struct VendorRow {
 
 // (pen, id) -> registry row, or null
 const IeRow *ie_find(uint32_t pen, uint16_t id);
+// (vendor display name or null for IANA, IE name) -> registry row, or null
+const IeRow *ie_find_name(const char *vendor, const std::string &name);
+// vendor display name -> PEN (0 if unknown)
+uint32_t vendor_pen(const std::string &vendor);
 
 // ------------------------------------------------------------------------
 // Template model
@@ -63,16 +67,44 @@ struct Spec {
 };
 
 struct Version {
-    uint8_t proto;  // 10 / 9
-    uint16_t tid;
+    uint8_t proto = 0;  // 10 / 9
+    uint16_t tid = 0;
     std::vector<Spec> specs;  // scope first
-    uint32_t n_scope;
-    DevPlan plan;
+    uint32_t n_scope = 0;
+    DevPlan plan{};                 // plan.f points into `fields` (re-pointed on copy / move)
+    std::vector<DevField> fields;   // one descriptor per spec
     std::vector<uint8_t> fail_sub;  // per field: 1 InvalidLength, 2 InvalidPaddingLength, 3 scope InvalidLength
     uint64_t processed = 0;
     uint64_t seen_records = 0;      // records decoded with this version (NGZ_OPT_SPECIALIZE 2)
-    int rtc_state = 0;              // specialised kernel: 0 not looked up, 1 ready, 2 unavailable
+    int rtc_state = 0;              // specialised kernel: 0 not looked up, 1 ready, 2 unavailable, 3 compiling
     void *rtc_fn = nullptr;
+    uint64_t rtc_key = 0;           // layout signature key of the (pending) specialised kernel
+
+    Version() = default;
+    Version(const Version &o) { *this = o; }
+    Version(Version &&o) noexcept { *this = std::move(o); }
+    Version &operator=(const Version &o) {
+        copy_scalars(o);
+        specs = o.specs;
+        fields = o.fields;
+        fail_sub = o.fail_sub;
+        plan.f = fields.data();
+        return *this;
+    }
+    Version &operator=(Version &&o) noexcept {
+        copy_scalars(o);
+        specs = std::move(o.specs);
+        fields = std::move(o.fields);
+        fail_sub = std::move(o.fail_sub);
+        plan.f = fields.data();
+        return *this;
+    }
+
+  private:
+    void copy_scalars(const Version &o) {
+        proto = o.proto; tid = o.tid; n_scope = o.n_scope; plan = o.plan; processed = o.processed;
+        seen_records = o.seen_records; rtc_state = o.rtc_state; rtc_fn = o.rtc_fn; rtc_key = o.rtc_key;
+    }
 };
 
 // serde_json helpers (ngz_host.cpp)
@@ -174,6 +206,7 @@ struct ngz_ctx {
     std::vector<int32_t> slot_version;          // slot -> version
     std::vector<int32_t> version_slot;          // version -> slot (this batch) or -1
     ngzh::DevBuf<DevPlan> d_plans;
+    ngzh::DevBuf<DevField> d_fields;             // field tables of the uploaded plans (DevPlan::f)
     ngzh::DevBuf<uint16_t> d_cur_slot;
     ngzh::DevBuf<uint32_t> d_tl_key, d_tl_dgram;
     ngzh::DevBuf<uint16_t> d_tl_slot;
@@ -241,4 +274,8 @@ struct ngz_ctx {
     std::vector<ngzh::TemplateSetJson> tmpl_sets;  // template sets of the last batch, (dgram, set_pos) order
     uint64_t batch_serial = 0;                      // bumped by every ngz_decode_batch
     std::shared_ptr<ngzh::JsonView> json_view;      // ngz_dgram_json cache of the last batch
+    // ngz_template_counts_device: pinned staging of the count table and the event of its last copy
+    uint64_t *h_counts_stage = nullptr;
+    uint32_t h_counts_cap = 0;
+    hipEvent_t counts_ev = nullptr;
 };

@@ -5,7 +5,9 @@
 
 #include "ngz/flow_decode.h"
 
-#define NGZ_MAXF 128          // fields (scope + non-scope) a device plan can hold
+#define NGZ_LANE_FIELDS 128   // field descriptors the generic kernel keeps in VGPRs (two per lane); the
+                              // rest of a wider template's table is read with scalar loads
+#define NGZ_RTC_MAX_FIELDS 512  // widest template that gets a generated kernel (wider: generic kernel)
 #define NGZ_MAX_SLOTS 1024    // template versions live in one batch
 #define NGZ_NO_SLOT 0xFFFFu
 #define NGZ_NO_ERR (~0ull)
@@ -89,7 +91,9 @@ struct DevPlan {
     uint32_t lds_waves;  // per-template kernel stages columns in LDS: waves (256-row sub-windows) per
                          // workgroup window, 0 = direct column stores (ngz_lds_waves)
     uint32_t reserved1;
-    DevField f[NGZ_MAXF];
+    const DevField *f;   // n_fields descriptors (scope first): host memory in the host's copy of a plan,
+                         // the context's device field table in the uploaded one.  No field cap: a
+                         // template may carry as many fields as its set holds (ipfix.rs:384-413).
 };
 
 // Records of one IPFIX data set whose template has variable-length (65535)

@@ -453,7 +453,7 @@ int json_render(ngz_ctx *ctx, const JsonView &v, uint32_t d, std::string &o, uin
         const uint8_t *cols = v.cols[si.slot].data();
         o += "{\"Data\":{\"id\":"; put_u64(o, ver_t.tid);
         o += ",\"records\":[";
-        const uint32_t nf = (uint32_t)std::min<size_t>(ver_t.specs.size(), NGZ_MAXF);
+        const uint32_t nf = (uint32_t)ver_t.specs.size();
         for (uint32_t r = 0; r < si.n; ++r) {
             const uint64_t row = (uint64_t)si.rec0 + r;
             o += r ? ",{\"scope_fields\":[" : "{\"scope_fields\":[";

@@ -445,6 +445,7 @@ __global__ void __launch_bounds__(256) k_decode_generic(BatchDev B) {
     const uint32_t lane = threadIdx.x & 63;
     uint32_t cached = 0xFFFFFFFFu, rl = 0, nf = 0, skip = 0, row_bytes = 0, has_vlen = 0;
     uint4 fA = make_uint4(0, 0, 0, 0), fB = make_uint4(0, 0, 0, 0);  // field descriptors f = lane, lane + 64
+    const uint4 *ft = nullptr;  // the slot's field table (descriptors past NGZ_LANE_FIELDS: scalar loads)
     auto want = [&](uint32_t slot) {
         if (slot != cached) {
             const DevPlan *pl = &B.plans[slot];
@@ -454,7 +455,7 @@ __global__ void __launch_bounds__(256) k_decode_generic(BatchDev B) {
             nf = h0.z & 0xFFFF;
             has_vlen = (h0.w >> 8) & 0xFF;
             skip = (h0.w >> 24) & 0xFF;  // DevPlan::spec: decoded by its own kernel
-            const uint4 *ft = (const uint4 *)pl->f;
+            ft = (const uint4 *)sload(&pl->f);
             fA = lane < nf ? ft[lane] : make_uint4(0, 0, 0, 0);
             fB = lane + 64 < nf ? ft[lane + 64] : make_uint4(0, 0, 0, 0);
             cached = slot;
@@ -477,10 +478,19 @@ __global__ void __launch_bounds__(256) k_decode_generic(BatchDev B) {
             }
         };
         for (uint32_t f = 0; f < nf; ++f) {
-            const uint4 &fs = f < 64 ? fA : fB;
-            const uint32_t fl = f & 63;
-            const uint32_t dx = lane_u32(fs.x, fl), dy = lane_u32(fs.y, fl);
-            const uint32_t col_off = lane_u32(fs.z, fl);
+            uint32_t dx, dy, col_off;
+            if (f < NGZ_LANE_FIELDS) {
+                const uint4 &fs = f < 64 ? fA : fB;
+                const uint32_t fl = f & 63;
+                dx = lane_u32(fs.x, fl);
+                dy = lane_u32(fs.y, fl);
+                col_off = lane_u32(fs.z, fl);
+            } else {  // wide template: wave-uniform descriptor through the scalar cache
+                const uint4 fs = sload(ft + f);
+                dx = fs.x;
+                dy = fs.y;
+                col_off = fs.z;
+            }
             const uint32_t len = dx >> 16, width = dy & 0xFFFF, kind = (dy >> 16) & 0xFF;
             const uint32_t off = seg + so;  // record offset of the field (per lane after a vlen field)
             if (kind == NGZ_K_FAIL) {

@@ -117,6 +117,17 @@ class DecodedBatch:
         s = self.error_json(d)
         return None if s is None else json.loads(s)
 
+    def error_struct(self, d):
+        """ngz_dgram_error: the structured FlowInfoCodecDecoderError of datagram
+        d as a dict (kind / layer names from flow_decode.h), or None."""
+        e = _lib.Error()
+        if lib().ngz_dgram_error(self._codec._ctx, d, ctypes.byref(e)) != 0:
+            return None
+        out = {k: getattr(e, k) for k, _ in _lib.Error._fields_}
+        out["kind"] = _lib.ERR_KINDS[e.kind]
+        out["layer"] = _lib.ERR_LAYERS[e.layer]
+        return out
+
     def json(self, d):
         """serde_json text of datagram d's FlowInfo (or of its error), rendered
         from the decoded columns (ngz_dgram_json); None for Ok(None)."""
@@ -226,6 +237,16 @@ class FlowInfoCodec:
         cnt = (ctypes.c_uint64 * max(n, 1))()
         lib().ngz_template_counts(self._ctx, proto, ids, cnt, n, 1 if reset else 0)
         return {ids[i]: cnt[i] for i in range(n)}
+
+    def template_counts_device(self, proto, dev_ptr, cap, reset=False, stream=None):
+        """ngz_template_counts_device: (id, processed_count) u64 pairs written to
+        device memory at dev_ptr (cap entries) on `stream`; returns the
+        template count (> cap: table too small)."""
+        n = lib().ngz_template_counts_device(self._ctx, proto, ctypes.c_void_p(dev_ptr), cap, 1 if reset else 0,
+                                             ctypes.c_void_p(stream) if stream else None)
+        if n < 0:
+            self._check(n)
+        return n
 
     def last_timing(self):
         a, b = ctypes.c_float(), ctypes.c_float()

@@ -61,4 +61,24 @@ KATS = [
     ("octets_fixed_small", 210, 26, SMALL_DATA, SMALL_DATA),
     ("octets_vlen_large", 210, 0xFFFF, bytes([0xff, 0x00, 0x01, 0x04]) + LARGE_DATA, LARGE_DATA),
     ("octets_fixed_large", 210, 260, LARGE_DATA, LARGE_DATA),
+] + [
+    # parse-utils/src/reader.rs:400-412, 481-493 (uint*_be_right_aligns_shortened_values): 0x0000ABCD in
+    # 2, 3 and 4 octets through the IEs whose decoders call read_unsigned64_be / read_unsigned32_be
+    # (packetDeltaCount unsigned64, ingressInterface unsigned32; generator.rs:1468-1496)
+    ("reader_u64_shortened_%d" % len(w), 2, len(w), w, 0xABCD)
+    for w in (bytes([0xAB, 0xCD]), bytes([0, 0xAB, 0xCD]), bytes([0, 0, 0xAB, 0xCD]))
+] + [
+    ("reader_u32_shortened_%d" % len(w), 10, len(w), w, 0xABCD)
+    for w in (bytes([0xAB, 0xCD]), bytes([0, 0xAB, 0xCD]), bytes([0, 0, 0xAB, 0xCD]))
+] + [
+    # reader.rs:414-420, 495-501 (full width equals the fixed read)
+    ("reader_u64_full_width", 2, 8, bytes([0x01, 0x23, 0x45, 0x67, 0x89, 0xAB, 0xCD, 0xEF]), 0x0123456789ABCDEF),
+    ("reader_u32_full_width", 10, 4, bytes([0x01, 0x23, 0x45, 0x67]), 0x01234567),
+    # reader.rs:529-551 through the one IANA signed32 IE, mibObjectValueInteger (read_signed32_be,
+    # generator.rs:1549-1562): -2 shortened to one octet sign-extends, 0x7F stays positive, full width
+    ("reader_i32_sign_extends_shortened", 434, 1, bytes([0xFE]), -2),
+    ("reader_i32_keeps_positive", 434, 1, bytes([0x7F]), 127),
+    ("reader_i32_full_width", 434, 4, bytes([0xFF, 0xFF, 0xFF, 0xFE]), -2),
+    # reader.rs:360-369 (read_padded left-aligns, zero-pads the tail) through an unsigned256 IE
+    ("reader_padded_short", 515, 2, bytes([0xAA, 0xBB]), bytes([0xAA, 0xBB]) + bytes(30)),
 ]

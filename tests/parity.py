@@ -63,6 +63,64 @@ def canon(val, fi):
     raise AssertionError("kind %d" % k)
 
 
+# innermost serde variant -> ngz_error.kind (flow_decode.h)
+_ERR_KIND = {"UnsupportedVersion": "UNSUPPORTED_VERSION", "InvalidLength": "INVALID_LENGTH",
+             "UnexpectedEof": "UNEXPECTED_EOF", "InvalidPaddingLength": "INVALID_PADDING_LENGTH",
+             "InvalidSetId": "INVALID_SET_ID", "NoTemplateDefinedFor": "NO_TEMPLATE",
+             "InvalidPaddingValue": "INVALID_PADDING_VALUE", "InvalidCount": "INVALID_COUNT",
+             "InvalidTemplateId": "INVALID_TEMPLATE_ID", "InvalidScopeFieldsCount": "INVALID_SCOPE_FIELDS_COUNT",
+             "UndefinedIANAIE": "UNDEFINED_IANA_IE", "InvalidTimestamp": "INVALID_TIMESTAMP",
+             "InvalidTimestampMillis": "INVALID_TIMESTAMP_MILLIS",
+             "InvalidTimestampFraction": "INVALID_TIMESTAMP_FRACTION", "Utf8Error": "UTF8"}
+
+
+def check_error_struct(batch, d, err):
+    """ngz_dgram_error of datagram d against the oracle's serde error value."""
+    st = batch.error_struct(d)
+    assert st is not None, d
+    tags, v = [], err
+    while isinstance(v, dict) and len(v) == 1:
+        (k, v), = v.items()
+        tags.append(k)
+    kind = tags[-1]
+    assert st["kind"] == _ERR_KIND[kind], (d, st, err)
+    layer = ("RECORD" if "DataRecordError" in tags else
+             "TEMPLATE" if {"TemplateRecordError", "OptionsTemplateRecordError", "FieldSpecifierError",
+                            "ScopeFieldSpecifierError", "IEError"} & set(tags) else
+             "SET" if {"SetParsingError", "SetError"} & set(tags) else
+             "MESSAGE" if {"IpfixParsingError", "NetFlowV9ParingError"} & set(tags) else "CODEC")
+    assert st["layer"] == layer, (d, st, err)
+    vendors = {n + "Error" for n in O.REGISTRY.vendors.values()}
+    assert st["vendor"] == (1 if vendors & set(tags) else 0), (d, st, err)
+    if isinstance(v, dict):
+        assert st["offset"] == v.get("offset", 0), (d, st, err)
+        expect = {"UnexpectedEof": {"length": v.get("needed"), "available": v.get("available")},
+                  "InvalidPaddingLength": {"length": v.get("requested"), "value": v.get("ret_len")},
+                  "InvalidSetId": {"value": v.get("id")}, "NoTemplateDefinedFor": {"value": v.get("id")},
+                  "InvalidPaddingValue": {"value": v.get("value")}, "InvalidCount": {"value": v.get("count")},
+                  "InvalidTemplateId": {"value": v.get("template_id")},
+                  "InvalidScopeFieldsCount": {"value": v.get("scope_fields_count"),
+                                              "length": v.get("total_fields_count")},
+                  "InvalidTimestamp": {"value": v.get("seconds")},
+                  "InvalidTimestampMillis": {"value": v.get("millis")},
+                  "InvalidTimestampFraction": {"value": v.get("seconds"), "length": v.get("fraction")},
+                  "InvalidLength": {"length": v.get("length")},
+                  "UnsupportedVersion": {"value": v.get("version")}}.get(kind, {})
+        for k, x in expect.items():
+            assert st[k] == x, (d, k, st, err)
+    elif kind == "UnsupportedVersion":
+        assert st["value"] == v
+    elif kind == "UndefinedIANAIE":
+        assert (st["ie_pen"], st["ie_id"]) == (0, v)
+    elif kind == "InvalidLength":  # FieldSpecifierError::InvalidLength(length, IE)
+        assert st["length"] == v[0]
+    if layer == "RECORD" and isinstance(v, dict) and "ie_name" in v:
+        assert st["field"] != 0xFFFF, (d, st)
+        ie = O.REGISTRY.by_key.get((st["ie_pen"], st["ie_id"]))
+        assert ie is not None and ie.name == v["ie_name"], (d, st, err)
+    return st
+
+
 def check_batch(batch, oracle, check_records=True, max_fail=5):
     """Compare; returns stats dict; raises AssertionError with context."""
     hdr = batch.dgram_headers()
@@ -93,6 +151,7 @@ def check_batch(batch, oracle, check_records=True, max_fail=5):
             assert st == L.NGZ_DG_ERROR, "dgram %d: expected error %s, status %d" % (d, O.dumps(val), st)
             got = batch.error_json(d)
             assert got == O.dumps(val), "dgram %d error:\n got %s\n exp %s" % (d, got, O.dumps(val))
+            check_error_struct(batch, d, val)
             stats["err"] += 1
             continue
         assert st == L.NGZ_DG_OK, "dgram %d: expected Ok(Some), status %d err %s" % (d, st, batch.error_json(d))

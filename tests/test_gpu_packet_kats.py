@@ -17,6 +17,7 @@ import json
 import pytest
 
 import kat_runner
+import parity
 import kats_packets as K
 import ngz_oracle as O
 from netgauze_amd import _lib as L
@@ -60,6 +61,8 @@ def product_step(codec, dgram):
         return st, None, 0
     assert len(lines) == 1 and lines[0][1] == st
     assert batch.json(0) == lines[0][2]
+    if st == L.NGZ_DG_ERROR:  # the structured error (ngz_dgram_error) says the same
+        parity.check_error_struct(batch, 0, json.loads(lines[0][2]))
     return st, lines[0][2], lines[0][3]
 
 

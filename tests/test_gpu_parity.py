@@ -535,3 +535,82 @@ def test_all_field_kinds(dev):
         data.append(ipfix_msg([ipfix_set(340, bytes(recs))], seq=m))
     stats, *_ = run_both([t] + data)
     assert stats["ok"] + stats["err"] == 7
+
+
+def test_wide_templates_no_field_cap(dev):
+    """Templates of 200 and 600 fields (no field cap; the reference has none,
+    ipfix.rs:384-413): the 200-field one gets a generated kernel, the 600-field
+    one (> NGZ_RTC_MAX_FIELDS) the generic kernel, whose descriptors past the
+    first 128 come through scalar loads.  NFv9 too."""
+    rng = np.random.default_rng(17)
+    kinds = [(7, 2), (8, 4), (1, 8), (4, 1), (27, 16), (152, 8), (82, 6), (2, 3), (61, 1), (210, 5)]
+    dgrams = []
+    for tid, nf in ((700, 200), (701, 600)):
+        fields = [kinds[i % len(kinds)] for i in range(nf)]
+        rl = sum(ln for _, ln in fields)
+        dgrams.append(ipfix_msg([ipfix_set(2, tmpl(tid, fields))]))
+        per = max(1, 60000 // rl)
+        for m in range(3):
+            recs = bytearray()
+            for _ in range(per):
+                for ie, ln in fields:
+                    if ie == 152:
+                        recs += int(rng.integers(0, 2**41)).to_bytes(8, "big")
+                    elif ie == 82:
+                        recs += bytes(rng.integers(97, 123, size=ln, dtype=np.uint8))
+                    else:
+                        recs += bytes(rng.integers(0, 256, size=ln, dtype=np.uint8))
+            dgrams.append(ipfix_msg([ipfix_set(tid, bytes(recs))], seq=m))
+    # NetFlow v9, 300 fields
+    nfields = [kinds[i % 5] for i in range(300)]
+    nrl = sum(ln for _, ln in nfields)
+    tset = struct.pack(">HH", 0, 8 + 4 * len(nfields)) + struct.pack(">HH", 710, len(nfields)) + \
+        b"".join(struct.pack(">HH", ie, ln) for ie, ln in nfields)
+    dgrams.append(nf_msg([tset], count=1))
+    for m in range(2):
+        body = bytearray()
+        for _ in range(20):
+            for ie, ln in nfields:
+                body += (int(rng.integers(0, 2**41)).to_bytes(8, "big") if ie == 152
+                         else bytes(rng.integers(0, 256, size=ln, dtype=np.uint8)))
+        dgrams.append(nf_msg([struct.pack(">HH", 710, 4 + len(body)) + bytes(body)], count=20))
+    stats, batch, codec, oc = run_both(dgrams)
+    assert stats["unsupported"] == 0 and stats["err"] == 0
+    assert {s.template_id: len(s.fields) for s in batch.slots} == {700: 200, 701: 600, 710: 300}
+    assert {s.template_id: batch.out.slots[i].n_fields for i, s in enumerate(batch.slots)} == \
+        {700: 200, 701: 600, 710: 300}
+    assert stats["records"] == sum(3 * max(1, 60000 // sum(ln for _, ln in [kinds[i % 10] for i in range(n)]))
+                                   for n in (200, 600)) + 40
+
+
+def test_template_counts_device(dev):
+    """ngz_template_counts_device writes the (id, processed_count) table for a
+    collective in one stream-ordered copy; ids ascending, tail zeroed, reset
+    as ngz_template_counts (flow_actor.rs:362-381)."""
+    from netgauze_amd import synth
+    tpls = synth.CFG3_TEMPLATES[:3]
+    codec = new_codec()
+    oc = O.FlowInfoCodec()
+    dgrams = [synth.templates_message(tpls)]
+    for i, (tid, fields) in enumerate(tpls):
+        rec = synth.template_records(fields, 500 * (i + 1), 40 + i)
+        _, rl = synth.field_offsets(fields)
+        buf, offs, lens = synth.ipfix_data_stream(rec, rl, tid=tid, rec_per_msg=37)
+        b = bytes(buf.numpy())
+        dgrams += [b[o:o + ln] for o, ln in zip(offs.tolist(), lens.tolist())]
+    codec.decode_datagrams(dgrams)
+    parity.oracle_datagrams(dgrams, oc)
+    exp = sorted((k, v.processed_count) for k, v in oc.ipfix_templates.items())
+    table = torch.full((8, 2), -1, dtype=torch.int64, device="cuda:0")
+    assert codec.template_counts_device(10, table.data_ptr(), 8) == 3
+    torch.cuda.synchronize()
+    got = table.cpu().tolist()
+    assert [tuple(r) for r in got[:3]] == exp and got[3:] == [[0, 0]] * 5
+    small = torch.zeros((2, 2), dtype=torch.int64, device="cuda:0")
+    assert codec.template_counts_device(10, small.data_ptr(), 2, reset=True) == 3  # > cap: re-agree the size
+    torch.cuda.synchronize()
+    assert [tuple(r) for r in small.cpu().tolist()] == exp[:2]
+    assert codec.template_counts(10) == {k: 0 for k, _ in exp}  # reset
+    assert codec.template_counts_device(9, table.data_ptr(), 8) == 0
+    torch.cuda.synchronize()
+    assert table.abs().sum().item() == 0
