@@ -274,8 +274,9 @@ int ngz_template_counts(ngz_ctx *ctx, int proto, uint16_t *ids, uint64_t *counts
  * ascending, entries [n, cap) zeroed.  One host-to-device copy queued on
  * hip_stream (NULL = the context's stream): an ncclAllGather / ncclAllReduce
  * queued after it on that stream sees the table, with no host synchronisation.
- * reset as ngz_template_counts.  Returns the number of templates n (> cap:
- * only the first cap were written; re-agree the table size and call again). */
+ * reset as ngz_template_counts, but only when all n templates fit (n <= cap).
+ * Returns the number of templates n (> cap: only the first cap were written
+ * and nothing was reset; re-agree the table size and call again). */
 int ngz_template_counts_device(ngz_ctx *ctx, int proto, uint64_t *dev_table, uint32_t cap, int reset,
                                void *hip_stream);
 

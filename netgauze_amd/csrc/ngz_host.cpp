@@ -1504,7 +1504,8 @@ int ngz_template_counts_device(ngz_ctx *ctx, int proto, uint64_t *dev_table, uin
     const int n = ngz_template_counts(ctx, proto, nullptr, nullptr, 0, 0);
     std::vector<uint16_t> ids(std::max(n, 1));
     std::vector<uint64_t> cnt(std::max(n, 1));
-    ngz_template_counts(ctx, proto, ids.data(), cnt.data(), (uint32_t)n, reset);
+    // a table too small resets nothing: the counts carry over to the call that has room for them
+    ngz_template_counts(ctx, proto, ids.data(), cnt.data(), (uint32_t)n, reset && (uint32_t)n <= cap);
     for (uint32_t i = 0; i < cap; ++i) {
         ctx->h_counts_stage[2 * i] = (int)i < n ? ids[i] : 0;
         ctx->h_counts_stage[2 * i + 1] = (int)i < n ? cnt[i] : 0;

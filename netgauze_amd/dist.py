@@ -6,13 +6,29 @@ ranges (each rank = its own set of exporter peers / its own context, as the
 reference's collector actors partition peers, flow_supervisor.rs:288-305).
 No record bytes cross GPUs.  The only collective is the per-template
 processed-count exchange that feeds netgauze.flow.decoder.templates.usage
-(flow_actor.rs:362-381): an all-reduce(max) of the template count, then an
-all-gather of a [max(16, templates) x 3] int64 table (proto, template id,
-count) per rank over RCCL (backend "nccl") or gloo.
+(flow_actor.rs:362-381), done by CountExchange:
+
+  * per step, each rank's counts of both protocols go into one fixed-size
+    device table with ngz_template_counts_device: a single stream-ordered H2D
+    copy per protocol, no per-element writes, no host synchronisation;
+  * one all_gather of that table over RCCL (backend "nccl", xGMI between the
+    GPUs of a node); ~2 KB per rank, latency-bound;
+  * the table size is agreed without an extra collective: row 0 of every
+    protocol block carries the rank's template count, and the next step reads
+    the previous gather's counts (long complete by then) - if any rank had more
+    templates than the table holds, every rank sees it in the same gathered
+    data and grows the table the same way.  A step whose table was too small
+    resets nothing: its counts are carried into the next exchange, which has
+    room for them (totals() reports whether a step fitted).
+
+With the gloo backend (CPU collectives: the CPU tests, or ranks rehearsing the
+multi-rank path on one shared GPU) the table is built on the host from
+ngz_template_counts instead.
 """
 import torch
 
-MAX_TEMPLATES = 16
+PROTOS = (10, 9)
+DEFAULT_CAP = 16
 
 
 def shard_range(n, rank, world):
@@ -20,35 +36,94 @@ def shard_range(n, rank, world):
     return n * rank // world, n * (rank + 1) // world
 
 
-def pack_counts(counts, proto=10, device="cpu", rows=None):
-    """{template_id: count} -> (rows, 3) int64 [proto, id, count]; id -1 = empty.
-    rows defaults to max(MAX_TEMPLATES, len(counts)); a table never drops a template."""
-    rows = max(MAX_TEMPLATES, len(counts)) if rows is None else rows
-    if rows < len(counts):
-        raise ValueError("%d templates do not fit a %d-row count table" % (len(counts), rows))
-    t = torch.full((rows, 3), -1, dtype=torch.int64, device=device)
-    for i, (tid, c) in enumerate(sorted(counts.items())):
-        t[i, 0] = proto
-        t[i, 1] = tid
-        t[i, 2] = c
-    return t
+class CountExchange:
+    """All-gather of every rank's per-template processed counts (both protocols).
+
+    codec: a netgauze_amd.flow.FlowInfoCodec, or any object with
+    template_counts(proto, reset) (the CPU tests use the oracle's counts)."""
+
+    def __init__(self, codec, group=None, cap=DEFAULT_CAP, stream=None):
+        import torch.distributed as dist
+        self.dist = dist
+        self.codec = codec
+        self.group = group
+        self.cap = cap
+        self.stream = stream
+        self.world = dist.get_world_size(group)
+        self.on_device = dist.get_backend(group) == "nccl"
+        self.device = torch.device("cuda", torch.cuda.current_device()) if self.on_device else torch.device("cpu")
+        self.gathered = None
+        self._alloc()
+
+    def _alloc(self):
+        # [proto block][row 0 = (template count, 0); rows 1..cap = (id, count)]
+        self.local = torch.zeros((len(PROTOS), self.cap + 1, 2), dtype=torch.int64, device=self.device)
+        self.out = torch.empty((self.world,) + tuple(self.local.shape), dtype=torch.int64, device=self.device)
+
+    def _fill(self, reset):
+        """Local table of this step; returns the template count per protocol."""
+        ns = []
+        for p, proto in enumerate(PROTOS):
+            if self.on_device:
+                row1 = self.local[p, 1:]
+                n = self.codec.template_counts_device(proto, row1.data_ptr(), self.cap, reset=reset,
+                                                      stream=self.stream)
+            else:
+                counts = sorted(self.codec.template_counts(proto, reset=False).items())
+                n = len(counts)
+                self.local[p, 1:].zero_()
+                if counts:
+                    kept = counts[:self.cap]
+                    self.local[p, 1:1 + len(kept)] = torch.tensor(kept, dtype=torch.int64)
+                if reset and n <= self.cap:
+                    self.codec.template_counts(proto, reset=True)
+            ns.append(n)
+        hdr = torch.tensor([[n, 0] for n in ns], dtype=torch.int64)
+        self.local[:, 0].copy_(hdr.to(self.device, non_blocking=True) if self.on_device else hdr)
+        return ns
+
+    def step(self, reset=True):
+        """Exchange this step's counts (collective: every rank calls it)."""
+        if self.gathered is not None:
+            # the previous gather is complete (its step's decode has returned since):
+            # grow the table if any rank had more templates than it holds
+            need = int(self.gathered[:, :, 0, 0].max().item())
+            if need > self.cap:
+                self.cap = need
+                self._alloc()
+        self._fill(reset)
+        self.dist.all_gather_into_tensor(self.out.view(-1), self.local.view(-1), group=self.group)
+        self.gathered = self.out
+
+    def totals(self):
+        """{(proto, template id): node-wide count} of the last exchange, and
+        whether every rank's templates fitted the table."""
+        g = self.gathered.cpu()
+        fitted = int(g[:, :, 0, 0].max()) <= self.cap
+        total = {}
+        for r in range(g.shape[0]):
+            for p, proto in enumerate(PROTOS):
+                n = min(int(g[r, p, 0, 0]), self.cap)
+                for tid, c in g[r, p, 1:1 + n].tolist():
+                    total[(proto, tid)] = total.get((proto, tid), 0) + c
+        return total, fitted
 
 
 def gather_template_counts(counts, proto=10, group=None, device="cpu"):
-    """All-gather every rank's per-template processed counts.
-
-    Returns {template_id: total} summed over ranks and the per-rank tables."""
+    """One-shot exchange of a {template_id: count} dict (no codec): returns
+    {template_id: total} summed over ranks and the per-rank (rows, 2) tables."""
     import torch.distributed as dist
-    # ranks agree on the table size first (8 bytes), so no rank's templates are dropped
-    n = torch.tensor([len(counts)], dtype=torch.int64, device=device)
-    dist.all_reduce(n, op=dist.ReduceOp.MAX, group=group)
-    local = pack_counts(counts, proto, device, max(MAX_TEMPLATES, int(n.item())))
-    world = dist.get_world_size(group)
-    tables = [torch.empty_like(local) for _ in range(world)]
-    dist.all_gather(tables, local, group=group)
-    total = {}
-    for tab in tables:
-        for row in tab.tolist():
-            if row[1] >= 0 and row[0] == proto:
-                total[row[1]] = total.get(row[1], 0) + row[2]
-    return total, tables
+
+    class _Fixed:
+        def template_counts(self, p, reset=False):
+            return dict(counts) if p == proto else {}
+
+    ex = CountExchange(_Fixed(), group=group)  # every rank starts at the same table size
+    ex.step(reset=False)
+    if not ex.totals()[1]:  # some rank had more templates than this one: agree on the size and redo
+        ex.step(reset=False)
+    total, _ = ex.totals()
+    g = ex.gathered.cpu()
+    p = PROTOS.index(proto)
+    tables = [g[r, p, 1:] for r in range(dist.get_world_size(group))]
+    return {tid: c for (pr, tid), c in total.items() if pr == proto}, tables

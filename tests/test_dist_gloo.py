@@ -106,4 +106,4 @@ def test_count_allgather_more_templates_than_default_table():
     exp[5000] = 9
     for _, total, shapes in res:
         assert total == exp
-        assert shapes == [(20, 3), (20, 3)]
+        assert shapes == [(20, 2), (20, 2)]

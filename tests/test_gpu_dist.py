@@ -1,0 +1,102 @@
+"""The multi-rank product path on the GPU: two processes share the one GPU of
+the test box (gloo carries the collective, as RCCL needs one GPU per rank),
+each decodes its contiguous message shard with libngz on cuda:0, and the
+per-template processed counts of both protocols (NetFlow v9 and IPFIX) are
+exchanged with netgauze_amd.dist.CountExchange.  The node-wide totals must
+equal a single oracle codec's over the whole stream, and every record must be
+decoded exactly once.  (The 8-GPU RCCL run is the driver's; not measured
+here.)"""
+import os
+import socket
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _stream(n):
+    sys.path.insert(0, ROOT)
+    from netgauze_amd import synth
+    dg = synth.cfg4_datagrams(n, seed=synth.SEED_CFG4 + 5)
+    t20 = synth.t20_records(3 * n, seed=synth.SEED_CFG2 + 5)
+    buf, offs, lens = synth.ipfix_data_stream(t20, 64, rec_per_msg=97)
+    b = bytes(buf.numpy())
+    data = dg[2:] + [b[o:o + ln] for o, ln in zip(offs.tolist(), lens.tolist())]
+    return dg[:2] + [synth.template_message()], data
+
+
+def _worker(rank, world, port, n, q):
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        from netgauze_amd import dist as ndist
+        from netgauze_amd.flow import FlowInfoCodec
+        templates, data = _stream(n)
+        first, last = ndist.shard_range(len(data), rank, world)
+        codec = FlowInfoCodec(0)
+        codec.decode_datagrams(templates)
+        batch = codec.decode_datagrams(data[first:last])
+        ok = int((batch.dgram_headers()["status"] == 0).sum())
+        ex = ndist.CountExchange(codec)
+        ex.step(reset=True)
+        total, fitted = ex.totals()
+        q.put((rank, int(batch.n_records), ok, last - first, total, fitted, codec.template_counts(10),
+               codec.template_counts(9)))
+    except Exception as e:  # surface the failure instead of hanging the parent
+        q.put((rank, "error", repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_ranks_decode_shards_and_exchange_counts():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import parity
+    n = 3000
+    templates, data = _stream(n)
+    oracle, oc = parity.oracle_datagrams(templates + data)
+    exp = {(10, t): v.processed_count for t, v in oc.ipfix_templates.items()}
+    exp.update({(9, t): v.processed_count for t, v in oc.netflow_templates.items()})
+    exp_records = sum(1 for kind, m in oracle if kind == "ok" for _ in m.data_records())
+    world = 2
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=240) for _ in range(world)), key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    assert all(r[1] != "error" for r in res), res
+    assert all(p.exitcode == 0 for p in procs)
+    assert sum(r[3] for r in res) == len(data)              # every message in exactly one shard
+    assert sum(r[1] for r in res) == exp_records            # every record decoded exactly once
+    assert sum(r[2] for r in res) == len(data)              # every data message Ok
+    for r in res:
+        total, fitted = r[4], r[5]
+        assert fitted and total == exp, (total, exp)        # node-wide templates.usage, protocols 10 and 9
+        assert r[6] == {t: 0 for t in oc.ipfix_templates}   # reset after the exchange
+        assert r[7] == {t: 0 for t in oc.netflow_templates}
+    assert {k[0] for k in exp} == {9, 10}

@@ -610,6 +610,8 @@ def test_template_counts_device(dev):
     assert codec.template_counts_device(10, small.data_ptr(), 2, reset=True) == 3  # > cap: re-agree the size
     torch.cuda.synchronize()
     assert [tuple(r) for r in small.cpu().tolist()] == exp[:2]
+    assert codec.template_counts(10) == dict(exp)  # too small a table resets nothing
+    assert codec.template_counts_device(10, table.data_ptr(), 8, reset=True) == 3
     assert codec.template_counts(10) == {k: 0 for k, _ in exp}  # reset
     assert codec.template_counts_device(9, table.data_ptr(), 8) == 0
     torch.cuda.synchronize()
