@@ -53,18 +53,22 @@ def cpu_baseline(seconds_budget=12.0, sample_records=4_000_000):
                       % (reps, sample_records, int(offs.numel()), threads, dt)}
 
 
-def committed_traffic(records):
-    """Per-launch HBM bytes of the decode kernel from the newest committed
-    rocprofv3 PMC profile of this same workload (profiles/*/traffic.json,
-    written by tools/summarize_profile.py), or None."""
+def committed_traffic(records, workload):
+    """Per-launch HBM bytes of the decode kernel from a committed rocprofv3 PMC
+    profile of this same workload (profiles/*/traffic.json, written by
+    tools/summarize_profile.py) taken of THIS source tree (its source hash,
+    netgauze_amd/buildinfo.py), or None: a profile of an older build is never
+    reported as this build's traffic."""
     import glob
+    from netgauze_amd import buildinfo
+    want = buildinfo.source_hash()
     best = None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "traffic.json"))):
         try:
             t = json.load(open(f))
         except (OSError, ValueError):
             continue
-        if t.get("records") == records:
+        if t.get("records") == records and t.get("workload") == workload and t.get("source_hash") == want:
             best = (t["traffic_bytes"], os.path.relpath(f, ROOT))
     return best
 
@@ -188,7 +192,14 @@ def main():
     value = total_records / elapsed
     dec_avg = sum(dec_ms) / len(dec_ms)
     achieved = alg_bytes / (dec_avg * 1e-3) / 1e9
-    traffic = committed_traffic(n) if args.workload == "t20" else None
+    workload_desc = {"t20": "T20 x %d records/GPU, 1023 records per 65,492-byte IPFIX message" % n,
+                     "mixed8": "config 3: %d records/GPU over templates %s, interleaved messages"
+                     % (n, ",".join(str(t) for t, _ in synth.CFG3_TEMPLATES)),
+                     "cfg5": "config 5: %d records/GPU (10^9 at 8 GPUs) over 16 templates %s"
+                     % (n, ",".join(str(t) for t, _ in synth.CFG5_TEMPLATES)),
+                     "cfg4": "config 4: %d records/GPU, NFv9 template 313 (130 B, 10/packet) + IPFIX "
+                             "template 900 (vlen strings/octets, VMware/Huawei IEs)" % n}[args.workload]
+    traffic = committed_traffic(n, workload_desc)
     out = {
         "metric": {"t20": "IPFIX flow records/sec + GB/s (device-resident), 20-field fixed template",
                    "mixed8": "IPFIX flow records/sec (device-resident), config 3: 8 templates",
@@ -207,13 +218,7 @@ def main():
         "dtype": "u8",
         "data": "synthetic (splitmix64 records, seed 0x4E475A450000000%d+rank)"
                 % {"t20": 2, "mixed8": 3, "cfg4": 4, "cfg5": 5}[args.workload],
-        "config": {"workload": {"t20": "T20 x %d records/GPU, 1023 records per 65,492-byte IPFIX message" % n,
-                                "mixed8": "config 3: %d records/GPU over templates %s, interleaved messages"
-                                % (n, ",".join(str(t) for t, _ in synth.CFG3_TEMPLATES)),
-                                "cfg5": "config 5: %d records/GPU (10^9 at 8 GPUs) over 16 templates %s"
-                                % (n, ",".join(str(t) for t, _ in synth.CFG5_TEMPLATES)),
-                                "cfg4": "config 4: %d records/GPU, NFv9 template 313 (130 B, 10/packet) + IPFIX "
-                                        "template 900 (vlen strings/octets, VMware/Huawei IEs)" % n}[args.workload],
+        "config": {"workload": workload_desc,
                    "records_per_gpu": n, "messages_per_gpu": int(offs.numel()),
                    "parallelism": "shard-per-gpu" if world > 1 else "single"},
         "gbps_step": alg_bytes * world * args.steps / elapsed / 1e9,
