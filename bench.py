@@ -25,32 +25,69 @@ BYTES_PER_RECORD_OUT = 63  # T20 canonical columns
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
-def cpu_baseline(seconds_budget=12.0, sample_records=4_000_000):
+def cpu_threads():
+    """Threads for the CPU baseline: the CPUs this process may run on
+    (sched_getaffinity), capped by OMP_NUM_THREADS when set (the GPU box sets
+    it to the box's CPU share, 16 per GPU, while nproc shows the whole
+    machine)."""
+    affinity = len(os.sched_getaffinity(0))
+    cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return (min(affinity, cap) if cap > 0 else affinity), affinity
+
+
+def cpu_sample(workload, n):
+    """Host sample of the workload's stream: (template messages, bytes, offsets, lengths, description)."""
+    import numpy as np
+    from netgauze_amd import synth
+    if workload == "t20":
+        rec = synth.t20_records(n, seed=synth.SEED_CFG2)
+        buf, offs, lens = synth.ipfix_data_stream(rec, 64)
+        return [synth.template_message()], buf.numpy(), offs.numpy(), lens.numpy(), "T20"
+    if workload in ("mixed8", "cfg5"):
+        tpls = synth.CFG3_TEMPLATES if workload == "mixed8" else synth.CFG5_TEMPLATES
+        seed = synth.SEED_CFG3 if workload == "mixed8" else synth.SEED_CFG5
+        buf, offs, lens, _ = synth.mixed_stream(n, templates=tpls, seed=seed)
+        return [synth.templates_message(tpls)], buf.numpy(), offs.numpy(), lens.numpy(), \
+            "%d templates, interleaved" % len(tpls)
+    dg = synth.cfg4_datagrams(n, seed=synth.SEED_CFG4)
+    lens = np.array([len(d) for d in dg[2:]], dtype=np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens[:-1], dtype=np.uint64)]).astype(np.uint64)
+    return dg[:2], np.frombuffer(b"".join(dg[2:]), dtype=np.uint8), offs, lens, "NFv9 313 + IPFIX vlen 900, MTU packets"
+
+
+def cpu_baseline(workload="t20", seconds_budget=10.0, single_budget=4.0):
     """The reference algorithm's restatement (oracle/cpu/ngz_cpu.c: record at
-    a time, one heap-allocated field array per record, per-field dispatch)
-    timed on this host's cores, one independent codec per thread over a
-    contiguous message range.  Bounded sample, repeated for ~seconds_budget."""
+    a time, one heap-allocated field array per record, per-field dispatch;
+    IPFIX and NetFlow v9) timed on this host's cores, one independent codec per
+    thread over a contiguous message range (one exporter peer per thread), plus
+    the same on one core.  A bounded sample of the workload, repeated for about
+    seconds_budget (all cores) + single_budget (one core)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import cpu_port
-    from netgauze_amd import synth
-    threads = max(1, min(16, os.cpu_count() or 1))
-    rec = synth.t20_records(sample_records, seed=synth.SEED_CFG2)
-    buf, offs, lens = synth.ipfix_data_stream(rec, 64)
-    b, o, ln = buf.numpy(), offs.numpy(), lens.numpy()
-    tm = synth.template_message()
-    n = 0
-    reps = 0
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < seconds_budget:
-        got, _, err = cpu_port.decode(b, o, ln, tm, threads=threads)
-        assert err == 0 and got == sample_records
-        n += got
-        reps += 1
-    dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "records/s", "cores": threads, "kind": "port",
-            "sample": "%d x %d T20 records (%d messages of 1023) through oracle/cpu/ngz_cpu.c, a C restatement "
-                      "of the reference decode (Rust reference not buildable here), %d threads, %.1f s"
-                      % (reps, sample_records, int(offs.numel()), threads, dt)}
+    threads, affinity = cpu_threads()
+    sample = {"t20": 4_000_000, "mixed8": 2_000_000, "cfg5": 2_000_000, "cfg4": 1_000_000}[workload]
+    tm, b, o, ln, desc = cpu_sample(workload, sample)
+    sb, so, sl, n_pre = cpu_port.stream(tm, b, o, ln)
+
+    def timed(th, budget):
+        n = reps = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < budget:
+            got, _, err = cpu_port.decode_stream(sb, so, sl, n_pre, threads=th)
+            assert err == 0 and got == sample, (got, err)
+            n += got
+            reps += 1
+        dt = time.perf_counter() - t0
+        return n / dt, reps, dt
+
+    v, reps, dt = timed(threads, seconds_budget)
+    v1, reps1, dt1 = timed(1, single_budget)
+    return {"value": v, "unit": "records/s", "cores": threads, "kind": "port",
+            "single_core": v1, "nproc": os.cpu_count(), "affinity": affinity,
+            "sample": "%d x %d records (%s; %d messages) through oracle/cpu/ngz_cpu.c, a C restatement of the "
+                      "reference decode (Rust reference not buildable here): %d threads (CPUs in this process's "
+                      "affinity: %d, capped by OMP_NUM_THREADS; nproc %d) for %.1f s, then 1 thread %d x for %.1f s"
+                      % (reps, sample, desc, len(o), threads, affinity, os.cpu_count(), dt, reps1, dt1)}
 
 
 def committed_traffic(records, workload):
@@ -230,8 +267,8 @@ def main():
                      "alg_bytes_per_launch": alg_bytes,
                      "read_gbps": read_bytes / (dec_avg * 1e-3) / 1e9},
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.workload == "t20":
-        out["cpu_baseline"] = cpu_baseline()
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.workload)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

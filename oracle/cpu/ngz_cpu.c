@@ -14,6 +14,10 @@
  *                            the IE (the generated match, generator.rs:2959-2978)
  *   Field::parse rules       generator.rs:1439-1807 (reduced-size ints, bytes,
  *                            vlen prefixes, tcpControlBits truncation)
+ *   NetFlowV9Packet::parse   netflow.rs:56-114 (count-driven set loop, InvalidCount),
+ *                            Set::parse :143-235 (exact record length, per-record
+ *                            processed_count, zero padding), templates :265-353,
+ *                            ScopeField :443-475
  * Records are freed when their message is dropped, as the Rust packet is.
  * Pinned: tests/test_cpu_port.py checks its per-field sums against the Python
  * oracle (itself pinned byte-exact to the reference's golden JSON).
@@ -46,7 +50,7 @@ typedef struct {
     union { uint64_t u; int64_t i; uint8_t *bytes; uint8_t small[16]; } v;
 } Field;
 
-typedef struct { int16_t ie; uint16_t len; } Spec;
+typedef struct { int16_t ie; uint16_t len; uint8_t scope; } Spec;  /* scope: NFv9 ScopeIE code (1..5), 0 = IE */
 typedef struct { int n; Spec *specs; int minlen; uint64_t processed; } Template;
 
 static int ie_lookup(uint32_t pen, uint16_t id) {
@@ -82,6 +86,20 @@ static inline uint64_t be(const uint8_t *p, int n) {
 static int parse_field(const uint8_t *p, int rem, const Spec *s, Field *f) {
     int len = s->len;
     f->ie = (uint16_t)s->ie;
+    if (s->scope) {  /* NFv9 ScopeField (netflow.rs:443-475) */
+        if (len > rem) return -1;
+        if (s->scope <= 3) {  /* System / Interface / LineCard: reduced u32 */
+            if (len > 4) return -1;
+            f->tag = DT_unsigned32;
+            f->v.u = be(p, len);
+            return len;
+        }
+        f->tag = DT_octetArray;  /* Cache / Template / Unknown: raw bytes */
+        f->len = (uint32_t)len;
+        f->v.bytes = (uint8_t *)malloc(len ? len : 1);
+        memcpy(f->v.bytes, p, len);
+        return len;
+    }
     int dt = s->ie >= 0 ? kIes[s->ie].dt : DT_octetArray;
     f->tag = (uint8_t)dt;
     int hdr = 0;
@@ -100,9 +118,10 @@ static int parse_field(const uint8_t *p, int rem, const Spec *s, Field *f) {
         f->v.i = ((int64_t)(u << sh)) >> sh;
         return len;
     }
-    case DT_dtMs:
+    case DT_dtMs:  /* chrono timestamp_millis_opt range (0.4.45) */
         if (len != 8 || rem < 8) return -1;
         f->v.u = be(p, 8);
+        if ((int64_t)f->v.u < -8334601315200000LL || (int64_t)f->v.u > 8210266876799999LL) return -1;
         return 8;
     case DT_dtUs: case DT_dtNs: {
         if (len != 8 || rem < 8) return -1;
@@ -148,83 +167,178 @@ typedef struct {
     const uint64_t *offs;
     const uint32_t *lens;
     uint32_t first, last;
-    const uint8_t *tmpl;  /* template message prepended to every thread's stream */
-    uint32_t tmpl_len;
+    uint32_t n_pre;  /* messages [0, n_pre) (the exporter's templates) are decoded by every thread first */
     uint64_t records, errors;
     uint64_t *sums;  /* per field index, wrapping sum of canonical u64 values */
     int nsums;
 } Job;
 
 typedef struct { Field *fields; int n; } Record;
+typedef struct { Record *recs; size_t n, cap; } Records;
 
-static void decode_message(const uint8_t *p, uint32_t dl, Template **tmap, Job *job) {
-    if (dl < 16) return;
-    uint32_t ver = (uint32_t)be(p, 2), len = (uint32_t)be(p + 2, 2);
-    if (dl < len || ver != 10 || len < 16) { job->errors++; return; }
-    /* the parsed packet owns its records until it is dropped */
-    Record *recs = NULL;
-    size_t nrec = 0, cap = 0;
-    uint32_t pos = 16;
+static void push_record(Records *rs, Record r) {
+    if (rs->n == rs->cap) { rs->cap = rs->cap ? rs->cap * 2 : 64; rs->recs = (Record *)realloc(rs->recs, rs->cap * sizeof(Record)); }
+    rs->recs[rs->n++] = r;
+}
+
+static void put_template(Template **tmap, uint32_t tid, Template *t) {
+    if (tmap[tid]) { free(tmap[tid]->specs); free(tmap[tid]); }
+    tmap[tid] = t;
+}
+
+/* FieldSpecifier::parse (deserializer/mod.rs:53-66); 0 = ok */
+static int parse_spec(const uint8_t *b, uint32_t bl, uint32_t *q, Spec *sp) {
+    if (bl - *q < 4) return -1;
+    uint32_t code = (uint32_t)be(b + *q, 2), fl = (uint32_t)be(b + *q + 2, 2);
+    *q += 4;
+    uint32_t pen = 0;
+    if (code & 0x8000) { if (bl - *q < 4) return -1; pen = (uint32_t)be(b + *q, 4); *q += 4; code &= 0x7FFF; }
+    int ie = ie_lookup(pen, (uint16_t)code);
+    if (ie == -1) return -1;  /* UndefinedIANAIE */
+    sp->ie = (int16_t)(ie < 0 ? -1 : ie);
+    sp->len = (uint16_t)fl;
+    sp->scope = 0;
+    return 0;
+}
+
+/* DataRecord::parse of one record at b[*q..bl) (ipfix.rs:335-370 / netflow.rs:399-432) */
+static int parse_record(const uint8_t *b, uint32_t bl, uint32_t *q, const Template *t, Records *rs) {
+    Record r;
+    r.n = t->n;
+    r.fields = (Field *)malloc(sizeof(Field) * (t->n ? t->n : 1));  /* Box<[Field]> */
     int ok = 1;
-    while (pos < len && ok) {
-        if (len - pos < 4) { ok = 0; break; }
+    for (int i = 0; i < t->n; ++i) {
+        int c = parse_field(b + *q, (int)(bl - *q), &t->specs[i], &r.fields[i]);
+        if (c < 0) { ok = 0; r.n = i; break; }
+        *q += (uint32_t)c;
+    }
+    push_record(rs, r);
+    return ok;
+}
+
+static int ipfix_message(const uint8_t *p, uint32_t len, Template **tmap, Records *rs) {
+    uint32_t pos = 16;
+    while (pos < len) {
+        if (len - pos < 4) return 0;
         uint32_t id = (uint32_t)be(p + pos, 2), sl = (uint32_t)be(p + pos + 2, 2);
-        if ((id != 2 && id != 3 && id < 256) || sl < 4 || sl > len - pos) { ok = 0; break; }
+        if ((id != 2 && id != 3 && id < 256) || sl < 4 || sl > len - pos) return 0;
         const uint8_t *b = p + pos + 4;
-        uint32_t bl = sl - 4;
-        if (id == 2) {
-            uint32_t q = 0;
-            while (q < bl) {
-                if (bl - q < 4) { ok = 0; break; }
-                uint32_t tid = (uint32_t)be(b + q, 2), cnt = (uint32_t)be(b + q + 2, 2);
+        uint32_t bl = sl - 4, q = 0;
+        if (id == 2 || id == 3) {  /* (options) template sets, ipfix.rs:162-181,276-327,384-413 */
+            while (id == 2 ? q < bl : bl - q > 3) {
+                if (bl - q < 4) return 0;
+                uint32_t tid = (uint32_t)be(b + q, 2), total = (uint32_t)be(b + q + 2, 2), scount = 0;
                 q += 4;
+                if (tid < 256) return 0;
+                if (id == 3) { if (bl - q < 2) return 0; scount = (uint32_t)be(b + q, 2); q += 2; if (scount > total) return 0; }
                 Template *t = (Template *)calloc(1, sizeof(Template));
-                t->specs = (Spec *)calloc(cnt ? cnt : 1, sizeof(Spec));
-                t->n = (int)cnt;
-                for (uint32_t i = 0; i < cnt; ++i) {
-                    if (bl - q < 4) { ok = 0; break; }
-                    uint32_t code = (uint32_t)be(b + q, 2), fl = (uint32_t)be(b + q + 2, 2);
-                    q += 4;
-                    uint32_t pen = 0;
-                    if (code & 0x8000) { pen = (uint32_t)be(b + q, 4); q += 4; code &= 0x7FFF; }
-                    int ie = ie_lookup(pen, (uint16_t)code);
-                    if (ie == -1) { ok = 0; break; }
-                    t->specs[i].ie = (int16_t)(ie < 0 ? -1 : ie);
-                    t->specs[i].len = (uint16_t)fl;
-                    t->minlen += fl == 0xFFFF ? 1 : (int)fl;
+                t->specs = (Spec *)calloc(total ? total : 1, sizeof(Spec));
+                t->n = (int)total;
+                for (uint32_t i = 0; i < total; ++i) {
+                    if (parse_spec(b, bl, &q, &t->specs[i])) { free(t->specs); free(t); return 0; }
+                    t->minlen += t->specs[i].len == 0xFFFF ? 1 : (int)t->specs[i].len;
                 }
-                if (!ok) { free(t->specs); free(t); break; }
-                if (tmap[tid]) { free(tmap[tid]->specs); free(tmap[tid]); }
-                tmap[tid] = t;
+                put_template(tmap, tid, t);
             }
-        } else if (id == 3) {
-            /* options templates are not part of the baseline workload */
+            for (; id == 3 && q < bl; ++q) if (b[q]) return 0;  /* options padding must be zero */
         } else {
             Template *t = tmap[id];
-            if (!t) { ok = 0; break; }
-            uint32_t q = 0;
-            while (t->minlen > 0 && bl - q >= (uint32_t)t->minlen) {
-                Record r;
-                r.n = t->n;
-                r.fields = (Field *)malloc(sizeof(Field) * (t->n ? t->n : 1));  /* Box<[Field]> */
-                for (int i = 0; i < t->n; ++i) {
-                    int c = parse_field(b + q, (int)(bl - q), &t->specs[i], &r.fields[i]);
-                    if (c < 0) { ok = 0; r.n = i; break; }
-                    q += (uint32_t)c;
-                }
-                if (nrec == cap) { cap = cap ? cap * 2 : 64; recs = (Record *)realloc(recs, cap * sizeof(Record)); }
-                recs[nrec++] = r;
-                if (!ok) break;
-            }
-            t->processed++;
+            if (!t) return 0;
+            while (t->minlen > 0 && bl - q >= (uint32_t)t->minlen)  /* ipfix.rs:219-222 */
+                if (!parse_record(b, bl, &q, t, rs)) return 0;
+            t->processed++;  /* once per set (ipfix.rs:223) */
         }
         pos += sl;
     }
+    return 1;
+}
+
+static int nfv9_message(const uint8_t *p, uint32_t dl, Template **tmap, Records *rs) {
+    if (dl < 20) return 0;
+    uint32_t count = (uint32_t)be(p + 2, 2), i = count, pos = 20;
+    while (i > 0 && dl - pos > 3) {  /* netflow.rs:89 */
+        uint32_t id = (uint32_t)be(p + pos, 2), sl = (uint32_t)be(p + pos + 2, 2);
+        if ((id != 0 && id != 1 && id < 256) || sl < 4 || sl > dl - pos) return 0;
+        const uint8_t *b = p + pos + 4;
+        uint32_t bl = sl - 4, q = 0;
+        if (id == 0) {  /* template set, netflow.rs:324-353 */
+            while (q < bl) {
+                if (bl - q < 4) return 0;
+                uint32_t tid = (uint32_t)be(b + q, 2), cnt = (uint32_t)be(b + q + 2, 2);
+                q += 4;
+                if (tid < 256) return 0;
+                Template *t = (Template *)calloc(1, sizeof(Template));
+                t->specs = (Spec *)calloc(cnt ? cnt : 1, sizeof(Spec));
+                t->n = (int)cnt;
+                for (uint32_t k = 0; k < cnt; ++k) {
+                    if (parse_spec(b, bl, &q, &t->specs[k])) { free(t->specs); free(t); return 0; }
+                    t->minlen += (int)t->specs[k].len;  /* exact record length, 65535 literal */
+                }
+                put_template(tmap, tid, t);
+            }
+            i -= 1;
+        } else if (id == 1) {  /* options template set, netflow.rs:265-310 */
+            while (bl - q > 3) {
+                if (bl - q < 6) return 0;
+                uint32_t tid = (uint32_t)be(b + q, 2), slen = (uint32_t)be(b + q + 2, 2), olen = (uint32_t)be(b + q + 4, 2);
+                q += 6;
+                if (tid < 256 || slen > bl - q || olen > bl - q - slen) return 0;
+                uint32_t n = slen / 4 + olen / 4;
+                Template *t = (Template *)calloc(1, sizeof(Template));
+                t->specs = (Spec *)calloc(n ? n : 1, sizeof(Spec));
+                uint32_t se = q + slen, oe = se + olen;
+                while (q < se) {  /* ScopeFieldSpecifier (netflow.rs:368-388) */
+                    if (se - q < 4) { free(t->specs); free(t); return 0; }
+                    uint32_t code = (uint32_t)be(b + q, 2), fl = (uint32_t)be(b + q + 2, 2);
+                    q += 4;
+                    if (code & 0x8000) { q += 4; code = 0; }  /* enterprise scope: raw bytes */
+                    Spec *sp = &t->specs[t->n++];
+                    sp->ie = -1; sp->len = (uint16_t)fl; sp->scope = (uint8_t)(code >= 1 && code <= 5 ? code : 4);
+                    t->minlen += (int)fl;
+                }
+                while (q < oe) {
+                    if (parse_spec(b, oe, &q, &t->specs[t->n])) { free(t->specs); free(t); return 0; }
+                    t->minlen += (int)t->specs[t->n++].len;
+                }
+                put_template(tmap, tid, t);
+            }
+            for (; q < bl; ++q) if (b[q]) return 0;
+            i -= 1;
+        } else {
+            Template *t = tmap[id];
+            if (!t) return 0;
+            uint32_t nrec = 0;
+            if (t->minlen)
+                while (bl - q >= (uint32_t)t->minlen) {
+                    if (!parse_record(b, bl, &q, t, rs)) return 0;
+                    t->processed++;  /* per record (netflow.rs:218) */
+                    ++nrec;
+                }
+            for (; q < bl; ++q) if (b[q]) return 0;  /* check_padding_value */
+            if (nrec > i) return 0;                   /* InvalidCount */
+            i -= nrec;
+        }
+        pos += sl;
+    }
+    return 1;
+}
+
+static void decode_message(const uint8_t *p, uint32_t dl, Template **tmap, Job *job) {
+    /* FlowInfoCodec::decode gate and dispatch (codec.rs:189-220) */
+    if (dl < 16) return;
+    uint32_t ver = (uint32_t)be(p, 2), len = (uint32_t)be(p + 2, 2);
+    if (dl < len) return;
+    /* the parsed packet owns its records until it is dropped */
+    Records rs = {NULL, 0, 0};
+    int ok;
+    if (ver == 10) ok = len >= 16 && ipfix_message(p, len, tmap + 0, &rs);
+    else if (ver == 9) ok = nfv9_message(p, dl, tmap + 65536, &rs);
+    else ok = 0;
     if (ok) {
-        job->records += nrec;
-        for (size_t k = 0; k < nrec; ++k)
-            for (int i = 0; i < recs[k].n && i < job->nsums; ++i) {
-                const Field *f = &recs[k].fields[i];
+        job->records += rs.n;
+        for (size_t k = 0; k < rs.n; ++k)
+            for (int i = 0; i < rs.recs[k].n && i < job->nsums; ++i) {
+                const Field *f = &rs.recs[k].fields[i];
                 uint64_t v = 0;
                 if (f->tag == DT_octetArray || f->tag == DT_string || f->tag >= DT_basicList ||
                     f->tag == DT_macAddress || f->tag == DT_ipv6) {
@@ -238,40 +352,46 @@ static void decode_message(const uint8_t *p, uint32_t dl, Template **tmap, Job *
     } else {
         job->errors++;
     }
-    for (size_t k = 0; k < nrec; ++k) {
-        for (int i = 0; i < recs[k].n; ++i) free_field(&recs[k].fields[i]);
-        free(recs[k].fields);
+    for (size_t k = 0; k < rs.n; ++k) {
+        for (int i = 0; i < rs.recs[k].n; ++i) free_field(&rs.recs[k].fields[i]);
+        free(rs.recs[k].fields);
     }
-    free(recs);
+    free(rs.recs);
 }
 
 static void *run(void *arg) {
     Job *job = (Job *)arg;
-    Template **tmap = (Template **)calloc(65536, sizeof(Template *));  /* per-peer TemplatesMap */
-    if (job->tmpl) decode_message(job->tmpl, job->tmpl_len, tmap, job);
+    /* per-peer codec: the IPFIX TemplatesMap [0, 65536) and the NFv9 one [65536, 131072) */
+    Template **tmap = (Template **)calloc(2 * 65536, sizeof(Template *));
+    for (uint32_t i = 0; i < job->n_pre; ++i) decode_message(job->bytes + job->offs[i], job->lens[i], tmap, job);
+    job->records = 0;
+    job->errors = 0;
+    for (int i = 0; i < job->nsums; ++i) job->sums[i] = 0;
     for (uint32_t i = job->first; i < job->last; ++i)
         decode_message(job->bytes + job->offs[i], job->lens[i], tmap, job);
-    for (int i = 0; i < 65536; ++i)
+    for (int i = 0; i < 2 * 65536; ++i)
         if (tmap[i]) { free(tmap[i]->specs); free(tmap[i]); }
     free(tmap);
     return NULL;
 }
 
-/* Decode messages [0, n) on `threads` threads, each an independent codec over
- * a contiguous message range (one exporter peer per thread, as collector
- * actors partition peers).  Returns records decoded; sums[nsums] (optional)
- * receive per-field wrapping sums of the canonical values. */
+/* Decode messages [n_pre, n) on `threads` threads, each an independent codec
+ * (one exporter peer per thread, as collector actors partition peers) over a
+ * contiguous message range, after decoding the template messages [0, n_pre)
+ * itself.  Returns records decoded; sums[nsums] (optional) receive per-field
+ * wrapping sums of the canonical values; *errors the failed messages. */
 uint64_t ngz_cpu_decode(const uint8_t *bytes, const uint64_t *offs, const uint32_t *lens, uint32_t n,
-                        const uint8_t *tmpl, uint32_t tmpl_len, int threads, uint64_t *sums, int nsums,
-                        uint64_t *errors) {
+                        uint32_t n_pre, int threads, uint64_t *sums, int nsums, uint64_t *errors) {
     if (threads < 1) threads = 1;
+    if (n_pre > n) n_pre = n;
     pthread_t *th = (pthread_t *)calloc((size_t)threads, sizeof(pthread_t));
     Job *jobs = (Job *)calloc((size_t)threads, sizeof(Job));
+    const uint32_t m = n - n_pre;
     for (int t = 0; t < threads; ++t) {
         jobs[t].bytes = bytes; jobs[t].offs = offs; jobs[t].lens = lens;
-        jobs[t].first = (uint32_t)((uint64_t)n * t / threads);
-        jobs[t].last = (uint32_t)((uint64_t)n * (t + 1) / threads);
-        jobs[t].tmpl = tmpl; jobs[t].tmpl_len = tmpl_len;
+        jobs[t].first = n_pre + (uint32_t)((uint64_t)m * t / threads);
+        jobs[t].last = n_pre + (uint32_t)((uint64_t)m * (t + 1) / threads);
+        jobs[t].n_pre = n_pre;
         jobs[t].nsums = nsums;
         jobs[t].sums = (uint64_t *)calloc(nsums > 0 ? (size_t)nsums : 1, 8);
         pthread_create(&th[t], NULL, run, &jobs[t]);
