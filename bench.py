@@ -159,7 +159,7 @@ def main():
 
     dev = torch.device("cuda", local)
     cdev = dev if dist is None or dist.get_backend() == "nccl" else torch.device("cpu")  # collective tensors
-    codec = FlowInfoCodec(local)
+    codec = FlowInfoCodec(local, rtc_sync=True)  # template kernels compiled when the template is learnt
     n = args.records
     if args.workload == "t20":
         codec.decode_datagrams([synth.template_message()])  # exporter's template, learnt before timing
@@ -285,7 +285,7 @@ def main_agg(args):
     from netgauze_amd.flow import FlowInfoCodec
     n = args.records or 100_000_000
     dev = torch.device("cuda", 0)
-    codec = FlowInfoCodec(0)
+    codec = FlowInfoCodec(0, rtc_sync=True)
     codec.decode_datagrams([synth.template_message()])
     rec = synth.t20_records(n, device=dev)
     buf, offs, lens = synth.ipfix_data_stream(rec, 64)
@@ -370,7 +370,7 @@ def main_e2e(args):
         return (time.perf_counter() - t0) / args.steps, moved
 
     # serial: one context, the whole batch per step
-    codec = FlowInfoCodec(0)
+    codec = FlowInfoCodec(0, rtc_sync=True)
     codec.decode_datagrams([tm])
     out = torch.empty(n * BYTES_PER_RECORD_OUT + (4 << 20), dtype=torch.uint8, pin_memory=True)
 
@@ -396,7 +396,7 @@ def main_e2e(args):
         ranges.append((hb.data_ptr() + b0, b1 - b0, o, hl[m0:m1].clone().pin_memory(), m1 - m0))
     codecs = []
     for _ in range(P):
-        c = FlowInfoCodec(0)
+        c = FlowInfoCodec(0, rtc_sync=True)
         c.decode_datagrams([tm])
         codecs.append(c)
     per_out = (n // K + 1024) * BYTES_PER_RECORD_OUT + (4 << 20)

@@ -158,6 +158,10 @@ const char *ngz_last_error(ngz_ctx *ctx);
 #define NGZ_OPT_CAP_PAD 4       /* extra row windows of column capacity per template slot (column spacing) */
 #define NGZ_OPT_ARENA_SHIFT 3   /* bytes (multiple of 256) the column blocks start into the context's
                                    device arena: moves the output onto other HBM pages */
+#define NGZ_OPT_RTC_SYNC 5      /* 0 (default): a template's kernel compiles on a background thread and the
+                                   generic kernel decodes its records until it is ready (a new template on
+                                   one peer never stalls a batch); 1: the first batch after a template
+                                   definition waits for its compile (deterministic kernel choice) */
 int ngz_ctx_set_option(ngz_ctx *ctx, int opt, int64_t value);
 
 /* --- decode ------------------------------------------------------------- */
@@ -171,6 +175,10 @@ int ngz_decode_batch(ngz_ctx *ctx, const ngz_batch_in *in, ngz_batch_out *out, v
 int ngz_decode_batch_host(ngz_ctx *ctx, const uint8_t *bytes, uint64_t bytes_size,
                           const uint64_t *offsets, const uint32_t *lengths, uint32_t n,
                           ngz_batch_out *out);
+
+/* Which kernel decoded a slot of the last batch: 1 its specialised kernel,
+ * 0 the generic kernel, 2 the generic kernel while its own compiles. */
+int ngz_slot_kernel(ngz_ctx *ctx, uint32_t slot);
 
 /* Column layout of a batch slot (valid with the last batch). */
 int ngz_slot_fields(ngz_ctx *ctx, uint32_t slot, ngz_field_info *fields, uint32_t cap);

@@ -21,7 +21,7 @@ ABI_FUNCTIONS = [
     "ngz_decode_batch_host", "ngz_slot_fields", "ngz_dgram_error_json",
     "ngz_templates_json", "ngz_template_counts", "ngz_last_timing", "ngz_ctx_set_option",
     "ngz_template_kernel", "ngz_columns_to_host", "ngz_dgram_json", "ngz_batch_json",
-    "ngz_dgram_error", "ngz_template_counts_device",
+    "ngz_dgram_error", "ngz_template_counts_device", "ngz_slot_kernel",
 ]
 NGZ_ABI_VERSION = 2
 # ngz_error.kind / .layer (flow_decode.h)
@@ -155,6 +155,8 @@ def load():
     lib.ngz_dgram_json.restype = ctypes.c_int64
     lib.ngz_batch_json.argtypes = [P, P, JSON_LINE_FN, P]
     lib.ngz_batch_json.restype = ctypes.c_int64
+    lib.ngz_slot_kernel.argtypes = [P, U32]
+    lib.ngz_slot_kernel.restype = I
     lib.ngz_dgram_error.argtypes = [P, U32, ctypes.POINTER(Error)]
     lib.ngz_dgram_error.restype = I
     lib.ngz_template_counts_device.argtypes = [P, I, P, U32, I, P]

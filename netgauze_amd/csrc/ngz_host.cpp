@@ -36,6 +36,8 @@ extern "C" int ngz_launch_layout_emit(const BatchDev *B, const uint32_t *hf_flag
                                       hipStream_t st);
 extern "C" int ngz_launch_decode_generic(const BatchDev *B, uint32_t grid, hipStream_t st);
 void *ngz_rtc_kernel(int device, const DevPlan &P);
+int ngz_rtc_kernel_async(int device, const DevPlan &P, void **fn, void **entry);
+int ngz_rtc_poll(void *entry, void **fn);
 std::string ngz_rtc_source(const DevPlan &P);
 int ngz_rtc_compile_only(const DevPlan &P, std::string *log_out);
 int ngz_rtc_launch(void *fn, const BatchDev *B, uint32_t slot, uint32_t grid, uint32_t block, hipStream_t st);
@@ -764,13 +766,21 @@ int upload_slots(ngz_ctx *ctx, const std::vector<int32_t> cur_start[2], hipStrea
         if (ctx->specialize && rtc_eligible(v.plan)) {
             // NGZ_OPT_SPECIALIZE 2: compile once the template has seen enough records to pay for it
             const bool want = ctx->specialize == 1 || v.seen_records >= NGZ_SPECIALIZE_MIN_RECORDS;
-            if (v.rtc_state == 0 && want) {
-                v.rtc_fn = ngz_rtc_kernel(ctx->device, v.plan);
-                v.rtc_state = v.rtc_fn ? 1 : 2;
+            if (want && (v.rtc_state == 0 || (v.rtc_state == 3 && ctx->rtc_sync))) {
+                if (ctx->rtc_sync) {  // wait for the compile (NGZ_OPT_RTC_SYNC)
+                    v.rtc_fn = ngz_rtc_kernel(ctx->device, v.plan);
+                    v.rtc_state = v.rtc_fn ? 1 : 2;
+                } else {  // compile in the background; the generic kernel decodes meanwhile
+                    const int r = ngz_rtc_kernel_async(ctx->device, v.plan, &v.rtc_fn, &v.rtc_entry);
+                    v.rtc_state = r == 1 ? 1 : r < 0 ? 2 : 3;
+                }
             }
             plans[s].spec = v.rtc_state == 1;
         }
     }
+    ctx->slot_spec.assign(S, 0);  // the kernel each slot's records go through (ngz_slot_kernel)
+    for (size_t s = 0; s < S; ++s)
+        ctx->slot_spec[s] = plans[s].spec ? 1 : ctx->versions[ctx->slot_version[s]].rtc_state == 3 ? 2 : 0;
     std::vector<uint16_t> cs(2 * 65536, NGZ_NO_SLOT);
     for (int pi = 0; pi < 2; ++pi)
         for (uint32_t id = 0; id < 65536; ++id)
@@ -1239,6 +1249,10 @@ int ngz_ctx_set_option(ngz_ctx *ctx, int opt, int64_t value) {
         if (value < 0 || value > 4096) return fail(ctx, NGZ_E_INVALID, "NGZ_OPT_CAP_PAD takes 0..4096");
         ctx->cap_pad_windows = (uint32_t)value;
         return NGZ_OK;
+    case NGZ_OPT_RTC_SYNC:
+        if (value < 0 || value > 1) return fail(ctx, NGZ_E_INVALID, "NGZ_OPT_RTC_SYNC takes 0 or 1");
+        ctx->rtc_sync = value != 0;
+        return NGZ_OK;
     case NGZ_OPT_BLOCKS_PER_CU:
         if (value < 1 || value > 32) return fail(ctx, NGZ_E_INVALID, "NGZ_OPT_BLOCKS_PER_CU takes 1..32");
         ctx->blocks_per_cu = (uint32_t)value;
@@ -1259,6 +1273,16 @@ int ngz_decode_batch(ngz_ctx *ctx, const ngz_batch_in *in, ngz_batch_out *out, v
     memset(out, 0, sizeof *out);
     int rc = ctx->assigned_gen == ctx->tmpl_gen ? 0 : assign_slots(ctx, {});
     if (rc) return rc;
+    // templates whose kernel was compiling: switch to it once it is ready
+    for (int32_t vid : ctx->slot_version) {
+        Version &v = ctx->versions[vid];
+        if (v.rtc_state != 3 || !v.rtc_entry) continue;
+        const int r = ngz_rtc_poll(v.rtc_entry, &v.rtc_fn);
+        if (r != 0) {
+            v.rtc_state = r > 0 ? 1 : 2;
+            ctx->plans_dirty = true;
+        }
+    }
     if (ctx->plans_dirty || ctx->uploaded_gen != ctx->tmpl_gen) {
         rc = upload_slots(ctx, ctx->cur, st);
         if (rc) return rc;
@@ -1460,6 +1484,11 @@ int ngz_slot_fields(ngz_ctx *ctx, uint32_t slot, ngz_field_info *fields, uint32_
         f.col_off = v.fields[i].col_off;
     }
     return (int)n;
+}
+
+int ngz_slot_kernel(ngz_ctx *ctx, uint32_t slot) {
+    if (!ctx || slot >= ctx->slot_spec.size()) return NGZ_E_INVALID;
+    return ctx->slot_spec[slot];
 }
 
 int ngz_last_timing(ngz_ctx *ctx, float *decode_ms, float *pipeline_ms) {

@@ -78,7 +78,7 @@ struct Version {
     uint64_t seen_records = 0;      // records decoded with this version (NGZ_OPT_SPECIALIZE 2)
     int rtc_state = 0;              // specialised kernel: 0 not looked up, 1 ready, 2 unavailable, 3 compiling
     void *rtc_fn = nullptr;
-    uint64_t rtc_key = 0;           // layout signature key of the (pending) specialised kernel
+    void *rtc_entry = nullptr;      // process-wide kernel cache entry (ngz_rtc.cpp), polled while compiling
 
     Version() = default;
     Version(const Version &o) { *this = o; }
@@ -103,7 +103,7 @@ struct Version {
   private:
     void copy_scalars(const Version &o) {
         proto = o.proto; tid = o.tid; n_scope = o.n_scope; plan = o.plan; processed = o.processed;
-        seen_records = o.seen_records; rtc_state = o.rtc_state; rtc_fn = o.rtc_fn; rtc_key = o.rtc_key;
+        seen_records = o.seen_records; rtc_state = o.rtc_state; rtc_fn = o.rtc_fn; rtc_entry = o.rtc_entry;
     }
 };
 
@@ -243,6 +243,8 @@ struct ngz_ctx {
     hipEvent_t fork_ev = nullptr;
     int n_cus = 256;
     int specialize = 1;                         // NGZ_OPT_SPECIALIZE
+    bool rtc_sync = false;                      // NGZ_OPT_RTC_SYNC: wait for a template's kernel compile
+    std::vector<uint8_t> slot_spec;             // last batch: slot decoded by its specialised kernel
     uint32_t blocks_per_cu = 4;                 // decode grid: 4 x 256 threads per CU
     uint32_t lds_blocks_per_cu = 8;             // LDS-staged decode grid (2 resident per CU at 64 KB)
     // device summary / processed_count increments alternate between two

@@ -13,15 +13,27 @@
 // Kernels are cached process-wide by (device, plan signature): every template
 // with the same layout -- the same template re-announced by an exporter, or
 // the same layout on another exporter peer -- shares one code object.
+//
+// Compiles are off the decode path: ngz_rtc_kernel_async starts generate +
+// hiprtc + module load on a background thread and returns at once; the
+// context decodes that template with the generic kernel until the entry is
+// ready (ngz_rtc_poll).  The cache lock is held only for the map lookup, never
+// across a compile, so a new template on one exporter's context never stalls
+// another context.  Each entry compiles once; concurrent askers wait on it
+// (ngz_rtc_kernel, synchronous) or poll it (async).
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 
+#include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -483,13 +495,42 @@ std::string generate_vlen(const DevPlan &P) {
 }
 
 struct Entry {
+    std::atomic<int> state{0};  // 0 new, 1 compiling, 2 ready, 3 failed
     hipModule_t mod = nullptr;
     hipFunction_t fn = nullptr;
-    bool failed = false;
 };
 
-std::mutex g_mu;
-std::map<std::pair<int, std::string>, Entry> g_cache;
+std::mutex g_mu;  // the map only; never held across a compile
+std::map<std::pair<int, std::string>, std::unique_ptr<Entry>> g_cache;
+
+// Background compiles never outlive the runtime they load modules into.
+// They are joined by an atexit handler registered when the first one starts:
+// it runs before every exit handler registered earlier -- those of the host
+// runtime (torch, HIP) included, which would otherwise tear the device state
+// down under a compile still loading its module.
+struct Workers {
+    std::mutex mu;
+    std::vector<std::thread> th;
+    void join_all() {
+        std::vector<std::thread> v;
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            v.swap(th);
+        }
+        for (auto &t : v)
+            if (t.joinable()) t.join();
+    }
+    ~Workers() { join_all(); }
+} g_workers;
+
+void join_workers_at_exit() { g_workers.join_all(); }
+
+Entry *entry_for(int device, const std::string &sig) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    std::unique_ptr<Entry> &e = g_cache[{device, sig}];
+    if (!e) e.reset(new Entry());
+    return e.get();
+}
 
 bool compile(const std::string &src, std::vector<char> &code, std::string &log) {
     hiprtcProgram prog;
@@ -519,32 +560,76 @@ bool compile(const std::string &src, std::vector<char> &code, std::string &log) 
     return ok;
 }
 
-}  // namespace
 
-// Specialised kernel for a plan on `device` (compiled on first use, cached);
-// nullptr when compilation failed (the caller falls back to the generic kernel).
-void *ngz_rtc_kernel(int device, const DevPlan &P) {
-    const std::string sig = signature(P);
-    std::lock_guard<std::mutex> lk(g_mu);
-    Entry &e = g_cache[{device, sig}];
-    if (e.fn || e.failed) return (void *)e.fn;
-    const std::string src = generate(P);
+
+// Compile + load one entry (the caller won the 0 -> 1 transition).
+void build(Entry *e, int device, const std::string &src, const std::string &sig) {
     std::vector<char> code;
     std::string log;
     if (getenv("NGZ_RTC_DUMP")) fprintf(stderr, "[ngz rtc] source:\n%s\n", src.c_str());
     if (!compile(src, code, log)) {
         fprintf(stderr, "[ngz rtc] compile failed for %s:\n%s\n", sig.c_str(), log.c_str());
-        e.failed = true;
-        return nullptr;
+        e->state.store(3, std::memory_order_release);
+        return;
     }
-    if (hipModuleLoadData(&e.mod, code.data()) != hipSuccess ||
-        hipModuleGetFunction(&e.fn, e.mod, "ngz_tpl") != hipSuccess) {
+    if (hipSetDevice(device) != hipSuccess || hipModuleLoadData(&e->mod, code.data()) != hipSuccess ||
+        hipModuleGetFunction(&e->fn, e->mod, "ngz_tpl") != hipSuccess) {
         fprintf(stderr, "[ngz rtc] module load failed for %s\n", sig.c_str());
-        e.failed = true;
-        e.fn = nullptr;
-        return nullptr;
+        e->fn = nullptr;
+        e->state.store(3, std::memory_order_release);
+        return;
     }
-    return (void *)e.fn;
+    e->state.store(2, std::memory_order_release);
+}
+
+}  // namespace
+
+// Specialised kernel for a plan on `device`, compiled on first use and cached,
+// waiting for it if needed; nullptr when compilation failed (the caller falls
+// back to the generic kernel).
+void *ngz_rtc_kernel(int device, const DevPlan &P) {
+    const std::string sig = signature(P);
+    Entry *e = entry_for(device, sig);
+    int st = 0;
+    if (e->state.compare_exchange_strong(st, 1)) {
+        build(e, device, generate(P), sig);
+    } else {
+        while ((st = e->state.load(std::memory_order_acquire)) == 1)  // another thread compiles it
+            std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    }
+    return e->state.load(std::memory_order_acquire) == 2 ? (void *)e->fn : nullptr;
+}
+
+// Asynchronous form: returns 1 (ready, *fn set), 0 (compiling in the
+// background; poll *entry with ngz_rtc_poll) or -1 (failed).
+int ngz_rtc_kernel_async(int device, const DevPlan &P, void **fn, void **entry) {
+    const std::string sig = signature(P);
+    Entry *e = entry_for(device, sig);
+    *entry = e;
+    int st = 0;
+    if (e->state.compare_exchange_strong(st, 1)) {
+        std::string src = generate(P);  // the plan's field table is the caller's: read it now
+        static std::once_flag once;
+        std::call_once(once, [] { std::atexit(join_workers_at_exit); });
+        std::lock_guard<std::mutex> lk(g_workers.mu);
+        g_workers.th.emplace_back(build, e, device, std::move(src), sig);
+        return 0;
+    }
+    if (st == 2) {
+        *fn = (void *)e->fn;
+        return 1;
+    }
+    return st == 3 ? -1 : 0;
+}
+
+int ngz_rtc_poll(void *entry, void **fn) {
+    Entry *e = (Entry *)entry;
+    const int st = e->state.load(std::memory_order_acquire);
+    if (st == 2) {
+        *fn = (void *)e->fn;
+        return 1;
+    }
+    return st == 3 ? -1 : 0;
 }
 
 // The generated source for a plan (introspection / tests).

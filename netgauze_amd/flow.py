@@ -117,6 +117,10 @@ class DecodedBatch:
         s = self.error_json(d)
         return None if s is None else json.loads(s)
 
+    def slot_kernel(self, slot):
+        """1: the slot was decoded by its specialised kernel, 0: generic, 2: generic while compiling."""
+        return lib().ngz_slot_kernel(self._codec._ctx, slot)
+
     def error_struct(self, d):
         """ngz_dgram_error: the structured FlowInfoCodecDecoderError of datagram
         d as a dict (kind / layer names from flow_decode.h), or None."""
@@ -158,10 +162,15 @@ class DecodedBatch:
 
 OPT_SPECIALIZE = 1
 OPT_BLOCKS_PER_CU = 2
+OPT_RTC_SYNC = 5
 
 
 class FlowInfoCodec:
-    def __init__(self, device=0, specialize=None):
+    def __init__(self, device=0, specialize=None, rtc_sync=None):
+        """specialize: None (library default: per-template kernels, compiled in
+        the background), True (per-template kernels, each template's first batch
+        waits for its compile: deterministic kernel choice), False (generic
+        kernel only).  rtc_sync overrides the waiting."""
         ctx = ctypes.c_void_p()
         rc = lib().ngz_ctx_create(device, ctypes.byref(ctx))
         if rc != 0:
@@ -169,6 +178,9 @@ class FlowInfoCodec:
         self._ctx = ctx
         if specialize is not None:
             self.set_option(OPT_SPECIALIZE, 1 if specialize else 0)
+        if rtc_sync is None:
+            rtc_sync = bool(specialize)
+        self.set_option(OPT_RTC_SYNC, 1 if rtc_sync else 0)
 
     def set_option(self, opt, value):
         self._check(lib().ngz_ctx_set_option(self._ctx, opt, int(value)))

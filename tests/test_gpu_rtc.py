@@ -1,0 +1,91 @@
+"""Run-time kernel compiles are off the decode path (ngz_rtc.cpp): a template
+with a new layout compiles on a background thread while its context decodes
+it with the generic kernel (bit-exact either way), and another context's
+batches are not delayed by that compile."""
+import os
+import struct
+import time
+
+import pytest
+
+import parity
+from netgauze_amd import _lib as L
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+def _msg(sets, seq=1):
+    body = b"".join(sets)
+    return struct.pack(">HHIII", 10, 16 + len(body), 1_700_000_000, seq, 7) + body
+
+
+def _set(sid, payload):
+    return struct.pack(">HH", sid, 4 + len(payload)) + payload
+
+
+def _fresh_layout(tid):
+    """A template layout no earlier test compiled (random octet-array widths)."""
+    w = os.urandom(3)
+    fields = [(8, 4), (210, 1 + w[0] % 61), (7, 2), (1, 8), (210, 1 + w[1] % 29), (4, 1), (210, 1 + w[2] % 13)]
+    body = struct.pack(">HH", tid, len(fields)) + b"".join(struct.pack(">HH", i, ln) for i, ln in fields)
+    rl = sum(ln for _, ln in fields)
+    return _msg([_set(2, body)]), rl
+
+
+def _data(tid, rl, n_msgs, per, seed):
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    return [_msg([_set(tid, rng.integers(0, 256, size=rl * per, dtype=np.uint8).tobytes())], seq=m)
+            for m in range(n_msgs)]
+
+
+def test_compile_is_off_the_decode_path():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from netgauze_amd.flow import FlowInfoCodec
+    # the compile time of a fresh layout, waited for (NGZ_OPT_RTC_SYNC 1)
+    s = FlowInfoCodec(0, rtc_sync=True)
+    tm, rl = _fresh_layout(700)
+    t0 = time.perf_counter()
+    b = s.decode_datagrams([tm])
+    t_compile = time.perf_counter() - t0
+    assert t_compile > 0.02, t_compile  # a hiprtc compile, not a cache hit
+    # context B: its template's kernel is ready
+    B = FlowInfoCodec(0, rtc_sync=True)
+    tmB, rlB = _fresh_layout(701)
+    B.decode_datagrams([tmB])
+    dataB = _data(701, rlB, 20, 30, 1)
+    B.decode_datagrams(dataB)
+    # context A (background compiles): a new layout and its data in one batch
+    A = FlowInfoCodec(0)
+    tmA, rlA = _fresh_layout(702)
+    dataA = _data(702, rlA, 20, 30, 2)
+    t0 = time.perf_counter()
+    bA = A.decode_datagrams([tmA] + dataA)
+    t_a = time.perf_counter() - t0
+    slot = [i for i, sl in enumerate(bA.slots) if sl.template_id == 702][0]
+    assert bA.slot_kernel(slot) == 2            # decoded by the generic kernel while its own compiles
+    oracle, _ = parity.oracle_datagrams([tmA] + dataA)
+    assert parity.check_batch(bA, oracle)["records"] == 20 * 30
+    # B's batch while A's compile may still run
+    t0 = time.perf_counter()
+    bB = B.decode_datagrams(dataB)
+    t_b = time.perf_counter() - t0
+    assert bB.slot_kernel([i for i, sl in enumerate(bB.slots) if sl.template_id == 701][0]) == 1
+    assert t_a < 0.5 * t_compile and t_b < 0.5 * t_compile, (t_a, t_b, t_compile)
+    # A switches to its specialised kernel once the compile is done, results unchanged
+    oc = parity.O.FlowInfoCodec()
+    oc.decode(bytearray(tmA))
+    deadline = time.time() + 30
+    while True:
+        b2 = A.decode_datagrams(dataA)
+        k = b2.slot_kernel([i for i, sl in enumerate(b2.slots) if sl.template_id == 702][0])
+        if k == 1 or time.time() > deadline:
+            break
+        time.sleep(0.05)
+    assert k == 1
+    o2, _ = parity.oracle_datagrams(dataA, oc)
+    assert parity.check_batch(b2, o2)["records"] == 20 * 30
+    assert int((b2.dgram_headers()["status"] == L.NGZ_DG_OK).sum()) == 20
