@@ -111,6 +111,8 @@ struct Pass {
     uint64_t rabs;                // row mode: this lane's record batch offset
     const uint64_t *offsets;      // datagram offsets (row-mode error positions)
     void *hdr;                    // ngz_dgram_hdr[] (errors)
+    uint32_t img;                 // staged row mode: dword index of the group's bytes in ngz_vstage
+                                  // (rbase/sh then relative to it); ~0: read through rsrc
 };
 
 // Load record dwords [wb/4, wb/4 + ND) of this lane's record into R[0, ND)
@@ -632,12 +634,10 @@ struct RowTableSrc {
 // no record), so a group's lanes may read records of different sets and
 // datagrams.  P[] is preset by the caller; row0 as in chunk_passes.
 template <int RPL, bool CONSEC, class SrcFn, class PassFn>
-__device__ __forceinline__ void row_window(const BatchDev &B, const SrcFn &srcfn, uint32_t total, uint32_t w, uint32_t row0,
-                                           Pass (&P)[RPL], PassFn &&pass) {
+__device__ __forceinline__ void row_group(const BatchDev &B, const SrcFn &srcfn, uint32_t total, uint32_t pr0, uint32_t row0,
+                                          Pass (&P)[RPL], PassFn &&pass) {
     const uint32_t lane = threadIdx.x & 63;
-    for (uint32_t p = 0; p < NGZ_REG_WINDOW; p += 64 * RPL) {
-        const uint32_t pr0 = w * NGZ_REG_WINDOW + p;
-        if (pr0 >= total) break;
+    {
         uint64_t src[RPL];
         uint64_t lo = ~0ull, hi = 0;
 #pragma unroll
@@ -716,6 +716,16 @@ __device__ __forceinline__ void row_window(const BatchDev &B, const SrcFn &srcfn
     }
 }
 
+template <int RPL, bool CONSEC, class SrcFn, class PassFn>
+__device__ __forceinline__ void row_window(const BatchDev &B, const SrcFn &srcfn, uint32_t total, uint32_t w, uint32_t row0,
+                                           Pass (&P)[RPL], PassFn &&pass) {
+    for (uint32_t p = 0; p < NGZ_REG_WINDOW; p += 64 * RPL) {
+        const uint32_t pr0 = w * NGZ_REG_WINDOW + p;
+        if (pr0 >= total) break;
+        row_group<RPL, CONSEC>(B, srcfn, total, pr0, row0, P, pass);
+    }
+}
+
 // P[] fields of a row-mode slot that do not change per window
 template <int RPL>
 __device__ __forceinline__ void row_preset(const BatchDev &B, const SlotRT &rt, Pass (&P)[RPL]) {
@@ -727,6 +737,7 @@ __device__ __forceinline__ void row_preset(const BatchDev &B, const SlotRT &rt, 
     P[0].recpos = 0xFFFFFFFFu;
     P[0].pos0 = 0;
     P[0].dgram = 0;
+    P[0].img = 0xFFFFFFFFu;
 #pragma unroll
     for (int k = 1; k < RPL; ++k) P[k] = P[0];
 }
@@ -745,6 +756,180 @@ __device__ __forceinline__ void run_windows(const BatchDev &B, uint32_t slot, Sh
     const uint32_t nwin = (rt.total + NGZ_REG_WINDOW - 1) / NGZ_REG_WINDOW;
     for (uint32_t w = wid; w < nwin; w += nw) row_window<RPL, CONSEC>(B, RowTableSrc{rs, rd}, rt.total, w, 0u, P, pass);
 }
+
+#ifdef NGZ_VSTAGE
+// ---------------------------------------------------------------------------
+// Row mode with each group's record bytes staged in LDS (variable-length
+// templates, generate_vlen).  The rows of a 64-row group are consecutive
+// records of the slot, so their bytes are a few contiguous runs (one per set:
+// a run ends where a record's end is not the next row's start).  The wave
+// copies the runs' 16-byte blocks into its LDS image -- every lane its own
+// record's blocks, all loads in flight at once -- and the generated decode
+// then reads its register windows, length prefixes and string bytes from LDS.
+// Without staging each lane walks its record with a chain of dependent global
+// loads (a window load per variable-length field), and the wave's records are
+// re-fetched from HBM between them (FETCH_SIZE 2x the record bytes on
+// config 4).  A record ends at the next row's start when that lies in its
+// datagram, else at its datagram's end (the last record of a set), so the
+// image never holds bytes of another datagram.  Groups whose image exceeds
+// NGZ_VSTAGE_BYTES per wave decode through global loads as before (row_group).
+// ---------------------------------------------------------------------------
+#ifndef NGZ_VSTAGE_BYTES
+#define NGZ_VSTAGE_BYTES 10240
+#endif
+constexpr uint32_t kVStageDw = NGZ_VSTAGE_BYTES / 4;
+constexpr uint32_t kVStageWaves = 4;  // the generated kernels run 256-thread workgroups
+__shared__ uint32_t ngz_vstage[kVStageWaves * kVStageDw];
+
+// win_load<ND> for the generated variable-length kernels: from the LDS image when the group is staged
+template <int ND>
+__device__ __forceinline__ void win_load_v(uint32_t (&R)[WIN_DW], const Pass &P, uint32_t wb) {
+    if (P.img == 0xFFFFFFFFu) {
+        win_load<ND>(R, P, wb);
+        return;
+    }
+    const uint32_t q = P.img + ((P.rbase + wb) >> 2);
+    constexpr int NR = ND + 1 < WIN_DW ? ND + 1 : WIN_DW;
+#pragma unroll
+    for (int j = 0; j < NR; ++j) R[j] = (j < ND || P.any_sh) ? ngz_vstage[q + j] : 0u;
+#pragma unroll
+    for (int j = NR; j < WIN_DW; ++j) R[j] = 0;
+    if (P.any_sh) {
+#pragma unroll
+        for (int j = 0; j < ND; ++j) R[j] = __builtin_amdgcn_alignbyte(R[j + 1], R[j], P.sh);
+    }
+}
+
+struct StageBytes {
+    uint32_t base;  // this lane's byte, relative to the wave's image
+    uint32_t img;
+    __device__ uint32_t operator()(uint32_t i) const {
+        const uint32_t b = base + i;
+        return (ngz_vstage[img + (b >> 2)] >> (8 * (b & 3))) & 0xFF;
+    }
+};
+
+// utf8_valid_global for the generated variable-length kernels; rel is
+// relative to the lane's rsrc / image base as P.rbase is
+__device__ __forceinline__ bool utf8_valid_v(const Pass &P, uint32_t rel, uint32_t len, bool stop_at_nul) {
+    if (P.img == 0xFFFFFFFFu) return utf8_valid_global(P.rsrc, rel, len, stop_at_nul);
+    const uint32_t end = rel + len;
+    uint32_t acc = 0;
+    for (uint32_t a = rel & ~3u; a < end; a += 4) {
+        uint32_t m = 0xFFFFFFFFu;
+        if (a < rel) m <<= 8 * (rel - a);
+        if (a + 4 > end) m &= 0xFFFFFFFFu >> (8 * (a + 4 - end));
+        acc |= ngz_vstage[P.img + (a >> 2)] & m;
+    }
+    if (!(acc & 0x80808080u)) return true;
+    return utf8_valid_prefix(StageBytes{rel, P.img}, len, stop_at_nul);
+}
+
+__device__ __forceinline__ uint32_t wave_excl_sum(uint32_t v, uint32_t lane, uint32_t &total) {
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= (uint32_t)d) x += y;
+    }
+    total = __shfl(x, 63, 64);
+    return x - v;
+}
+
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        const uint32_t o = __shfl_xor(v, m, 64);
+        v = o > v ? o : v;
+    }
+    return v;
+}
+
+template <class PassFn>
+__device__ __forceinline__ void run_windows_staged(const BatchDev &B, uint32_t slot, PassFn &&pass) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wv = threadIdx.x >> 6;
+    const uint32_t wpb = blockDim.x >> 6;
+    const uint32_t wid = sgpr(blockIdx.x * wpb + wv);
+    const uint32_t nw = gridDim.x * wpb;
+    const SlotRT rt = sload(&B.slots[slot]);
+    const uint64_t *rs = (const uint64_t *)(B.arena + rt.rows);
+    const uint32_t *rd = (const uint32_t *)(B.arena + rt.rows + 8ull * rt.cap);
+    const RowTableSrc srcfn{rs, rd};
+    Pass P[1];
+    row_preset<1>(B, rt, P);
+    const uint32_t img0 = sgpr(wv * kVStageDw);
+    const uint32_t total = rt.total;
+    const uint32_t ngroups = (total + 63) / 64;
+    for (uint32_t g = wid; g < ngroups; g += nw) {
+        Pass &Q = P[0];
+        Q.img = 0xFFFFFFFFu;
+        const uint32_t pr0 = g * 64;
+        Q.prow = pr0;
+        Q.wrow = pr0;
+        Q.lrow = lane;
+        Q.row = pr0 + lane;
+        uint64_t src = 0;
+        Q.valid = Q.row < total && srcfn(Q, src);
+        if (!Q.valid) {
+            src = 0;
+            Q.dgram = 0;
+        }
+        Q.rabs = src;
+        // the record's end bound: the next row's start inside this datagram, else the datagram's end
+        uint64_t nx = __shfl_down(src, 1, 64);
+        if (lane == 63) nx = Q.row + 1 < total ? rs[Q.row + 1] : 0;
+        const uint64_t dend = Q.valid ? B.offsets[Q.dgram] + B.lengths[Q.dgram] : 0;
+        const bool nx_in = Q.row + 1 < total && nx > src && nx <= dend;
+        const uint64_t bound = Q.valid ? (nx_in ? nx : dend) : 0;
+        const uint64_t pb = __shfl_up(bound, 1, 64);
+        const bool cont = lane > 0 && Q.valid && pb == src;  // the previous row's record ends where this one starts
+        const uint64_t blo = cont ? (src + 15) >> 4 : src >> 4;
+        const uint64_t bhi = (bound + 15) >> 4;
+        const uint32_t c = Q.valid && bhi > blo ? (uint32_t)(bhi - blo) : 0u;
+        uint32_t T;
+        const uint32_t pc = wave_excl_sum(c, lane, T);
+        const uint64_t base = wave_min_u64(Q.valid ? src : ~0ull) & ~15ull;
+        const uint64_t top = wave_max_u64(bound);
+        if (T == 0 || 16 * T > NGZ_VSTAGE_BYTES || top - base >= 0x7FFF0000ull) {
+            row_group<1, false>(B, srcfn, total, pr0, 0u, P, pass);
+            continue;
+        }
+        const uint64_t avail64 = (B.bytes_size - base + 3) & ~3ull;
+        const uint32_t avail = avail64 > 0x7FFFFFF0ull ? 0x7FFFFFF0u : (uint32_t)avail64;
+        const __amdgpu_buffer_rsrc_t r =
+            __builtin_amdgcn_make_buffer_rsrc((void *)(B.bytes + base), (short)0, (int)avail, 0x00020000);
+        // copy: lane's blocks [blo, bhi) -> image pieces [pc, pc + c); 8 loads in flight per lane
+        const uint32_t g0 = (uint32_t)((blo << 4) - base);
+        const uint32_t cmax = wave_max_u32(c);
+        for (uint32_t j0 = 0; j0 < cmax; j0 += 8) {
+            v4u v[8];
+#pragma unroll
+            for (uint32_t k = 0; k < 8; ++k)
+                v[k] = __builtin_amdgcn_raw_buffer_load_b128(r, j0 + k < c ? g0 + 16 * (j0 + k) : 0x80000000u, 0, 0);
+#pragma unroll
+            for (uint32_t k = 0; k < 8; ++k)
+                if (j0 + k < c) *(v4u *)&ngz_vstage[img0 + 4 * (pc + j0 + k)] = v[k];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // the record's first byte in the image: its block is this lane's first piece,
+        // or the previous contribution's last one when a continuing record starts mid-block
+        const uint32_t rel = Q.valid ? 16 * (pc - (cont && (src & 15) ? 1u : 0u)) + (uint32_t)(src & 15) : 0u;
+        Q.img = img0;
+        Q.rsrc = r;
+        Q.a0 = base;
+        Q.rbase = rel & ~3u;
+        Q.sh = rel & 3u;
+        Q.any_sh = __builtin_amdgcn_ballot_w64(Q.sh != 0) != 0;
+        pass(P);
+        // the next group's copy overwrites the image: every lane's reads of it are done
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+#endif  // NGZ_VSTAGE
 
 #ifdef NGZ_LDS_WAVES
 // Row source of a chunk-mode window: the window's chunk descriptors, one per

@@ -275,6 +275,29 @@ void build_plan(Version &v) {
         col += width;
     }
     P.f = v.fields.data();
+    // walk program of variable-length records (ngz_vlen_walk fast path)
+    P.walk_nv = 0;
+    {
+        uint32_t k = 0, acc = 0;
+        bool usable = true;
+        for (const DevField &fd : v.fields) {
+            if (fd.kind == NGZ_K_FAIL) usable = false;
+            if (fd.kind == NGZ_K_VLEN) {
+                if (k >= NGZ_WALK_MAX) { usable = false; break; }
+                P.walk_fixed[k++] = (uint16_t)acc;
+                acc = 0;
+            } else {
+                acc += fd.len;
+                if (acc > 0xFFFF) usable = false;
+            }
+        }
+        if (usable) {
+            P.walk_fixed[k] = (uint16_t)acc;
+            P.walk_nv = (uint8_t)k;
+        } else {
+            P.walk_nv = 0xFF;
+        }
+    }
     P.n_fields = (uint16_t)v.specs.size();
     P.rec_len = rl;
     P.row_bytes = col;
@@ -891,7 +914,7 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
         any_vlen = any_vlen || (P.has_vlen && P.rpl);
     }
     if (any_vlen && getenv("NGZ_RECMAP") == nullptr) {  // NGZ_RECMAP set: walk twice (A/B)
-        if (ctx->d_recmap.ensure(in->bytes_size / 32 + 2)) return fail(ctx, NGZ_E_NOMEM, "device alloc (record map)");
+        if (ctx->d_recmap.ensure(in->bytes_size / 32 + 8)) return fail(ctx, NGZ_E_NOMEM, "device alloc (record map)");
         B.recmap = ctx->d_recmap.p;
     }
     B.summary = d_sum;
@@ -900,7 +923,7 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
     // k_frame zeroes the count matrix itself; the summary and increments of
     // this parity were zeroed by the previous batch's k_export
     if (!N) HIPCHK(hipMemsetAsync(ctx->d_counts.p, 0, n_items * 4, st));
-    if (B.recmap) HIPCHK(hipMemsetAsync(B.recmap, 0, (in->bytes_size / 32 + 2) * 4, st));
+    if (B.recmap) HIPCHK(hipMemsetAsync(B.recmap, 0, (in->bytes_size / 32 + 8) * 4, st));
     if (!ctx->clean[par]) {
         HIPCHK(hipMemsetAsync(d_sum, 0, sizeof(BatchSummary), st));
         HIPCHK(hipMemsetAsync(d_proc, 0, NGZ_MAX_SLOTS * 8, st));

@@ -8,6 +8,7 @@
 #define NGZ_LANE_FIELDS 128   // field descriptors the generic kernel keeps in VGPRs (two per lane); the
                               // rest of a wider template's table is read with scalar loads
 #define NGZ_RTC_MAX_FIELDS 512  // widest template that gets a generated kernel (wider: generic kernel)
+#define NGZ_WALK_MAX 15       // variable-length fields a walk program holds (more: the exact field walk)
 #define NGZ_MAX_SLOTS 1024    // template versions live in one batch
 #define NGZ_NO_SLOT 0xFFFFu
 #define NGZ_NO_ERR (~0ull)
@@ -94,19 +95,26 @@ struct DevPlan {
     const DevField *f;   // n_fields descriptors (scope first): host memory in the host's copy of a plan,
                          // the context's device field table in the uploaded one.  No field cap: a
                          // template may carry as many fields as its set holds (ipfix.rs:384-413).
+    // Walk program of a variable-length template (ngz_vlen_walk's fast path): a record is
+    // walk_fixed[0] fixed bytes, then for each of walk_nv variable-length fields its length
+    // prefix + value followed by walk_fixed[k+1] fixed bytes.  walk_nv = 0xFF: no program
+    // (template-constant field failures, or more than NGZ_WALK_MAX variable-length fields).
+    uint8_t walk_nv;
+    uint8_t walk_pad[3];
+    uint16_t walk_fixed[NGZ_WALK_MAX + 1];
 };
 
 // Records of one IPFIX data set whose template has variable-length (65535)
 // fields, walked as Set::parse + DataRecord::parse + Field::parse would
 // (ipfix.rs:193-222, 335-370; vlen prefix generator.rs:1775-1793: u8, 255 ->
 // 3-byte length).  p = datagram, [pos, end) = set payload.  Calls
-// on_rec(k, record_offset) for each complete record only (a failing record
-// has no row); returns the number of complete records; on UnexpectedEof / a
-// template-constant field failure sets *err to the error key (parsing stops
-// there).
+// on_rec(n0 + k, record_offset) for each complete record only (a failing
+// record has no row); returns the number of complete records; on
+// UnexpectedEof / a template-constant field failure sets *err to the error
+// key (parsing stops there).  Exact form: one step per field.
 template <class F>
-__host__ __device__ inline uint32_t ngz_vlen_walk(const uint8_t *p, uint32_t pos, uint32_t end, const DevPlan &pl,
-                                                  uint64_t *err, F &&on_rec) {
+__host__ __device__ inline uint32_t ngz_vlen_walk_exact(const uint8_t *p, uint32_t pos, uint32_t end, const DevPlan &pl,
+                                                        uint64_t *err, F &&on_rec, uint32_t n0 = 0) {
     const uint32_t minlen = pl.rec_len;  // vlen counted as 1
     uint32_t n = 0;
     while (minlen > 0 && end - pos >= minlen) {
@@ -140,6 +148,49 @@ __host__ __device__ inline uint32_t ngz_vlen_walk(const uint8_t *p, uint32_t pos
             if (rem < fd.len) { *err = ngz_err_key(pos, E_REC_EOF, f, fd.len); return n; }
             pos += fd.len;
         }
+        on_rec(n0 + n, start);
+        ++n;
+    }
+    return n;
+}
+
+// The same walk through the plan's walk program: per record only the length
+// prefixes are read (no per-field descriptor loads, the program sits in
+// registers), each step checking that the bytes it skips are there.  Any
+// record the fast steps cannot complete is re-walked from its start by the
+// exact form, which reports the reference's error for it (a record fails
+// exactly when some field runs past the set: both forms agree on that).
+template <class F>
+__host__ __device__ inline uint32_t ngz_vlen_walk(const uint8_t *p, uint32_t pos, uint32_t end, const DevPlan &pl,
+                                                  uint64_t *err, F &&on_rec) {
+    if (pl.walk_nv > NGZ_WALK_MAX) return ngz_vlen_walk_exact(p, pos, end, pl, err, on_rec);
+    const uint32_t minlen = pl.rec_len, nv = pl.walk_nv;
+    uint32_t fx[NGZ_WALK_MAX + 1];
+#pragma unroll
+    for (uint32_t k = 0; k <= NGZ_WALK_MAX; ++k) fx[k] = pl.walk_fixed[k];
+    uint32_t n = 0;
+    while (minlen > 0 && end - pos >= minlen) {
+        const uint32_t start = pos;
+        bool ok = end - pos >= fx[0];
+        pos += fx[0];
+#pragma unroll
+        for (uint32_t k = 0; k < NGZ_WALK_MAX; ++k) {
+            if (k < nv && ok) {
+                uint32_t len = 0, hdr = 1;
+                ok = end - pos >= 1;
+                if (ok) {
+                    len = p[pos];
+                    if (len == 255) {
+                        ok = end - pos >= 4;
+                        if (ok) len = ((uint32_t)p[pos + 1] << 16) | ((uint32_t)p[pos + 2] << 8) | p[pos + 3];
+                        hdr = 4;
+                    }
+                }
+                ok = ok && end - pos - hdr >= len && end - pos - hdr - len >= fx[k + 1];
+                pos += hdr + len + fx[k + 1];
+            }
+        }
+        if (!ok) return n + ngz_vlen_walk_exact(p, start, end, pl, err, on_rec, n);
         on_rec(n, start);
         ++n;
     }

@@ -200,6 +200,8 @@ __device__ bool has_template_sets(const BatchDev &B, uint32_t d) {
     return false;
 }
 
+constexpr uint32_t kFrameBlock = 256;
+
 // Count matrix, slot-major rows of N datagrams (scanned in one pass):
 //   rows [0, S)      records of slot s in datagram d
 //   rows [S, 2S)     decode chunks of slot s in datagram d
@@ -228,7 +230,7 @@ struct CountVis {
     }
 };
 
-__global__ void k_frame(BatchDev B, const uint32_t *hf_flag, const uint32_t *hf_first) {
+__global__ void __launch_bounds__(kFrameBlock) k_frame(BatchDev B, const uint32_t *hf_flag, const uint32_t *hf_first) {
     const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
     if (d >= B.n) return;
     // this datagram's column of the count matrix starts at zero (no memset pass)
@@ -282,8 +284,14 @@ __global__ void k_layout(BatchDev B) {
         rt.nchunks = B.scan[(uint64_t)(S + s + 1) * N] - B.scan[(uint64_t)(S + s) * N];
         rt.chunk_scan0 = B.scan[(uint64_t)(S + s) * N];
         // row mode for variable-length records and for sets so small that
-        // set-relative chunks would leave most lanes idle (< 25 % of rows used)
-        rt.mode = (B.plans[s].has_vlen || 4ull * total < (uint64_t)rt.nchunks * w) ? NGZ_MODE_ROW : NGZ_MODE_CHUNK;
+        // set-relative chunks would leave most lanes idle (< 25 % of rows used).
+        // A specialised LDS-staged kernel gathers the rows of a window across
+        // its chunks (ChunkGatherSrc, up to 64 chunk entries per 256-row
+        // sub-window), so small sets stay in chunk mode there: two 32-byte
+        // chunk entries per set instead of a 12-byte row entry per record.
+        const bool gather = B.plans[s].spec && B.plans[s].lds_waves && 256ull * rt.nchunks <= 48ull * total;
+        rt.mode = (B.plans[s].has_vlen || (!gather && 4ull * total < (uint64_t)rt.nchunks * w)) ? NGZ_MODE_ROW
+                                                                                                  : NGZ_MODE_CHUNK;
         rt.reserved = 0;
         const uint64_t col_bytes = ((uint64_t)cap * B.plans[s].row_bytes + 7) & ~7ull;
         rt.rows = rt.mode == NGZ_MODE_ROW ? off + col_bytes : 0;
@@ -330,16 +338,27 @@ struct EmitVis {
             // dependent length-prefix chain)
             const uint64_t g0 = dg_off + pos, g1 = dg_off + end;
             uint32_t k = 0;
-            for (uint64_t w = g0 >> 5; g0 < g1 && w <= (g1 - 1) >> 5; ++w) {
-                uint32_t bits = B->recmap[w];
-                if ((w << 5) < g0) bits &= 0xFFFFFFFFu << (g0 & 31);
-                if (((w + 1) << 5) > g1) bits &= 0xFFFFFFFFu >> (32 - (g1 & 31));
-                while (bits) {
-                    const uint32_t bit = (uint32_t)__builtin_ctz(bits);
-                    rs[k] = (w << 5) + bit;
-                    rd[k] = d;
-                    ++k;
-                    bits &= bits - 1;
+            if (g0 < g1) {
+                const uint64_t w0 = g0 >> 5, w1 = (g1 - 1) >> 5;
+                // 16-byte loads of the map (4 words = 128 batch bytes each; the map has slack past its end)
+                for (uint64_t wq = w0 & ~3ull; wq <= w1; wq += 4) {
+                    const uint4 q = *(const uint4 *)&B->recmap[wq];
+                    const uint32_t words[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+                    for (uint32_t j = 0; j < 4; ++j) {
+                        const uint64_t w = wq + j;
+                        if (w < w0 || w > w1) continue;
+                        uint32_t bits = words[j];
+                        if ((w << 5) < g0) bits &= 0xFFFFFFFFu << (g0 & 31);
+                        if (((w + 1) << 5) > g1) bits &= 0xFFFFFFFFu >> (32 - (g1 & 31));
+                        while (bits) {
+                            const uint32_t bit = (uint32_t)__builtin_ctz(bits);
+                            rs[k] = (w << 5) + bit;
+                            rd[k] = d;
+                            ++k;
+                            bits &= bits - 1;
+                        }
+                    }
                 }
             }
             // the walk stopped inside (or right at the end of) this set: k_frame
@@ -662,8 +681,8 @@ __global__ void __launch_bounds__(256) k_export(BatchDev B, BatchSummary *h_summ
 // launch wrappers (C linkage, used by ngz_host.cpp)
 // ---------------------------------------------------------------------------
 extern "C" int ngz_launch_frame(const BatchDev *B, const uint32_t *hf_flag, const uint32_t *hf_first, hipStream_t st) {
-    const uint32_t nb = (B->n + 255) / 256;
-    if (nb) hipLaunchKernelGGL(k_frame, dim3(nb), dim3(256), 0, st, *B, hf_flag, hf_first);
+    const uint32_t nb = (B->n + kFrameBlock - 1) / kFrameBlock;
+    if (nb) hipLaunchKernelGGL(k_frame, dim3(nb), dim3(kFrameBlock), 0, st, *B, hf_flag, hf_first);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -423,7 +423,7 @@ std::string generate_vlen(const DevPlan &P) {
             const Item &it = items[i];
             const int w = item_win[i];
             if (w >= 0 && w != cur) {
-                snprintf(b, sizeof b, "        win_load<%u>(R[0], Q, %uu);\n", wins[w].second, 4 * wins[w].first);
+                snprintf(b, sizeof b, "        win_load_v<%u>(R[0], Q, %uu);\n", wins[w].second, 4 * wins[w].first);
                 body += b;
                 cur = w;
             }
@@ -443,7 +443,7 @@ std::string generate_vlen(const DevPlan &P) {
                 break;
             case 3:
                 snprintf(b, sizeof b,
-                         "        if (P0.valid && !utf8_valid_global(P0.rsrc, rel0 + seg + %uu, %uu, true))"
+                         "        if (P0.valid && !utf8_valid_v(P0, rel0 + seg + %uu, %uu, true))"
                          " rec_error(P0, seg + %uu, E_REC_UTF8, %uu);\n",
                          it.off, it.len, it.off, it.f);
                 break;
@@ -459,12 +459,12 @@ std::string generate_vlen(const DevPlan &P) {
                          "            if (L == 255) { L = (uint32_t)rbe(R[0], %uu, 3); hdr = 4; }\n"
                          "            const uint32_t data = seg + %uu + hdr;\n"
                          "            if (P0.valid) {\n"
-                         "                const uint64_t at = P0.a0 + rel0 + data;\n"
+                         "                const uint64_t at = P0.rabs + data;\n"
                          "                ColSt(P0, %uu, 16).b128(P0.lrow * 16, (uint32_t)at, (uint32_t)(at >> 32), L, 0);\n",
                          it.off - wb, it.off + 1 - wb, it.off, d.col_off);
                 body += b;
                 if (d.flags & 0x80)  // string: every byte UTF-8 checked
-                    body += "                if (!utf8_valid_global(P0.rsrc, rel0 + data, L, false))\n"
+                    body += "                if (!utf8_valid_v(P0, rel0 + data, L, false))\n"
                             "                    rec_error(P0, data, E_REC_UTF8, " + F + "u, L);\n";
                 body += "            }\n"
                         "            seg = data + L;\n"
@@ -481,16 +481,14 @@ std::string generate_vlen(const DevPlan &P) {
     }
     std::string src;
     src += "// generated by ngz_rtc.cpp for plan " + signature(P) + "\n";
-    src += "#include \"ngz_dev.h\"\nusing namespace ngzdev;\n";
+    src += "#define NGZ_VSTAGE 1\n#include \"ngz_dev.h\"\nusing namespace ngzdev;\n";
     src += "extern \"C\" __global__ void __launch_bounds__(256) ngz_tpl(BatchDev B, uint32_t slot) {\n";
     src += "    if (sload(&B.summary->overflow)) return;\n";
-    src += "    auto shape = [](uint32_t) { return RecShape{" + std::to_string(P.rec_len) + "u, " +
-           std::to_string(P.row_bytes) + "u, true}; };\n";
     src += "    auto pass = [&](const Pass (&P)[1]) {\n";
     src += "        uint32_t R[1][WIN_DW];\n";
     src += body;
     src += "    };\n";
-    src += "    run_windows<1, false>(B, slot, shape, pass);\n}\n";
+    src += "    run_windows_staged(B, slot, pass);\n}\n";
     return src;
 }
 

@@ -1,6 +1,6 @@
 """Write the generated per-template decode kernel of a synthetic template to a
 .hip file (for offline hipcc resource-usage / ISA inspection):
-python tools/rtc_dump.py t20 /tmp/rtc/t20.hip"""
+python tools/rtc_dump.py t20|v900 /tmp/rtc/t20.hip"""
 import ctypes
 import os
 import sys
@@ -12,6 +12,8 @@ from netgauze_amd import _lib, synth  # noqa: E402
 def template_record(name):
     if name == "t20":
         return synth.template_message()[20:]
+    if name == "v900":
+        return synth._ipfix_template_v900()[20:]
     raise SystemExit("unknown template " + name)
 
 
