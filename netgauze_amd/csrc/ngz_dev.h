@@ -606,6 +606,27 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
     return v;
 }
 
+// exclusive prefix sum over the wave's lanes (total: the sum over all 64)
+__device__ __forceinline__ uint32_t wave_excl_sum(uint32_t v, uint32_t lane, uint32_t &total) {
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= (uint32_t)d) x += y;
+    }
+    total = __shfl(x, 63, 64);
+    return x - v;
+}
+
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        const uint32_t o = __shfl_xor(v, m, 64);
+        v = o > v ? o : v;
+    }
+    return v;
+}
+
 // Row mode: walk the slot's output in windows of NGZ_REG_WINDOW rows (wave
 // strided), groups of 64*RPL rows as in run_chunks, every row's record found
 // through rowsrc/rowdg (k_emit).  A group's records are read through one
@@ -823,26 +844,6 @@ __device__ __forceinline__ bool utf8_valid_v(const Pass &P, uint32_t rel, uint32
     }
     if (!(acc & 0x80808080u)) return true;
     return utf8_valid_prefix(StageBytes{rel, P.img}, len, stop_at_nul);
-}
-
-__device__ __forceinline__ uint32_t wave_excl_sum(uint32_t v, uint32_t lane, uint32_t &total) {
-    uint32_t x = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(x, d, 64);
-        if (lane >= (uint32_t)d) x += y;
-    }
-    total = __shfl(x, 63, 64);
-    return x - v;
-}
-
-__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
-#pragma unroll
-    for (int m = 32; m >= 1; m >>= 1) {
-        const uint32_t o = __shfl_xor(v, m, 64);
-        v = o > v ? o : v;
-    }
-    return v;
 }
 
 template <class PassFn>
