@@ -639,7 +639,7 @@ struct RowTableSrc {
     const uint64_t *rs;
     const uint32_t *rd;
     __device__ __forceinline__ bool operator()(Pass &Q, uint64_t &src) const {
-        src = rs[Q.row];
+        src = rs[Q.row] & NGZ_ROW_OFF_MASK;
         Q.dgram = rd[Q.row];
         Q.recpos = 0xFFFFFFFFu;
         Q.rec0 = Q.row;
@@ -790,9 +790,9 @@ __device__ __forceinline__ void run_windows(const BatchDev &B, uint32_t slot, Sh
 // Without staging each lane walks its record with a chain of dependent global
 // loads (a window load per variable-length field), and the wave's records are
 // re-fetched from HBM between them (FETCH_SIZE 2x the record bytes on
-// config 4).  A record ends at the next row's start when that lies in its
-// datagram, else at its datagram's end (the last record of a set), so the
-// image never holds bytes of another datagram.  Groups whose image exceeds
+// config 4).  A record's bytes run to the next record of its set, or to the
+// set's end (the span k_emit stores with the offset, ngz_row_entry), so the
+// image never holds bytes of another set.  Groups whose image exceeds
 // NGZ_VSTAGE_BYTES per wave decode through global loads as before (row_group).
 // ---------------------------------------------------------------------------
 #ifndef NGZ_VSTAGE_BYTES
@@ -870,19 +870,15 @@ __device__ __forceinline__ void run_windows_staged(const BatchDev &B, uint32_t s
         Q.wrow = pr0;
         Q.lrow = lane;
         Q.row = pr0 + lane;
-        uint64_t src = 0;
-        Q.valid = Q.row < total && srcfn(Q, src);
-        if (!Q.valid) {
-            src = 0;
-            Q.dgram = 0;
-        }
+        Q.valid = Q.row < total;
+        const uint64_t ent = Q.valid ? rs[Q.row] : 0;
+        Q.dgram = Q.valid ? rd[Q.row] : 0;
+        Q.recpos = 0xFFFFFFFFu;
+        Q.rec0 = Q.row;
+        const uint64_t src = ent & NGZ_ROW_OFF_MASK;
         Q.rabs = src;
-        // the record's end bound: the next row's start inside this datagram, else the datagram's end
-        uint64_t nx = __shfl_down(src, 1, 64);
-        if (lane == 63) nx = Q.row + 1 < total ? rs[Q.row + 1] : 0;
-        const uint64_t dend = Q.valid ? B.offsets[Q.dgram] + B.lengths[Q.dgram] : 0;
-        const bool nx_in = Q.row + 1 < total && nx > src && nx <= dend;
-        const uint64_t bound = Q.valid ? (nx_in ? nx : dend) : 0;
+        // the record's bytes: up to the next record of its set, or to the set's end (ngz_row_entry)
+        const uint64_t bound = Q.valid ? src + (ent >> 48) : 0;
         const uint64_t pb = __shfl_up(bound, 1, 64);
         const bool cont = lane > 0 && Q.valid && pb == src;  // the previous row's record ends where this one starts
         const uint64_t blo = cont ? (src + 15) >> 4 : src >> 4;

@@ -197,6 +197,15 @@ __host__ __device__ inline uint32_t ngz_vlen_walk(const uint8_t *p, uint32_t pos
     return n;
 }
 
+// Row-mode record table entry (rowsrc): the record's batch offset in the low
+// 48 bits, the bytes from it to the next record of its set (or to the set's
+// end; at most 65535) in the high 16 -- the staged decode copies exactly
+// those bytes to LDS without looking up the datagram's extent.
+__host__ __device__ inline uint64_t ngz_row_entry(uint64_t off, uint64_t span) {
+    return off | ((span < 0xFFFFu ? span : 0xFFFFull) << 48);
+}
+#define NGZ_ROW_OFF_MASK 0x0000FFFFFFFFFFFFull
+
 struct SlotRT {          // per batch slot, computed on device by k_layout
     uint64_t block;      // byte offset of the slot's columns in the arena
     uint32_t cap;        // rows allocated
@@ -207,7 +216,7 @@ struct SlotRT {          // per batch slot, computed on device by k_layout
     uint32_t chunk_scan0;  // scanned count at the slot's first chunk cell (k_emit cursor base)
     uint32_t mode;       // NGZ_MODE_*
     uint32_t reserved;
-    uint64_t rows;       // row mode: arena offset of u64 rowsrc[cap] (batch offset of each record),
+    uint64_t rows;       // row mode: arena offset of u64 rowsrc[cap] (ngz_row_entry of each record),
                          // followed by u32 rowdg[cap] (its datagram)
     uint64_t wtab;       // chunk mode: arena offset of u32 wfirst[cap/window]: first chunk of
                          // every output window (k_emit), for the LDS-staged kernels

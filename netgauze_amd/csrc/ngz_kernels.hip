@@ -358,6 +358,7 @@ struct EmitVis {
             // dependent length-prefix chain)
             const uint64_t g0 = dg_off + pos, g1 = dg_off + end;
             uint32_t k = 0;
+            uint64_t prev = 0;  // the previous record's start: its span ends at this one
             if (g0 < g1) {
                 const uint64_t w0 = g0 >> 5, w1 = (g1 - 1) >> 5;
                 // 16-byte loads of the map (4 words = 128 batch bytes each; the map has slack past its end)
@@ -373,7 +374,9 @@ struct EmitVis {
                         if (((w + 1) << 5) > g1) bits &= 0xFFFFFFFFu >> (32 - (g1 & 31));
                         while (bits) {
                             const uint32_t bit = (uint32_t)__builtin_ctz(bits);
-                            rs[k] = (w << 5) + bit;
+                            const uint64_t at = (w << 5) + bit;
+                            if (k) rs[k - 1] = ngz_row_entry(prev, at - prev);
+                            prev = at;
                             rd[k] = d;
                             ++k;
                             bits &= bits - 1;
@@ -381,6 +384,7 @@ struct EmitVis {
                     }
                 }
             }
+            if (k) rs[k - 1] = ngz_row_entry(prev, g1 - prev);  // the last record: up to the set's end
             // the walk stopped inside (or right at the end of) this set: k_frame
             // recorded that framing error in the datagram header
             const uint64_t ek = ((const ngz_dgram_hdr *)B->hdr)[d].err_key;
@@ -388,10 +392,15 @@ struct EmitVis {
             if (ek != NGZ_NO_ERR && stop >= pos && stop <= end) *err = ek;
             return k;
         }
-        return ngz_vlen_walk(p, pos, end, pl, err, [&](uint32_t k, uint32_t at) {
+        const uint32_t n = ngz_vlen_walk(p, pos, end, pl, err, [&](uint32_t k, uint32_t at) {
             rs[k] = dg_off + at;
             rd[k] = d;
         });
+        for (uint32_t k = 0; k < n; ++k) {
+            const uint64_t next = k + 1 < n ? rs[k + 1] : dg_off + end;
+            rs[k] = ngz_row_entry(rs[k], next - rs[k]);
+        }
+        return n;
     }
     __device__ void on_set(uint32_t set_pos, uint32_t slot, uint32_t n, uint32_t payload_pos, uint32_t rl) {
         const uint64_t N = B->n;
@@ -412,7 +421,7 @@ struct EmitVis {
             uint64_t *rs = rowsrc(slot) + rec0;
             uint32_t *rd = rowdg(slot) + rec0;
             for (uint32_t k = 0; k < n; ++k) {
-                rs[k] = dg_off + payload_pos + (uint64_t)k * rl;
+                rs[k] = ngz_row_entry(dg_off + payload_pos + (uint64_t)k * rl, rl);
                 rd[k] = d;
             }
             return;
