@@ -12,13 +12,22 @@
  *   get_window_start                 aggregation.rs:79-89    (timestamp floored to the minute)
  *   validate_operation_compatibility aggregation/config.rs:212-250, generator.rs:580-629
  *
+ *   AggFlowInfo::into_flowinfo_with_extra_fields  aggregator.rs:203-277 (ngz_agg_flowinfo_json)
+ *
  * The group table lives in HBM and persists across ngz_agg_push calls; one
  * aggregator serves one exporter peer IP (the window key, aggregator.rs:109-117).
- * Records are grouped by (window start, flow type, key fields); a record whose
- * message export time is more than `lateness` behind the peer's event time is
- * late and is counted, not aggregated (aggregation.rs:139-141).  Window
- * contents do not depend on when windows are flushed, so
- * ngz_agg_flush returns every group at once, as WindowAggregator::flush does.
+ * Records are grouped by (window start, flow type, key fields) exactly: keys are
+ * compared, never identified by a hash.  A record whose message export time is
+ * more than `lateness` behind the peer's event time is late and is counted, not
+ * aggregated (aggregation.rs:139-141).  Windows whose start is at or before
+ * get_window_start(event time - lateness) - window_duration are closed
+ * (aggregation.rs:154-160): ngz_agg_emit hands their groups out and frees their
+ * room; ngz_agg_flush hands out every group (WindowAggregator::flush).
+ *
+ * A push is all-or-nothing: when it fails (NGZ_AGG_E_OVERFLOW, NGZ_E_LIMIT, ...)
+ * the groups, the set dictionaries and the event time are as they were before
+ * it.  Only a device error or an internal inconsistency poisons the aggregator
+ * (NGZ_AGG_E_POISONED from then on, until ngz_agg_reset).
  */
 #ifndef NGZ_FLOW_AGGREGATE_H
 #define NGZ_FLOW_AGGREGATE_H
@@ -41,11 +50,13 @@ extern "C" {
 
 #define NGZ_AGG_MAX_KEYS 16
 #define NGZ_AGG_MAX_VALUES 32
-#define NGZ_AGG_MAX_KEY_BYTES 128   /* sum of key column widths, each rounded up to 4 */
-#define NGZ_AGG_SET_BITS 64         /* distinct template ids / peer ports; 128 observation domains */
+#define NGZ_AGG_MAX_KEY_BYTES 128   /* sum of key row slots (see ngz_agg_key_desc) */
+#define NGZ_AGG_SET_BITS 64         /* distinct template ids / peer ports among the live groups; 128 observation
+                                       domains (entries no live group uses are reused) */
 
-#define NGZ_AGG_E_OVERFLOW (-10)    /* group table full (capacity) or a set dictionary is full */
-#define NGZ_AGG_E_COLLISION (-11)   /* two distinct keys share a 64-bit key hash (detected, ~1e-8 per 1e6 groups) */
+#define NGZ_AGG_E_OVERFLOW (-10)    /* more groups than the capacity, or a set dictionary full of live entries */
+#define NGZ_AGG_E_COLLISION (-11)   /* no longer returned: hash collisions are resolved by comparing keys */
+#define NGZ_AGG_E_POISONED (-12)    /* an earlier device error / internal inconsistency; ngz_agg_reset clears it */
 
 /* One transform entry: (IE, occurrence index) -> op  (FieldRef + Op, config.rs:152-176). */
 typedef struct {
@@ -59,9 +70,13 @@ typedef struct {
 typedef struct ngz_agg ngz_agg;
 
 /* Validates the config like AggregationConfig::validate + validate_operation_compatibility
- * (window > 0, lateness <= window, op allowed for the IE's data type).  Key fields keep
- * their order (key_select), aggregated fields theirs (agg_select).  capacity: groups the
- * HBM table holds (rounded up to a power of two; the table is half full at most). */
+ * (window > 0, lateness <= window; the op allowed by IE::supports_{arithmetic,comparison,
+ * bitwise}_ops, generator.rs:1176-1272 -- data type, sub-registry and dataTypeSemantics
+ * identifier/flags): NGZ_E_INVALID where the reference rejects the config, NGZ_E_LIMIT where
+ * it accepts one the device does not run (Min/Max over list types or the nested reason-code
+ * sub-registry of forwardingStatus).  Key fields keep their order (key_select), aggregated
+ * fields theirs (agg_select).  capacity: live groups held at most (the HBM table has at
+ * least twice as many slots). */
 int ngz_agg_create(int device, const ngz_agg_field *fields, uint32_t n_fields, uint64_t window_ms,
                    uint64_t lateness_ms, uint64_t capacity, ngz_agg **out);
 void ngz_agg_destroy(ngz_agg *a);
@@ -108,14 +123,66 @@ int ngz_agg_layout(ngz_agg *a, uint32_t *row_bytes, uint32_t *key_off, uint16_t 
 int64_t ngz_agg_groups(ngz_agg *a);
 
 /* Copies every group (unordered) into dst (cap bytes, row_bytes each), then empties
- * the table and forgets the peer's event time (WindowAggregator::flush).  Returns the
- * groups written or <0 (NGZ_E_INVALID: cap too small; nothing is emptied). */
+ * the table, the set dictionaries and forgets the peer's event time
+ * (WindowAggregator::flush).  Returns the groups written or <0 (NGZ_E_INVALID: cap too
+ * small; nothing is emptied). */
 int64_t ngz_agg_flush(ngz_agg *a, void *dst, uint64_t cap);
 
-/* Set dictionaries: template ids (proto<<16 | id), peer ports and observation domain
- * ids, in bit order.  Each array receives up to cap entries; returns 0. */
+/* Groups of the windows the event time has closed (aggregation.rs:154-160), and the
+ * emission of those groups: copied into dst like ngz_agg_flush, then removed.  The
+ * reference emits a closed window from the process_item call that closes it; here the
+ * windows closed by a push are emitted after it, with the same contents (an item is
+ * never late for a window that is still open, and never lands in a closed one). */
+int64_t ngz_agg_closed(ngz_agg *a);
+int64_t ngz_agg_emit(ngz_agg *a, void *dst, uint64_t cap);
+
+/* Empties the aggregator and clears a poisoned state. */
+int ngz_agg_reset(ngz_agg *a);
+
+/* Set dictionaries of the rows last returned by ngz_agg_flush / ngz_agg_emit: template
+ * ids (proto<<16 | id), peer ports and observation domain ids, entry i <-> bit i (free
+ * entries read all-ones).  Each array receives up to cap entries; returns 0. */
 int ngz_agg_sets(ngz_agg *a, uint32_t *templates, uint32_t *n_templates, uint16_t *ports, uint32_t *n_ports,
                  uint32_t *domains, uint32_t *n_domains, uint32_t cap);
+
+/* How a key / value is stored in an output row.
+ * Key kkind: 0 the decoded column cell (width bytes), 1 a fixed string up to its first
+ * NUL (zero padded to the slot), 2 an octet array: u32 length, then the bytes.
+ * Value vclass: 0 unsigned / 1 signed integer (little-endian at the IE width, the
+ * Rust type's wrap-around for Add), 2 dateTime micro/nanoseconds (u64 secs<<32 | nanos),
+ * 3 bytes (OR), 4 sub-registry / TCP flags value (little-endian at the width), 5 f32,
+ * 6 f64, 7 IPv6 address (16 bytes, network order).  kind: the decoded column kind
+ * (NGZ_K_*) and width the column width, both as first seen (0 before). */
+typedef struct {
+    uint8_t kkind;
+    uint8_t kind;
+    uint16_t slot;      /* row bytes */
+    uint16_t width;
+    uint16_t reserved;
+} ngz_agg_key_desc;
+typedef struct {
+    uint8_t vclass;
+    uint8_t kind;
+    uint16_t width;
+    uint32_t reserved;
+} ngz_agg_value_desc;
+int ngz_agg_key_info(ngz_agg *a, uint32_t k, ngz_agg_key_desc *out);
+int ngz_agg_value_info(ngz_agg *a, uint32_t v, ngz_agg_value_desc *out);
+
+/* AggFlowInfo::into_flowinfo_with_extra_fields (aggregator.rs:203-277) of output rows
+ * (n rows of ngz_agg_flush / ngz_agg_emit, read with the dictionaries of that call):
+ * one FlowInfo per group, as the serde JSON text of the decode path (ngz_batch_json):
+ * an IPFIX or NetFlow v9 packet whose one data set (id 65535) holds one record: the
+ * present key fields, the present aggregated fields, originalFlowsPresent,
+ * minExportSeconds, maxExportSeconds, collectionTimeMilliseconds (the max), then one
+ * NetGauze originalExporterTransportPort per peer port, one originalObservationDomainId
+ * per domain and one NetGauze originalTemplateId per template id, each set in ascending
+ * order (the reference iterates HashSets: unspecified order).  Packet header: export
+ * time export_time_ms (the reference uses Utc::now()), sequence numbers seq0, seq0+1, ...,
+ * observation domain / source id shard_id, NetFlow v9 sys_up_time = the group's max.
+ * fn gets (row index, NGZ_DG_OK, text, length).  Returns rows rendered or <0. */
+int64_t ngz_agg_flowinfo_json(ngz_agg *a, const void *rows, uint64_t n, uint32_t shard_id, uint32_t seq0,
+                              int64_t export_time_ms, ngz_json_line_fn fn, void *user);
 
 /* Device time of the last push (HIP events around its kernels), milliseconds. */
 int ngz_agg_last_timing(ngz_agg *a, float *push_ms);

@@ -39,10 +39,14 @@ INGEST_FUNCTIONS = [
 # include/ngz/flow_aggregate.h
 AGG_FUNCTIONS = [
     "ngz_agg_create", "ngz_agg_destroy", "ngz_agg_last_error", "ngz_agg_push", "ngz_agg_layout",
-    "ngz_agg_groups", "ngz_agg_flush", "ngz_agg_sets", "ngz_agg_last_timing",
+    "ngz_agg_groups", "ngz_agg_flush", "ngz_agg_closed", "ngz_agg_emit", "ngz_agg_reset", "ngz_agg_sets",
+    "ngz_agg_key_info", "ngz_agg_value_info", "ngz_agg_flowinfo_json", "ngz_agg_last_timing",
 ]
 NGZ_AGG_KEY, NGZ_AGG_ADD, NGZ_AGG_MIN, NGZ_AGG_MAX, NGZ_AGG_OR = range(5)
-NGZ_AGG_E_OVERFLOW, NGZ_AGG_E_COLLISION = -10, -11
+NGZ_AGG_E_OVERFLOW, NGZ_AGG_E_COLLISION, NGZ_AGG_E_POISONED = -10, -11, -12
+# ngz_agg_key_desc.kkind / ngz_agg_value_desc.vclass
+AGG_KK_FIXED, AGG_KK_STR, AGG_KK_OCTETS = range(3)
+AGG_VC_UINT, AGG_VC_SINT, AGG_VC_DTFRAC, AGG_VC_BYTES, AGG_VC_RANK, AGG_VC_F32, AGG_VC_F64, AGG_VC_IPV6 = range(8)
 NGZ_COLLECT_PCAP_DECODER, NGZ_COLLECT_FLOW_INFO = 0, 1
 NGZ_PROTO_TCP, NGZ_PROTO_UDP = 6, 17
 
@@ -103,6 +107,18 @@ class AggField(ctypes.Structure):
     _fields_ = [("pen", ctypes.c_uint32), ("ie_id", ctypes.c_uint16), ("index", ctypes.c_uint16),
                 ("op", ctypes.c_uint8), ("reserved", ctypes.c_uint8 * 7)]
 
+
+class AggKeyDesc(ctypes.Structure):
+    _fields_ = [("kkind", ctypes.c_uint8), ("kind", ctypes.c_uint8), ("slot", ctypes.c_uint16),
+                ("width", ctypes.c_uint16), ("reserved", ctypes.c_uint16)]
+
+
+class AggValueDesc(ctypes.Structure):
+    _fields_ = [("vclass", ctypes.c_uint8), ("kind", ctypes.c_uint8), ("width", ctypes.c_uint16),
+                ("reserved", ctypes.c_uint32)]
+
+
+assert ctypes.sizeof(AggKeyDesc) == 8 and ctypes.sizeof(AggValueDesc) == 8
 
 AGG_ROW_DTYPE = np.dtype([("window_start", "<u4"), ("flow_type", "u1"), ("reserved0", "u1", 3),
                           ("key_present", "<u4"), ("val_present", "<u4"), ("record_count", "<u8"),
@@ -183,6 +199,18 @@ def load():
     lib.ngz_agg_sets.restype = I
     lib.ngz_agg_last_timing.argtypes = [P, ctypes.POINTER(ctypes.c_float)]
     lib.ngz_agg_last_timing.restype = I
+    lib.ngz_agg_closed.argtypes = [P]
+    lib.ngz_agg_closed.restype = ctypes.c_int64
+    lib.ngz_agg_emit.argtypes = [P, P, U64]
+    lib.ngz_agg_emit.restype = ctypes.c_int64
+    lib.ngz_agg_reset.argtypes = [P]
+    lib.ngz_agg_reset.restype = I
+    lib.ngz_agg_key_info.argtypes = [P, U32, ctypes.POINTER(AggKeyDesc)]
+    lib.ngz_agg_key_info.restype = I
+    lib.ngz_agg_value_info.argtypes = [P, U32, ctypes.POINTER(AggValueDesc)]
+    lib.ngz_agg_value_info.restype = I
+    lib.ngz_agg_flowinfo_json.argtypes = [P, P, U64, U32, U32, ctypes.c_int64, JSON_LINE_FN, P]
+    lib.ngz_agg_flowinfo_json.restype = ctypes.c_int64
     # ingest (flow_ingest.h)
     lib.ngz_pcap_open.argtypes = [ctypes.c_char_p, ctypes.POINTER(P)]
     lib.ngz_pcap_open.restype = I

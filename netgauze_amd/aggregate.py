@@ -6,11 +6,20 @@ AggregationConfig.transform shape (crates/collector/src/flow/aggregation/config.
 152-176, 252-335): an ordered mapping IE -> Op, or IE -> {index: Op}, where IE is
 (pen, ie_id).  `push(batch, peer_port, collection_ms)` explodes and reduces every
 data record of a decoded batch (aggregator.rs:78-90, 159-198, 286-354);
-`flush()` returns every group (WindowAggregator::flush, analytics/src/aggregation.rs:
-175-185) as dicts with canonical values: ints for integer-like fields, bytes for
-byte-like ones, str for fixed strings.
+`emit()` returns the groups of the windows the event time has closed
+(analytics/src/aggregation.rs:154-160) and `flush()` every group
+(WindowAggregator::flush, :175-185), as dicts with canonical values: ints for
+integer-like fields, bytes for byte-like ones, str for strings, floats, and
+(secs, nanos) for date-times -- each field rendered from its IE's data type in
+the registry (netgauze_amd/data/ie_registry.json) and the device's storage
+class (ngz_agg_key_info / ngz_agg_value_info).  `flowinfo_json(rows)` renders
+output rows as the reference's aggregated FlowInfo
+(AggFlowInfo::into_flowinfo_with_extra_fields, aggregator.rs:203-277).
 """
 import ctypes
+import json
+import os
+import struct
 
 import numpy as np
 
@@ -21,6 +30,7 @@ OPS = {"Key": _lib.NGZ_AGG_KEY, "Add": _lib.NGZ_AGG_ADD, "Min": _lib.NGZ_AGG_MIN
        "BoolMapOr": _lib.NGZ_AGG_OR}
 
 _LIB = None
+_DTYPES = None
 
 
 def lib():
@@ -28,6 +38,17 @@ def lib():
     if _LIB is None:
         _LIB = _lib.load()
     return _LIB
+
+
+def ie_dtype(pen, ie_id):
+    """IE data type from the registry the library is built from (None: IE::Unknown)."""
+    global _DTYPES
+    if _DTYPES is None:
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "ie_registry.json")
+        with open(path) as f:
+            reg = json.load(f)
+        _DTYPES = {(r["pen"], r["id"]): r["type"] for r in reg["ies"]}
+    return _DTYPES.get((pen, ie_id))
 
 
 class AggError(RuntimeError):
@@ -46,6 +67,11 @@ def unify(transform):
     return out
 
 
+def _datetime_ms(ms):
+    secs = ms // 1000
+    return (secs, (ms - secs * 1000) * 1_000_000)
+
+
 class FlowAggregator:
     def __init__(self, transform, window_s=60, lateness_s=10, capacity=1 << 20, device=0, kinds=None):
         self.fields = unify(transform) if isinstance(transform, dict) else list(transform)
@@ -58,7 +84,7 @@ class FlowAggregator:
         if rc != 0:
             raise AggError("ngz_agg_create failed (%d)" % rc)
         self._h = h
-        # kinds[(pen, ie_id)] = "sint" | "str" | "bytes" | "uint" (how flush renders values)
+        # optional override of the rendering per (pen, ie_id): "sint" | "uint" | "bytes" | "str"
         self.kinds = kinds or {}
 
     def close(self):
@@ -78,7 +104,11 @@ class FlowAggregator:
         return rc
 
     def push(self, batch, peer_port=4739, collection_ms=0):
-        """Aggregate every data record of a DecodedBatch; returns the late records."""
+        """Aggregate every data record of a DecodedBatch; returns the late records.
+        The batch must be the latest one its codec decoded (its device arrays are
+        reused by the next decode)."""
+        if batch.generation != batch._codec.generation:
+            raise AggError("stale DecodedBatch: its codec has decoded another batch since")
         late = ctypes.c_uint64()
         self._check(lib().ngz_agg_push(self._h, batch._codec._ctx, ctypes.byref(batch.out), peer_port,
                                        collection_ms, ctypes.byref(late), None))
@@ -92,6 +122,12 @@ class FlowAggregator:
     def n_groups(self):
         return self._check(lib().ngz_agg_groups(self._h))
 
+    def n_closed(self):
+        return self._check(lib().ngz_agg_closed(self._h))
+
+    def reset(self):
+        self._check(lib().ngz_agg_reset(self._h))
+
     def layout(self):
         nk, nv = len(self.key_fields), len(self.val_fields)
         rb = ctypes.c_uint32()
@@ -100,6 +136,18 @@ class FlowAggregator:
         self._check(lib().ngz_agg_layout(self._h, ctypes.byref(rb), ko, kw, vo, vw))
         return rb.value, list(ko)[:nk], list(kw)[:nk], list(vo)[:nv], list(vw)[:nv]
 
+    def descs(self):
+        kd, vd = [], []
+        for k in range(len(self.key_fields)):
+            d = _lib.AggKeyDesc()
+            self._check(lib().ngz_agg_key_info(self._h, k, ctypes.byref(d)))
+            kd.append(d)
+        for v in range(len(self.val_fields)):
+            d = _lib.AggValueDesc()
+            self._check(lib().ngz_agg_value_info(self._h, v, ctypes.byref(d)))
+            vd.append(d)
+        return kd, vd
+
     def sets(self):
         cap = 128
         t, p, d = (ctypes.c_uint32 * cap)(), (ctypes.c_uint16 * cap)(), (ctypes.c_uint32 * cap)()
@@ -107,19 +155,45 @@ class FlowAggregator:
         self._check(lib().ngz_agg_sets(self._h, t, ctypes.byref(nt), p, ctypes.byref(np_), d, ctypes.byref(nd), cap))
         return list(t)[:nt.value], list(p)[:np_.value], list(d)[:nd.value]
 
-    def flush_raw(self):
-        """Every group as (rows: AGG_ROW_DTYPE view, raw bytes [n, row_bytes]); empties the table."""
+    def _take(self, fn, n):
         rb = self.layout()[0]
-        n = self.n_groups()
         buf = np.zeros(max(n, 1) * rb, dtype=np.uint8)
-        got = self._check(lib().ngz_agg_flush(self._h, buf.ctypes.data, buf.nbytes))
+        got = self._check(fn(self._h, buf.ctypes.data, buf.nbytes))
         raw = buf[:got * rb].reshape(got, rb)
         return raw[:, :88].copy().view(AGG_ROW_DTYPE).reshape(got), raw
 
+    def flush_raw(self):
+        """Every group as (rows: AGG_ROW_DTYPE view, raw bytes [n, row_bytes]); empties the table."""
+        return self._take(lib().ngz_agg_flush, self.n_groups())
+
+    def emit_raw(self):
+        """The groups of closed windows as (rows, raw bytes); removes them."""
+        return self._take(lib().ngz_agg_emit, self.n_closed())
+
     def flush(self):
+        return self.render(*self.flush_raw())
+
+    def emit(self):
+        return self.render(*self.emit_raw())
+
+    def flowinfo_json(self, raw, shard_id=0, seq0=0, export_time_ms=0):
+        """AggFlowInfo -> FlowInfo serde JSON of rows just returned by flush_raw / emit_raw."""
+        out = []
+
+        def cb(_user, _i, _status, text, n, _consumed):
+            out.append(ctypes.string_at(text, n).decode())
+            return 0
+
+        fn = _lib.JSON_LINE_FN(cb)
+        raw = np.ascontiguousarray(raw)
+        self._check(lib().ngz_agg_flowinfo_json(self._h, raw.ctypes.data if len(raw) else None, len(raw), shard_id,
+                                                seq0, export_time_ms, fn, None))
+        return out
+
+    def render(self, hdr, raw):
         rb, ko, kw, vo, vw = self.layout()
+        kd, vd = self.descs()
         tpl, ports, doms = self.sets()
-        hdr, raw = self.flush_raw()
 
         def bits(x, dictionary):
             return {dictionary[i] for i in range(len(dictionary)) if (int(x) >> i) & 1}
@@ -132,19 +206,13 @@ class FlowAggregator:
                 if not (int(h["key_present"]) >> k) & 1:
                     key.append(None)
                     continue
-                b = bytes(r[ko[k]:ko[k] + kw[k]])
-                key.append(self._render(pen, ie, b))
+                key.append(self._render_key(pen, ie, kd[k], bytes(r[ko[k]:ko[k] + kd[k].slot])))
             vals = []
             for v, (pen, ie, _i, op) in enumerate(self.val_fields):
                 if not (int(h["val_present"]) >> v) & 1:
                     vals.append(None)
                     continue
-                kind = self.kinds.get((pen, ie), "uint")
-                if kind == "bytes":
-                    vals.append(bytes(r[vo[v]:vo[v] + vw[v]]))
-                else:
-                    x = int.from_bytes(bytes(r[vo[v]:vo[v] + 8]), "little", signed=(kind == "sint"))
-                    vals.append((x >> 32, x & 0xFFFFFFFF) if kind == "dtfrac" else x)
+                vals.append(self._render_value(pen, ie, vd[v], bytes(r[vo[v]:vo[v] + 32])))
             dom_bits = int(h["domain_bits"][0]) | (int(h["domain_bits"][1]) << 64)
             out.append(dict(window_start=int(h["window_start"]), flow_type=int(h["flow_type"]), key=tuple(key),
                             vals=tuple(vals), record_count=int(h["record_count"]),
@@ -155,10 +223,45 @@ class FlowAggregator:
                             ports=bits(h["port_bits"], ports), domains=bits(dom_bits, doms)))
         return out
 
-    def _render(self, pen, ie, b):
-        kind = self.kinds.get((pen, ie), "uint")
-        if kind == "bytes":
-            return b
-        if kind == "str":
+    def _render_key(self, pen, ie, d, b):
+        kind = self.kinds.get((pen, ie))
+        if d.kkind == _lib.AGG_KK_STR or kind == "str":
             return b.split(b"\0", 1)[0].decode("utf-8")
-        return int.from_bytes(b, "little", signed=(kind == "sint"))
+        if d.kkind == _lib.AGG_KK_OCTETS:
+            n = int.from_bytes(b[:4], "little")
+            return b[4:4 + n]
+        return self._render_cell(pen, ie, d.kind, d.width, b, kind)
+
+    def _render_value(self, pen, ie, d, b):
+        kind = self.kinds.get((pen, ie))
+        vc = d.vclass
+        if vc == _lib.AGG_VC_F32:
+            return struct.unpack("<f", b[:4])[0]
+        if vc == _lib.AGG_VC_F64:
+            return struct.unpack("<d", b[:8])[0]
+        if vc == _lib.AGG_VC_IPV6:
+            return b[:16]
+        if vc == _lib.AGG_VC_BYTES:
+            return b[:d.width]
+        if vc == _lib.AGG_VC_DTFRAC:
+            x = int.from_bytes(b[:8], "little")
+            return (x >> 32, x & 0xFFFFFFFF)
+        return self._render_cell(pen, ie, d.kind, 8, b[:8], kind, value=True)
+
+    def _render_cell(self, pen, ie, ckind, width, b, kind, value=False):
+        """A column cell / integer accumulator as the oracle's canonical value."""
+        dt = ie_dtype(pen, ie)
+        if kind == "bytes" or (kind is None and (dt is None or dt in ("octetArray", "macAddress", "ipv6Address",
+                                                                      "unsigned256"))):
+            return b[:width]
+        signed = kind == "sint" or (kind is None and (dt or "").startswith("signed")) or ckind == 7  # NGZ_K_DTMS
+        x = int.from_bytes(b[:width], "little", signed=signed)
+        if dt == "dateTimeMilliseconds":
+            return _datetime_ms(x)
+        if dt in ("dateTimeMicroseconds", "dateTimeNanoseconds"):
+            return (x & 0xFFFFFFFF, x >> 32) if not value else (x >> 32, x & 0xFFFFFFFF)
+        if dt == "dateTimeSeconds":
+            return (x, 0)
+        if dt in ("float32", "float64") and not value:
+            return struct.unpack("<f" if width == 4 else "<d", b[:width])[0]
+        return x

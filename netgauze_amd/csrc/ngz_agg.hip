@@ -2,25 +2,44 @@
 // (crates/collector/src/flow/aggregation/aggregator.rs) over the columns the
 // decode path leaves in HBM.  C ABI: include/ngz/flow_aggregate.h.
 //
-// Pipeline of one ngz_agg_push (all on one stream):
-//   k_agg_dgram   per datagram: event time it contributes (OK status and >= 1
-//                 data record, aggregator.rs:308 yields one item per record),
-//                 observation-domain dictionary bit (device CAS table)
-//   hipcub max-scan over event times -> k_agg_late: lateness flag per datagram
+// Pipeline of one ngz_agg_push (one stream; the push is all-or-nothing):
+//   k_agg_dgram   datagrams that carry >= 1 data record (aggregator.rs:308
+//                 yields one item per record)
+//   hipcub max-scan over export times -> k_agg_late: lateness per datagram
 //                 (aggregation.rs:139-141: ts < current_time - lateness, with
-//                 current_time the running max of earlier non-late items)
+//                 current_time the running max of the earlier non-late items)
+//                 and its observation-domain dictionary entry (new domains are
+//                 listed for the host, which assigns them: k_agg_domfix)
 //   hipcub sum-scan over set record counts -> k_agg_setidx: set of every record
-//   k_agg_insert  one lane per record: key hash over the key columns, open
-//                 addressing insert into the HBM group table (64-bit CAS on the
-//                 tag), then the reductions of FlowCacheRecord::reduce
-//                 (aggregator.rs:159-198) as atomics on the group row
-//   k_agg_verify  (after all inserts) re-hashes every record and compares its
-//                 key bytes with the stored key of the group it landed in; a
-//                 mismatch is a 64-bit hash collision -> NGZ_AGG_E_COLLISION
+//   k_agg_claim   one lane per record: its group's slot in the HBM table
+//                 (open addressing; a new group's first record claims a slot
+//                 with a CAS on the 64-bit tag and writes the exact key).  Keys
+//                 that fit 63 bits are their own tag.  Other keys are hashed:
+//                 k_agg_check compares every record's key with its slot's key,
+//                 and records of a key whose hash collided re-probe comparing
+//                 keys (k_agg_claim in exact mode) until every record sits in
+//                 its own key's slot -- groups are exact, collisions only cost
+//                 probes.
+//   validation    table full / too many groups / dictionaries full: the slots
+//                 claimed by this push are released and the dictionaries put
+//                 back, so a failed push leaves the aggregator as it was
+//   k_agg_apply   FlowCacheRecord::reduce (aggregator.rs:159-198) of every
+//                 record into its group: wave and workgroup pre-aggregation,
+//                 then atomics on the group row (integer Add wraps like
+//                 release-mode `+=`; Min / Max / BoolMapOr)
+//   k_agg_ordered reductions whose result depends on record order (float Add,
+//                 float Min / Max ties, IPv6 Min / Max): records sorted by group
+//                 (stable radix sort), one sequential fold per group in record
+//                 order, starting from the group's value -- the reference's
+//                 order exactly
+// Windows close as the event time advances (aggregation.rs:154-160): their
+// groups are handed out by ngz_agg_emit and their slots freed (tombstones;
+// the table is rebuilt when they pile up).
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -36,17 +55,39 @@ namespace {
 constexpr uint32_t ROW_HDR = 88;  // sizeof(ngz_agg_row)
 static_assert(sizeof(ngz_agg_row) == ROW_HDR, "ngz_agg_row layout");
 constexpr uint32_t DOM_SLOTS = 128;
+constexpr uint32_t SET_BITS = 64;
+constexpr uint32_t NEWDOM_SLOTS = 256;  // distinct new observation domains one push may bring
+constexpr uint64_t TAG_EMPTY = 0, TAG_TOMB = 1;
+constexpr uint32_t NONE = 0xFFFFFFFFu;
 
-// value classes (how a column value becomes the 64-bit accumulator operand)
-enum : uint8_t { VC_UINT = 0, VC_SINT = 1, VC_DTFRAC = 2, VC_BYTES = 3 };
+// dginfo bits (per datagram)
+constexpr uint16_t DG_USE = 1, DG_LATE = 2, DG_MISSING = 0x200;  // domain index in bits 2..8
+
+// value classes: how a column value becomes the accumulator operand
+enum : uint8_t {
+    VC_UINT = 0,   // unsigned integer / ipv4 / boolean / dateTimeSeconds (min/max/add/or in u64)
+    VC_SINT = 1,   // signed integer, dateTimeMilliseconds (sign-extended; min/max with the sign bit flipped)
+    VC_DTFRAC = 2, // dateTime micro/nanoseconds: (secs << 32 | nanos), ordered like DateTime
+    VC_BYTES = 3,  // byte-wise OR (octetArray, macAddress, ipv6Address, unsigned256)
+    VC_RANK = 4,   // sub-registry enum / TCPHeaderFlags Min-Max: the value's rank in the Rust Ord
+    VC_F32 = 5,    // OrderedFloat<f32> (ordered path)
+    VC_F64 = 6,    // OrderedFloat<f64> (ordered path)
+    VC_IPV6 = 7,   // Ipv6Addr Min / Max (16 bytes, big-endian order; ordered path)
+};
+__host__ __device__ inline bool vc_ordered(uint8_t vc) { return vc == VC_F32 || vc == VC_F64 || vc == VC_IPV6; }
+
+// key kinds: canonical key bytes in the row
+enum : uint8_t {
+    KK_FIXED = 0,  // the column cell, zero padded
+    KK_STR = 1,    // fixed string: bytes up to the first NUL (Field::String, generator.rs:1654-1669), zero padded
+    KK_OCTETS = 2, // octetArray: u32 length + bytes (Box<[u8]> compares its length too)
+};
 
 struct AggSlotPlan {            // per batch slot, built on the host every push
     const uint8_t *key_col[NGZ_AGG_MAX_KEYS];   // null: the record has no such field (None)
     const uint8_t *val_col[NGZ_AGG_MAX_VALUES];
     uint16_t key_w[NGZ_AGG_MAX_KEYS];
     uint16_t val_w[NGZ_AGG_MAX_VALUES];
-    uint8_t key_str[NGZ_AGG_MAX_KEYS];          // fixed string: bytes after the first NUL do not count
-    uint8_t val_vc[NGZ_AGG_MAX_VALUES];
     uint64_t tpl_bit;
     uint32_t proto;
     uint32_t usable;                            // 0: slot not aggregated (no records / not device-decoded)
@@ -55,34 +96,41 @@ struct AggSlotPlan {            // per batch slot, built on the host every push
 struct AggParams {
     uint32_t n_keys, n_vals;
     uint32_t key_off[NGZ_AGG_MAX_KEYS];
-    uint32_t key_w[NGZ_AGG_MAX_KEYS];   // packed mode: the IE's fixed column width
+    uint32_t key_slot[NGZ_AGG_MAX_KEYS];   // row bytes of the key (multiple of 4)
+    uint8_t key_kind[NGZ_AGG_MAX_KEYS];
+    uint32_t key_pw[NGZ_AGG_MAX_KEYS];     // packed mode: the IE's fixed column width
     uint32_t val_off[NGZ_AGG_MAX_VALUES];
     uint8_t val_op[NGZ_AGG_MAX_VALUES];
+    uint8_t val_vc[NGZ_AGG_MAX_VALUES];
+    uint8_t val_tcp[NGZ_AGG_MAX_VALUES];   // VC_RANK of TCPHeaderFlags (else a sub-registry)
+    const uint32_t *rank_known[NGZ_AGG_MAX_VALUES];  // VC_RANK sub-registry: bitmap of registered values
     uint32_t row_bytes;
-    uint64_t mask;              // capacity - 1
+    uint64_t mask;              // table slots - 1
     uint32_t push_id;
     uint32_t port_bit;
     uint64_t coll_flip;         // collection time ms, sign bit flipped (unsigned order == signed order)
     uint32_t lds_ok;            // 1: no byte-wise OR values (wave results may be combined in LDS)
-    uint32_t packed;            // 1: the whole group key packs into 63 bits (exact tag, no verify pass)
+    uint32_t packed;            // 1: the whole group key packs into 63 bits (exact tag)
+    uint64_t hash_mask;         // hashed keys: bits of the hash kept (tests force collisions with NGZ_AGG_HASH_BITS)
 };
 
-// dginfo: bit 0 usable (OK + has records + not late), bits 1..7 domain bit
 __device__ __forceinline__ uint64_t mix64(uint64_t h, uint64_t v) {
     h ^= v + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
     h *= 0xBF58476D1CE4E5B9ull;
     return h ^ (h >> 31);
 }
 
-__device__ __forceinline__ uint64_t slot_of(uint64_t h) {  // table position of a tag (tags may be packed keys)
+__host__ __device__ __forceinline__ uint64_t slot_of(uint64_t h) {  // table position of a tag
     h ^= h >> 33;
     h *= 0xFF51AFD7ED558CCDull;
     return h ^ (h >> 33);
 }
 
-__device__ __forceinline__ uint32_t load_word(const uint8_t *p, uint32_t w, uint32_t j, bool str, bool &nul) {
-    // word j (4 bytes, zero padded past w) of a w-byte value at p
-    if ((w & 3) == 0 && !str) return *(const uint32_t *)(p + 4 * j);
+__device__ __forceinline__ bool tag_live(uint64_t t) { return t > TAG_TOMB; }
+
+// word j (4 bytes, little-endian, zero padded past w) of a w-byte cell; str: NUL truncated
+__device__ __forceinline__ uint32_t cell_word(const uint8_t *p, uint32_t w, uint32_t j, bool str, bool &nul) {
+    if ((w & 3) == 0 && !str && 4 * j < w) return *(const uint32_t *)(p + 4 * j);
     uint32_t r = 0;
 #pragma unroll
     for (uint32_t b = 0; b < 4; ++b) {
@@ -97,11 +145,23 @@ __device__ __forceinline__ uint32_t load_word(const uint8_t *p, uint32_t w, uint
     return r;
 }
 
-__device__ __forceinline__ uint64_t key_hash(const AggSlotPlan &sp, const AggParams &P, uint64_t row, uint32_t win,
-                                             uint32_t &present) {
-    if (P.packed) {  // exact tag: bit 63 | window/60 (27 bits) | flow type | presence bits | key bits
+// canonical key word j of key k (KK_OCTETS: word 0 is the length)
+struct KeyWords {
+    const uint8_t *p;
+    uint32_t w;
+    uint8_t kind;
+    bool nul = false;
+    __device__ uint32_t operator()(uint32_t j) {
+        if (kind == KK_OCTETS) return j == 0 ? w : cell_word(p, w, j - 1, false, nul);
+        return cell_word(p, w, j, kind == KK_STR, nul);
+    }
+};
+
+__device__ __forceinline__ uint64_t key_tag(const AggSlotPlan &sp, const AggParams &P, uint64_t row, uint32_t win,
+                                            uint32_t &present) {
+    present = 0;
+    if (P.packed) {  // exact tag: bit 63 | window/60 | flow type | per key: presence bit + value bits
         uint64_t x = ((uint64_t)(win / 60) << 1) | (sp.proto == 9);
-        present = 0;
         for (uint32_t k = 0; k < P.n_keys; ++k) {
             const uint8_t *c = sp.key_col[k];
             const uint32_t w = sp.key_w[k];
@@ -111,31 +171,60 @@ __device__ __forceinline__ uint64_t key_hash(const AggSlotPlan &sp, const AggPar
                 const uint8_t *q = c + row * w;
                 v = w == 4 ? *(const uint32_t *)q : w == 2 ? *(const uint16_t *)q : w == 8 ? *(const uint64_t *)q : *q;
             }
-            x = (((x << 1) | (c != nullptr)) << (8 * P.key_w[k])) | v;
+            x = (((x << 1) | (c != nullptr)) << (8 * P.key_pw[k])) | v;
         }
         return x | (1ull << 63);
     }
     uint64_t h = mix64(0x4E475A41474731ull, ((uint64_t)win << 8) | sp.proto);
-    present = 0;
     for (uint32_t k = 0; k < P.n_keys; ++k) {
         const uint8_t *c = sp.key_col[k];
-        const uint32_t w = sp.key_w[k];
-        h = mix64(h, c ? (0x10000u | w) : 0u);
+        h = mix64(h, c ? 0x100u : 0u);
         if (!c) continue;
         present |= 1u << k;
-        const uint8_t *p = c + row * w;
-        bool nul = false;
-        for (uint32_t j = 0; j < (w + 3) / 4; ++j) h = mix64(h, load_word(p, w, j, sp.key_str[k], nul));
+        KeyWords kw{c + row * sp.key_w[k], sp.key_w[k], P.key_kind[k]};
+        for (uint32_t j = 0; j < P.key_slot[k] / 4; ++j) h = mix64(h, kw(j));
     }
-    return h ? h : 1;
+    h &= P.hash_mask;
+    return h < 2 ? h + 2 : h;  // 0 / 1 are the empty and tombstone tags
+}
+
+__device__ __forceinline__ bool key_equal(const uint8_t *R, const AggSlotPlan &sp, const AggParams &P, uint64_t row,
+                                          uint32_t win, uint32_t kp) {
+    bool same = *(const uint32_t *)(R + 0) == win && *(const uint32_t *)(R + 4) == sp.proto &&
+                *(const uint32_t *)(R + 8) == kp;
+    for (uint32_t k = 0; k < P.n_keys && same; ++k) {
+        const uint8_t *c = sp.key_col[k];
+        if (!c) continue;
+        KeyWords kw{c + row * sp.key_w[k], sp.key_w[k], P.key_kind[k]};
+        for (uint32_t j = 0; j < P.key_slot[k] / 4 && same; ++j)
+            same = ((const uint32_t *)(R + P.key_off[k]))[j] == kw(j);
+    }
+    return same;
+}
+
+__device__ __forceinline__ void key_write(uint8_t *R, const AggSlotPlan &sp, const AggParams &P, uint64_t row,
+                                          uint32_t win, uint32_t kp) {
+    *(uint32_t *)(R + 0) = win;
+    *(uint32_t *)(R + 4) = sp.proto;
+    *(uint32_t *)(R + 8) = kp;
+    for (uint32_t k = 0; k < P.n_keys; ++k) {
+        uint32_t *dst = (uint32_t *)(R + P.key_off[k]);
+        const uint8_t *c = sp.key_col[k];
+        if (!c) {
+            for (uint32_t j = 0; j < P.key_slot[k] / 4; ++j) dst[j] = 0;
+            continue;
+        }
+        KeyWords kw{c + row * sp.key_w[k], sp.key_w[k], P.key_kind[k]};
+        for (uint32_t j = 0; j < P.key_slot[k] / 4; ++j) dst[j] = kw(j);
+    }
 }
 
 __device__ __forceinline__ uint64_t load_value(const uint8_t *p, uint32_t w, uint8_t vc) {
-    uint64_t v = 0;
     if (vc == VC_DTFRAC) {  // {u32 secs, u32 nanos} -> ordered (secs, nanos)
         const uint32_t s = *(const uint32_t *)p, ns = *(const uint32_t *)(p + 4);
         return ((uint64_t)s << 32) | ns;
     }
+    uint64_t v = 0;
     if (w == 8) v = *(const uint64_t *)p;
     else if (w == 4) v = *(const uint32_t *)p;
     else if (w == 2) v = *(const uint16_t *)p;
@@ -147,9 +236,34 @@ __device__ __forceinline__ uint64_t load_value(const uint8_t *p, uint32_t w, uin
     return v;
 }
 
-__global__ void k_agg_dgram(const ngz_dgram_hdr *__restrict__ hdr, const ngz_set_info *__restrict__ sets,
-                            uint32_t n_sets, uint32_t n_dgrams, uint32_t *__restrict__ has_rec) {
-    // has_rec[d] = 1 if the datagram carries >= 1 data record (in any set)
+__host__ __device__ __forceinline__ uint32_t bitrev8(uint32_t x) {
+    x = ((x & 0xF0u) >> 4) | ((x & 0x0Fu) << 4);
+    x = ((x & 0xCCu) >> 2) | ((x & 0x33u) << 2);
+    return ((x & 0xAAu) >> 1) | ((x & 0x55u) << 1);
+}
+
+// Operand of value v for the atomic path.  Signed min/max: sign bit flipped so unsigned order
+// holds.  Ranks: TCPHeaderFlags derives Ord over (FIN, SYN, ..., CWR) in declaration order, so
+// FIN is the most significant (iana/src/tcp.rs:41-70); a sub-registry enum orders by its
+// discriminant: a registered value is its own discriminant, Unassigned(x) comes after every
+// registered variant (generator_sub_registries.rs: `Unassigned(ty)` declared last).
+__device__ __forceinline__ uint64_t value_operand(const AggSlotPlan &sp, const AggParams &P, uint32_t v, uint64_t row) {
+    const uint8_t vc = P.val_vc[v];
+    uint64_t x = load_value(sp.val_col[v] + row * sp.val_w[v], sp.val_w[v], vc == VC_RANK ? VC_UINT : vc);
+    if (vc == VC_SINT && (P.val_op[v] == NGZ_AGG_MIN || P.val_op[v] == NGZ_AGG_MAX)) x ^= 1ull << 63;
+    if (vc == VC_RANK) {
+        if (P.val_tcp[v]) x = bitrev8((uint32_t)x & 0xFF);
+        else {
+            const uint32_t *known = P.rank_known[v];
+            const bool reg = x < 65536 && known && ((known[x >> 5] >> (x & 31)) & 1);
+            if (!reg) x |= 1ull << 32;
+        }
+    }
+    return x;
+}
+
+__global__ void k_agg_dgram(const ngz_set_info *__restrict__ sets, uint32_t n_sets, uint32_t n_dgrams,
+                            uint32_t *__restrict__ has_rec) {
     for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < n_sets; s += gridDim.x * blockDim.x)
         if (sets[s].n && sets[s].dgram < n_dgrams) has_rec[sets[s].dgram] = 1;
 }
@@ -160,36 +274,68 @@ __global__ void k_agg_ts(const ngz_dgram_hdr *__restrict__ hdr, const uint32_t *
         ts[d] = (hdr[d].status == NGZ_DG_OK && has_rec[d]) ? hdr[d].time : 0u;
 }
 
+__device__ __forceinline__ int dom_find(const unsigned long long *dict, uint32_t id) {
+    const unsigned long long key = (1ull << 32) | id;
+    for (int i = 0; i < (int)DOM_SLOTS; ++i)
+        if (dict[i] == key) return i;
+    return -1;
+}
+
 __global__ void k_agg_late(const ngz_dgram_hdr *__restrict__ hdr, const uint32_t *__restrict__ has_rec,
                            const uint32_t *__restrict__ pmax, uint32_t n, uint32_t state_ct, uint64_t lateness_ms,
-                           unsigned long long *__restrict__ dom_tab, uint8_t *__restrict__ dginfo,
-                           unsigned int *__restrict__ err) {
-    for (uint32_t d = blockIdx.x * blockDim.x + threadIdx.x; d < n; d += gridDim.x * blockDim.x) {
-        uint8_t info = 0;
+                           const unsigned long long *__restrict__ dom_dict, uint16_t *__restrict__ dginfo,
+                           unsigned long long *__restrict__ newdom, unsigned int *__restrict__ err) {
+    __shared__ unsigned long long dict[DOM_SLOTS];
+    for (uint32_t i = threadIdx.x; i < DOM_SLOTS; i += blockDim.x) dict[i] = dom_dict[i];
+    __syncthreads();
+    for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
+        const uint32_t d = base + threadIdx.x;
+        if (d >= n) continue;
+        uint16_t info = 0;
         if (hdr[d].status == NGZ_DG_OK && has_rec[d]) {
             uint32_t ct = state_ct;
             if (d > 0 && pmax[d - 1] > ct) ct = pmax[d - 1];
             const bool late = ct != 0 && (int64_t)hdr[d].time * 1000 < (int64_t)ct * 1000 - (int64_t)lateness_ms;
-            if (!late) {
-                // observation domain dictionary: linear probing over DOM_SLOTS entries (1<<32 | id)
-                const unsigned long long key = (1ull << 32) | hdr[d].domain;
-                uint32_t i = (hdr[d].domain * 2654435761u) % DOM_SLOTS, probes = 0;
-                for (;;) {
-                    unsigned long long cur = dom_tab[i];
-                    if (cur == 0) {
-                        cur = atomicCAS(&dom_tab[i], 0ull, key);
-                        if (cur == 0) break;
-                    }
-                    if (cur == key) break;
-                    i = (i + 1) % DOM_SLOTS;
-                    if (++probes == DOM_SLOTS) { atomicOr(err, 1u); i = 0xFF; break; }
-                }
-                if (i != 0xFF) info = (uint8_t)(1u | (i << 1));
+            if (late) {
+                info = DG_LATE;
             } else {
-                info = 0x80;  // late marker (bit 0 clear)
+                const uint32_t id = hdr[d].domain;
+                const int i = dom_find(dict, id);
+                if (i >= 0) {
+                    info = (uint16_t)(DG_USE | (i << 2));
+                } else {
+                    // not in the dictionary yet: list it for the host (set of distinct ids)
+                    info = DG_USE | DG_MISSING;
+                    const unsigned long long key = (1ull << 32) | id;
+                    uint32_t j = (id * 2654435761u) % NEWDOM_SLOTS, probes = 0;
+                    for (;;) {
+                        unsigned long long cur = newdom[j];
+                        if (cur == 0) {
+                            cur = atomicCAS(&newdom[j], 0ull, key);
+                            if (cur == 0) break;
+                        }
+                        if (cur == key) break;
+                        j = (j + 1) % NEWDOM_SLOTS;
+                        if (++probes == NEWDOM_SLOTS) { atomicOr(err, 1u); break; }
+                    }
+                }
             }
         }
         dginfo[d] = info;
+    }
+}
+
+__global__ void k_agg_domfix(const ngz_dgram_hdr *__restrict__ hdr, const unsigned long long *__restrict__ dom_dict,
+                             uint16_t *__restrict__ dginfo, uint32_t n, unsigned int *__restrict__ err) {
+    __shared__ unsigned long long dict[DOM_SLOTS];
+    for (uint32_t i = threadIdx.x; i < DOM_SLOTS; i += blockDim.x) dict[i] = dom_dict[i];
+    __syncthreads();
+    for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
+        const uint32_t d = base + threadIdx.x;
+        if (d >= n || !(dginfo[d] & DG_MISSING)) continue;
+        const int i = dom_find(dict, hdr[d].domain);
+        if (i < 0) { atomicOr(err, 16u); continue; }
+        dginfo[d] = (uint16_t)(DG_USE | (i << 2));
     }
 }
 
@@ -203,6 +349,145 @@ __global__ void k_agg_setidx(const ngz_set_info *__restrict__ sets, const uint32
         const uint32_t n = sets[s].n, r0 = rstart[s];
         for (uint32_t i = lane; i < n; i += 64) setidx[r0 + i] = s;
     }
+}
+
+// Everything the record kernels share: record t -> its set, datagram, row and plan
+struct RecCtx {
+    const ngz_dgram_hdr *hdr;
+    const ngz_set_info *sets;
+    const uint32_t *rstart;
+    const uint32_t *setidx;
+    uint64_t n_rec;
+    uint32_t n_dgrams, n_slots;
+    const uint16_t *dginfo;
+    const AggSlotPlan *plans;
+};
+
+struct Rec {
+    bool valid = false, late = false;
+    ngz_set_info si{};
+    uint16_t info = 0;
+    uint64_t row = 0;
+};
+
+__device__ __forceinline__ Rec rec_of(const RecCtx &C, uint64_t t, unsigned int *err) {
+    Rec r;
+    if (t >= C.n_rec) return r;
+    const uint32_t s = C.setidx[t];
+    r.si = C.sets[s];
+    if (r.si.dgram >= C.n_dgrams || r.si.slot >= C.n_slots) {
+        atomicOr(err, 16u);
+        return r;
+    }
+    r.info = C.dginfo[r.si.dgram];
+    r.late = (r.info & DG_LATE) != 0;
+    r.valid = (r.info & DG_USE) && C.plans[r.si.slot].usable;
+    r.row = r.si.rec0 + (uint32_t)(t - C.rstart[s]);
+    return r;
+}
+
+// Open-addressing probe for one record's group.  exact = false (first pass): a slot whose tag
+// equals the record's is taken as its group (k_agg_check then compares the keys); exact = true
+// (records whose hash collided): keys are compared at every equal tag, probing on past a
+// different key.  Claiming a free slot: CAS on the tag, then the key bytes.
+template <bool EXACT>
+__device__ __forceinline__ uint32_t probe(const AggSlotPlan &sp, const AggParams &P, uint64_t row, uint32_t win,
+                                          uint32_t kp, uint64_t h, unsigned long long *__restrict__ tags,
+                                          uint8_t *__restrict__ rows, uint32_t *__restrict__ claims,
+                                          unsigned long long *__restrict__ n_claims, unsigned int *__restrict__ err) {
+    uint64_t g = slot_of(h) & P.mask;
+    for (uint64_t probes = 0; probes <= P.mask; ++probes, g = (g + 1) & P.mask) {
+        unsigned long long cur = tags[g];
+        if (cur == TAG_EMPTY) {
+            cur = atomicCAS(&tags[g], TAG_EMPTY, (unsigned long long)h);
+            if (cur == TAG_EMPTY) {
+                key_write(rows + g * P.row_bytes, sp, P, row, win, kp);
+                claims[atomicAdd(n_claims, 1ull)] = (uint32_t)g;
+                return (uint32_t)g;
+            }
+        }
+        if (cur != h) continue;
+        if (!EXACT || key_equal(rows + g * P.row_bytes, sp, P, row, win, kp)) return (uint32_t)g;
+    }
+    atomicOr(err, 2u);  // table full
+    return NONE;
+}
+
+// First pass: every record of the push
+__global__ __launch_bounds__(256) void k_agg_claim(const RecCtx C, const AggParams P,
+                                                   unsigned long long *__restrict__ tags, uint8_t *__restrict__ rows,
+                                                   uint32_t *__restrict__ rec_g, uint32_t *__restrict__ claims,
+                                                   unsigned long long *__restrict__ n_claims,
+                                                   unsigned long long *__restrict__ late_count,
+                                                   unsigned int *__restrict__ err) {
+    for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < C.n_rec; base += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t t = base + threadIdx.x;
+        const Rec r = rec_of(C, t, err);
+        const uint64_t late_mask = __ballot(r.late);
+        if ((threadIdx.x & 63) == 0 && late_mask) atomicAdd(late_count, (unsigned long long)__popcll(late_mask));
+        if (t >= C.n_rec) continue;
+        uint32_t g = NONE;
+        if (r.valid) {
+            const AggSlotPlan &sp = C.plans[r.si.slot];
+            const uint32_t ts = C.hdr[r.si.dgram].time, win = ts - ts % 60;  // get_window_start
+            uint32_t kp;
+            const uint64_t h = key_tag(sp, P, r.row, win, kp);
+            g = probe<false>(sp, P, r.row, win, kp, h, tags, rows, claims, n_claims, err);
+        }
+        rec_g[t] = g;
+    }
+}
+
+// Hashed keys: compare each record's key with its slot's (all slots' keys are written by now);
+// a record on another key's slot (64-bit tag collision) is listed for the exact re-probe.
+// list == null: every record; else the records listed.
+__global__ __launch_bounds__(256) void k_agg_check(const RecCtx C, const AggParams P, const uint8_t *__restrict__ rows,
+                                                   uint32_t *__restrict__ rec_g, const uint32_t *__restrict__ list,
+                                                   uint32_t n_list, uint32_t *__restrict__ collided,
+                                                   unsigned int *__restrict__ n_collided,
+                                                   unsigned int *__restrict__ err) {
+    const uint64_t n = list ? n_list : C.n_rec;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t t = list ? list[i] : i;
+        const uint32_t g = rec_g[t];
+        if (g == NONE) continue;
+        const Rec r = rec_of(C, t, err);
+        if (!r.valid) continue;
+        const AggSlotPlan &sp = C.plans[r.si.slot];
+        const uint32_t ts = C.hdr[r.si.dgram].time, win = ts - ts % 60;
+        uint32_t kp;
+        (void)key_tag(sp, P, r.row, win, kp);
+        if (!key_equal(rows + (uint64_t)g * P.row_bytes, sp, P, r.row, win, kp)) {
+            rec_g[t] = NONE;
+            collided[atomicAdd(n_collided, 1u)] = (uint32_t)t;
+        }
+    }
+}
+
+// Exact re-probe of the listed records
+__global__ __launch_bounds__(256) void k_agg_reprobe(const RecCtx C, const AggParams P,
+                                                     unsigned long long *__restrict__ tags, uint8_t *__restrict__ rows,
+                                                     uint32_t *__restrict__ rec_g, const uint32_t *__restrict__ list,
+                                                     uint32_t n_list, uint32_t *__restrict__ claims,
+                                                     unsigned long long *__restrict__ n_claims,
+                                                     unsigned int *__restrict__ err) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n_list; i += gridDim.x * blockDim.x) {
+        const uint64_t t = list[i];
+        const Rec r = rec_of(C, t, err);
+        if (!r.valid) continue;
+        const AggSlotPlan &sp = C.plans[r.si.slot];
+        const uint32_t ts = C.hdr[r.si.dgram].time, win = ts - ts % 60;
+        uint32_t kp;
+        const uint64_t h = key_tag(sp, P, r.row, win, kp);
+        rec_g[t] = probe<true>(sp, P, r.row, win, kp, h, tags, rows, claims, n_claims, err);
+    }
+}
+
+// A failed push releases the slots it claimed (their rows still hold the identity values:
+// a claim writes only the key)
+__global__ void k_agg_unclaim(unsigned long long *__restrict__ tags, const uint32_t *__restrict__ claims, uint64_t n) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        tags[claims[i]] = TAG_EMPTY;
 }
 
 __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
@@ -222,51 +507,6 @@ __device__ __forceinline__ uint64_t wave_reduce(uint64_t v) {  // butterfly over
         v = OP == R_ADD ? v + o : OP == R_MIN ? (o < v ? o : v) : OP == R_MAX ? (o > v ? o : v) : (v | o);
     }
     return v;
-}
-
-// Open-addressing insert of hash h: returns the group's row, the key written by the
-// record that claimed the slot (64-bit CAS on the tag).
-__device__ __forceinline__ uint8_t *group_row(const AggSlotPlan &sp, const AggParams &P, uint64_t row, uint32_t win,
-                                              uint32_t kp, uint64_t h, unsigned long long *__restrict__ tags,
-                                              uint8_t *__restrict__ rows, unsigned int *__restrict__ err,
-                                              bool *claimed = nullptr) {
-    uint64_t g = slot_of(h) & P.mask;
-    bool won = false;
-    if (claimed) *claimed = false;
-    for (uint64_t probes = 0;; ++probes) {
-        unsigned long long cur = tags[g];
-        if (cur == 0) {
-            cur = atomicCAS(&tags[g], 0ull, (unsigned long long)h);
-            if (cur == 0) { won = true; break; }
-        }
-        if (cur == h) break;
-        g = (g + 1) & P.mask;
-        if (probes > P.mask) { atomicOr(err, 2u); return nullptr; }
-    }
-    uint8_t *R = rows + g * P.row_bytes;
-    if (claimed) *claimed = won;
-    if (won) {  // plain stores; read by later kernels only (flush, verify)
-        *(uint32_t *)(R + 0) = win;
-        *(uint32_t *)(R + 4) = sp.proto;
-        *(uint32_t *)(R + 8) = kp;
-        for (uint32_t k = 0; k < P.n_keys; ++k) {
-            const uint8_t *c = sp.key_col[k];
-            const uint32_t w = sp.key_w[k];
-            uint32_t *dst = (uint32_t *)(R + P.key_off[k]);
-            bool nul = false;
-            if (c)
-                for (uint32_t j = 0; j < (w + 3) / 4; ++j) dst[j] = load_word(c + row * w, w, j, sp.key_str[k], nul);
-        }
-    }
-    return R;
-}
-
-// Operand of value v for the accumulator (signed min/max: sign bit flipped so unsigned order holds).
-__device__ __forceinline__ uint64_t value_operand(const AggSlotPlan &sp, const AggParams &P, uint32_t v, uint64_t row) {
-    const uint8_t vc = sp.val_vc[v];
-    uint64_t x = load_value(sp.val_col[v] + row * sp.val_w[v], sp.val_w[v], vc);
-    if (vc == VC_SINT && (P.val_op[v] == NGZ_AGG_MIN || P.val_op[v] == NGZ_AGG_MAX)) x ^= 1ull << 63;
-    return x;
 }
 
 // Conditional atomics: a plain load of the accumulator first.  Min / max / OR only ever
@@ -301,301 +541,211 @@ __device__ __forceinline__ void apply_value_hot(uint8_t *dst, uint8_t op, uint64
     }
 }
 
-template <bool HOT = false>
 __device__ __forceinline__ void apply_push_constants(uint8_t *R, const AggParams &P) {
     // per-push constants once per (group, push): collection time bounds, peer port
-    if ((HOT || peek32(R + 36) != P.push_id) && atomicExch((unsigned int *)(R + 36), P.push_id) != P.push_id) {
+    if (peek32(R + 36) != P.push_id && atomicExch((unsigned int *)(R + 36), P.push_id) != P.push_id) {
         atomicMin((unsigned long long *)(R + 40), (unsigned long long)P.coll_flip);
         atomicMax((unsigned long long *)(R + 48), (unsigned long long)P.coll_flip);
         atomicOr((unsigned long long *)(R + 64), 1ull << P.port_bit);
     }
 }
 
-// One lane per record.  Lanes of a wave that share a group (same key hash) are first
-// reduced across the wave and applied by one lane (wave pre-aggregation: low-cardinality
-// keys would otherwise serialise on a few hot rows); once the largest remaining group of
-// the wave has fewer than 4 records, every remaining lane applies its own record.  Wave
-// results are combined further in a per-workgroup LDS table (CN entries) across all the
-// tiles the workgroup walks, and applied to HBM once per workgroup: hot rows then see one
-// set of atomics per workgroup instead of one per wave.
+// One lane per record, its group's row known (k_agg_claim).  Lanes of a wave that share a
+// group are first reduced across the wave and applied by one lane (wave pre-aggregation:
+// low-cardinality keys would otherwise serialise on a few hot rows); once the largest
+// remaining group of the wave has fewer than 4 records, every remaining lane applies its own
+// record.  Wave results are combined further in a per-workgroup LDS table (CN entries) across
+// all the tiles the workgroup walks, and applied to HBM once per workgroup.  Values of the
+// ordered classes are left to k_agg_ordered.
 constexpr int CN = 64;
-// (256, 4): 4 waves per SIMD (<= 128 VGPRs, no spills); the kernel is latency-bound
 template <int MAXV>  // aggregated fields held in registers (value loads issued together, before any atomic)
-__global__ __launch_bounds__(256, 4) void k_agg_insert(const ngz_dgram_hdr *__restrict__ hdr,
-                                                    const ngz_set_info *__restrict__ sets,
-                                                    const uint32_t *__restrict__ rstart,
-                                                    const uint32_t *__restrict__ setidx, uint64_t n_rec,
-                                                    uint32_t n_dgrams, uint32_t n_slots,
-                                                    const uint8_t *__restrict__ dginfo,
-                                                    const AggSlotPlan *__restrict__ plans, const AggParams P,
-                                                    unsigned long long *__restrict__ tags, uint8_t *__restrict__ rows,
-                                                    unsigned long long *__restrict__ late_count,
+__global__ __launch_bounds__(256, 4) void k_agg_apply(const RecCtx C, const AggParams P,
+                                                    const uint32_t *__restrict__ rec_g, uint8_t *__restrict__ rows,
                                                     unsigned int *__restrict__ err) {
-    __shared__ unsigned long long c_tag[CN], c_cnt[CN], c_tpl[CN], c_d0[CN], c_d1[CN];
+    __shared__ uint32_t c_g[CN];
+    __shared__ unsigned long long c_cnt[CN], c_tpl[CN], c_d0[CN], c_d1[CN];
     __shared__ unsigned long long c_val[CN][NGZ_AGG_MAX_VALUES];
-    __shared__ uint32_t c_slot[CN], c_row[CN], c_win[CN], c_kp[CN], c_tmin[CN], c_tmax[CN], c_smax[CN], c_vp[CN];
+    __shared__ uint32_t c_tmin[CN], c_tmax[CN], c_smax[CN], c_vp[CN];
     for (int e = threadIdx.x; e < CN; e += blockDim.x) {
-        c_tag[e] = c_cnt[e] = c_tpl[e] = c_d0[e] = c_d1[e] = 0;
+        c_g[e] = NONE;
+        c_cnt[e] = c_tpl[e] = c_d0[e] = c_d1[e] = 0;
         c_tmin[e] = 0xFFFFFFFFu;
         c_tmax[e] = c_smax[e] = c_vp[e] = 0;
         for (uint32_t v = 0; v < P.n_vals; ++v) c_val[e][v] = P.val_op[v] == NGZ_AGG_MIN ? ~0ull : 0ull;
     }
     __syncthreads();
     const int lane = threadIdx.x & 63;
-    for (uint64_t tile = blockIdx.x; tile * blockDim.x < n_rec; tile += gridDim.x) {
-    const uint64_t t = tile * blockDim.x + threadIdx.x;
-    bool valid = false, late = false;
-    ngz_set_info si{};
-    uint8_t info = 0;
-    if (t < n_rec) {
-        const uint32_t s = setidx[t];
-        si = sets[s];
-        if (si.dgram >= n_dgrams || si.slot >= n_slots) atomicOr(err, 16u);
-        else {
-            info = dginfo[si.dgram];
-            late = info == 0x80;
-            valid = (info & 1) && plans[si.slot].usable;
-            if (valid) si.rec0 += (uint32_t)(t - rstart[s]);  // the record's row
+    for (uint64_t tile = blockIdx.x; tile * blockDim.x < C.n_rec; tile += gridDim.x) {
+        const uint64_t t = tile * blockDim.x + threadIdx.x;
+        uint32_t g = t < C.n_rec ? rec_g[t] : NONE;
+        Rec r;
+        if (g != NONE) r = rec_of(C, t, err);
+        const bool valid = g != NONE && r.valid;
+        if (!valid) g = NONE;
+        const AggSlotPlan &sp = C.plans[valid ? r.si.slot : 0];
+        const uint64_t row = r.row;
+        uint32_t ts = 0, sysup = 0;
+        uint64_t tpl = 0, dom0 = 0, dom1 = 0;
+        if (valid) {
+            ts = C.hdr[r.si.dgram].time;
+            sysup = C.hdr[r.si.dgram].version == 9 ? C.hdr[r.si.dgram].sys_up_time : 0u;
+            tpl = sp.tpl_bit;
+            const uint32_t db = (r.info >> 2) & 0x7F;
+            (db < 64 ? dom0 : dom1) = 1ull << (db & 63);
         }
-    }
-    const uint64_t late_mask = __ballot(late);
-    if (lane == 0 && late_mask) atomicAdd(late_count, (unsigned long long)__popcll(late_mask));
-    const AggSlotPlan &sp = plans[valid ? si.slot : 0];
-    const uint64_t row = si.rec0;
-    uint32_t ts = 0, win = 0, kp = 0, sysup = 0;
-    uint64_t h = 0, tpl = 0, dom0 = 0, dom1 = 0;
-    if (valid) {
-        ts = hdr[si.dgram].time;
-        win = ts - ts % 60;  // get_window_start: minute floor
-        h = key_hash(sp, P, row, win, kp);
-        sysup = hdr[si.dgram].version == 9 ? hdr[si.dgram].sys_up_time : 0u;
-        tpl = sp.tpl_bit;
-        const uint32_t db = info >> 1;
-        (db < 64 ? dom0 : dom1) = 1ull << (db & 63);
-    }
-    uint64_t xv[MAXV];
-    uint32_t hv = 0, hb = 0;  // aggregated fields present: numeric (in xv) / byte-wise OR
+        uint64_t xv[MAXV];
+        uint32_t hv = 0, hb = 0;  // aggregated fields present: numeric (in xv) / byte-wise OR
 #pragma unroll
-    for (int v = 0; v < MAXV; ++v) {
-        xv[v] = 0;
-        if (valid && v < (int)P.n_vals && sp.val_col[v]) {
-            if (sp.val_vc[v] == VC_BYTES) hb |= 1u << v;
-            else { xv[v] = value_operand(sp, P, v, row); hv |= 1u << v; }
+        for (int v = 0; v < MAXV; ++v) {
+            xv[v] = 0;
+            if (valid && v < (int)P.n_vals && sp.val_col[v] && !vc_ordered(P.val_vc[v])) {
+                if (P.val_vc[v] == VC_BYTES) hb |= 1u << v;
+                else { xv[v] = value_operand(sp, P, v, row); hv |= 1u << v; }
+            }
         }
-    }
-    uint64_t todo = __ballot(valid);
-    // records of one datagram share export time, sys-up time, template and domain: when the
-    // whole wave does, the wave reductions of those are skipped
-    bool hdr_uniform = false;
-    if (todo) {
-        const int l0 = __ffsll((unsigned long long)todo) - 1;
-        const uint64_t u0 = readlane64(((uint64_t)ts << 32) | sysup, l0), u1 = readlane64(tpl, l0),
-                       u2 = readlane64(dom0 | (dom1 ? (1ull << 63) | dom1 : 0ull), l0);
-        const bool same = !valid || ((((uint64_t)ts << 32) | sysup) == u0 && tpl == u1 &&
-                                     (dom0 | (dom1 ? (1ull << 63) | dom1 : 0ull)) == u2);
-        hdr_uniform = __ballot(!same) == 0;
-    }
-    while (todo) {
-        const int leader = __ffsll((unsigned long long)todo) - 1;
-        const uint64_t lh = readlane64(h, leader);
-        const bool mine = valid && ((todo >> lane) & 1) && h == lh;
-        const uint64_t match = __ballot(mine);
-        if (__popcll(match) < 4) break;
-        todo &= ~match;
-        const uint64_t cnt = __popcll(match);
-        if (P.lds_ok) {
-            // combine-table path: the leader claims the group's LDS entry and every matching
-            // lane applies its own record with LDS atomics (no cross-lane reductions)
-            int e0 = -1;
+        uint64_t todo = __ballot(valid);
+        // records of one datagram share export time, sys-up time, template and domain: when the
+        // whole wave does, the wave reductions of those are skipped
+        bool hdr_uniform = false;
+        if (todo) {
+            const int l0 = __ffsll((unsigned long long)todo) - 1;
+            const uint64_t u0 = readlane64(((uint64_t)ts << 32) | sysup, l0), u1 = readlane64(tpl, l0),
+                           u2 = readlane64(dom0 | (dom1 ? (1ull << 63) | dom1 : 0ull), l0);
+            const bool same = !valid || ((((uint64_t)ts << 32) | sysup) == u0 && tpl == u1 &&
+                                         (dom0 | (dom1 ? (1ull << 63) | dom1 : 0ull)) == u2);
+            hdr_uniform = __ballot(!same) == 0;
+        }
+        while (todo) {
+            const int leader = __ffsll((unsigned long long)todo) - 1;
+            const uint32_t lg = (uint32_t)__shfl((int)g, leader);
+            const bool mine = valid && ((todo >> lane) & 1) && g == lg;
+            const uint64_t match = __ballot(mine);
+            if (__popcll(match) < 4) break;
+            todo &= ~match;
+            const uint64_t cnt = __popcll(match);
+            uint8_t *R = rows + (uint64_t)lg * P.row_bytes;
+            if (P.lds_ok) {
+                // combine-table path: the leader claims the group's LDS entry and every matching
+                // lane applies its own record with LDS atomics (no cross-lane reductions)
+                int e0 = -1;
+                if (lane == leader) {
+                    int i = (int)(slot_of(lg) & (CN - 1));
+                    for (int probes = 0; probes < CN; ++probes, i = (i + 1) & (CN - 1)) {
+                        uint32_t cur = c_g[i];
+                        if (cur == NONE) {
+                            cur = atomicCAS(&c_g[i], NONE, lg);
+                            if (cur == NONE) { e0 = i; break; }
+                        }
+                        if (cur == lg) { e0 = i; break; }
+                    }
+                }
+                const int e = __shfl(e0, leader);
+                if (e >= 0) {
+                    if (lane == leader) atomicAdd(&c_cnt[e], (unsigned long long)cnt);
+                    if (hdr_uniform ? lane == leader : mine) {
+                        atomicMin(&c_tmin[e], ts);
+                        atomicMax(&c_tmax[e], ts);
+                        if (sysup) atomicMax(&c_smax[e], sysup);
+                        atomicOr(&c_tpl[e], (unsigned long long)tpl);
+                        if (dom0) atomicOr(&c_d0[e], (unsigned long long)dom0);
+                        if (dom1) atomicOr(&c_d1[e], (unsigned long long)dom1);
+                    }
+                    uint32_t vp = 0;
+#pragma unroll
+                    for (int v = 0; v < MAXV; ++v) {
+                        if (v >= (int)P.n_vals) break;
+                        const bool hasn = mine && ((hv >> v) & 1);
+                        if (__ballot(hasn)) vp |= 1u << v;
+                        if (hasn) {
+                            unsigned long long *c = &c_val[e][v];
+                            switch (P.val_op[v]) {
+                            case NGZ_AGG_ADD: atomicAdd(c, (unsigned long long)xv[v]); break;
+                            case NGZ_AGG_MIN: atomicMin(c, (unsigned long long)xv[v]); break;
+                            case NGZ_AGG_MAX: atomicMax(c, (unsigned long long)xv[v]); break;
+                            default: atomicOr(c, (unsigned long long)xv[v]); break;
+                            }
+                        }
+                    }
+                    if (lane == leader && vp) atomicOr(&c_vp[e], vp);
+                    continue;  // the wave's next group
+                }
+            }
+            uint64_t tmin = ts, tmax = ts, smax = sysup, tpls = tpl, d0 = dom0, d1 = dom1;  // (leader's own)
+            if (!hdr_uniform) {
+                tmin = wave_reduce<R_MIN>(mine ? ts : 0xFFFFFFFFull);
+                tmax = wave_reduce<R_MAX>(mine ? ts : 0ull);
+                smax = wave_reduce<R_MAX>(mine ? sysup : 0ull);
+                tpls = wave_reduce<R_OR>(mine ? tpl : 0ull);
+                d0 = wave_reduce<R_OR>(mine ? dom0 : 0ull);
+                d1 = wave_reduce<R_OR>(mine ? dom1 : 0ull);
+            }
             if (lane == leader) {
-                int i = (int)(slot_of(h) & (CN - 1));
-                for (int probes = 0; probes < CN; ++probes, i = (i + 1) & (CN - 1)) {
-                    unsigned long long cur = c_tag[i];
-                    if (cur == 0) {
-                        cur = atomicCAS(&c_tag[i], 0ull, (unsigned long long)h);
-                        if (cur == 0) {
-                            c_slot[i] = si.slot;
-                            c_row[i] = (uint32_t)row;
-                            c_win[i] = win;
-                            c_kp[i] = kp;
-                            e0 = i;
-                            break;
-                        }
-                    }
-                    if (cur == h) { e0 = i; break; }
-                }
-            }
-            const int e = __shfl(e0, leader);
-            if (e >= 0) {
-                if (lane == leader) atomicAdd(&c_cnt[e], (unsigned long long)cnt);
-                if (hdr_uniform ? lane == leader : mine) {
-                    atomicMin(&c_tmin[e], ts);
-                    atomicMax(&c_tmax[e], ts);
-                    if (sysup) atomicMax(&c_smax[e], sysup);
-                    atomicOr(&c_tpl[e], (unsigned long long)tpl);
-                    if (dom0) atomicOr(&c_d0[e], (unsigned long long)dom0);
-                    if (dom1) atomicOr(&c_d1[e], (unsigned long long)dom1);
-                }
-                uint32_t vp = 0;
-#pragma unroll
-                for (int v = 0; v < MAXV; ++v) {
-                    if (v >= (int)P.n_vals) break;
-                    const bool hasn = mine && ((hv >> v) & 1);
-                    if (__ballot(hasn)) vp |= 1u << v;
-                    if (hasn) {
-                        unsigned long long *c = &c_val[e][v];
-                        switch (P.val_op[v]) {
-                        case NGZ_AGG_ADD: atomicAdd(c, (unsigned long long)xv[v]); break;
-                        case NGZ_AGG_MIN: atomicMin(c, (unsigned long long)xv[v]); break;
-                        case NGZ_AGG_MAX: atomicMax(c, (unsigned long long)xv[v]); break;
-                        default: atomicOr(c, (unsigned long long)xv[v]); break;
-                        }
-                    }
-                }
-                if (lane == leader && vp) atomicOr(&c_vp[e], vp);
-                continue;  // the wave's next group
-            }
-        }
-        uint64_t tmin = ts, tmax = ts, smax = sysup, tpls = tpl, d0 = dom0, d1 = dom1;  // (leader's own)
-        if (!hdr_uniform) {
-            tmin = wave_reduce<R_MIN>(mine ? ts : 0xFFFFFFFFull);
-            tmax = wave_reduce<R_MAX>(mine ? ts : 0ull);
-            smax = wave_reduce<R_MAX>(mine ? sysup : 0ull);
-            tpls = wave_reduce<R_OR>(mine ? tpl : 0ull);
-            d0 = wave_reduce<R_OR>(mine ? dom0 : 0ull);
-            d1 = wave_reduce<R_OR>(mine ? dom1 : 0ull);
-        }
-        uint8_t *R = nullptr;
-        int e = -1;
-        if (lane == leader && P.lds_ok) {  // workgroup combine table (linear probing, CAS on the tag)
-            int i = (int)(slot_of(h) & (CN - 1));
-            for (int probes = 0; probes < CN; ++probes, i = (i + 1) & (CN - 1)) {
-                unsigned long long cur = c_tag[i];
-                if (cur == 0) {
-                    cur = atomicCAS(&c_tag[i], 0ull, (unsigned long long)h);
-                    if (cur == 0) {
-                        c_slot[i] = si.slot;
-                        c_row[i] = (uint32_t)row;
-                        c_win[i] = win;
-                        c_kp[i] = kp;
-                        e = i;
-                        break;
-                    }
-                }
-                if (cur == h) { e = i; break; }
-            }
-            if (e >= 0) {
-                atomicAdd(&c_cnt[e], (unsigned long long)cnt);
-                atomicMin(&c_tmin[e], (uint32_t)tmin);
-                atomicMax(&c_tmax[e], (uint32_t)tmax);
-                atomicMax(&c_smax[e], (uint32_t)smax);
-                atomicOr(&c_tpl[e], (unsigned long long)tpls);
-                atomicOr(&c_d0[e], (unsigned long long)d0);
-                atomicOr(&c_d1[e], (unsigned long long)d1);
-            }
-        }
-        if (lane == leader && e < 0) {
-            R = group_row(sp, P, row, win, kp, h, tags, rows, err);
-            if (R) {
-                atomicAdd((unsigned long long *)(R + 16), (unsigned long long)cnt);
                 // hot rows: fire-and-forget atomics (a load of a contended line costs more)
+                atomicAdd((unsigned long long *)(R + 16), (unsigned long long)cnt);
                 atomicMin((unsigned int *)(R + 24), (uint32_t)tmin);
                 atomicMax((unsigned int *)(R + 28), (uint32_t)tmax);
                 if (smax) atomicMax((unsigned int *)(R + 32), (uint32_t)smax);
                 atomicOr((unsigned long long *)(R + 56), (unsigned long long)tpls);
                 if (d0) atomicOr((unsigned long long *)(R + 72), (unsigned long long)d0);
                 if (d1) atomicOr((unsigned long long *)(R + 80), (unsigned long long)d1);
-                apply_push_constants<true>(R, P);
+                apply_push_constants(R, P);
             }
-        }
-        uint32_t vp = 0;
+            uint32_t vp = 0;
 #pragma unroll
-        for (int v = 0; v < MAXV; ++v) {
-            if (v >= (int)P.n_vals) break;
-            const bool hasn = mine && ((hv >> v) & 1), bytes = mine && ((hb >> v) & 1);
-            const bool any_num = __ballot(hasn) != 0, any_bytes = __ballot(bytes) != 0;
-            if (!any_num && !any_bytes) continue;
-            vp |= 1u << v;
-            const uint8_t op = P.val_op[v];
-            const uint64_t x = hasn ? xv[v] : (op == NGZ_AGG_MIN ? ~0ull : 0ull);
-            uint64_t r = 0;
-            if (any_num) switch (op) {
-            case NGZ_AGG_ADD: r = wave_reduce<R_ADD>(x); break;
-            case NGZ_AGG_MIN: r = wave_reduce<R_MIN>(x); break;
-            case NGZ_AGG_MAX: r = wave_reduce<R_MAX>(x); break;
-            default: r = wave_reduce<R_OR>(x); break;
-            }
-            if (lane == leader && any_num) {
-                if (e >= 0) {
-                    unsigned long long *c = &c_val[e][v];
-                    switch (op) {
-                    case NGZ_AGG_ADD: atomicAdd(c, (unsigned long long)r); break;
-                    case NGZ_AGG_MIN: atomicMin(c, (unsigned long long)r); break;
-                    case NGZ_AGG_MAX: atomicMax(c, (unsigned long long)r); break;
-                    default: atomicOr(c, (unsigned long long)r); break;
-                    }
-                } else if (R) {
-                    apply_value_hot(R + P.val_off[v], op, r);
+            for (int v = 0; v < MAXV; ++v) {
+                if (v >= (int)P.n_vals) break;
+                const bool hasn = mine && ((hv >> v) & 1), bytes = mine && ((hb >> v) & 1);
+                const bool any_num = __ballot(hasn) != 0, any_bytes = __ballot(bytes) != 0;
+                if (!any_num && !any_bytes) continue;
+                vp |= 1u << v;
+                const uint8_t op = P.val_op[v];
+                const uint64_t x = hasn ? xv[v] : (op == NGZ_AGG_MIN ? ~0ull : 0ull);
+                uint64_t rr = 0;
+                if (any_num) switch (op) {
+                case NGZ_AGG_ADD: rr = wave_reduce<R_ADD>(x); break;
+                case NGZ_AGG_MIN: rr = wave_reduce<R_MIN>(x); break;
+                case NGZ_AGG_MAX: rr = wave_reduce<R_MAX>(x); break;
+                default: rr = wave_reduce<R_OR>(x); break;
                 }
-            }
-            if (any_bytes) {  // byte ORs: each matching lane ORs its words into the leader's row
-                const uint64_t Rl = readlane64((uint64_t)R, leader);
-                if (bytes && Rl) {
+                if (lane == leader && any_num) apply_value_hot(R + P.val_off[v], op, rr);
+                if (bytes) {  // byte ORs: each matching lane ORs its words into the row
                     const uint32_t w = sp.val_w[v];
                     bool nul = false;
-                    for (uint32_t j = 0; j < (w + 3) / 4; ++j) {
-                        const uint32_t y = load_word(sp.val_col[v] + row * w, w, j, false, nul);
-                        or32((uint8_t *)Rl + P.val_off[v] + 4 * j, y);
-                    }
+                    for (uint32_t j = 0; j < (w + 3) / 4; ++j)
+                        or32(R + P.val_off[v] + 4 * j, cell_word(sp.val_col[v] + row * w, w, j, false, nul));
                 }
             }
+            if (lane == leader && vp) atomicOr((unsigned int *)(R + 12), vp);
         }
-        if (lane == leader && e >= 0 && vp) atomicOr(&c_vp[e], vp);
-        if (lane == leader && R && vp) atomicOr((unsigned int *)(R + 12), vp);
-    }
-    if (!(valid && ((todo >> lane) & 1))) continue;
-    // per-record path
-    bool claimed;
-    uint8_t *R = group_row(sp, P, row, win, kp, h, tags, rows, err, &claimed);
-    if (!R) continue;
-    atomicAdd((unsigned long long *)(R + 16), 1ull);
-    if (claimed) {  // a row this record just claimed: a pre-load would only read the identities back
-        atomicMin((unsigned int *)(R + 24), ts);
-        atomicMax((unsigned int *)(R + 28), ts);
-        if (sysup) atomicMax((unsigned int *)(R + 32), sysup);
-        atomicOr((unsigned long long *)(R + 56), (unsigned long long)tpl);
-        atomicOr((unsigned long long *)(R + (dom0 ? 72 : 80)), (unsigned long long)(dom0 | dom1));
-        apply_push_constants<true>(R, P);
-    } else {
+        if (!(valid && ((todo >> lane) & 1))) continue;
+        // per-record path
+        uint8_t *R = rows + (uint64_t)g * P.row_bytes;
+        atomicAdd((unsigned long long *)(R + 16), 1ull);
         min32(R + 24, ts);
         max32(R + 28, ts);
         max32(R + 32, sysup);
         or64(R + 56, tpl);
         or64(R + (dom0 ? 72 : 80), dom0 | dom1);
         apply_push_constants(R, P);
-    }
 #pragma unroll
-    for (int v = 0; v < MAXV; ++v) {
-        if (v >= (int)P.n_vals) break;
-        uint8_t *dst = R + P.val_off[v];
-        if ((hv >> v) & 1) {
-            if (claimed) apply_value_hot(dst, P.val_op[v], xv[v]);
-            else apply_value(dst, P.val_op[v], xv[v]);
-        } else if ((hb >> v) & 1) {  // BoolMapOr over bytes (mac, mpls label, octetArray, u256)
-            const uint32_t w = sp.val_w[v];
-            bool nul = false;
-            for (uint32_t j = 0; j < (w + 3) / 4; ++j) or32(dst + 4 * j, load_word(sp.val_col[v] + row * w, w, j, false, nul));
+        for (int v = 0; v < MAXV; ++v) {
+            if (v >= (int)P.n_vals) break;
+            uint8_t *dst = R + P.val_off[v];
+            if ((hv >> v) & 1) {
+                apply_value(dst, P.val_op[v], xv[v]);
+            } else if ((hb >> v) & 1) {  // BoolMapOr over bytes (mac, mpls label, octetArray, u256)
+                const uint32_t w = sp.val_w[v];
+                bool nul = false;
+                for (uint32_t j = 0; j < (w + 3) / 4; ++j) or32(dst + 4 * j, cell_word(sp.val_col[v] + row * w, w, j, false, nul));
+            }
         }
-    }
-    if (claimed) atomicOr((unsigned int *)(R + 12), hv | hb);
-    else or32(R + 12, hv | hb);
+        or32(R + 12, hv | hb);
     }  // tiles
     __syncthreads();
     for (int e = threadIdx.x; e < CN; e += blockDim.x) {  // the workgroup's combined groups -> HBM
-        const unsigned long long h = c_tag[e];
-        if (!h) continue;
-        uint8_t *R = group_row(plans[c_slot[e]], P, c_row[e], c_win[e], c_kp[e], h, tags, rows, err);
-        if (!R) continue;
+        const uint32_t gg = c_g[e];
+        if (gg == NONE) continue;
+        uint8_t *R = rows + (uint64_t)gg * P.row_bytes;
         atomicAdd((unsigned long long *)(R + 16), c_cnt[e]);
         min32(R + 24, c_tmin[e]);
         max32(R + 28, c_tmax[e]);
@@ -611,45 +761,85 @@ __global__ __launch_bounds__(256, 4) void k_agg_insert(const ngz_dgram_hdr *__re
     }
 }
 
-__global__ __launch_bounds__(256) void k_agg_verify(const ngz_dgram_hdr *__restrict__ hdr,
-                                                    const ngz_set_info *__restrict__ sets,
-                                                    const uint32_t *__restrict__ rstart,
-                                                    const uint32_t *__restrict__ setidx, uint64_t n_rec,
-                                                    uint32_t n_dgrams, uint32_t n_slots,
-                                                    const uint8_t *__restrict__ dginfo,
-                                                    const AggSlotPlan *__restrict__ plans, const AggParams P,
-                                                    const unsigned long long *__restrict__ tags,
-                                                    const uint8_t *__restrict__ rows, unsigned int *__restrict__ err) {
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n_rec) return;
-    const uint32_t s = setidx[t];
-    const ngz_set_info si = sets[s];
-    if (si.dgram >= n_dgrams || si.slot >= n_slots) return;
-    if (!(dginfo[si.dgram] & 1)) return;
-    const AggSlotPlan &sp = plans[si.slot];
-    if (!sp.usable) return;
-    const uint64_t row = si.rec0 + (uint32_t)(t - rstart[s]);
-    const uint32_t ts = hdr[si.dgram].time;
-    const uint32_t win = ts - ts % 60;
-    uint32_t kp;
-    const uint64_t h = key_hash(sp, P, row, win, kp);
-    uint64_t g = slot_of(h) & P.mask;
-    for (uint64_t probes = 0; tags[g] != h; ++probes) {
-        g = (g + 1) & P.mask;
-        if (probes > P.mask) { atomicOr(err, 4u); return; }
+__global__ void k_agg_iota(uint32_t *__restrict__ x, uint64_t n) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        x[i] = (uint32_t)i;
+}
+
+// OrderedFloat's Ord (ordered_float: NaN equals NaN and is greater than every number; -0 == +0)
+template <class F>
+__device__ __forceinline__ int ofloat_cmp(F a, F b) {
+    const bool na = a != a, nb = b != b;
+    if (na || nb) return na == nb ? 0 : (na ? 1 : -1);
+    return a < b ? -1 : (a > b ? 1 : 0);
+}
+
+// Ord::min / Ord::max (core::cmp::min_by / max_by): on equal, min keeps the first argument
+// (the group's value) and max takes the second (the record's) -- `*v1 = (*v1).min(*v2)`
+__device__ __forceinline__ bool take_new(uint8_t op, int cmp_cur_new) {
+    return op == NGZ_AGG_MIN ? cmp_cur_new > 0 : cmp_cur_new <= 0;
+}
+
+// One thread per group present in the sorted record list: the ordered reductions folded in
+// record order (the stable sort kept it within a group), from the group's value.
+__global__ __launch_bounds__(256) void k_agg_ordered(const RecCtx C, const AggParams P,
+                                                     const uint32_t *__restrict__ sg, const uint32_t *__restrict__ sr,
+                                                     uint64_t n, uint8_t *__restrict__ rows,
+                                                     unsigned int *__restrict__ err) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t g = sg[i];
+        if (g == NONE || (i > 0 && sg[i - 1] == g)) continue;  // not the first record of its group
+        uint8_t *R = rows + (uint64_t)g * P.row_bytes;
+        uint32_t vp = *(const uint32_t *)(R + 12);
+        for (uint32_t v = 0; v < P.n_vals; ++v) {
+            const uint8_t vc = P.val_vc[v];
+            if (!vc_ordered(vc)) continue;
+            const uint8_t op = P.val_op[v];
+            bool have = (vp >> v) & 1;
+            uint8_t *dst = R + P.val_off[v];
+            double cd = 0;
+            float cf = 0;
+            uint8_t c6[16];
+            if (have) {
+                if (vc == VC_F64) memcpy(&cd, dst, 8);
+                else if (vc == VC_F32) memcpy(&cf, dst, 4);
+                else memcpy(c6, dst, 16);
+            }
+            for (uint64_t j = i; j < n && sg[j] == g; ++j) {
+                const Rec r = rec_of(C, sr[j], err);
+                if (!r.valid) continue;
+                const AggSlotPlan &sp = C.plans[r.si.slot];
+                if (!sp.val_col[v]) continue;
+                const uint8_t *cell = sp.val_col[v] + r.row * sp.val_w[v];
+                if (vc == VC_F64) {
+                    double x;
+                    memcpy(&x, cell, 8);
+                    if (!have) cd = x;
+                    else if (op == NGZ_AGG_ADD) cd = cd + x;
+                    else if (take_new(op, ofloat_cmp(cd, x))) cd = x;
+                } else if (vc == VC_F32) {
+                    float x;
+                    memcpy(&x, cell, 4);
+                    if (!have) cf = x;
+                    else if (op == NGZ_AGG_ADD) cf = cf + x;
+                    else if (take_new(op, ofloat_cmp(cf, x))) cf = x;
+                } else {  // Ipv6Addr: octets in order
+                    int c = 0;
+                    if (have)
+                        for (int b = 0; b < 16 && c == 0; ++b) c = (int)c6[b] - (int)cell[b];
+                    if (!have || take_new(op, c)) memcpy(c6, cell, 16);
+                }
+                have = true;
+            }
+            if (have) {
+                if (vc == VC_F64) memcpy(dst, &cd, 8);
+                else if (vc == VC_F32) { memcpy(dst, &cf, 4); memset(dst + 4, 0, 4); }
+                else memcpy(dst, c6, 16);
+                vp |= 1u << v;
+            }
+        }
+        *(uint32_t *)(R + 12) = vp;
     }
-    const uint8_t *R = rows + g * P.row_bytes;
-    bool same = *(const uint32_t *)(R + 0) == win && *(const uint32_t *)(R + 4) == sp.proto &&
-                *(const uint32_t *)(R + 8) == kp;
-    for (uint32_t k = 0; k < P.n_keys && same; ++k) {
-        const uint8_t *c = sp.key_col[k];
-        if (!c) continue;
-        const uint32_t w = sp.key_w[k];
-        bool nul = false;
-        for (uint32_t j = 0; j < (w + 3) / 4; ++j)
-            same = same && ((const uint32_t *)(R + P.key_off[k]))[j] == load_word(c + row * w, w, j, sp.key_str[k], nul);
-    }
-    if (!same) atomicOr(err, 8u);
 }
 
 __global__ void k_agg_init(uint8_t *__restrict__ rows, uint64_t n_groups, uint32_t row_bytes,
@@ -661,24 +851,72 @@ __global__ void k_agg_init(uint8_t *__restrict__ rows, uint64_t n_groups, uint32
         ((uint32_t *)rows)[i] = ident[i % ident_words];
 }
 
-__global__ void k_agg_count(const unsigned long long *__restrict__ tags, uint64_t n_groups,
+// groups selected for output: every live group (cutoff == INT64_MAX) or the closed windows
+__device__ __forceinline__ bool selected(uint64_t tag, const uint8_t *R, int64_t cutoff_s) {
+    return tag_live(tag) && (int64_t)*(const uint32_t *)R <= cutoff_s;
+}
+
+__global__ void k_agg_count(const unsigned long long *__restrict__ tags, const uint8_t *__restrict__ rows,
+                            uint64_t n_slots, uint32_t row_bytes, int64_t cutoff_s,
                             unsigned long long *__restrict__ cursor) {
     uint32_t c = 0;
-    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n_groups;
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n_slots;
          g += (uint64_t)gridDim.x * blockDim.x)
-        c += tags[g] != 0;
+        c += selected(tags[g], rows + g * row_bytes, cutoff_s);
     if (c) atomicAdd(cursor, (unsigned long long)c);
 }
 
-__global__ void k_agg_compact(const unsigned long long *__restrict__ tags, const uint8_t *__restrict__ rows,
-                              uint64_t n_groups, uint32_t row_bytes, uint8_t *__restrict__ out,
-                              unsigned long long *__restrict__ cursor) {
-    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n_groups;
+// copies the selected groups to out; tomb: their slots become tombstones (closed windows)
+__global__ void k_agg_take(unsigned long long *__restrict__ tags, const uint8_t *__restrict__ rows, uint64_t n_slots,
+                           uint32_t row_bytes, int64_t cutoff_s, int tomb, uint8_t *__restrict__ out,
+                           unsigned long long *__restrict__ cursor) {
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n_slots;
          g += (uint64_t)gridDim.x * blockDim.x) {
-        if (!tags[g]) continue;
+        const uint8_t *R = rows + g * row_bytes;
+        if (!selected(tags[g], R, cutoff_s)) continue;
         const uint64_t o = atomicAdd(cursor, 1ull);
-        const uint32_t *src = (const uint32_t *)(rows + g * row_bytes);
+        const uint32_t *src = (const uint32_t *)R;
         uint32_t *dst = (uint32_t *)(out + o * row_bytes);
+        for (uint32_t i = 0; i < row_bytes / 4; ++i) dst[i] = src[i];
+        if (tomb) tags[g] = TAG_TOMB;
+    }
+}
+
+// OR of the set bitmaps of every live group (dictionary entries still in use)
+__global__ void k_agg_bits(const unsigned long long *__restrict__ tags, const uint8_t *__restrict__ rows,
+                           uint64_t n_slots, uint32_t row_bytes, unsigned long long *__restrict__ used) {
+    unsigned long long tpl = 0, port = 0, d0 = 0, d1 = 0;
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n_slots;
+         g += (uint64_t)gridDim.x * blockDim.x) {
+        if (!tag_live(tags[g])) continue;
+        const uint8_t *R = rows + g * row_bytes;
+        tpl |= *(const uint64_t *)(R + 56);
+        port |= *(const uint64_t *)(R + 64);
+        d0 |= *(const uint64_t *)(R + 72);
+        d1 |= *(const uint64_t *)(R + 80);
+    }
+    if (tpl) atomicOr(&used[0], tpl);
+    if (port) atomicOr(&used[1], port);
+    if (d0) atomicOr(&used[2], d0);
+    if (d1) atomicOr(&used[3], d1);
+}
+
+// rehash the live groups into an empty table (drops the tombstones)
+__global__ void k_agg_rehash(const unsigned long long *__restrict__ tags, const uint8_t *__restrict__ rows,
+                             uint64_t n_slots, uint32_t row_bytes, unsigned long long *__restrict__ ntags,
+                             uint8_t *__restrict__ nrows, unsigned int *__restrict__ err) {
+    const uint64_t mask = n_slots - 1;
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n_slots;
+         g += (uint64_t)gridDim.x * blockDim.x) {
+        const unsigned long long h = tags[g];
+        if (!tag_live(h)) continue;
+        uint64_t s = slot_of(h) & mask, probes = 0;
+        while (atomicCAS(&ntags[s], TAG_EMPTY, h) != TAG_EMPTY) {  // every live group is distinct
+            s = (s + 1) & mask;
+            if (++probes > mask) { atomicOr(err, 2u); break; }
+        }
+        const uint32_t *src = (const uint32_t *)(rows + g * row_bytes);
+        uint32_t *dst = (uint32_t *)(nrows + s * row_bytes);
         for (uint32_t i = 0; i < row_bytes / 4; ++i) dst[i] = src[i];
     }
 }
@@ -693,16 +931,19 @@ struct ngz_agg {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     std::string last_error;
+    bool poisoned = false;
     std::vector<ngz_agg_field> keys, vals;
     uint64_t window_ms = 0, lateness_ms = 0;
-    uint64_t cap = 0;
+    uint64_t slots = 0;      // table slots (power of two)
+    uint64_t limit = 0;      // groups held at most (the capacity asked for)
+    uint64_t live = 0, tombs = 0;
     AggParams P{};
-    // per-value state fixed at first sight: column width and value class
-    std::vector<int> val_w, val_vc, key_w;
-    std::vector<uint8_t> val_dtype;
-    // dictionaries (host) for template ids and peer ports
-    std::vector<uint32_t> templates;
-    std::vector<uint16_t> ports;
+    // fixed at first sight: column width and decoded kind of every key / value
+    std::vector<int> val_w, key_w, key_kind_seen, val_kind_seen;
+    // dictionaries: entry = value, -1 = free (bits of groups refer to entry positions)
+    std::vector<int64_t> templates, ports, domains;
+    // the dictionaries as of the last flush / emit (the rows it returned refer to them)
+    std::vector<int64_t> out_templates, out_ports, out_domains;
     uint32_t current_time = 0;  // the peer's event time (seconds), 0 = none yet
     uint32_t push_id = 0;
     float t_push = 0;
@@ -710,17 +951,22 @@ struct ngz_agg {
     unsigned long long *tags = nullptr;
     uint8_t *rows = nullptr;
     uint32_t *ident = nullptr;
-    unsigned long long *dom_tab = nullptr;
+    unsigned long long *dom_dict = nullptr;
+    unsigned long long *newdom = nullptr;
     unsigned int *err = nullptr;
     unsigned long long *late = nullptr;
     unsigned long long *cursor = nullptr;
+    unsigned long long *n_claims = nullptr;
+    unsigned int *n_coll = nullptr;
+    unsigned long long *used = nullptr;
+    uint32_t *rank_maps = nullptr;  // one 65536-bit map per VC_RANK sub-registry value
     AggSlotPlan *plans = nullptr;
     uint32_t plans_cap = 0;
     // scratch, grown on demand
     void *scratch = nullptr;
     size_t scratch_cap = 0;
-    uint32_t *setidx = nullptr;
-    uint64_t setidx_cap = 0;
+    uint8_t *rec_buf = nullptr;  // setidx, rec_g, claims, collided lists, sort buffers
+    size_t rec_cap = 0;
 };
 
 namespace {
@@ -733,7 +979,10 @@ int fail(ngz_agg *a, int rc, const std::string &msg) {
 #define AGG_HIP(a, x)                                                                     \
     do {                                                                                  \
         hipError_t e_ = (x);                                                              \
-        if (e_ != hipSuccess) return fail(a, NGZ_E_DEVICE, std::string(#x ": ") + hipGetErrorString(e_)); \
+        if (e_ != hipSuccess) {                                                           \
+            (a)->poisoned = true;                                                         \
+            return fail(a, NGZ_E_DEVICE, std::string(#x ": ") + hipGetErrorString(e_));   \
+        }                                                                                 \
     } while (0)
 
 uint32_t grid_for(uint64_t n, uint32_t block = 256, uint32_t max_blocks = 8192) {
@@ -742,54 +991,212 @@ uint32_t grid_for(uint64_t n, uint32_t block = 256, uint32_t max_blocks = 8192) 
     return (uint32_t)std::min<uint64_t>(g, max_blocks);
 }
 
-int reset_table(ngz_agg *a) {
-    AGG_HIP(a, hipMemsetAsync(a->tags, 0, a->cap * 8, a->stream));
-    hipLaunchKernelGGL(k_agg_init, dim3(8192), dim3(256), 0, a->stream, a->rows, a->cap, a->P.row_bytes, a->ident,
+int reset_rows(ngz_agg *a, unsigned long long *tags, uint8_t *rows) {
+    AGG_HIP(a, hipMemsetAsync(tags, 0, a->slots * 8, a->stream));
+    hipLaunchKernelGGL(k_agg_init, dim3(8192), dim3(256), 0, a->stream, rows, a->slots, a->P.row_bytes, a->ident,
                        a->P.row_bytes / 4);
     AGG_HIP(a, hipGetLastError());
     return NGZ_OK;
 }
 
-// Which reductions the device runs for an IE data type (generator.rs:580-629,
-// config.rs:212-250).  Returns the value class or -1 with a reason.
+// Value class of (IE, op), following IE::supports_{arithmetic,comparison,bitwise}_ops
+// (generator.rs:1176-1272) for acceptance and the generated Field ops (generator.rs:580-629,
+// 896-1080) for the arithmetic.  Returns the value class or -1 (rejected by the reference's
+// validate_operation_compatibility, config.rs:212-250) or -2 (accepted there, not on the
+// device: why says which).
 int value_class(const ngzh::IeRow *r, uint8_t op, std::string &why) {
     using namespace ngzh;
-    const uint8_t dt = r ? r->dtype : DT_octetArray;
+    const uint8_t dt = r ? r->dtype : DT_octetArray;  // IE::Unknown: octetArray
     const bool subreg = r && (r->flags & 4);
     const bool tcp = r && (r->flags & 2);
+    const bool ident_or_flags = r && (r->flags & (8 | 16));
     const bool integer = dt == DT_unsigned8 || dt == DT_unsigned16 || dt == DT_unsigned32 || dt == DT_unsigned64 ||
                          dt == DT_signed8 || dt == DT_signed16 || dt == DT_signed32 || dt == DT_signed64;
     const bool sgn = dt == DT_signed8 || dt == DT_signed16 || dt == DT_signed32 || dt == DT_signed64;
+    const bool flt = dt == DT_float32 || dt == DT_float64;
     switch (op) {
     case NGZ_AGG_ADD:
-        if (dt == DT_float32 || dt == DT_float64) { why = "float addition is order dependent (not on device)"; return -1; }
-        if (!integer || subreg || tcp) { why = "field does not support arithmetic operations"; return -1; }
+        if (ident_or_flags || subreg || !(integer || flt)) { why = "field does not support arithmetic operations"; return -1; }
+        if (flt) return dt == DT_float32 ? VC_F32 : VC_F64;
         return sgn ? VC_SINT : VC_UINT;
     case NGZ_AGG_MIN:
     case NGZ_AGG_MAX:
-        if (dt == DT_float32 || dt == DT_float64 || dt == DT_macAddress || dt == DT_ipv6Address || subreg || tcp ||
-            dt == DT_boolean) {
-            why = "comparison of this type is not on the device yet";
+        if (!(integer || flt || dt == DT_dateTimeSeconds || dt == DT_dateTimeMilliseconds ||
+              dt == DT_dateTimeMicroseconds || dt == DT_dateTimeNanoseconds || dt == DT_ipv4Address ||
+              dt == DT_ipv6Address || dt == DT_basicList || dt == DT_subTemplateList || dt == DT_subTemplateMultiList)) {
+            why = "field does not support comparison operations";
             return -1;
+        }
+        if (dt == DT_basicList || dt == DT_subTemplateList || dt == DT_subTemplateMultiList) {
+            why = "list fields are variable-length (not on the device)";
+            return -2;
+        }
+        if (flt) return dt == DT_float32 ? VC_F32 : VC_F64;
+        if (dt == DT_ipv6Address) return VC_IPV6;
+        if (tcp || subreg) {
+            if (subreg && !tcp && ngzh::subreg_kind(r->pen, r->id) != 1) {
+                why = "Min/Max over a nested reason-code sub-registry is not on the device";
+                return -2;
+            }
+            return VC_RANK;
         }
         if (integer || dt == DT_ipv4Address || dt == DT_dateTimeSeconds) return sgn ? VC_SINT : VC_UINT;
         if (dt == DT_dateTimeMilliseconds) return VC_SINT;
-        if (dt == DT_dateTimeMicroseconds || dt == DT_dateTimeNanoseconds) return VC_DTFRAC;
-        why = "field does not support comparison operations";
-        return -1;
+        return VC_DTFRAC;
     case NGZ_AGG_OR:
-        if (dt == DT_float32 || dt == DT_float64 || dt == DT_string || dt == DT_basicList ||
-            dt == DT_subTemplateList || dt == DT_subTemplateMultiList || dt == DT_dateTimeSeconds ||
-            dt == DT_dateTimeMilliseconds || dt == DT_dateTimeMicroseconds || dt == DT_dateTimeNanoseconds) {
+        if (flt || dt == DT_string || dt == DT_basicList || dt == DT_subTemplateList || dt == DT_subTemplateMultiList ||
+            dt == DT_dateTimeSeconds || dt == DT_dateTimeMilliseconds || dt == DT_dateTimeMicroseconds ||
+            dt == DT_dateTimeNanoseconds) {
             why = "field does not support bitwise operations";
             return -1;
         }
-        if (subreg && !tcp) { why = "bitwise OR of sub-registry values is not on the device yet"; return -1; }
+        // sub-registry enums OR their raw values (generator_sub_registries.rs: BitOrAssign)
         if (integer || dt == DT_boolean || dt == DT_ipv4Address) return VC_UINT;
         return VC_BYTES;  // octetArray, macAddress, ipv6Address, unsigned256
     }
     why = "unknown op";
     return -1;
+}
+
+uint32_t value_slot_bytes(int vc) { return vc == VC_BYTES ? 32 : vc == VC_IPV6 ? 16 : 8; }
+
+// dictionary entry for value x (reusing a free position), or -1 when all SET_BITS / cap are used
+int dict_put(std::vector<int64_t> &d, int64_t x, uint32_t cap) {
+    for (size_t i = 0; i < d.size(); ++i)
+        if (d[i] == x) return (int)i;
+    for (size_t i = 0; i < d.size(); ++i)
+        if (d[i] < 0) { d[i] = x; return (int)i; }
+    if (d.size() >= cap) return -1;
+    d.push_back(x);
+    return (int)d.size() - 1;
+}
+
+// Frees the dictionary entries no live group refers to any more (set bits of the live rows).
+int dict_gc(ngz_agg *a) {
+    AGG_HIP(a, hipMemsetAsync(a->used, 0, 32, a->stream));
+    hipLaunchKernelGGL(k_agg_bits, dim3(grid_for(a->slots, 256, 2048)), dim3(256), 0, a->stream, a->tags, a->rows,
+                       a->slots, a->P.row_bytes, a->used);
+    unsigned long long used[4];
+    AGG_HIP(a, hipMemcpyAsync(used, a->used, 32, hipMemcpyDeviceToHost, a->stream));
+    AGG_HIP(a, hipStreamSynchronize(a->stream));
+    for (size_t i = 0; i < a->templates.size(); ++i)
+        if (!(used[0] >> i & 1)) a->templates[i] = -1;
+    for (size_t i = 0; i < a->ports.size(); ++i)
+        if (!(used[1] >> i & 1)) a->ports[i] = -1;
+    for (size_t i = 0; i < a->domains.size(); ++i)
+        if (!((i < 64 ? used[2] >> i : used[3] >> (i - 64)) & 1)) a->domains[i] = -1;
+    return NGZ_OK;
+}
+
+int upload_domains(ngz_agg *a) {
+    unsigned long long tab[DOM_SLOTS] = {};
+    for (size_t i = 0; i < a->domains.size() && i < DOM_SLOTS; ++i)
+        if (a->domains[i] >= 0) tab[i] = (1ull << 32) | (uint64_t)a->domains[i];
+    AGG_HIP(a, hipMemcpyAsync(a->dom_dict, tab, sizeof tab, hipMemcpyHostToDevice, a->stream));
+    return NGZ_OK;
+}
+
+// rebuild the table without its tombstones (same size)
+int rehash(ngz_agg *a) {
+    unsigned long long *ntags = nullptr;
+    uint8_t *nrows = nullptr;
+    if (hipMalloc(&ntags, a->slots * 8) != hipSuccess || hipMalloc(&nrows, a->slots * a->P.row_bytes) != hipSuccess) {
+        hipFree(ntags);
+        hipFree(nrows);
+        return NGZ_OK;  // keep the tombstones (correct, only slower probes); retried at the next emit
+    }
+    int rc = reset_rows(a, ntags, nrows);
+    if (rc) { hipFree(ntags); hipFree(nrows); return rc; }
+    AGG_HIP(a, hipMemsetAsync(a->err, 0, 4, a->stream));
+    hipLaunchKernelGGL(k_agg_rehash, dim3(grid_for(a->slots)), dim3(256), 0, a->stream, a->tags, a->rows, a->slots,
+                       a->P.row_bytes, ntags, nrows, a->err);
+    unsigned int e = 0;
+    AGG_HIP(a, hipMemcpyAsync(&e, a->err, 4, hipMemcpyDeviceToHost, a->stream));
+    AGG_HIP(a, hipStreamSynchronize(a->stream));
+    if (e) {
+        hipFree(ntags);
+        hipFree(nrows);
+        a->poisoned = true;
+        return fail(a, NGZ_E_DEVICE, "rehash lost groups");
+    }
+    hipFree(a->tags);
+    hipFree(a->rows);
+    a->tags = ntags;
+    a->rows = nrows;
+    a->tombs = 0;
+    return NGZ_OK;
+}
+
+// host finish of output rows: collection times back to signed, per-push marker cleared,
+// values at the IE width, ranks back to values
+void finish_rows(ngz_agg *a, uint8_t *dst, int64_t n) {
+    const uint32_t RB = a->P.row_bytes;
+    for (int64_t g = 0; g < n; ++g) {
+        uint8_t *R = dst + (uint64_t)g * RB;
+        uint64_t c;
+        memcpy(&c, R + 40, 8); c ^= 1ull << 63; memcpy(R + 40, &c, 8);
+        memcpy(&c, R + 48, 8); c ^= 1ull << 63; memcpy(R + 48, &c, 8);
+        memset(R + 36, 0, 4);
+        uint32_t vp;
+        memcpy(&vp, R + 12, 4);
+        for (uint32_t v = 0; v < a->P.n_vals; ++v) {
+            const int vc = a->P.val_vc[v];
+            uint8_t *p = R + a->P.val_off[v];
+            if (!(vp >> v & 1)) { memset(p, 0, value_slot_bytes(vc)); continue; }
+            if (vc == VC_BYTES || vc == VC_IPV6 || vc == VC_F32 || vc == VC_F64) continue;
+            uint64_t x;
+            memcpy(&x, p, 8);
+            const uint8_t op = a->P.val_op[v];
+            if (vc == VC_SINT && (op == NGZ_AGG_MIN || op == NGZ_AGG_MAX)) x ^= 1ull << 63;
+            if (vc == VC_RANK) x = a->P.val_tcp[v] ? bitrev8((uint32_t)x & 0xFF) : (x & 0xFFFFFFFFull);
+            const int w = a->val_w[v];
+            if (vc != VC_DTFRAC && w > 0 && w < 8) {  // wrap at the Rust width (release-mode +=), then extend
+                const uint32_t sh = 64 - 8 * w;
+                x = vc == VC_SINT ? (uint64_t)(((int64_t)(x << sh)) >> sh) : (x << sh) >> sh;
+            }
+            memcpy(p, &x, 8);
+        }
+    }
+}
+
+// groups selected by cutoff (INT64_MAX: all) -> dst (host); tomb: free their slots
+int64_t take_rows(ngz_agg *a, void *dst, uint64_t cap, int64_t cutoff_s, bool tomb) {
+    AGG_HIP(a, hipSetDevice(a->device));
+    unsigned long long n = 0;
+    AGG_HIP(a, hipMemsetAsync(a->cursor, 0, 8, a->stream));
+    hipLaunchKernelGGL(k_agg_count, dim3(grid_for(a->slots)), dim3(256), 0, a->stream, a->tags, a->rows, a->slots,
+                       a->P.row_bytes, cutoff_s, a->cursor);
+    AGG_HIP(a, hipMemcpyAsync(&n, a->cursor, 8, hipMemcpyDeviceToHost, a->stream));
+    AGG_HIP(a, hipStreamSynchronize(a->stream));
+    const uint32_t RB = a->P.row_bytes;
+    if ((uint64_t)n * RB > cap || (n && !dst)) return fail(a, NGZ_E_INVALID, "output buffer too small");
+    if (n) {
+        uint8_t *tmp = nullptr;
+        if (hipMalloc(&tmp, (uint64_t)n * RB) != hipSuccess) return fail(a, NGZ_E_NOMEM, "output staging");
+        AGG_HIP(a, hipMemsetAsync(a->cursor, 0, 8, a->stream));
+        hipLaunchKernelGGL(k_agg_take, dim3(grid_for(a->slots)), dim3(256), 0, a->stream, a->tags, a->rows, a->slots, RB,
+                           cutoff_s, tomb ? 1 : 0, tmp, a->cursor);
+        hipError_t e = hipMemcpyAsync(dst, tmp, (uint64_t)n * RB, hipMemcpyDeviceToHost, a->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(a->stream);
+        hipFree(tmp);
+        if (e != hipSuccess) { a->poisoned = true; return fail(a, NGZ_E_DEVICE, hipGetErrorString(e)); }
+        finish_rows(a, (uint8_t *)dst, (int64_t)n);
+    }
+    a->out_templates = a->templates;
+    a->out_ports = a->ports;
+    a->out_domains = a->domains;
+    return (int64_t)n;
+}
+
+int64_t floordiv64(int64_t x, int64_t d) { return x / d - ((x % d != 0) && ((x < 0) != (d < 0))); }
+
+// Windows closed by the current event time (aggregation.rs:154-160): starts <= cutoff =
+// get_window_start(current_time - lateness) - window_duration, in seconds (floored).
+int64_t cutoff_s(const ngz_agg *a) {
+    if (!a->current_time) return INT64_MIN;
+    const int64_t t = (int64_t)a->current_time * 1000 - (int64_t)a->lateness_ms;
+    const int64_t cut_ms = floordiv64(t, 60000) * 60000 - (int64_t)a->window_ms;
+    return floordiv64(cut_ms, 1000);
 }
 
 }  // namespace
@@ -805,92 +1212,103 @@ int ngz_agg_create(int device, const ngz_agg_field *fields, uint32_t n_fields, u
     a->device = device;
     a->window_ms = window_ms;
     a->lateness_ms = lateness_ms;
+    std::vector<int> vcs;
     for (uint32_t i = 0; i < n_fields; ++i) {
         const ngz_agg_field &f = fields[i];
         if (f.op > NGZ_AGG_OR) { delete a; return NGZ_E_INVALID; }
-        if (f.op == NGZ_AGG_KEY) a->keys.push_back(f);
-        else {
-            std::string why;
-            if (value_class(ngzh::ie_find(f.pen, f.ie_id), f.op, why) < 0) { delete a; return NGZ_E_INVALID; }
-            a->vals.push_back(f);
-        }
+        if (f.op == NGZ_AGG_KEY) { a->keys.push_back(f); continue; }
+        std::string why;
+        const int vc = value_class(ngzh::ie_find(f.pen, f.ie_id), f.op, why);
+        if (vc == -1) { delete a; return NGZ_E_INVALID; }
+        if (vc == -2) { delete a; return NGZ_E_LIMIT; }
+        a->vals.push_back(f);
+        vcs.push_back(vc);
     }
     if (a->keys.size() > NGZ_AGG_MAX_KEYS || a->vals.size() > NGZ_AGG_MAX_VALUES) { delete a; return NGZ_E_LIMIT; }
     a->key_w.assign(a->keys.size(), -1);
+    a->key_kind_seen.assign(a->keys.size(), -1);
     a->val_w.assign(a->vals.size(), -1);
-    a->val_vc.assign(a->vals.size(), -1);
-    // row layout: header, keys (IE width rounded to 4; the width is fixed by the IE's Rust type except
-    // for octet arrays, whose width is fixed at first sight), values (8 B; byte ORs up to 32 B)
+    a->val_kind_seen.assign(a->vals.size(), -1);
+    // row layout: header, keys (canonical bytes, slot a multiple of 4), values (8 B; IPv6 16 B;
+    // byte ORs up to 32 B)
     uint32_t off = ROW_HDR;
     AggParams &P = a->P;
     P.n_keys = (uint32_t)a->keys.size();
     P.n_vals = (uint32_t)a->vals.size();
     for (uint32_t k = 0; k < P.n_keys; ++k) {
         const ngzh::IeRow *r = ngzh::ie_find(a->keys[k].pen, a->keys[k].ie_id);
-        uint32_t w = 32;  // octetArray / string keys: up to 32 bytes on the device
+        uint32_t slot = 32;
+        uint8_t kind = KK_OCTETS;
+        int fw = 0;  // packed-key eligibility: IEs whose column width is fixed by the Rust type (1/2/4/8 bytes)
         if (r) {
+            kind = KK_FIXED;
             switch (r->dtype) {
-            case ngzh::DT_unsigned8: case ngzh::DT_signed8: case ngzh::DT_boolean: w = 4; break;
-            case ngzh::DT_unsigned16: case ngzh::DT_signed16: w = 4; break;
+            case ngzh::DT_unsigned8: case ngzh::DT_signed8: case ngzh::DT_boolean: slot = 4; fw = 1; break;
+            case ngzh::DT_unsigned16: slot = 4; fw = (r->flags & 2) ? 1 : 2; break;  // tcpControlBits column is u8
+            case ngzh::DT_signed16: slot = 4; fw = 2; break;
             case ngzh::DT_unsigned32: case ngzh::DT_signed32: case ngzh::DT_float32: case ngzh::DT_ipv4Address:
-            case ngzh::DT_dateTimeSeconds: w = 4; break;
+            case ngzh::DT_dateTimeSeconds: slot = 4; fw = 4; break;
             case ngzh::DT_unsigned64: case ngzh::DT_signed64: case ngzh::DT_float64:
             case ngzh::DT_dateTimeMilliseconds: case ngzh::DT_dateTimeMicroseconds:
-            case ngzh::DT_dateTimeNanoseconds: w = 8; break;
-            case ngzh::DT_macAddress: w = 8; break;
-            case ngzh::DT_ipv6Address: w = 16; break;
-            default: w = 32; break;
+            case ngzh::DT_dateTimeNanoseconds: slot = 8; break;
+            case ngzh::DT_macAddress: slot = 8; break;
+            case ngzh::DT_ipv6Address: slot = 16; break;
+            case ngzh::DT_unsigned256: slot = 32; break;
+            case ngzh::DT_string: slot = 32; kind = KK_STR; break;
+            default: slot = 36; kind = KK_OCTETS; break;  // octetArray (and MPLS sections): length + 32 bytes
             }
+            if ((r->flags & 1) && r->dtype == ngzh::DT_octetArray) { slot = 4; kind = KK_FIXED; }  // [u8; 3]
+        } else {
+            slot = 36;  // IE::Unknown: raw bytes
         }
         P.key_off[k] = off;
-        off += w;
-        // packed-key eligibility: IEs whose column width is fixed by the Rust type (1/2/4/8 bytes)
-        int fw = 0;
-        if (r) switch (r->dtype) {
-            case ngzh::DT_unsigned8: case ngzh::DT_signed8: case ngzh::DT_boolean: fw = 1; break;
-            case ngzh::DT_unsigned16: fw = (r->flags & 2) ? 1 : 2; break;  // tcpControlBits column is u8
-            case ngzh::DT_signed16: fw = 2; break;
-            case ngzh::DT_unsigned32: case ngzh::DT_signed32: case ngzh::DT_ipv4Address:
-            case ngzh::DT_dateTimeSeconds: case ngzh::DT_float32: fw = 4; break;
-            default: fw = 0; break;
-        }
-        P.key_w[k] = (uint32_t)fw;
+        P.key_slot[k] = slot;
+        P.key_kind[k] = kind;
+        P.key_pw[k] = (uint32_t)fw;
+        off += slot;
     }
     if (off - ROW_HDR > NGZ_AGG_MAX_KEY_BYTES + 64) { delete a; return NGZ_E_LIMIT; }
     off = (off + 7) & ~7u;
+    bool ranks = false;
     for (uint32_t v = 0; v < P.n_vals; ++v) {
-        std::string why;
-        const int vc = value_class(ngzh::ie_find(a->vals[v].pen, a->vals[v].ie_id), a->vals[v].op, why);
+        const ngzh::IeRow *r = ngzh::ie_find(a->vals[v].pen, a->vals[v].ie_id);
         P.val_off[v] = off;
         P.val_op[v] = a->vals[v].op;
-        off += vc == VC_BYTES ? 32 : 8;
+        P.val_vc[v] = (uint8_t)vcs[v];
+        P.val_tcp[v] = vcs[v] == VC_RANK && r && (r->flags & 2);
+        ranks = ranks || (vcs[v] == VC_RANK && !P.val_tcp[v]);
+        off += value_slot_bytes(vcs[v]);
     }
     P.row_bytes = (off + 7) & ~7u;
     {
         uint32_t bits = 28;  // window/60 + flow type
         bool ok = true;
         for (uint32_t k = 0; k < P.n_keys; ++k) {
-            ok = ok && P.key_w[k] != 0;
-            bits += 1 + 8 * P.key_w[k];
+            ok = ok && P.key_pw[k] != 0;
+            bits += 1 + 8 * P.key_pw[k];
         }
         P.packed = ok && bits <= 63 && getenv("NGZ_AGG_NO_PACK") == nullptr;
     }
     P.lds_ok = 1;
-    for (uint32_t v = 0; v < P.n_vals; ++v) {
-        std::string why;
-        if (value_class(ngzh::ie_find(a->vals[v].pen, a->vals[v].ie_id), a->vals[v].op, why) == VC_BYTES) P.lds_ok = 0;
+    for (uint32_t v = 0; v < P.n_vals; ++v)
+        if (P.val_vc[v] == VC_BYTES) P.lds_ok = 0;
+    P.hash_mask = ~0ull;
+    if (const char *hb = getenv("NGZ_AGG_HASH_BITS")) {  // test knob: a narrow hash makes distinct keys collide
+        const int b = atoi(hb);
+        if (b > 0 && b < 64) P.hash_mask = (1ull << b) - 1;
     }
-    uint64_t cap = 1024;
-    while (cap < 2 * std::max<uint64_t>(capacity, 1)) cap <<= 1;
-    a->cap = cap;
-    P.mask = cap - 1;
+    uint64_t slots = 1024;
+    while (slots < 2 * std::max<uint64_t>(capacity, 1)) slots <<= 1;
+    a->slots = slots;
+    a->limit = std::max<uint64_t>(capacity, 1);
+    P.mask = slots - 1;
     // identity row: min fields at their maximum
     std::vector<uint32_t> ident(P.row_bytes / 4, 0);
     ident[24 / 4] = 0xFFFFFFFFu;                      // min_export_time
     ident[40 / 4] = ident[44 / 4] = 0xFFFFFFFFu;      // min_collection (flipped order)
     for (uint32_t v = 0; v < P.n_vals; ++v)
-        if (P.val_op[v] == NGZ_AGG_MIN) ident[P.val_off[v] / 4] = ident[P.val_off[v] / 4 + 1] = 0xFFFFFFFFu;
-    int rc = NGZ_OK;
+        if (P.val_op[v] == NGZ_AGG_MIN && !vc_ordered(P.val_vc[v]))
+            ident[P.val_off[v] / 4] = ident[P.val_off[v] / 4 + 1] = 0xFFFFFFFFu;
     auto bail = [&](int r, const char *what) {
         a->last_error = what;
         ngz_agg_destroy(a);
@@ -900,15 +1318,31 @@ int ngz_agg_create(int device, const ngz_agg_field *fields, uint32_t n_fields, u
     if (hipStreamCreateWithFlags(&a->stream, hipStreamNonBlocking) != hipSuccess) return bail(NGZ_E_DEVICE, "stream");
     hipEventCreate(&a->ev0);
     hipEventCreate(&a->ev1);
-    if (hipMalloc(&a->tags, cap * 8) != hipSuccess || hipMalloc(&a->rows, cap * P.row_bytes) != hipSuccess ||
-        hipMalloc(&a->ident, P.row_bytes) != hipSuccess || hipMalloc(&a->dom_tab, DOM_SLOTS * 8) != hipSuccess ||
-        hipMalloc(&a->err, 4) != hipSuccess || hipMalloc(&a->late, 8) != hipSuccess ||
-        hipMalloc(&a->cursor, 8) != hipSuccess)
+    if (hipMalloc(&a->tags, slots * 8) != hipSuccess || hipMalloc(&a->rows, slots * P.row_bytes) != hipSuccess ||
+        hipMalloc(&a->ident, P.row_bytes) != hipSuccess || hipMalloc(&a->dom_dict, DOM_SLOTS * 8) != hipSuccess ||
+        hipMalloc(&a->newdom, NEWDOM_SLOTS * 8) != hipSuccess || hipMalloc(&a->err, 4) != hipSuccess ||
+        hipMalloc(&a->late, 8) != hipSuccess || hipMalloc(&a->cursor, 8) != hipSuccess ||
+        hipMalloc(&a->n_claims, 8) != hipSuccess || hipMalloc(&a->n_coll, 4) != hipSuccess ||
+        hipMalloc(&a->used, 32) != hipSuccess)
         return bail(NGZ_E_NOMEM, "hipMalloc (group table)");
+    if (ranks) {
+        // sub-registry ranks: which values are registered variants (known bitmap per value)
+        if (hipMalloc(&a->rank_maps, (size_t)P.n_vals * 8192) != hipSuccess) return bail(NGZ_E_NOMEM, "hipMalloc (ranks)");
+        std::vector<uint32_t> map(2048);
+        for (uint32_t v = 0; v < P.n_vals; ++v) {
+            if (P.val_vc[v] != VC_RANK || P.val_tcp[v]) continue;
+            std::fill(map.begin(), map.end(), 0u);
+            for (uint32_t x = 0; x < 65536; ++x)
+                if (ngzh::subreg_known(a->vals[v].pen, a->vals[v].ie_id, x)) map[x >> 5] |= 1u << (x & 31);
+            uint32_t *dst = a->rank_maps + (size_t)v * 2048;
+            hipMemcpy(dst, map.data(), 8192, hipMemcpyHostToDevice);
+            P.rank_known[v] = dst;
+        }
+    }
     hipMemcpy(a->ident, ident.data(), P.row_bytes, hipMemcpyHostToDevice);
-    hipMemset(a->dom_tab, 0, DOM_SLOTS * 8);
+    hipMemset(a->dom_dict, 0, DOM_SLOTS * 8);
     hipMemset(a->err, 0, 4);
-    rc = reset_table(a);
+    int rc = reset_rows(a, a->tags, a->rows);
     if (rc == NGZ_OK && hipStreamSynchronize(a->stream) != hipSuccess) rc = NGZ_E_DEVICE;
     if (rc != NGZ_OK) return bail(rc, "table init");
     *out = a;
@@ -921,13 +1355,18 @@ void ngz_agg_destroy(ngz_agg *a) {
     hipFree(a->tags);
     hipFree(a->rows);
     hipFree(a->ident);
-    hipFree(a->dom_tab);
+    hipFree(a->dom_dict);
+    hipFree(a->newdom);
     hipFree(a->err);
     hipFree(a->late);
     hipFree(a->cursor);
+    hipFree(a->n_claims);
+    hipFree(a->n_coll);
+    hipFree(a->used);
+    hipFree(a->rank_maps);
     hipFree(a->plans);
     hipFree(a->scratch);
-    hipFree(a->setidx);
+    hipFree(a->rec_buf);
     if (a->ev0) hipEventDestroy(a->ev0);
     if (a->ev1) hipEventDestroy(a->ev1);
     if (a->stream) hipStreamDestroy(a->stream);
@@ -946,7 +1385,10 @@ int ngz_agg_layout(ngz_agg *a, uint32_t *row_bytes, uint32_t *key_off, uint16_t 
     }
     for (uint32_t v = 0; v < a->P.n_vals; ++v) {
         if (val_off) val_off[v] = a->P.val_off[v];
-        if (val_width) val_width[v] = (uint16_t)std::max(a->val_w[v], 0);
+        if (val_width) {
+            const int vc = a->P.val_vc[v];
+            val_width[v] = (uint16_t)(vc == VC_IPV6 ? 16 : std::max(a->val_w[v], 0));
+        }
     }
     return NGZ_OK;
 }
@@ -955,19 +1397,35 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, uint16_t pe
                  uint64_t *late_records, void *hip_stream) {
     if (!a || !ctx || !out) return NGZ_E_INVALID;
     if (late_records) *late_records = 0;
+    if (a->poisoned) return fail(a, NGZ_AGG_E_POISONED, "aggregator failed earlier: ngz_agg_reset it");
     AGG_HIP(a, hipSetDevice(a->device));
     if (hip_stream) AGG_HIP(a, hipStreamSynchronize((hipStream_t)hip_stream));
-    // port dictionary
-    uint32_t port_bit = 0;
-    {
-        auto it = std::find(a->ports.begin(), a->ports.end(), peer_port);
-        if (it == a->ports.end()) {
-            if (a->ports.size() >= NGZ_AGG_SET_BITS) return fail(a, NGZ_AGG_E_OVERFLOW, "more than 64 peer ports");
-            a->ports.push_back(peer_port);
-            it = a->ports.end() - 1;
+    // dictionaries as they were: a failed push puts them back
+    const std::vector<int64_t> keep_t = a->templates, keep_p = a->ports, keep_d = a->domains;
+    const std::vector<int> keep_vw = a->val_w, keep_kw = a->key_w, keep_kk = a->key_kind_seen, keep_vk = a->val_kind_seen;
+    bool gc_done = false;
+    auto restore = [&]() {
+        a->templates = keep_t;
+        a->ports = keep_p;
+        a->domains = keep_d;
+        a->val_w = keep_vw;
+        a->key_w = keep_kw;
+        a->key_kind_seen = keep_kk;
+        a->val_kind_seen = keep_vk;
+    };
+    auto put = [&](std::vector<int64_t> &d, int64_t x, uint32_t cap, int &bit) -> int {
+        bit = dict_put(d, x, cap);
+        if (bit < 0 && !gc_done) {  // full: free the entries no live group uses, then retry
+            const int r = dict_gc(a);
+            if (r) return r;
+            gc_done = true;
+            bit = dict_put(d, x, cap);
         }
-        port_bit = (uint32_t)(it - a->ports.begin());
-    }
+        return NGZ_OK;
+    };
+    int port_bit;
+    if (int r = put(a->ports, peer_port, SET_BITS, port_bit)) { restore(); return r; }
+    if (port_bit < 0) { restore(); return fail(a, NGZ_AGG_E_OVERFLOW, "more than 64 peer ports in live windows"); }
     // per-slot plans: FieldRef lookup (IE, occurrence among non-scope fields), types fixed at first sight
     const uint32_t S = out->n_slots;
     std::vector<AggSlotPlan> plans(std::max<uint32_t>(S, 1));
@@ -979,17 +1437,13 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, uint16_t pe
         sp.proto = si.proto;
         if (!si.n_records || !si.columns) continue;
         const int nf = ngz_slot_fields(ctx, s, nullptr, 0);
-        if (nf < 0) return fail(a, NGZ_E_INVALID, "ngz_slot_fields");
+        if (nf < 0) { restore(); return fail(a, NGZ_E_INVALID, "ngz_slot_fields"); }
         fi.resize(std::max(nf, 1));
         ngz_slot_fields(ctx, s, fi.data(), (uint32_t)nf);
-        const uint32_t tkey = ((uint32_t)si.proto << 16) | si.template_id;
-        auto it = std::find(a->templates.begin(), a->templates.end(), tkey);
-        if (it == a->templates.end()) {
-            if (a->templates.size() >= NGZ_AGG_SET_BITS) return fail(a, NGZ_AGG_E_OVERFLOW, "more than 64 template ids");
-            a->templates.push_back(tkey);
-            it = a->templates.end() - 1;
-        }
-        sp.tpl_bit = 1ull << (it - a->templates.begin());
+        int tbit;
+        if (int r = put(a->templates, ((int64_t)si.proto << 16) | si.template_id, SET_BITS, tbit)) { restore(); return r; }
+        if (tbit < 0) { restore(); return fail(a, NGZ_AGG_E_OVERFLOW, "more than 64 template ids in live windows"); }
+        sp.tpl_bit = 1ull << tbit;
         auto find_field = [&](const ngz_agg_field &f) -> int {
             uint32_t seen = 0;
             for (int i = 0; i < nf; ++i) {
@@ -1005,214 +1459,326 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, uint16_t pe
             const int i = find_field(a->keys[k]);
             if (i < 0) continue;
             const ngz_field_info &f = fi[i];
-            if (f.kind == NGZ_K_VLEN || f.kind == NGZ_K_FAIL)
-                return fail(a, NGZ_E_LIMIT, "variable-length key field (not on the device yet)");
-            const uint32_t room = (k + 1 < a->P.n_keys ? a->P.key_off[k + 1] : ((a->P.n_vals ? a->P.val_off[0] : a->P.row_bytes))) - a->P.key_off[k];
-            if (f.width > room) return fail(a, NGZ_E_LIMIT, "key field wider than its row slot");
-            if (a->P.packed && f.width != a->P.key_w[k])
+            if (f.kind == NGZ_K_VLEN || f.kind == NGZ_K_FAIL) {
+                restore();
+                return fail(a, NGZ_E_LIMIT, "variable-length key field (not on the device)");
+            }
+            const uint32_t room = a->P.key_slot[k] - (a->P.key_kind[k] == KK_OCTETS ? 4 : 0);
+            if (f.width > room) { restore(); return fail(a, NGZ_E_LIMIT, "key field wider than its row slot"); }
+            if (a->P.packed && f.width != a->P.key_pw[k]) {
+                restore();
                 return fail(a, NGZ_E_LIMIT, "key column width differs from the IE's width");
+            }
             sp.key_col[k] = si.columns + (uint64_t)si.capacity * f.col_off;
             sp.key_w[k] = f.width;
-            sp.key_str[k] = f.kind == NGZ_K_STR;
             if (a->key_w[k] < 0) a->key_w[k] = f.width;
+            if (a->key_kind_seen[k] < 0) a->key_kind_seen[k] = f.kind;
         }
         for (uint32_t v = 0; v < a->P.n_vals; ++v) {
             const int i = find_field(a->vals[v]);
             if (i < 0) continue;
             const ngz_field_info &f = fi[i];
-            std::string why;
-            const int vc = value_class(ngzh::ie_find(a->vals[v].pen, a->vals[v].ie_id), a->vals[v].op, why);
-            if (f.kind == NGZ_K_VLEN || f.kind == NGZ_K_FAIL || (vc == VC_BYTES && f.width > 32))
+            const int vc = a->P.val_vc[v];
+            if (f.kind == NGZ_K_VLEN || f.kind == NGZ_K_FAIL || (vc == VC_BYTES && f.width > 32)) {
+                restore();
                 return fail(a, NGZ_E_LIMIT, "aggregated field is variable-length or wider than 32 bytes");
-            if (vc != VC_BYTES && vc != VC_DTFRAC && f.width != 1 && f.width != 2 && f.width != 4 && f.width != 8)
-                return fail(a, NGZ_E_LIMIT, "aggregated integer field of odd width");
-            if (a->val_w[v] >= 0 && a->val_w[v] != f.width)
+            }
+            const bool int_like = vc == VC_UINT || vc == VC_SINT || vc == VC_RANK;
+            if ((int_like && f.width != 1 && f.width != 2 && f.width != 4 && f.width != 8) ||
+                (vc == VC_F32 && f.width != 4) || (vc == VC_F64 && f.width != 8) || (vc == VC_IPV6 && f.width != 16) ||
+                (vc == VC_DTFRAC && f.width != 8)) {
+                restore();
+                return fail(a, NGZ_E_LIMIT, "aggregated field of an unexpected column width");
+            }
+            if (a->val_w[v] >= 0 && a->val_w[v] != f.width) {
+                restore();
                 return fail(a, NGZ_E_LIMIT, "aggregated field width differs between templates");
+            }
             a->val_w[v] = f.width;
-            a->val_vc[v] = vc;
+            if (a->val_kind_seen[v] < 0) a->val_kind_seen[v] = f.kind;
             sp.val_col[v] = si.columns + (uint64_t)si.capacity * f.col_off;
             sp.val_w[v] = f.width;
-            sp.val_vc[v] = (uint8_t)vc;
         }
         sp.usable = 1;
     }
     const uint32_t D = out->n_dgrams, NS = out->n_sets;
     if (!D || !NS) return NGZ_OK;
-    // scratch: has_rec[D], ts[D], pm[D], dginfo[D], cnt/rstart[NS+1], cub temp; then setidx[R]
+    // scratch: has_rec[D], ts[D], pm[D], dginfo[D], cnt/rstart[NS+1], cub temp
     size_t cub_max = 0, cub_sum = 0;
     hipcub::DeviceScan::InclusiveScan(nullptr, cub_max, (uint32_t *)nullptr, (uint32_t *)nullptr, hipcub::Max(), D,
                                       a->stream);
     hipcub::DeviceScan::ExclusiveSum(nullptr, cub_sum, (uint32_t *)nullptr, (uint32_t *)nullptr, NS + 1, a->stream);
     auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
     const size_t o_has = 0, o_ts = o_has + al(4ull * D), o_pm = o_ts + al(4ull * D), o_dg = o_pm + al(4ull * D),
-                 o_cnt = o_dg + al(D), o_rs = o_cnt + al(4ull * (NS + 1)), o_cub = o_rs + al(4ull * (NS + 1)),
+                 o_cnt = o_dg + al(2ull * D), o_rs = o_cnt + al(4ull * (NS + 1)), o_cub = o_rs + al(4ull * (NS + 1)),
                  need = o_cub + al(std::max(cub_max, cub_sum));
     if (need > a->scratch_cap) {
         hipFree(a->scratch);
         a->scratch = nullptr;
-        if (hipMalloc(&a->scratch, need) != hipSuccess) { a->scratch_cap = 0; return fail(a, NGZ_E_NOMEM, "scratch"); }
+        if (hipMalloc(&a->scratch, need) != hipSuccess) { a->scratch_cap = 0; restore(); return fail(a, NGZ_E_NOMEM, "scratch"); }
         a->scratch_cap = need;
     }
     uint8_t *sc = (uint8_t *)a->scratch;
     uint32_t *has_rec = (uint32_t *)(sc + o_has), *ts = (uint32_t *)(sc + o_ts), *pm = (uint32_t *)(sc + o_pm);
-    uint8_t *dginfo = sc + o_dg;
+    uint16_t *dginfo = (uint16_t *)(sc + o_dg);
     uint32_t *cnt = (uint32_t *)(sc + o_cnt), *rstart = (uint32_t *)(sc + o_rs);
     void *cub_tmp = sc + o_cub;
     if (S > a->plans_cap) {
         hipFree(a->plans);
         a->plans = nullptr;
-        if (hipMalloc(&a->plans, sizeof(AggSlotPlan) * S) != hipSuccess) { a->plans_cap = 0; return fail(a, NGZ_E_NOMEM, "plans"); }
+        if (hipMalloc(&a->plans, sizeof(AggSlotPlan) * S) != hipSuccess) {
+            a->plans_cap = 0;
+            restore();
+            return fail(a, NGZ_E_NOMEM, "plans");
+        }
         a->plans_cap = S;
     }
     hipStream_t st = a->stream;
     AGG_HIP(a, hipMemcpyAsync(a->plans, plans.data(), sizeof(AggSlotPlan) * S, hipMemcpyHostToDevice, st));
     AggParams P = a->P;
     P.push_id = ++a->push_id;
-    P.port_bit = port_bit;
+    P.port_bit = (uint32_t)port_bit;
     P.coll_flip = (uint64_t)collection_time_ms ^ (1ull << 63);
     AGG_HIP(a, hipEventRecord(a->ev0, st));
     AGG_HIP(a, hipMemsetAsync(has_rec, 0, 4ull * D, st));
     AGG_HIP(a, hipMemsetAsync(a->late, 0, 8, st));
     AGG_HIP(a, hipMemsetAsync(a->err, 0, 4, st));
+    AGG_HIP(a, hipMemsetAsync(a->newdom, 0, NEWDOM_SLOTS * 8, st));
+    AGG_HIP(a, hipMemsetAsync(a->n_claims, 0, 8, st));
     const ngz_dgram_hdr *hdr = out->dgrams;
     const ngz_set_info *sets = out->sets;
-    hipLaunchKernelGGL(k_agg_dgram, dim3(grid_for(NS)), dim3(256), 0, st, hdr, sets, NS, D, has_rec);
+    hipLaunchKernelGGL(k_agg_dgram, dim3(grid_for(NS)), dim3(256), 0, st, sets, NS, D, has_rec);
     hipLaunchKernelGGL(k_agg_ts, dim3(grid_for(D)), dim3(256), 0, st, hdr, has_rec, D, ts);
     size_t tmp = cub_max;
     AGG_HIP(a, hipcub::DeviceScan::InclusiveScan(cub_tmp, tmp, ts, pm, hipcub::Max(), D, st));
     hipLaunchKernelGGL(k_agg_late, dim3(grid_for(D)), dim3(256), 0, st, hdr, has_rec, pm, D, a->current_time,
-                       a->lateness_ms, a->dom_tab, dginfo, a->err);
+                       a->lateness_ms, a->dom_dict, dginfo, a->newdom, a->err);
     // record starts of every set: n copied out of the set table (stride 16 B) then scanned
     AGG_HIP(a, hipMemsetAsync(cnt + NS, 0, 4, st));
     AGG_HIP(a, hipMemcpy2DAsync(cnt, 4, (const uint8_t *)sets + offsetof(ngz_set_info, n), sizeof(ngz_set_info), 4, NS,
                                 hipMemcpyDeviceToDevice, st));
     tmp = cub_sum;
     AGG_HIP(a, hipcub::DeviceScan::ExclusiveSum(cub_tmp, tmp, cnt, rstart, NS + 1, st));
-    // records of the set table (synchronises once: the grid of the record kernels depends on it)
+    // one synchronisation: the record count sizes the record kernels, new domains need entries
     uint32_t n_rec = 0;
+    unsigned long long newdom[NEWDOM_SLOTS];
+    unsigned int errv = 0;
     AGG_HIP(a, hipMemcpyAsync(&n_rec, rstart + NS, 4, hipMemcpyDeviceToHost, st));
+    AGG_HIP(a, hipMemcpyAsync(newdom, a->newdom, sizeof newdom, hipMemcpyDeviceToHost, st));
+    AGG_HIP(a, hipMemcpyAsync(&errv, a->err, 4, hipMemcpyDeviceToHost, st));
     AGG_HIP(a, hipStreamSynchronize(st));
-    if ((uint64_t)n_rec * 4 > a->setidx_cap) {
-        hipFree(a->setidx);
-        a->setidx = nullptr;
-        a->setidx_cap = 0;
-        if (hipMalloc(&a->setidx, std::max<uint64_t>(n_rec, 1) * 4) != hipSuccess) return fail(a, NGZ_E_NOMEM, "setidx");
-        a->setidx_cap = std::max<uint64_t>(n_rec, 1) * 4;
+    if (errv & 1) { restore(); return fail(a, NGZ_AGG_E_OVERFLOW, "more than 256 new observation domains in one push"); }
+    bool fix = false;
+    for (uint32_t i = 0; i < NEWDOM_SLOTS; ++i) {
+        if (!newdom[i]) continue;
+        int bit;
+        if (int r = put(a->domains, (int64_t)(uint32_t)newdom[i], DOM_SLOTS, bit)) { restore(); return r; }
+        if (bit < 0) {
+            restore();
+            upload_domains(a);
+            return fail(a, NGZ_AGG_E_OVERFLOW, "more than 128 observation domains in live windows");
+        }
+        fix = true;
     }
-    uint32_t *setidx = a->setidx;
+    if (fix) {
+        if (int r = upload_domains(a)) { restore(); return r; }
+        hipLaunchKernelGGL(k_agg_domfix, dim3(grid_for(D)), dim3(256), 0, st, hdr, a->dom_dict, dginfo, D, a->err);
+    }
+    // per-record buffers: setidx, rec_g, claims, two record lists, sort keys / values (x2)
+    const uint64_t R4 = al(4ull * std::max<uint32_t>(n_rec, 1));
+    const bool ordered = [&] {
+        for (uint32_t v = 0; v < P.n_vals; ++v)
+            if (vc_ordered(P.val_vc[v])) return true;
+        return false;
+    }();
+    size_t sort_tmp = 0;
+    if (ordered)
+        hipcub::DeviceRadixSort::SortPairs(nullptr, sort_tmp, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                           (uint32_t *)nullptr, (uint32_t *)nullptr, (int)std::max<uint32_t>(n_rec, 1),
+                                           0, 32, st);
+    const size_t rec_need = 5 * R4 + (ordered ? 4 * R4 + al(sort_tmp) : 0);
+    if (rec_need > a->rec_cap) {
+        hipFree(a->rec_buf);
+        a->rec_buf = nullptr;
+        a->rec_cap = 0;
+        if (hipMalloc(&a->rec_buf, rec_need) != hipSuccess) { restore(); upload_domains(a); return fail(a, NGZ_E_NOMEM, "record buffers"); }
+        a->rec_cap = rec_need;
+    }
+    uint32_t *setidx = (uint32_t *)a->rec_buf, *rec_g = (uint32_t *)(a->rec_buf + R4),
+             *claims = (uint32_t *)(a->rec_buf + 2 * R4), *list_a = (uint32_t *)(a->rec_buf + 3 * R4),
+             *list_b = (uint32_t *)(a->rec_buf + 4 * R4);
     hipLaunchKernelGGL(k_agg_setidx, dim3(grid_for(64ull * NS, 256, 4096)), dim3(256), 0, st, sets, rstart, NS, setidx);
     AGG_HIP(a, hipGetLastError());
+    const RecCtx C{hdr, sets, rstart, setidx, (uint64_t)n_rec, D, S, dginfo, a->plans};
     const uint32_t blocks = (uint32_t)((n_rec + 255) / 256);
-    // insert grid: workgroups walk tiles of 256 records (NGZ_AGG_GRID overrides the default 4096)
     static const uint32_t grid_cap = getenv("NGZ_AGG_GRID") ? (uint32_t)std::max(1, atoi(getenv("NGZ_AGG_GRID"))) : 4096u;
-    const uint32_t ig = std::min<uint32_t>(blocks, grid_cap);
+    const uint32_t ig = std::max<uint32_t>(1, std::min<uint32_t>(blocks, grid_cap));
+    unsigned long long n_claims = 0;
+    auto rollback = [&](int rc, const std::string &why) {
+        if (n_claims)
+            hipLaunchKernelGGL(k_agg_unclaim, dim3(grid_for(n_claims)), dim3(256), 0, st, a->tags, claims, (uint64_t)n_claims);
+        restore();
+        upload_domains(a);
+        if (hipStreamSynchronize(st) != hipSuccess) a->poisoned = true;
+        return fail(a, rc, why);
+    };
+    if (n_rec) {
+        hipLaunchKernelGGL(k_agg_claim, dim3(ig), dim3(256), 0, st, C, P, a->tags, a->rows, rec_g, claims, a->n_claims,
+                           a->late, a->err);
+        if (!P.packed) {
+            // hashed keys: compare, and re-probe the records of collided keys comparing keys
+            AGG_HIP(a, hipMemsetAsync(a->n_coll, 0, 4, st));
+            hipLaunchKernelGGL(k_agg_check, dim3(grid_for(n_rec)), dim3(256), 0, st, C, P, a->rows, rec_g, nullptr, 0u,
+                               list_a, a->n_coll, a->err);
+            for (int round = 0;; ++round) {
+                unsigned int nc = 0;
+                AGG_HIP(a, hipMemcpyAsync(&nc, a->n_coll, 4, hipMemcpyDeviceToHost, st));
+                AGG_HIP(a, hipStreamSynchronize(st));
+                if (!nc) break;
+                if (round == 64) {
+                    AGG_HIP(a, hipMemcpyAsync(&n_claims, a->n_claims, 8, hipMemcpyDeviceToHost, st));
+                    AGG_HIP(a, hipStreamSynchronize(st));
+                    return rollback(NGZ_E_DEVICE, "key collision resolution did not converge");
+                }
+                hipLaunchKernelGGL(k_agg_reprobe, dim3(grid_for(nc)), dim3(256), 0, st, C, P, a->tags, a->rows, rec_g,
+                                   list_a, nc, claims, a->n_claims, a->err);
+                AGG_HIP(a, hipMemsetAsync(a->n_coll, 0, 4, st));
+                hipLaunchKernelGGL(k_agg_check, dim3(grid_for(nc)), dim3(256), 0, st, C, P, a->rows, rec_g, list_a, nc,
+                                   list_b, a->n_coll, a->err);
+                std::swap(list_a, list_b);
+            }
+        }
+    }
+    AGG_HIP(a, hipGetLastError());
+    AGG_HIP(a, hipMemcpyAsync(&n_claims, a->n_claims, 8, hipMemcpyDeviceToHost, st));
+    AGG_HIP(a, hipMemcpyAsync(&errv, a->err, 4, hipMemcpyDeviceToHost, st));
+    AGG_HIP(a, hipStreamSynchronize(st));
+    if (errv & 16) { a->poisoned = true; return rollback(NGZ_E_DEVICE, "set table entry out of range"); }
+    if (errv & 2) return rollback(NGZ_AGG_E_OVERFLOW, "group table full");
+    if (a->live + n_claims > a->limit) return rollback(NGZ_AGG_E_OVERFLOW, "more groups than the aggregator's capacity");
+    // commit: every record has its group; reduce
     if (n_rec) {
         if (P.n_vals <= 8)
-            hipLaunchKernelGGL(k_agg_insert<8>, dim3(ig), dim3(256), 0, st, hdr, sets,
-                               rstart, setidx, (uint64_t)n_rec, D, S, dginfo, a->plans, P, a->tags, a->rows, a->late,
-                               a->err);
+            hipLaunchKernelGGL(k_agg_apply<8>, dim3(ig), dim3(256), 0, st, C, P, rec_g, a->rows, a->err);
         else
-            hipLaunchKernelGGL(k_agg_insert<NGZ_AGG_MAX_VALUES>, dim3(ig), dim3(256), 0,
-                               st, hdr, sets, rstart, setidx, (uint64_t)n_rec, D, S, dginfo, a->plans, P, a->tags,
-                               a->rows, a->late, a->err);
-        if (!P.packed) hipLaunchKernelGGL(k_agg_verify, dim3(blocks), dim3(256), 0, st, hdr, sets, rstart, setidx, (uint64_t)n_rec,
-                           D, S, dginfo, a->plans, P, a->tags, a->rows, a->err);
+            hipLaunchKernelGGL(k_agg_apply<NGZ_AGG_MAX_VALUES>, dim3(ig), dim3(256), 0, st, C, P, rec_g, a->rows, a->err);
+        if (ordered) {
+            uint32_t *sk = (uint32_t *)(a->rec_buf + 5 * R4), *sv = (uint32_t *)(a->rec_buf + 6 * R4),
+                     *sk2 = (uint32_t *)(a->rec_buf + 7 * R4), *sv2 = (uint32_t *)(a->rec_buf + 8 * R4);
+            void *stmp = a->rec_buf + 9 * R4;
+            AGG_HIP(a, hipMemcpyAsync(sk, rec_g, 4ull * n_rec, hipMemcpyDeviceToDevice, st));
+            hipLaunchKernelGGL(k_agg_iota, dim3(grid_for(n_rec)), dim3(256), 0, st, sv, (uint64_t)n_rec);
+            int end_bit = 1;
+            while (end_bit < 32 && (1ull << end_bit) <= a->slots) ++end_bit;
+            end_bit = 32;  // NONE (all ones) must sort after every slot
+            size_t tb = sort_tmp;
+            AGG_HIP(a, hipcub::DeviceRadixSort::SortPairs(stmp, tb, sk, sk2, sv, sv2, (int)n_rec, 0, end_bit, st));
+            hipLaunchKernelGGL(k_agg_ordered, dim3(grid_for(n_rec)), dim3(256), 0, st, C, P, sk2, sv2, (uint64_t)n_rec,
+                               a->rows, a->err);
+        }
     }
     AGG_HIP(a, hipGetLastError());
     AGG_HIP(a, hipEventRecord(a->ev1, st));
-    uint32_t last_pm = 0, errv = 0;
+    uint32_t last_pm = 0;
     unsigned long long late = 0;
     AGG_HIP(a, hipMemcpyAsync(&last_pm, pm + (D - 1), 4, hipMemcpyDeviceToHost, st));
-    AGG_HIP(a, hipMemcpyAsync(&errv, a->err, 4, hipMemcpyDeviceToHost, st));
     AGG_HIP(a, hipMemcpyAsync(&late, a->late, 8, hipMemcpyDeviceToHost, st));
     AGG_HIP(a, hipStreamSynchronize(st));
     hipEventElapsedTime(&a->t_push, a->ev0, a->ev1);
+    a->live += n_claims;
     if (last_pm > a->current_time) a->current_time = last_pm;
     if (late_records) *late_records = late;
-    if (errv & 1) return fail(a, NGZ_AGG_E_OVERFLOW, "more than 128 observation domains");
-    if (errv & 6) return fail(a, NGZ_AGG_E_OVERFLOW, "group table full");
-    if (errv & 8) return fail(a, NGZ_AGG_E_COLLISION, "64-bit key hash collision");
-    if (errv & 16) return fail(a, NGZ_E_INVALID, "set table entry out of range");
     return NGZ_OK;
 }
 
 int64_t ngz_agg_groups(ngz_agg *a) {
     if (!a) return NGZ_E_INVALID;
-    AGG_HIP(a, hipSetDevice(a->device));
-    unsigned long long n = 0;
-    AGG_HIP(a, hipMemsetAsync(a->cursor, 0, 8, a->stream));
-    hipLaunchKernelGGL(k_agg_count, dim3(grid_for(a->cap)), dim3(256), 0, a->stream, a->tags, a->cap, a->cursor);
-    AGG_HIP(a, hipMemcpyAsync(&n, a->cursor, 8, hipMemcpyDeviceToHost, a->stream));
-    AGG_HIP(a, hipStreamSynchronize(a->stream));
-    return (int64_t)n;
+    return (int64_t)a->live;
 }
 
 int64_t ngz_agg_flush(ngz_agg *a, void *dst, uint64_t cap) {
     if (!a) return NGZ_E_INVALID;
-    const int64_t n = ngz_agg_groups(a);
+    if (a->poisoned) return fail(a, NGZ_AGG_E_POISONED, "aggregator failed earlier: ngz_agg_reset it");
+    const int64_t n = take_rows(a, dst, cap, INT64_MAX, false);
     if (n < 0) return n;
-    const uint32_t RB = a->P.row_bytes;
-    if ((uint64_t)n * RB > cap || (n && !dst)) return fail(a, NGZ_E_INVALID, "flush buffer too small");
-    if (n) {
-        uint8_t *tmp = nullptr;
-        if (hipMalloc(&tmp, (uint64_t)n * RB) != hipSuccess) return fail(a, NGZ_E_NOMEM, "flush staging");
-        AGG_HIP(a, hipMemsetAsync(a->cursor, 0, 8, a->stream));
-        hipLaunchKernelGGL(k_agg_compact, dim3(grid_for(a->cap)), dim3(256), 0, a->stream, a->tags, a->rows, a->cap, RB,
-                           tmp, a->cursor);
-        hipError_t e = hipMemcpyAsync(dst, tmp, (uint64_t)n * RB, hipMemcpyDeviceToHost, a->stream);
-        if (e == hipSuccess) e = hipStreamSynchronize(a->stream);
-        hipFree(tmp);
-        if (e != hipSuccess) return fail(a, NGZ_E_DEVICE, hipGetErrorString(e));
-        // host finish: collection times back to signed, per-push marker cleared, values at the IE width
-        for (int64_t g = 0; g < n; ++g) {
-            uint8_t *R = (uint8_t *)dst + (uint64_t)g * RB;
-            uint64_t c;
-            memcpy(&c, R + 40, 8); c ^= 1ull << 63; memcpy(R + 40, &c, 8);
-            memcpy(&c, R + 48, 8); c ^= 1ull << 63; memcpy(R + 48, &c, 8);
-            memset(R + 36, 0, 4);
-            uint32_t vp;
-            memcpy(&vp, R + 12, 4);
-            for (uint32_t v = 0; v < a->P.n_vals; ++v) {
-                if (a->val_vc[v] == VC_BYTES || a->val_vc[v] < 0) continue;
-                uint8_t *p = R + a->P.val_off[v];
-                uint64_t x;
-                memcpy(&x, p, 8);
-                if (!(vp >> v & 1)) x = 0;
-                else {
-                    const int vc = a->val_vc[v];
-                    const uint8_t op = a->P.val_op[v];
-                    if (vc == VC_SINT && (op == NGZ_AGG_MIN || op == NGZ_AGG_MAX)) x ^= 1ull << 63;
-                    const int w = a->val_w[v];
-                    if (vc != VC_DTFRAC && w < 8) {  // wrap at the Rust width (release-mode +=), then extend
-                        const uint32_t sh = 64 - 8 * w;
-                        x = vc == VC_SINT ? (uint64_t)(((int64_t)(x << sh)) >> sh) : (x << sh) >> sh;
-                    }
-                }
-                memcpy(p, &x, 8);
-            }
-        }
-    }
-    a->current_time = 0;  // WindowAggregator::flush clears current_time
-    int rc = reset_table(a);
+    // WindowAggregator::flush: every window out, the event time forgotten; the set
+    // dictionaries start over (the rows just returned refer to out_*)
+    a->current_time = 0;
+    a->templates.clear();
+    a->ports.clear();
+    a->domains.clear();
+    a->live = a->tombs = 0;
+    int rc = reset_rows(a, a->tags, a->rows);
+    if (rc == NGZ_OK) rc = upload_domains(a);
     if (rc != NGZ_OK) return rc;
     AGG_HIP(a, hipStreamSynchronize(a->stream));
     return n;
 }
 
+int64_t ngz_agg_closed(ngz_agg *a) {
+    if (!a) return NGZ_E_INVALID;
+    if (a->poisoned) return fail(a, NGZ_AGG_E_POISONED, "aggregator failed earlier: ngz_agg_reset it");
+    const int64_t cut = cutoff_s(a);
+    if (cut == INT64_MIN) return 0;
+    AGG_HIP(a, hipSetDevice(a->device));
+    unsigned long long n = 0;
+    AGG_HIP(a, hipMemsetAsync(a->cursor, 0, 8, a->stream));
+    hipLaunchKernelGGL(k_agg_count, dim3(grid_for(a->slots)), dim3(256), 0, a->stream, a->tags, a->rows, a->slots,
+                       a->P.row_bytes, cut, a->cursor);
+    AGG_HIP(a, hipMemcpyAsync(&n, a->cursor, 8, hipMemcpyDeviceToHost, a->stream));
+    AGG_HIP(a, hipStreamSynchronize(a->stream));
+    return (int64_t)n;
+}
+
+int64_t ngz_agg_emit(ngz_agg *a, void *dst, uint64_t cap) {
+    if (!a) return NGZ_E_INVALID;
+    if (a->poisoned) return fail(a, NGZ_AGG_E_POISONED, "aggregator failed earlier: ngz_agg_reset it");
+    const int64_t cut = cutoff_s(a);
+    if (cut == INT64_MIN) {
+        a->out_templates = a->templates;
+        a->out_ports = a->ports;
+        a->out_domains = a->domains;
+        return 0;
+    }
+    const int64_t n = take_rows(a, dst, cap, cut, true);
+    if (n <= 0) return n;
+    a->live -= (uint64_t)n;
+    a->tombs += (uint64_t)n;
+    if (a->live + a->tombs > a->slots / 2) {
+        const int rc = rehash(a);
+        if (rc) return rc;
+    }
+    return n;
+}
+
+int ngz_agg_reset(ngz_agg *a) {
+    if (!a) return NGZ_E_INVALID;
+    AGG_HIP(a, hipSetDevice(a->device));
+    a->poisoned = false;
+    a->current_time = 0;
+    a->templates.clear();
+    a->ports.clear();
+    a->domains.clear();
+    a->live = a->tombs = 0;
+    int rc = reset_rows(a, a->tags, a->rows);
+    if (rc == NGZ_OK) rc = upload_domains(a);
+    if (rc != NGZ_OK) return rc;
+    AGG_HIP(a, hipStreamSynchronize(a->stream));
+    return NGZ_OK;
+}
+
 int ngz_agg_sets(ngz_agg *a, uint32_t *templates, uint32_t *n_templates, uint16_t *ports, uint32_t *n_ports,
                  uint32_t *domains, uint32_t *n_domains, uint32_t cap) {
     if (!a) return NGZ_E_INVALID;
-    if (n_templates) *n_templates = (uint32_t)a->templates.size();
-    if (n_ports) *n_ports = (uint32_t)a->ports.size();
-    for (uint32_t i = 0; i < a->templates.size() && i < cap; ++i)
-        if (templates) templates[i] = a->templates[i];
-    for (uint32_t i = 0; i < a->ports.size() && i < cap; ++i)
-        if (ports) ports[i] = a->ports[i];
-    unsigned long long tab[DOM_SLOTS];
-    AGG_HIP(a, hipMemcpy(tab, a->dom_tab, sizeof tab, hipMemcpyDeviceToHost));
-    if (n_domains) *n_domains = DOM_SLOTS;
-    for (uint32_t i = 0; i < DOM_SLOTS && i < cap; ++i)  // bit i <-> slot i; absent slots read 0xFFFFFFFF
-        if (domains) domains[i] = tab[i] ? (uint32_t)tab[i] : 0xFFFFFFFFu;
+    // entry i <-> bit i of the rows last returned by ngz_agg_flush / ngz_agg_emit; free entries read 0xFFFFFFFF
+    auto out = [cap](const std::vector<int64_t> &d, auto *dst, uint32_t *n, auto none) {
+        if (n) *n = (uint32_t)d.size();
+        for (uint32_t i = 0; i < d.size() && i < cap; ++i)
+            if (dst) dst[i] = d[i] < 0 ? none : (decltype(none))d[i];
+    };
+    out(a->out_templates, templates, n_templates, 0xFFFFFFFFu);
+    out(a->out_ports, ports, n_ports, (uint16_t)0xFFFF);
+    out(a->out_domains, domains, n_domains, 0xFFFFFFFFu);
     return NGZ_OK;
 }
 
@@ -1222,4 +1788,36 @@ int ngz_agg_last_timing(ngz_agg *a, float *push_ms) {
     return NGZ_OK;
 }
 
+int ngz_agg_value_info(ngz_agg *a, uint32_t v, ngz_agg_value_desc *out) {
+    if (!a || !out || v >= a->P.n_vals) return NGZ_E_INVALID;
+    memset(out, 0, sizeof *out);
+    out->vclass = a->P.val_vc[v];
+    out->width = (uint16_t)std::max(a->val_w[v], 0);
+    out->kind = (uint8_t)std::max(a->val_kind_seen[v], 0);
+    return NGZ_OK;
+}
+
+int ngz_agg_key_info(ngz_agg *a, uint32_t k, ngz_agg_key_desc *out) {
+    if (!a || !out || k >= a->P.n_keys) return NGZ_E_INVALID;
+    memset(out, 0, sizeof *out);
+    out->kkind = a->P.key_kind[k];
+    out->slot = (uint16_t)a->P.key_slot[k];
+    out->width = (uint16_t)std::max(a->key_w[k], 0);
+    out->kind = (uint8_t)std::max(a->key_kind_seen[k], 0);
+    return NGZ_OK;
+}
+
 }  // extern "C"
+
+// FlowInfo rendering of aggregated groups lives in ngz_agg_json.cpp (needs the IE registry
+// and the JSON field writers); it reads the aggregator through these.
+namespace ngzh {
+const std::vector<ngz_agg_field> &agg_keys(const ngz_agg *a) { return a->keys; }
+const std::vector<ngz_agg_field> &agg_vals(const ngz_agg *a) { return a->vals; }
+void agg_out_dicts(const ngz_agg *a, const std::vector<int64_t> **t, const std::vector<int64_t> **p,
+                   const std::vector<int64_t> **d) {
+    *t = &a->out_templates;
+    *p = &a->out_ports;
+    *d = &a->out_domains;
+}
+}  // namespace ngzh

@@ -161,6 +161,8 @@ const IeRow *ie_find_name(const char *vendor, const std::string &name) {
     return nullptr;
 }
 
+const char *vendor_name(uint32_t pen) { return ies().vendor(pen); }
+
 uint32_t vendor_pen(const std::string &vendor) {
     for (const auto &v : kVendors)
         if (vendor == v.name) return v.pen;

@@ -11,6 +11,7 @@
 #include <string>
 #include <vector>
 
+#include "ngz/flow_aggregate.h"
 #include "ngz/flow_decode.h"
 #include "ngz_internal.h"
 
@@ -48,6 +49,12 @@ const IeRow *ie_find(uint32_t pen, uint16_t id);
 const IeRow *ie_find_name(const char *vendor, const std::string &name);
 // vendor display name -> PEN (0 if unknown)
 uint32_t vendor_pen(const std::string &vendor);
+// vendor display name of a PEN with its own IE package, or null
+const char *vendor_name(uint32_t pen);
+// sub-registry of an IE: 0 none, 1 value-name enum, 2 nested reason codes (ngz_json.cpp)
+int subreg_kind(uint32_t pen, uint16_t id);
+// is v a registered variant of the IE's sub-registry enum
+bool subreg_known(uint32_t pen, uint16_t id, uint64_t v);
 
 // ------------------------------------------------------------------------
 // Template model
@@ -179,7 +186,13 @@ struct JsonView {
 }  // namespace ngzh
 
 struct ngz_ctx;
+struct ngz_agg;
 namespace ngzh {
+// aggregator internals the FlowInfo renderer reads (ngz_agg.hip)
+const std::vector<ngz_agg_field> &agg_keys(const ngz_agg *a);
+const std::vector<ngz_agg_field> &agg_vals(const ngz_agg *a);
+void agg_out_dicts(const ngz_agg *a, const std::vector<int64_t> **t, const std::vector<int64_t> **p,
+                   const std::vector<int64_t> **d);
 // Host template state of a context (both TemplatesMaps): saved before a
 // speculative batch and restored when its framing guess was wrong (ngz_collector.cpp)
 struct TemplateState {

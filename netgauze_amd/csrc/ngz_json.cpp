@@ -473,7 +473,175 @@ int json_render(ngz_ctx *ctx, const JsonView &v, uint32_t d, std::string &o, uin
     return NGZ_DG_OK;
 }
 
+int subreg_kind(uint32_t pen, uint16_t id) {
+    const SubReg *r = subreg_find(pen, id);
+    return r ? (r->nested ? 2 : 1) : 0;
+}
+
+bool subreg_known(uint32_t pen, uint16_t id, uint64_t v) {
+    const SubReg *r = subreg_find(pen, id);
+    if (!r || r->nested) return false;
+    for (uint32_t i = r->first; i < r->first + r->count; ++i)
+        if (kSubVals[i].v == v) return true;
+    return false;
+}
+
 }  // namespace ngzh
+
+// ---------------------------------------------------------------------------
+// AggFlowInfo::into_flowinfo_with_extra_fields (aggregator.rs:203-277)
+// ---------------------------------------------------------------------------
+namespace {
+
+Spec spec_of(uint32_t pen, uint16_t id) {
+    Spec s{};
+    s.pen = pen;
+    s.id = id;
+    if (pen == 0) {
+        const IeRow *r = ie_find(0, id);
+        if (r) { s.kind = IK_IANA; s.dtype = r->dtype; s.flags = r->flags; s.name = r->name; }
+        else { s.kind = IK_UNKNOWN; s.dtype = DT_octetArray; }
+    } else if (const char *vn = vendor_name(pen)) {
+        const IeRow *r = ie_find(pen, id);
+        s.vendor = vn;
+        if (r) { s.kind = IK_VENDOR; s.dtype = r->dtype; s.flags = r->flags; s.name = r->name; }
+        else { s.kind = IK_VENDOR_UNKNOWN; s.dtype = DT_octetArray; }
+    } else {
+        s.kind = IK_UNKNOWN;
+        s.dtype = DT_octetArray;
+    }
+    return s;
+}
+
+void put_cell(std::string &o, uint32_t pen, uint16_t id, uint8_t kind, uint16_t width, const uint8_t *cell) {
+    DevField fd{};
+    fd.kind = kind;
+    fd.width = width;
+    put_field(o, spec_of(pen, id), fd, cell, nullptr);
+}
+
+}  // namespace
+
+extern "C" int64_t ngz_agg_flowinfo_json(ngz_agg *a, const void *rows, uint64_t n, uint32_t shard_id, uint32_t seq0,
+                                         int64_t export_time_ms, ngz_json_line_fn fn, void *user) {
+    if (!a || (n && (!rows || !fn))) return NGZ_E_INVALID;
+    const auto &keys = agg_keys(a);
+    const auto &vals = agg_vals(a);
+    uint32_t rb = 0;
+    std::vector<uint32_t> ko(keys.size() + 1), vo(vals.size() + 1);
+    std::vector<uint16_t> kw(keys.size() + 1), vw(vals.size() + 1);
+    ngz_agg_layout(a, &rb, ko.data(), kw.data(), vo.data(), vw.data());
+    std::vector<ngz_agg_key_desc> kd(keys.size());
+    std::vector<ngz_agg_value_desc> vd(vals.size());
+    for (uint32_t k = 0; k < keys.size(); ++k) ngz_agg_key_info(a, k, &kd[k]);
+    for (uint32_t v = 0; v < vals.size(); ++v) ngz_agg_value_info(a, v, &vd[v]);
+    const std::vector<int64_t> *dt, *dp, *dd;
+    agg_out_dicts(a, &dt, &dp, &dd);
+    const int64_t es = floordiv(export_time_ms, 1000);
+    const uint32_t ens = (uint32_t)(export_time_ms - es * 1000) * 1000000u;
+    std::string o;
+    for (uint64_t g = 0; g < n; ++g) {
+        const uint8_t *R = (const uint8_t *)rows + g * rb;
+        ngz_agg_row h;
+        memcpy(&h, R, sizeof h);
+        o.clear();
+        const bool v10 = h.flow_type == 10;
+        if (v10) {
+            o += "{\"IPFIX\":{\"version\":10,\"export_time\":";
+            put_datetime(o, es, ens);
+            o += ",\"sequence_number\":"; put_u64(o, (uint32_t)(seq0 + g));
+            o += ",\"observation_domain_id\":"; put_u64(o, shard_id);
+        } else {
+            o += "{\"NetFlowV9\":{\"version\":9,\"sys_up_time\":"; put_u64(o, h.max_sys_up_time);
+            o += ",\"unix_time\":"; put_datetime(o, es, ens);
+            o += ",\"sequence_number\":"; put_u64(o, (uint32_t)(seq0 + g));
+            o += ",\"source_id\":"; put_u64(o, shard_id);
+        }
+        o += ",\"sets\":[{\"Data\":{\"id\":65535,\"records\":[{\"scope_fields\":[],\"fields\":[";
+        bool first = true;
+        auto sep = [&]() { if (!first) o += ','; first = false; };
+        // key fields, then aggregated fields: the present ones (flatten over Option)
+        for (uint32_t k = 0; k < keys.size(); ++k) {
+            if (!(h.key_present >> k & 1)) continue;
+            sep();
+            const uint8_t *c = R + ko[k];
+            if (kd[k].kkind == 2) {  // octet array: length, bytes
+                uint32_t len;
+                memcpy(&len, c, 4);
+                put_cell(o, keys[k].pen, keys[k].ie_id, NGZ_K_BYTES, (uint16_t)len, c + 4);
+            } else if (kd[k].kkind == 1) {
+                put_cell(o, keys[k].pen, keys[k].ie_id, NGZ_K_STR, kd[k].slot, c);
+            } else {
+                put_cell(o, keys[k].pen, keys[k].ie_id, kd[k].kind, kd[k].width, c);
+            }
+        }
+        for (uint32_t v = 0; v < vals.size(); ++v) {
+            if (!(h.val_present >> v & 1)) continue;
+            sep();
+            const uint8_t *c = R + vo[v];
+            uint8_t cell[32];
+            switch (vd[v].vclass) {
+            case 2: {  // secs<<32 | nanos -> {u32 secs, u32 nanos}
+                uint64_t x;
+                memcpy(&x, c, 8);
+                const uint32_t secs = (uint32_t)(x >> 32), ns = (uint32_t)x;
+                memcpy(cell, &secs, 4);
+                memcpy(cell + 4, &ns, 4);
+                put_cell(o, vals[v].pen, vals[v].ie_id, NGZ_K_DTFRAC, 8, cell);
+                break;
+            }
+            case 5: put_cell(o, vals[v].pen, vals[v].ie_id, NGZ_K_UINT, 4, c); break;
+            case 6: put_cell(o, vals[v].pen, vals[v].ie_id, NGZ_K_UINT, 8, c); break;
+            case 7: put_cell(o, vals[v].pen, vals[v].ie_id, NGZ_K_BYTES, 16, c); break;
+            default: put_cell(o, vals[v].pen, vals[v].ie_id, vd[v].kind, vd[v].width, c); break;
+            }
+        }
+        uint8_t cell[8];
+        sep();
+        memcpy(cell, &h.record_count, 8);
+        put_cell(o, 0, 375, NGZ_K_UINT, 8, cell);  // originalFlowsPresent
+        sep();
+        memcpy(cell, &h.min_export_time, 4);
+        put_cell(o, 0, 264, NGZ_K_UINT, 4, cell);  // minExportSeconds
+        sep();
+        memcpy(cell, &h.max_export_time, 4);
+        put_cell(o, 0, 260, NGZ_K_UINT, 4, cell);  // maxExportSeconds
+        sep();
+        memcpy(cell, &h.max_collection_ms, 8);
+        put_cell(o, 0, 258, NGZ_K_DTMS, 8, cell);  // collectionTimeMilliseconds
+        auto bits_sorted = [](const std::vector<int64_t> &d, const uint64_t *bits, int words) {
+            std::vector<int64_t> out;
+            for (size_t i = 0; i < d.size() && (int)(i / 64) < words; ++i)
+                if ((bits[i / 64] >> (i % 64) & 1) && d[i] >= 0) out.push_back(d[i]);
+            std::sort(out.begin(), out.end());
+            return out;
+        };
+        for (int64_t p : bits_sorted(*dp, &h.port_bits, 1)) {
+            sep();
+            const uint16_t x = (uint16_t)p;
+            memcpy(cell, &x, 2);
+            put_cell(o, 3746, 4, NGZ_K_UINT, 2, cell);  // NetGauze originalExporterTransportPort
+        }
+        for (int64_t dm : bits_sorted(*dd, h.domain_bits, 2)) {
+            sep();
+            const uint32_t x = (uint32_t)dm;
+            memcpy(cell, &x, 4);
+            put_cell(o, 0, 405, NGZ_K_UINT, 4, cell);  // originalObservationDomainId
+        }
+        std::vector<int64_t> tids;
+        for (int64_t t : bits_sorted(*dt, &h.template_bits, 1)) tids.push_back(t & 0xFFFF);
+        std::sort(tids.begin(), tids.end());
+        for (int64_t t : tids) {
+            sep();
+            const uint16_t x = (uint16_t)t;
+            memcpy(cell, &x, 2);
+            put_cell(o, 3746, 3, NGZ_K_UINT, 2, cell);  // NetGauze originalTemplateId
+        }
+        o += "]}]}}]}}";
+        if (fn(user, (uint32_t)g, NGZ_DG_OK, o.data(), o.size(), 0)) return (int64_t)g + 1;
+    }
+    return (int64_t)n;
+}
 
 extern "C" int64_t ngz_dgram_json(ngz_ctx *ctx, uint32_t dgram, char *buf, size_t cap) {
     if (!ctx || dgram >= ctx->last_in.n) return NGZ_E_INVALID;

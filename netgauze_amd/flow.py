@@ -73,6 +73,8 @@ class Slot:
 class DecodedBatch:
     def __init__(self, codec, out, source=None):
         self._codec = codec
+        codec.generation += 1
+        self.generation = codec.generation  # device arrays valid while it is the codec's latest
         self._source = source  # the batch bytes: host numpy array or device tensor
         self.out = out
         self.n_dgrams = out.n_dgrams
@@ -171,6 +173,7 @@ class FlowInfoCodec:
         the background), True (per-template kernels, each template's first batch
         waits for its compile: deterministic kernel choice), False (generic
         kernel only).  rtc_sync overrides the waiting."""
+        self.generation = 0  # batches decoded so far (DecodedBatch.generation)
         ctx = ctypes.c_void_p()
         rc = lib().ngz_ctx_create(device, ctypes.byref(ctx))
         if rc != 0:

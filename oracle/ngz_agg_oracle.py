@@ -13,7 +13,15 @@ It restates, over the packets of ngz_oracle.FlowInfoCodec:
                                  release-mode wrapping at the Rust width; `min`/`max`; `|=`,
                                  byte-wise zip for arrays)
   - WindowAggregator::process_item crates/analytics/src/aggregation.rs:124-172 (lateness drop,
-                                 window start = get_window_start :79-89, minute floor)
+                                 window start = get_window_start :79-89, minute floor, and the
+                                 windows the cutoff closes, :154-160)
+  - Ord of the Field types for Min / Max: ordered_float's OrderedFloat (NaN greatest and equal
+    to itself, -0 == +0), Ipv6Addr by octets, DateTime chronological, derived Ord of
+    TCPHeaderFlags (FIN most significant, iana/src/tcp.rs:41-70) and of sub-registry enums
+    (by discriminant: registered value, then Unassigned(x) after every registered variant);
+    Ord::min keeps the left argument on equality, Ord::max takes the right one
+  - AggFlowInfo::into_flowinfo_with_extra_fields (aggregator.rs:203-277), sets in ascending
+    order
 Pinned by the reference's own unit tests (aggregator/tests.rs: test_reduce_add_operations
 :244-337, test_explode_ipfix_repeating_ie_fields :755-827, test_explode_ipfix_missing_fields
 :830-893, test_explode_simple_netflowv9_packet :946-1017), restated as vectors in tests/kats_agg.py.
@@ -21,6 +29,8 @@ Pinned by the reference's own unit tests (aggregator/tests.rs: test_reduce_add_o
 Values are canonical Python values: ints for integer / ipv4 / tcpControlBits / bool / date-time
 seconds, bytes for byte-like fields, str for strings.
 """
+import struct
+
 import ngz_oracle as O
 
 OP_KEY, OP_ADD, OP_MIN, OP_MAX, OP_OR = 0, 1, 2, 3, 4
@@ -36,6 +46,10 @@ def canon(field):
         return v & 0xFF                                # low 8 bits (iana/src/tcp.rs:165-168)
     if isinstance(v, tuple) and v and v[0] in ("v4", "v6"):
         return v[1] if v[0] == "v4" else v[1].to_bytes(16, "big")
+    if isinstance(v, tuple) and v and v[0] == "f32":
+        return struct.unpack("<f", struct.pack("<I", v[1]))[0]
+    if isinstance(v, tuple) and v and v[0] == "f64":
+        return struct.unpack("<d", struct.pack("<Q", v[1]))[0]
     if isinstance(v, bool):
         return int(v)
     if isinstance(v, O.DateTime):
@@ -53,14 +67,45 @@ def _wrap(ie, x):
     return x
 
 
+def _f32(x):
+    return struct.unpack("<f", struct.pack("<f", x))[0]
+
+
+def _ofloat_cmp(a, b):
+    """ordered_float::OrderedFloat Ord: NaN == NaN, NaN > every number, -0 == +0."""
+    na, nb = a != a, b != b
+    if na or nb:
+        return 0 if na == nb else (1 if na else -1)
+    return -1 if a < b else (1 if a > b else 0)
+
+
+def _rank(ie, v):
+    """Position of a value in the Rust Ord of its Field type (derived Ord)."""
+    if ie.kind == "iana" and ie.id == 6:  # TCPHeaderFlags {FIN, SYN, ...}: FIN most significant
+        return int("{:08b}".format(v & 0xFF)[::-1], 2)
+    if ie.subreg is not None and ie.subreg["kind"] == "vnd":
+        known = {val for val, _ in ie.subreg["entries"]}
+        return v if v in known else (1 << 32) | v  # Unassigned(x) after every registered variant
+    return v
+
+
 def reduce_value(ie, op, lhs, rhs):
-    """Field::{add,min,max,bitwise_or}_assign_field on canonical values (generator.rs:896-1080)."""
+    """Field::{add,min,max,bitwise_or}_assign_field on canonical values (generator.rs:896-1080).
+    Ord::min keeps lhs on equality, Ord::max takes rhs (core::cmp::min_by / max_by)."""
+    flt = ie.dtype in ("float32", "float64")
     if op == OP_ADD:
+        if flt:
+            return _f32(lhs + rhs) if ie.dtype == "float32" else lhs + rhs
         return _wrap(ie, lhs + rhs)
-    if op == OP_MIN:
-        return min(lhs, rhs)
-    if op == OP_MAX:
-        return max(lhs, rhs)
+    if op in (OP_MIN, OP_MAX):
+        if flt:
+            c = _ofloat_cmp(lhs, rhs)
+        else:
+            a, b = _rank(ie, lhs), _rank(ie, rhs)
+            c = -1 if a < b else (1 if a > b else 0)
+        if op == OP_MIN:
+            return rhs if c > 0 else lhs
+        return lhs if c > 0 else rhs
     if isinstance(lhs, (bytes, bytearray)):  # lhs.iter_mut().zip(rhs): lhs keeps its length
         out = bytearray(lhs)
         for i, b in enumerate(rhs[:len(out)]):
@@ -93,6 +138,8 @@ class FlowAggregatorOracle:
         self.current_time = None
         self.groups = {}   # (window_start, flow_type, key tuple) -> record dict
         self.late = 0
+        self.closed = []   # groups of the windows the cutoff closed, not yet taken by emit()
+        self._cutoff = None
 
     def explode(self, pkt, peer_port, collection_ms):
         """aggregator.rs:286-354: one item per data record (non-scope fields)."""
@@ -125,6 +172,18 @@ class FlowAggregatorOracle:
                 self.groups[g] = rec
             else:
                 self.reduce(cur, rec)
+            self._close_windows()
+
+    def _close_windows(self):
+        """aggregation.rs:154-160: windows starting at or before
+        get_window_start(current_time - lateness) - window_duration leave the active set."""
+        t = self.current_time - self.lateness_s
+        cutoff = t - t % 60 - self.window_s
+        if self._cutoff is not None and cutoff <= self._cutoff:
+            return
+        self._cutoff = cutoff
+        for g in [g for g in self.groups if g[0] <= cutoff]:
+            self.closed.append(self._out(g, self.groups.pop(g)))
 
     def reduce(self, lhs, rhs):
         """FlowCacheRecord::reduce (aggregator.rs:159-198)."""
@@ -144,18 +203,80 @@ class FlowAggregatorOracle:
             elif a is None and b is not None:
                 lhs["vals"][i] = b
 
+    @staticmethod
+    def _out(g, r):
+        win, ft, key = g
+        return dict(window_start=win, flow_type=ft, key=key,
+                    vals=tuple(None if v is None else v[1] for v in r["vals"]),
+                    record_count=r["count"], min_export=r["min_export"], max_export=r["max_export"],
+                    max_sysup=r["max_sysup"], min_coll=r["min_coll"], max_coll=r["max_coll"],
+                    templates=set(r["templates"]), ports=set(r["ports"]), domains=set(r["domains"]))
+
+    def emit(self):
+        """The groups of every window closed so far (and not emitted yet)."""
+        out, self.closed = self.closed, []
+        return out
+
     def flush(self):
-        """WindowAggregator::flush: every group, then forget the event time."""
-        out = []
-        for (win, ft, key), r in self.groups.items():
-            out.append(dict(window_start=win, flow_type=ft, key=key,
-                            vals=tuple(None if v is None else v[1] for v in r["vals"]),
-                            record_count=r["count"], min_export=r["min_export"], max_export=r["max_export"],
-                            max_sysup=r["max_sysup"], min_coll=r["min_coll"], max_coll=r["max_coll"],
-                            templates=set(r["templates"]), ports=set(r["ports"]), domains=set(r["domains"])))
+        """WindowAggregator::flush: every active group, then forget the event time."""
+        out = [self._out(g, r) for g, r in self.groups.items()]
         self.groups = {}
         self.current_time = None
+        self._cutoff = None
         return out
+
+    def flowinfo_json(self, group, shard_id=0, seq=0, export_time_ms=0):
+        """AggFlowInfo::into_flowinfo_with_extra_fields (aggregator.rs:203-277) of one output
+        group, serde JSON text; the peer port / domain / template sets in ascending order."""
+        reg = O.REGISTRY
+        fields = []
+        for (p, i, _x), v in zip(self.keys, group["key"]):
+            if v is not None:
+                ie = reg.lookup(p, i)
+                fields.append(O.Field(ie, to_field_value(ie, v)))
+        for ((p, i, _x), _op), v in zip(self.vals, group["vals"]):
+            if v is not None:
+                ie = reg.lookup(p, i)
+                fields.append(O.Field(ie, to_field_value(ie, v)))
+        ms = group["max_coll"]
+        fields += [O.Field(reg.lookup(0, 375), group["record_count"]),
+                   O.Field(reg.lookup(0, 264), O.DateTime(group["min_export"], 0)),
+                   O.Field(reg.lookup(0, 260), O.DateTime(group["max_export"], 0)),
+                   O.Field(reg.lookup(0, 258), O.DateTime(ms // 1000, (ms % 1000) * 1_000_000))]
+        fields += [O.Field(reg.lookup(3746, 4), p) for p in sorted(group["ports"])]
+        fields += [O.Field(reg.lookup(0, 405), d) for d in sorted(group["domains"])]
+        fields += [O.Field(reg.lookup(3746, 3), t) for t in sorted(t for _ft, t in group["templates"])]
+        es = export_time_ms // 1000
+        et = O.DateTime(es, (export_time_ms - es * 1000) * 1_000_000).to_json()
+        sets = [{"Data": {"id": 65535, "records": [{"scope_fields": [],
+                                                     "fields": [O.field_json(f) for f in fields]}]}}]
+        if group["flow_type"] == 10:
+            pkt = {"IPFIX": {"version": 10, "export_time": et, "sequence_number": seq,
+                             "observation_domain_id": shard_id, "sets": sets}}
+        else:
+            pkt = {"NetFlowV9": {"version": 9, "sys_up_time": group["max_sysup"], "unix_time": et,
+                                 "sequence_number": seq, "source_id": shard_id, "sets": sets}}
+        return O.dumps(pkt)
+
+
+def to_field_value(ie, v):
+    """Canonical value -> the oracle's Field value convention (ngz_oracle.Field)."""
+    dt = ie.dtype
+    if ie.kind in ("unknown", "vendor_unknown"):
+        return v
+    if dt == "ipv4Address":
+        return ("v4", v)
+    if dt == "ipv6Address":
+        return ("v6", int.from_bytes(v, "big"))
+    if dt == "float32":
+        return ("f32", struct.unpack("<I", struct.pack("<f", v))[0])
+    if dt == "float64":
+        return ("f64", struct.unpack("<Q", struct.pack("<d", v))[0])
+    if dt == "boolean":
+        return bool(v)
+    if dt.startswith("dateTime"):
+        return O.DateTime(*v)
+    return v
 
 
 def aggregate_datagrams(fields, datagrams, peer_port=4739, collection_ms=0, window_s=60, lateness_s=10):

@@ -28,8 +28,11 @@ def test_header_declares_abi():
 
 def test_agg_config_validation_without_device():
     """AggregationConfig::validate / validate_operation_compatibility are checked before any
-    device call (config.rs:107-119, 212-250): zero window, lateness > window, Add on a
-    non-numeric IE, Min on a float all fail; the row layout matches ngz_agg_row."""
+    device call (config.rs:107-119, 212-250) with IE::supports_{arithmetic,comparison,bitwise}_ops
+    (generator.rs:1176-1272): the reference's accept / reject table, row by row.  Accepted
+    configs go on to the device (no GPU here: NGZ_E_DEVICE / NGZ_E_NOMEM); rejected ones
+    return NGZ_E_INVALID; the two the reference accepts but the device does not run return
+    NGZ_E_LIMIT."""
     from netgauze_amd import _lib
     lib = _lib.load()
     A = _lib.AggField
@@ -41,11 +44,60 @@ def test_agg_config_validation_without_device():
     ok = [(0, 8, 0, _lib.NGZ_AGG_KEY), (0, 1, 0, _lib.NGZ_AGG_ADD)]
     assert create(ok, window=0) == -1
     assert create(ok, window=1000, lateness=2000) == -1
-    assert create([(0, 8, 0, _lib.NGZ_AGG_ADD)]) == -1        # sourceIPv4Address: not arithmetic
-    assert create([(0, 4, 0, _lib.NGZ_AGG_ADD)]) == -1        # protocolIdentifier: sub-registry
-    assert create([(0, 6, 0, _lib.NGZ_AGG_OR)]) in (-2, -3)   # tcpControlBits OR: valid, needs the device
-    assert create([(0, 56, 0, _lib.NGZ_AGG_ADD)]) == -1       # sourceMacAddress
     assert create([(0, 1, 0, 9)]) == -1                       # unknown op
+    ADD, MIN, MAX, OR = _lib.NGZ_AGG_ADD, _lib.NGZ_AGG_MIN, _lib.NGZ_AGG_MAX, _lib.NGZ_AGG_OR
+    ACCEPT, REJECT, LIMIT = "accept", "reject", "limit"
+    table = [
+        # (IE, op, reference verdict): arithmetic = numeric type, no sub-registry, not identifier / flags
+        ((0, 1), ADD, ACCEPT),      # octetDeltaCount unsigned64 deltaCounter
+        ((0, 434), ADD, ACCEPT),    # mibObjectValueInteger signed32
+        ((0, 311), ADD, ACCEPT),    # samplingProbability float64
+        ((0, 10), ADD, REJECT),     # ingressInterface: identifier semantics
+        ((0, 6), ADD, REJECT),      # tcpControlBits: flags semantics
+        ((0, 4), ADD, REJECT),      # protocolIdentifier: sub-registry
+        ((0, 8), ADD, REJECT),      # sourceIPv4Address
+        ((0, 56), ADD, REJECT),     # sourceMacAddress
+        ((0, 515), ADD, REJECT),    # unsigned256
+        ((0, 150), ADD, REJECT),    # dateTimeSeconds
+        # comparison: by data type only
+        ((0, 311), MIN, ACCEPT),    # float64
+        ((0, 27), MAX, ACCEPT),     # ipv6Address
+        ((0, 8), MIN, ACCEPT),      # ipv4Address
+        ((0, 150), MAX, ACCEPT),    # dateTimeSeconds
+        ((0, 152), MIN, ACCEPT),    # dateTimeMilliseconds
+        ((0, 154), MAX, ACCEPT),    # dateTimeMicroseconds
+        ((0, 156), MIN, ACCEPT),    # dateTimeNanoseconds
+        ((0, 4), MAX, ACCEPT),      # protocolIdentifier: sub-registry enum order
+        ((0, 6), MIN, ACCEPT),      # tcpControlBits: TCPHeaderFlags order
+        ((0, 10), MAX, ACCEPT),     # identifier semantics do not matter for comparison
+        ((0, 56), MIN, REJECT),     # macAddress
+        ((0, 276), MAX, REJECT),    # boolean
+        ((0, 82), MIN, REJECT),     # string
+        ((0, 70), MAX, REJECT),     # octetArray
+        ((0, 515), MIN, REJECT),    # unsigned256
+        ((0, 291), MIN, LIMIT),     # basicList: accepted, variable-length
+        ((0, 89), MAX, LIMIT),      # forwardingStatus: nested reason-code sub-registry
+        # bitwise
+        ((0, 6), OR, ACCEPT),       # tcpControlBits
+        ((0, 4), OR, ACCEPT),       # protocolIdentifier: BitOrAssign of the raw values
+        ((0, 56), OR, ACCEPT),      # macAddress
+        ((0, 27), OR, ACCEPT),      # ipv6Address
+        ((0, 276), OR, ACCEPT),     # boolean
+        ((0, 515), OR, ACCEPT),     # unsigned256
+        ((0, 70), OR, ACCEPT),      # octetArray
+        ((0, 311), OR, REJECT),     # float64
+        ((0, 82), OR, REJECT),      # string
+        ((0, 150), OR, REJECT),     # dateTimeSeconds
+        ((0, 292), OR, REJECT),     # subTemplateList
+    ]
+    for (pen, ie), op, verdict in table:
+        rc = create([(pen, ie, 0, op)])
+        if verdict == ACCEPT:
+            assert rc in (-2, -3) or rc == 0, ((pen, ie), op, rc)
+        elif verdict == REJECT:
+            assert rc == -1, ((pen, ie), op, rc)
+        else:
+            assert rc == -4, ((pen, ie), op, rc)
 
 
 def test_library_exports_every_declared_symbol():

@@ -5,7 +5,8 @@ pinned by the reference's aggregation unit tests (tests/kats_agg.py).
 
 Every comparison is exact: group set, key values, aggregated values (adds wrap at the
 IE's Rust width), record counts, export/collection time bounds, sys-up time and the
-template / port / observation-domain sets."""
+template / port / observation-domain sets -- for the windows each push closes
+(ngz_agg_emit, aggregation.rs:154-160) and for the final flush."""
 import os
 import struct
 import sys
@@ -24,8 +25,6 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 OK, ADD, MN, MX, OR = K.OP_KEY, K.OP_ADD, K.OP_MIN, K.OP_MAX, K.OP_OR
-# rendering of flushed values per IE (pen, id): byte-like IEs stay bytes
-KINDS = {(0, 27): "bytes", (0, 28): "bytes", (0, 56): "bytes", (0, 80): "bytes"}
 
 
 @pytest.fixture(scope="module")
@@ -51,51 +50,79 @@ def dset(tid, recs):
     return struct.pack(">HH", tid, 4 + len(body)) + body
 
 
+def _exact(v):
+    # floats by bit pattern (-0 vs +0), every NaN alike (the NaN an x86 and a GPU add produce
+    # differ in sign; serde renders every NaN as null)
+    if isinstance(v, float):
+        return b"NaN" if v != v else struct.pack("<d", v)
+    return v
+
+
 def norm(groups):
     out = {}
     for g in groups:
-        k = (g["window_start"], g["flow_type"], tuple(g["key"]))
+        k = (g["window_start"], g["flow_type"], tuple(_exact(x) for x in g["key"]))
         assert k not in out, k
-        out[k] = (tuple(g["vals"]), g["record_count"], g["min_export"], g["max_export"], g["max_sysup"],
+        out[k] = (tuple(_exact(v) for v in g["vals"]), g["record_count"], g["min_export"], g["max_export"],
+                  g["max_sysup"],
                   g["min_coll"], g["max_coll"], frozenset(g["templates"]), frozenset(g["ports"]),
                   frozenset(g["domains"]))
     return out
 
 
 def run_device(fields, batches, port=4739, coll=1_700_000_000_000, lateness_s=10, capacity=1 << 16):
-    """batches: list of lists of datagrams, decoded in order on one codec (one peer)."""
+    """batches: list of lists of datagrams, decoded in order on one codec (one peer).
+    Returns (groups emitted after each push, groups of the final flush, late records)."""
     from netgauze_amd.aggregate import FlowAggregator
     from netgauze_amd.flow import FlowInfoCodec
     codec = FlowInfoCodec()
-    agg = FlowAggregator(fields, lateness_s=lateness_s, capacity=capacity, kinds=KINDS)
+    agg = FlowAggregator(fields, lateness_s=lateness_s, capacity=capacity)
     late = 0
+    emitted = []
     for b in batches:
         batch = codec.decode_datagrams(b)
         late += agg.push(batch, port, coll)
+        emitted.append(agg.emit())
     groups = agg.flush()
     assert agg.n_groups() == 0
     agg.close()
     codec.close()
-    return groups, late
+    return emitted, groups, late
 
 
 def run_oracle(fields, batches, port=4739, coll=1_700_000_000_000, lateness_s=10):
-    o = A.aggregate_datagrams(fields, [d for b in batches for d in b], peer_port=port, collection_ms=coll,
-                              lateness_s=lateness_s)
-    late = o.late
-    return o.flush(), late
+    import ngz_oracle as O
+    codec = O.FlowInfoCodec()
+    o = A.FlowAggregatorOracle(fields, 60, lateness_s)
+    emitted = []
+    for b in batches:
+        for d in b:
+            try:
+                pkt = codec.decode(bytearray(d))
+            except O.ParseFail:
+                continue
+            if pkt is not None:
+                o.push_packet(pkt, port, coll)
+        emitted.append(o.emit())
+    return emitted, o.flush(), o.late
 
 
-def check(fields, batches, **kw):
-    g_dev, late_dev = run_device(fields, batches, **kw)
-    kw.pop("capacity", None)
-    g_ref, late_ref = run_oracle(fields, batches, **kw)
-    assert late_dev == late_ref
-    a, b = norm(g_dev), norm(g_ref)
+def same_groups(a, b):
+    a, b = norm(a), norm(b)
     assert set(a) == set(b), (len(a), len(b), sorted(set(a) ^ set(b))[:5])
     for k in b:
         assert a[k] == b[k], (k, a[k], b[k])
-    return g_dev
+
+
+def check(fields, batches, **kw):
+    e_dev, g_dev, late_dev = run_device(fields, batches, **kw)
+    kw.pop("capacity", None)
+    e_ref, g_ref, late_ref = run_oracle(fields, batches, **kw)
+    assert late_dev == late_ref
+    for a, b in zip(e_dev, e_ref):  # the windows each push closed
+        same_groups(a, b)
+    same_groups(g_dev, g_ref)
+    return [g for e in e_dev for g in e] + g_dev
 
 
 def test_kat_repeating_ie_fields(dev):
@@ -125,11 +152,10 @@ def test_wrapping_add_and_signed_min_max(dev):
     recs = [struct.pack(">BiQ", 200, -5, 1), struct.pack(">BiQ", 100, 7, 2), struct.pack(">BiQ", 250, -9, 3)]
     d = [ipfix_msg([tset(500, tpl), dset(500, recs)], 1_700_000_000)]
     fields = [(0, 192, 0, ADD), (0, 434, 0, MN), (0, 434, 0, MX), (0, 1, 0, ADD)]
-    kinds = dict(KINDS)
     from netgauze_amd.aggregate import FlowAggregator
     from netgauze_amd.flow import FlowInfoCodec
     codec = FlowInfoCodec()
-    agg = FlowAggregator(fields, kinds={**kinds, (0, 434): "sint"})
+    agg = FlowAggregator(fields)
     agg.push(codec.decode_datagrams(d))
     (g,) = agg.flush()
     assert g["vals"] == ((200 + 100 + 250) & 0xFF, -9, 7, 6)
@@ -175,7 +201,7 @@ def test_t20_multi_port_collection_times(dev):
     keys = [(0, 4, 0, OK)]
     d = t20_datagrams(3000, 300, [1_700_000_000])
     codec = FlowInfoCodec()
-    agg = FlowAggregator(keys + T20_AGG, kinds=KINDS)
+    agg = FlowAggregator(keys + T20_AGG)
     agg.push(codec.decode_datagrams(d[:6]), 1000, 5_000)
     agg.push(codec.decode_datagrams(d[6:]), 2000, 9_000)
     o = A.FlowAggregatorOracle(keys + T20_AGG)
@@ -239,7 +265,7 @@ def test_wave_preaggregation_bytes_and_presence(dev):
     from netgauze_amd.aggregate import FlowAggregator
     from netgauze_amd.flow import FlowInfoCodec
     codec = FlowInfoCodec()
-    agg = FlowAggregator(fields, kinds={**KINDS, (0, 434): "sint"})
+    agg = FlowAggregator(fields)
     agg.push(codec.decode_datagrams(d))
     got = norm(agg.flush())
     ref = norm(A.aggregate_datagrams(fields, d, collection_ms=0).flush())
@@ -249,17 +275,18 @@ def test_wave_preaggregation_bytes_and_presence(dev):
 
 
 def test_table_full_and_flush_buffer_errors(dev):
-    """A group table that fills up reports NGZ_AGG_E_OVERFLOW (no hang); a flush buffer that is
-    too small is refused without emptying the table."""
+    """More groups than the capacity report NGZ_AGG_E_OVERFLOW (no hang) and leave the
+    aggregator as it was; a flush buffer that is too small is refused without emptying
+    the table."""
     import numpy as np
-    from netgauze_amd import _lib
     from netgauze_amd.aggregate import AggError, FlowAggregator, lib
     from netgauze_amd.flow import FlowInfoCodec
     d = t20_datagrams(5000, 500, [1_700_000_000])
     codec = FlowInfoCodec()
-    agg = FlowAggregator([(0, 8, 0, OK), (0, 12, 0, OK)] + T20_AGG, capacity=16)  # 2048 slots
-    with pytest.raises(AggError, match="group table full"):
+    agg = FlowAggregator([(0, 8, 0, OK), (0, 12, 0, OK)] + T20_AGG, capacity=16)
+    with pytest.raises(AggError, match="capacity|table full"):
         agg.push(codec.decode_datagrams(d))
+    assert agg.n_groups() == 0 and agg.flush() == []
     agg2 = FlowAggregator([(0, 4, 0, OK)] + T20_AGG)
     agg2.push(codec.decode_datagrams(d[:3]))
     n = agg2.n_groups()
@@ -286,3 +313,157 @@ def test_flow_type_separates_groups(dev):
     g = check(K.NF_FIELDS, [[K.nf_packet(), ipfix]], port=9995, coll=K.T_2025_01_01_10_MS)
     assert sorted((x["flow_type"], x["record_count"], x["vals"]) for x in g) == [(9, 1, (1000, 10)),
                                                                                  (10, 2, (2000, 20))]
+
+
+FIVE_TUPLE = [(0, 8, 0, OK), (0, 12, 0, OK), (0, 7, 0, OK), (0, 11, 0, OK), (0, 4, 0, OK)]
+
+
+def test_hash_collisions_stay_exact(dev, monkeypatch):
+    """A 3-bit key hash makes nearly every distinct 5-tuple collide: groups are still exact
+    (keys compared, collided records re-probed), where the previous design returned
+    NGZ_AGG_E_COLLISION."""
+    monkeypatch.setenv("NGZ_AGG_HASH_BITS", "3")
+    d = t20_datagrams(3000, 100, [1_700_000_010, 1_700_000_070])
+    g = check(FIVE_TUPLE + T20_AGG, [d[:10], d[10:]])
+    assert len(g) > 1000
+
+
+def test_string_key_declared_at_two_lengths(dev):
+    """interfaceName "eth0" in a 16- and a 32-byte fixed string field is one key: the reference
+    compares the NUL-truncated Field::String (generator.rs:1654-1669)."""
+    t1, t2 = [(82, 16), (1, 8)], [(82, 32), (1, 8)]
+    r1 = [b"eth0".ljust(16, b"\0") + struct.pack(">Q", 5)]
+    r2 = [b"eth0".ljust(32, b"\0") + struct.pack(">Q", 7), b"eth1".ljust(32, b"\0") + struct.pack(">Q", 1)]
+    d = [ipfix_msg([tset(700, t1), tset(701, t2), dset(700, r1), dset(701, r2)], 1_700_000_000)]
+    g = check([(0, 82, 0, OK), (0, 1, 0, ADD)], [d])
+    assert sorted((x["key"], x["vals"], x["record_count"]) for x in g) == [(("eth0",), (12,), 2), (("eth1",), (1,), 1)]
+
+
+def test_octet_key_lengths_are_part_of_the_key(dev):
+    """An octetArray key is a Box<[u8]>: [1,2,3,4] and [1,2,3,4,0,0] are different keys."""
+    t1, t2 = [(95, 4), (1, 8)], [(95, 6), (1, 8)]
+    d = [ipfix_msg([tset(710, t1), tset(711, t2), dset(710, [b"\x01\x02\x03\x04" + struct.pack(">Q", 1)]),
+                    dset(711, [b"\x01\x02\x03\x04\x00\x00" + struct.pack(">Q", 2)])], 1_700_000_000)]
+    g = check([(0, 95, 0, OK), (0, 1, 0, ADD)], [d])
+    assert sorted(x["key"] for x in g) == [(b"\x01\x02\x03\x04",), (b"\x01\x02\x03\x04\x00\x00",)]
+
+
+def test_peer_ports_across_flush_cycles(dev):
+    """More than 64 distinct peer ports over the aggregator's life: the set dictionaries start
+    over at every flush, so only 64 live ones are a limit (the reference sets are unbounded)."""
+    from netgauze_amd.aggregate import FlowAggregator
+    from netgauze_amd.flow import FlowInfoCodec
+    d = t20_datagrams(200, 100, [1_700_000_000])
+    codec = FlowInfoCodec()
+    agg = FlowAggregator([(0, 4, 0, OK), (0, 1, 0, ADD)])
+    for cycle in range(8):
+        for i in range(10):
+            agg.push(codec.decode_datagrams(d), 10000 + 10 * cycle + i, 0)
+        out = agg.flush()
+        assert out and all(x["ports"] == {10000 + 10 * cycle + i for i in range(10)} for x in out)
+
+
+def test_closed_windows_free_dictionary_entries(dev):
+    """A long stream whose export time moves on: each push closes the previous windows
+    (emitted, aggregation.rs:154-160), their ports / templates / domains no longer count,
+    and a stream with 100 distinct ports never overflows a 64-entry dictionary."""
+    from netgauze_amd.aggregate import FlowAggregator
+    from netgauze_amd.flow import FlowInfoCodec
+    import ngz_oracle as O
+    fields = [(0, 4, 0, OK), (0, 1, 0, ADD), (0, 2, 0, MX)]
+    codec, oc = FlowInfoCodec(), O.FlowInfoCodec()
+    agg = FlowAggregator(fields, lateness_s=10, capacity=64)
+    o = A.FlowAggregatorOracle(fields, 60, 10)
+    tmpl = t20_datagrams(100, 100, [1_700_000_000])[0]
+    oc.decode(bytearray(tmpl))
+    codec.decode_datagrams([tmpl])
+    for i in range(100):
+        d = t20_datagrams(300, 100, [1_700_000_000 + 120 * i], seed_first=1000 * i)[1:]
+        agg.push(codec.decode_datagrams(d), 20000 + i, i)
+        for x in d:
+            o.push_packet(oc.decode(bytearray(x)), 20000 + i, i)
+        same_groups(agg.emit(), o.emit())
+    same_groups(agg.flush(), o.flush())
+
+
+def test_failed_push_leaves_the_aggregator_unchanged(dev):
+    """A push that would exceed the capacity fails without touching the groups, the set
+    dictionaries or the event time: the flush afterwards equals the oracle of the pushes
+    that succeeded."""
+    from netgauze_amd.aggregate import AggError, FlowAggregator
+    from netgauze_amd.flow import FlowInfoCodec
+    fields = [(0, 11, 0, OK)] + T20_AGG
+    a = t20_datagrams(400, 100, [1_700_000_000])
+    b = t20_datagrams(4000, 100, [1_700_000_030], seed_first=777)[1:]
+    codec = FlowInfoCodec()
+    o = A.aggregate_datagrams(fields, a, peer_port=1, collection_ms=5)
+    n_a = len(o.groups)
+    agg = FlowAggregator(fields, capacity=n_a + 10)
+    agg.push(codec.decode_datagrams(a), 1, 5)
+    with pytest.raises(AggError, match="capacity|table full"):
+        agg.push(codec.decode_datagrams(b), 2, 9)
+    assert agg.n_groups() == n_a
+    same_groups(agg.flush(), o.flush())
+
+
+def test_ordered_reductions(dev):
+    """Reductions whose result depends on record order or on a Rust Ord the atomics do not
+    have: float64 Add / Min / Max (OrderedFloat: NaN greatest, -0 == +0 with min keeping the
+    group's value and max taking the record's), IPv6 Min / Max, and Min / Max over a
+    sub-registry enum (protocolIdentifier: Unassigned values after every registered one) and
+    TCPHeaderFlags (FIN most significant).  Two pushes: the second folds into the first's values."""
+    import random
+    rnd = random.Random(11)
+    tpl = [(8, 4), (311, 8), (27, 16), (4, 1), (6, 1)]
+    specials = [0.0, -0.0, float("nan"), float("inf"), -float("inf"), 1e-300, 1.5, -2.25, 3.0e10]
+
+    def rec():
+        f = rnd.choice(specials) if rnd.random() < 0.5 else rnd.uniform(-1e6, 1e6)
+        return struct.pack(">Id16sBB", rnd.choice([1, 2, 3]), f, bytes(rnd.getrandbits(8) for _ in range(16)),
+                           rnd.choice([6, 17, 147, 148, 200, 255]), rnd.getrandbits(8))
+    d1 = [ipfix_msg([tset(720, tpl), dset(720, [rec() for _ in range(300)])], 1_700_000_000)]
+    d2 = [ipfix_msg([dset(720, [rec() for _ in range(300)])], 1_700_000_001) for _ in range(3)]
+    fields = [(0, 8, 0, OK), (0, 311, 0, ADD), (0, 311, 0, MN), (0, 311, 0, MX), (0, 27, 0, MN), (0, 27, 0, MX),
+              (0, 4, 0, MN), (0, 4, 0, MX), (0, 6, 0, MN), (0, 6, 0, MX)]
+    g = check(fields, [d1, d2])
+    assert len(g) == 3
+
+
+def test_flowinfo_rendering(dev):
+    """AggFlowInfo::into_flowinfo_with_extra_fields (aggregator.rs:203-277): key and aggregated
+    fields, originalFlowsPresent, min/maxExportSeconds, collectionTimeMilliseconds, then the
+    port / domain / template sets (ascending), as the oracle renders the same groups."""
+    from netgauze_amd.aggregate import FlowAggregator
+    from netgauze_amd.flow import FlowInfoCodec
+    import ngz_oracle as O
+    ipfix = ipfix_msg([tset(256, K.NF_TEMPLATE), dset(256, [K.NF_RECORD, K.NF_RECORD])], K.T_2025_01_01_12,
+                      domain=100)
+    d = [K.nf_packet(), ipfix] + t20_datagrams(500, 100, [1_700_000_000])
+    fields = K.NF_FIELDS + [(0, 6, 0, OR), (0, 22, 0, MN)]
+    codec = FlowInfoCodec()
+    agg = FlowAggregator(fields, lateness_s=10 ** 6 // 1000, window_s=10 ** 6 // 1000)
+    agg.push(codec.decode_datagrams(d), 9995, K.T_2025_01_01_10_MS)
+    hdr, raw = agg.flush_raw()
+    groups = agg.render(hdr, raw)
+    lines = agg.flowinfo_json(raw, shard_id=3, seq0=40, export_time_ms=1_760_000_000_123)
+    o = A.aggregate_datagrams(fields, d, peer_port=9995, collection_ms=K.T_2025_01_01_10_MS,
+                              window_s=1000, lateness_s=1000)
+    ref = {k: g for k, g in ((k, g) for g in o.emit() + o.flush() for k in [(g["window_start"], g["flow_type"],
+                                                                            tuple(_exact(x) for x in g["key"]))])}
+    assert len(lines) == len(groups) == len(ref)
+    for i, (g, line) in enumerate(zip(groups, lines)):
+        k = (g["window_start"], g["flow_type"], tuple(_exact(x) for x in g["key"]))
+        assert line == o.flowinfo_json(ref[k], shard_id=3, seq=40 + i, export_time_ms=1_760_000_000_123), k
+    assert any('"NetFlowV9"' in x for x in lines) and any('"IPFIX"' in x for x in lines)
+
+
+def test_stale_batch_is_refused(dev):
+    from netgauze_amd.aggregate import AggError, FlowAggregator
+    from netgauze_amd.flow import FlowInfoCodec
+    codec = FlowInfoCodec()
+    d = t20_datagrams(200, 100, [1_700_000_000])
+    old = codec.decode_datagrams(d)
+    codec.decode_datagrams(d[1:])
+    agg = FlowAggregator([(0, 4, 0, OK), (0, 1, 0, ADD)])
+    with pytest.raises(AggError, match="stale"):
+        agg.push(old)

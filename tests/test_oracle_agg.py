@@ -66,8 +66,12 @@ def test_lateness_and_minute_windows():
     d = [ipfix_msg(t + rec, times[0])] + [ipfix_msg(rec, x) for x in times[1:]]
     agg = A.aggregate_datagrams(K.MISSING_FIELDS, d, lateness_s=10)
     assert agg.late == 2  # 165 and 169 are more than 10 s behind 180
+    # event time 180: cutoff = get_window_start(180 - 10) - 60 = 100 closes the first window
+    # (aggregation.rs:154-160); the second stays active until the flush
+    closed = [(g["window_start"], g["record_count"]) for g in agg.emit()]
+    assert closed == [(1_700_000_100, 1)] and agg.emit() == []
     got = sorted((g["window_start"], g["record_count"]) for g in agg.flush())
-    assert got == [(1_700_000_100, 1), (1_700_000_160, 2)]  # minute floors
+    assert got == [(1_700_000_160, 2)]  # minute floors
 
 
 def test_netflowv9_explode():
@@ -75,3 +79,28 @@ def test_netflowv9_explode():
     (g,) = agg.flush()
     for k, v in K.NF_EXPECTED.items():
         assert g[k] == v, k
+
+
+def test_float_and_enum_orders():
+    """Min / Max follow the Rust Ord of each Field type; Ord::min keeps the group's value
+    on equality, Ord::max takes the record's."""
+    import ngz_oracle as O
+    f64 = next(ie for ie in O.REGISTRY.by_key.values() if ie.dtype == "float64")
+    nan = float("nan")
+    assert A.reduce_value(f64, A.OP_MIN, 1.0, nan) == 1.0          # NaN is the greatest
+    assert A.reduce_value(f64, A.OP_MAX, 1.0, nan) != A.reduce_value(f64, A.OP_MAX, 1.0, nan)  # -> NaN
+    import math
+    assert math.copysign(1, A.reduce_value(f64, A.OP_MIN, 0.0, -0.0)) == 1    # equal: keep lhs
+    assert math.copysign(1, A.reduce_value(f64, A.OP_MAX, 0.0, -0.0)) == -1   # equal: take rhs
+    f32ie = type("IE", (), {"dtype": "float32", "kind": "iana", "id": 0, "subreg": None})()  # no float32 IE is registered
+    assert A.reduce_value(f32ie, A.OP_ADD, 16777216.0, 1.0) == 16777216.0  # f32 rounding
+    assert A.reduce_value(f64, A.OP_ADD, 16777216.0, 1.0) == 16777217.0
+    proto = O.REGISTRY.lookup(0, 4)  # protocolIdentifier: sub-registry enum
+    unassigned = next(v for v in range(256) if v not in {x for x, _ in proto.subreg["entries"]})
+    assert A.reduce_value(proto, A.OP_MAX, 200 if 200 in {x for x, _ in proto.subreg["entries"]} else 6,
+                          unassigned) == unassigned  # Unassigned(x) after every registered variant
+    assert A.reduce_value(proto, A.OP_MIN, 147, unassigned) == 147  # registered 147 < Unassigned(148)
+    assert A.reduce_value(proto, A.OP_MIN, 250, unassigned) == unassigned  # Unassigned(148) < Unassigned(250)
+    tcp = O.REGISTRY.lookup(0, 6)
+    assert A.reduce_value(tcp, A.OP_MAX, 0x01, 0x80) == 0x01  # FIN (bit 0) outranks CWR (bit 7)
+    assert A.reduce_value(tcp, A.OP_MIN, 0x02, 0x01) == 0x02  # {SYN} < {FIN}

@@ -246,8 +246,10 @@ def parse_ies(ie_node, pen, ext):
             continue
         if child_text(rec, "date") is None:
             continue
+        # dataTypeSemantics (xml_parsers/ipfix.rs:194-195): identifier / flags IEs do not
+        # support arithmetic (generator.rs:584-589, IE::supports_arithmetic_ops :1176-1180)
         out.append({"pen": pen, "id": eid, "name": name, "type": dt,
-                    "subreg": subs.get(eid)})
+                    "semantics": child_text(rec, "dataTypeSemantics"), "subreg": subs.get(eid)})
     return out
 
 
@@ -309,7 +311,8 @@ def write_c_table(ies, vendors, path):
         " * Do not edit. One row per registered IE: {pen, id, data type, flags, name}.",
         " * flags: bit0 MPLS label ([u8;3], generator.rs:2753-2755),",
         " *        bit1 tcpControlBits (TCPHeaderFlags::from truncates to u8, iana/src/tcp.rs:165-168),",
-        " *        bit2 has sub-registry (lossless enum wrap, generator_sub_registries.rs:215-247). */",
+        " *        bit2 has sub-registry (lossless enum wrap, generator_sub_registries.rs:215-247),",
+        " *        bit3 dataTypeSemantics identifier, bit4 dataTypeSemantics flags (generator.rs:584-589). */",
     ]
     for ie in ies:
         flags = 0
@@ -319,6 +322,10 @@ def write_c_table(ies, vendors, path):
             flags |= 2
         if ie["subreg"] is not None:
             flags |= 4
+        if ie.get("semantics") == "identifier":
+            flags |= 8
+        if ie.get("semantics") == "flags":
+            flags |= 16
         lines.append('NGZ_IE(%du, %du, %d, %d, "%s")' % (ie["pen"], ie["id"], DATA_TYPES.index(ie["type"]), flags, ie["name"]))
     lines.append("")
     lines.append("/* vendor PENs with their own IE package (build.rs:271); other PENs decode as IE::Unknown. */")
