@@ -17,6 +17,7 @@ output rows as the reference's aggregated FlowInfo
 (AggFlowInfo::into_flowinfo_with_extra_fields, aggregator.rs:203-277).
 """
 import ctypes
+import sys
 import json
 import os
 import struct
@@ -93,6 +94,8 @@ class FlowAggregator:
             self._h = ctypes.c_void_p()
 
     def __del__(self):
+        if sys.is_finalizing():  # the HIP runtime may be torn down already: leave it to the process exit
+            return
         try:
             self.close()
         except Exception:

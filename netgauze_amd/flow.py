@@ -10,6 +10,7 @@ columns in HBM.  `template_counts(reset=True)` is reset_processed_count
 (crates/flow-pkt/src/ipfix.rs:65-69).
 """
 import ctypes
+import sys
 import json
 
 import numpy as np
@@ -194,6 +195,8 @@ class FlowInfoCodec:
             self._ctx = None
 
     def __del__(self):
+        if sys.is_finalizing():  # the HIP runtime may be torn down already: leave it to the process exit
+            return
         try:
             self.close()
         except Exception:

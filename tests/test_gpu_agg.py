@@ -211,7 +211,7 @@ def test_t20_multi_port_collection_times(dev):
         pkt = oc.decode(bytearray(x))
         if pkt is not None:
             o.push_packet(pkt, 1000 if i < 6 else 2000, 5_000 if i < 6 else 9_000)
-    assert norm(agg.flush()) == norm(o.flush())
+    assert norm(agg.emit() + agg.flush()) == norm(o.emit() + o.flush())
 
 
 def peers_of(name):
@@ -353,9 +353,9 @@ def test_peer_ports_across_flush_cycles(dev):
     over at every flush, so only 64 live ones are a limit (the reference sets are unbounded)."""
     from netgauze_amd.aggregate import FlowAggregator
     from netgauze_amd.flow import FlowInfoCodec
-    d = t20_datagrams(200, 100, [1_700_000_000])
+    d = t20_datagrams(200, 100, [1_700_000_000])  # two data messages, one minute apart
     codec = FlowInfoCodec()
-    agg = FlowAggregator([(0, 4, 0, OK), (0, 1, 0, ADD)])
+    agg = FlowAggregator([(0, 4, 0, OK), (0, 1, 0, ADD)], lateness_s=60)  # nothing late, no window closes
     for cycle in range(8):
         for i in range(10):
             agg.push(codec.decode_datagrams(d), 10000 + 10 * cycle + i, 0)
@@ -397,13 +397,13 @@ def test_failed_push_leaves_the_aggregator_unchanged(dev):
     b = t20_datagrams(4000, 100, [1_700_000_030], seed_first=777)[1:]
     codec = FlowInfoCodec()
     o = A.aggregate_datagrams(fields, a, peer_port=1, collection_ms=5)
-    n_a = len(o.groups)
+    n_a = len(o.groups) + len(o.closed)
     agg = FlowAggregator(fields, capacity=n_a + 10)
     agg.push(codec.decode_datagrams(a), 1, 5)
     with pytest.raises(AggError, match="capacity|table full"):
         agg.push(codec.decode_datagrams(b), 2, 9)
     assert agg.n_groups() == n_a
-    same_groups(agg.flush(), o.flush())
+    same_groups(agg.emit() + agg.flush(), o.emit() + o.flush())
 
 
 def test_ordered_reductions(dev):
