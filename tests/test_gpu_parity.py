@@ -208,6 +208,46 @@ def test_t20_full_size_1e8(dev):
     assert codec.template_counts(10) == {256: offs.numel()}  # one processed_count per data set
 
 
+def test_cfg4_full_size_batch_over_2gib(dev):
+    """Config 4 at 1.6e7 records: the batch spans more than 2 GiB, so row-mode groups whose
+    records lie more than 2 GiB apart go one record per pass (ngz_dev.h row_group), and the
+    staged variable-length decode and the record map work above 2 GiB.  Every datagram
+    decodes, the per-template record counts hold, every NetFlow v9 column equals its re-laid
+    wire bytes (on the GPU), and the FlowInfo JSON of datagrams sampled at the start, the
+    middle and past 2 GiB equals the oracle's."""
+    from netgauze_amd import synth
+    n = 16_000_000
+    seed = synth.SEED_CFG4 + 99
+    dg = synth.cfg4_datagrams(n, seed=seed)
+    codec = new_codec()
+    codec.decode_datagrams(dg[:2])
+    data = dg[2:]
+    buf, offs, lens = synth.host_batch(data, device=dev)
+    assert buf.numel() > (1 << 31)
+    batch = codec.decode_batch(buf, offs, lens)
+    hdr = batch.dgram_headers()
+    assert (hdr["status"] == 0).all() and len(hdr) == len(data)
+    by_tid = {s.template_id: s for s in batch.slots}
+    assert by_tid[synth.NF313_ID].n_records == n // 2 and by_tid[synth.V900_ID].n_records == n - n // 2
+    nf = synth.template_records(synth.NF313, n // 2, seed, dev)
+    slot = by_tid[synth.NF313_ID]
+    for f, fi in enumerate(slot.fields):
+        if fi.kind not in (L.K_UINT, L.K_DTMS, L.K_BYTES, L.K_TCPFLAGS):
+            continue
+        got = column_on_device(slot, f, n // 2)
+        assert torch.equal(got, expected_column(nf, fi)), f
+    del nf
+    oc = O.FlowInfoCodec()
+    for t in dg[:2]:
+        oc.decode(bytearray(t))
+    past = int(torch.searchsorted(offs, torch.tensor([1 << 31], device=offs.device)).item())
+    sample = list(range(0, 40)) + list(range(len(data) // 2, len(data) // 2 + 40)) + list(range(past, past + 40)) + \
+        list(range(len(data) - 40, len(data)))
+    for d in sample:
+        exp = O.dumps(oc.decode(bytearray(data[d])).to_json())
+        assert batch.json(d) == exp, d
+
+
 def test_cfg3_mixed_templates_oracle(dev):
     """Config 3 shape (8 templates, 40-153 B records, interleaved messages)
     against the oracle, every field."""
