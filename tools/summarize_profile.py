@@ -59,14 +59,20 @@ if traces and bench:
 
 out = {}
 for c in ("FETCH_SIZE", "WRITE_SIZE"):
-    vals = {}
+    vals, frames = {}, []
     for f in glob.glob(os.path.join(d, "pmc_" + c, "*counter_collection.csv")):
         for r in csv.DictReader(open(f)):
+            i = int(r["Dispatch_Id"])
+            if "k_frame" in r["Kernel_Name"]:
+                frames.append(i)
             if any(k in r["Kernel_Name"] for k in DECODE):
-                vals[r["Dispatch_Id"]] = vals.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
+                vals[i] = vals.get(i, 0.0) + float(r["Counter_Value"])
     if vals:
-        out[c] = max(vals.values())
-print("== PMC per decode-kernel launch (largest dispatch = bench batch)")
+        # one step may launch several decode kernels (one per active template): the
+        # decode dispatches after the last step's framing kernel, summed
+        last = max(frames) if frames else -1
+        out[c] = sum(v for i, v in vals.items() if i > last)
+print("== PMC per step's decode launches (the last step's dispatches, summed)")
 for c, v in out.items():
     print("%s = %.0f KiB" % (c, v))
 if "FETCH_SIZE" in out and "WRITE_SIZE" in out:
@@ -81,7 +87,7 @@ if "FETCH_SIZE" in out and "WRITE_SIZE" in out:
                "alg_bytes_per_launch": alg, "traffic_over_alg": (fetch + write) / alg if alg else None,
                "timed_kernel_ms_trace": timed, "bench_kernel_ms": bench["roofline"]["kernel_ms"] if bench else None,
                "source_hash": buildinfo.source_hash(), "git_sha": os.environ.get("GIT_SHA"),
-               "kernel": "decode (largest dispatch)",
+               "kernel": "decode (every decode dispatch of one step)",
                "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes; FETCH_SIZE x2 (gfx950 "
                          "wide-read correction, MI355X_MICROARCH.md HBM)"},
               open(os.path.join(d, "traffic.json"), "w"), indent=1)
