@@ -386,16 +386,20 @@ __device__ __forceinline__ Rec rec_of(const RecCtx &C, uint64_t t, unsigned int 
     return r;
 }
 
-// Open-addressing probe for one record's group.  exact = false (first pass): a slot whose tag
-// equals the record's is taken as its group (k_agg_check then compares the keys); exact = true
-// (records whose hash collided): keys are compared at every equal tag, probing on past a
-// different key.  Claiming a free slot: CAS on the tag, then the key bytes.
+// Open-addressing probe for one record's group.  Claiming a free slot: CAS on the tag, then
+// the key bytes.  At a slot whose tag equals the record's, hashed keys are compared when the
+// slot's key is known to be written: its group was reduced by an earlier push (the row's
+// per-push marker is set), or exact = true (records whose hash collided, re-probed after the
+// pass that wrote every key).  A slot claimed by another record of this same pass is taken
+// tentatively (*tentative): k_agg_check compares the keys once the pass is over.
 template <bool EXACT>
 __device__ __forceinline__ uint32_t probe(const AggSlotPlan &sp, const AggParams &P, uint64_t row, uint32_t win,
                                           uint32_t kp, uint64_t h, unsigned long long *__restrict__ tags,
                                           uint8_t *__restrict__ rows, uint32_t *__restrict__ claims,
-                                          unsigned long long *__restrict__ n_claims, unsigned int *__restrict__ err) {
+                                          unsigned long long *__restrict__ n_claims, unsigned int *__restrict__ err,
+                                          bool *tentative) {
     uint64_t g = slot_of(h) & P.mask;
+    *tentative = false;
     for (uint64_t probes = 0; probes <= P.mask; ++probes, g = (g + 1) & P.mask) {
         unsigned long long cur = tags[g];
         if (cur == TAG_EMPTY) {
@@ -407,7 +411,14 @@ __device__ __forceinline__ uint32_t probe(const AggSlotPlan &sp, const AggParams
             }
         }
         if (cur != h) continue;
-        if (!EXACT || key_equal(rows + g * P.row_bytes, sp, P, row, win, kp)) return (uint32_t)g;
+        if (P.packed) return (uint32_t)g;
+        const uint8_t *R = rows + g * P.row_bytes;
+        if (EXACT || *(const volatile uint32_t *)(R + 36) != 0) {
+            if (key_equal(R, sp, P, row, win, kp)) return (uint32_t)g;
+            continue;
+        }
+        *tentative = true;
+        return (uint32_t)g;
     }
     atomicOr(err, 2u);  // table full
     return NONE;
@@ -419,6 +430,7 @@ __global__ __launch_bounds__(256) void k_agg_claim(const RecCtx C, const AggPara
                                                    uint32_t *__restrict__ rec_g, uint32_t *__restrict__ claims,
                                                    unsigned long long *__restrict__ n_claims,
                                                    unsigned long long *__restrict__ late_count,
+                                                   uint32_t *__restrict__ tent, unsigned int *__restrict__ n_tent,
                                                    unsigned int *__restrict__ err) {
     for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < C.n_rec; base += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t t = base + threadIdx.x;
@@ -432,7 +444,9 @@ __global__ __launch_bounds__(256) void k_agg_claim(const RecCtx C, const AggPara
             const uint32_t ts = C.hdr[r.si.dgram].time, win = ts - ts % 60;  // get_window_start
             uint32_t kp;
             const uint64_t h = key_tag(sp, P, r.row, win, kp);
-            g = probe<false>(sp, P, r.row, win, kp, h, tags, rows, claims, n_claims, err);
+            bool tentative;
+            g = probe<false>(sp, P, r.row, win, kp, h, tags, rows, claims, n_claims, err, &tentative);
+            if (tentative) tent[atomicAdd(n_tent, 1u)] = (uint32_t)t;
         }
         rec_g[t] = g;
     }
@@ -479,7 +493,8 @@ __global__ __launch_bounds__(256) void k_agg_reprobe(const RecCtx C, const AggPa
         const uint32_t ts = C.hdr[r.si.dgram].time, win = ts - ts % 60;
         uint32_t kp;
         const uint64_t h = key_tag(sp, P, r.row, win, kp);
-        rec_g[t] = probe<true>(sp, P, r.row, win, kp, h, tags, rows, claims, n_claims, err);
+        bool tentative;
+        rec_g[t] = probe<true>(sp, P, r.row, win, kp, h, tags, rows, claims, n_claims, err, &tentative);
     }
 }
 
@@ -1622,14 +1637,23 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, uint16_t pe
         if (hipStreamSynchronize(st) != hipSuccess) a->poisoned = true;
         return fail(a, rc, why);
     };
+    // claim / check keep no state across tiles: one record per thread, all of them in flight
+    const uint32_t fg = std::max<uint32_t>(1, std::min<uint32_t>(blocks, 1u << 20));
     if (n_rec) {
-        hipLaunchKernelGGL(k_agg_claim, dim3(ig), dim3(256), 0, st, C, P, a->tags, a->rows, rec_g, claims, a->n_claims,
-                           a->late, a->err);
+        AGG_HIP(a, hipMemsetAsync(a->n_coll, 0, 4, st));
+        hipLaunchKernelGGL(k_agg_claim, dim3(fg), dim3(256), 0, st, C, P, a->tags, a->rows, rec_g, claims, a->n_claims,
+                           a->late, list_b, a->n_coll, a->err);
         if (!P.packed) {
-            // hashed keys: compare, and re-probe the records of collided keys comparing keys
+            // hashed keys: the records that took a slot another record of this pass claimed are
+            // compared now that every key is written; the records of collided keys re-probe
+            // comparing keys
+            unsigned int nt = 0;
+            AGG_HIP(a, hipMemcpyAsync(&nt, a->n_coll, 4, hipMemcpyDeviceToHost, st));
+            AGG_HIP(a, hipStreamSynchronize(st));
             AGG_HIP(a, hipMemsetAsync(a->n_coll, 0, 4, st));
-            hipLaunchKernelGGL(k_agg_check, dim3(grid_for(n_rec)), dim3(256), 0, st, C, P, a->rows, rec_g, nullptr, 0u,
-                               list_a, a->n_coll, a->err);
+            if (nt)
+                hipLaunchKernelGGL(k_agg_check, dim3(grid_for(nt, 256, 1u << 20)), dim3(256), 0, st, C, P, a->rows, rec_g,
+                                   list_b, nt, list_a, a->n_coll, a->err);
             for (int round = 0;; ++round) {
                 unsigned int nc = 0;
                 AGG_HIP(a, hipMemcpyAsync(&nc, a->n_coll, 4, hipMemcpyDeviceToHost, st));
@@ -1656,12 +1680,15 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, uint16_t pe
     if (errv & 16) { a->poisoned = true; return rollback(NGZ_E_DEVICE, "set table entry out of range"); }
     if (errv & 2) return rollback(NGZ_AGG_E_OVERFLOW, "group table full");
     if (a->live + n_claims > a->limit) return rollback(NGZ_AGG_E_OVERFLOW, "more groups than the aggregator's capacity");
-    // commit: every record has its group; reduce
+    // commit: every record has its group; reduce.  Few groups: a bounded grid whose workgroups
+    // walk many tiles, so the LDS combine table collects each group's records across them; many
+    // groups (about one record per group and push): one tile per workgroup, all records in flight
     if (n_rec) {
+        const uint32_t ag = (a->live + n_claims) * 8 > n_rec ? fg : ig;
         if (P.n_vals <= 8)
-            hipLaunchKernelGGL(k_agg_apply<8>, dim3(ig), dim3(256), 0, st, C, P, rec_g, a->rows, a->err);
+            hipLaunchKernelGGL(k_agg_apply<8>, dim3(ag), dim3(256), 0, st, C, P, rec_g, a->rows, a->err);
         else
-            hipLaunchKernelGGL(k_agg_apply<NGZ_AGG_MAX_VALUES>, dim3(ig), dim3(256), 0, st, C, P, rec_g, a->rows, a->err);
+            hipLaunchKernelGGL(k_agg_apply<NGZ_AGG_MAX_VALUES>, dim3(ag), dim3(256), 0, st, C, P, rec_g, a->rows, a->err);
         if (ordered) {
             uint32_t *sk = (uint32_t *)(a->rec_buf + 5 * R4), *sv = (uint32_t *)(a->rec_buf + 6 * R4),
                      *sk2 = (uint32_t *)(a->rec_buf + 7 * R4), *sv2 = (uint32_t *)(a->rec_buf + 8 * R4);
