@@ -75,8 +75,8 @@ typedef struct ngz_agg ngz_agg;
  * identifier/flags): NGZ_E_INVALID where the reference rejects the config, NGZ_E_LIMIT where
  * it accepts one the device does not run (Min/Max over list types or the nested reason-code
  * sub-registry of forwardingStatus).  Key fields keep their order (key_select), aggregated
- * fields theirs (agg_select).  capacity: live groups held at most (the HBM table has at
- * least twice as many slots). */
+ * fields theirs (agg_select).  capacity: live groups held at most, up to 2^30 (the HBM table
+ * has at least twice as many slots). */
 int ngz_agg_create(int device, const ngz_agg_field *fields, uint32_t n_fields, uint64_t window_ms,
                    uint64_t lateness_ms, uint64_t capacity, ngz_agg **out);
 void ngz_agg_destroy(ngz_agg *a);
@@ -111,8 +111,8 @@ typedef struct {
     uint64_t domain_bits[2];    /* observation_domain_ids set */
 } ngz_agg_row;
 
-/* Row layout of ngz_agg_flush output: row_bytes per group; key field k at
- * key_off[k] (column width of the IE, rounded to 4; width in key_width[k]: 0 if the
+/* Row layout of ngz_agg_flush output: row_bytes per group (a multiple of 16); the
+ * ngz_agg_row header, 8 bytes of device bookkeeping, then key field k at key_off[k] (column width of the IE, rounded to 4; width in key_width[k]: 0 if the
  * field never appeared), value v at val_off[v] (8 bytes; OR of byte fields: width
  * rounded to 4, in val_width[v]).  Integer values are little-endian at the IE's
  * Rust width (adds wrap at that width, as release-mode `+=`). */

@@ -10,7 +10,8 @@
 //                 current_time the running max of the earlier non-late items)
 //                 and its observation-domain dictionary entry (new domains are
 //                 listed for the host, which assigns them: k_agg_domfix)
-//   hipcub sum-scan over set record counts -> k_agg_setidx: set of every record
+//   hipcub sum-scan over set record counts -> k_agg_recinfo: every record's row, times, plan
+//                 and datagram info, 16 bytes (one load in the record kernels)
 //   k_agg_claim   one lane per record: its group's slot in the HBM table
 //                 (open addressing; a new group's first record claims a slot
 //                 with a CAS on the 64-bit tag and writes the exact key).  Keys
@@ -53,12 +54,15 @@
 namespace {
 
 constexpr uint32_t ROW_HDR = 88;  // sizeof(ngz_agg_row)
+constexpr uint32_t OWN_OFF = 88;  // device bookkeeping after the header: the record owning the row in this push
+constexpr uint32_t KEY0 = 96;     // first key byte
 static_assert(sizeof(ngz_agg_row) == ROW_HDR, "ngz_agg_row layout");
 constexpr uint32_t DOM_SLOTS = 128;
 constexpr uint32_t SET_BITS = 64;
 constexpr uint32_t NEWDOM_SLOTS = 256;  // distinct new observation domains one push may bring
 constexpr uint64_t TAG_EMPTY = 0, TAG_TOMB = 1;
 constexpr uint32_t NONE = 0xFFFFFFFFu;
+constexpr uint32_t OWN_BIT = 0x80000000u;  // rec_g: the record is its group's owner (slots < 2^31)
 
 // dginfo bits (per datagram)
 constexpr uint16_t DG_USE = 1, DG_LATE = 2, DG_MISSING = 0x200;  // domain index in bits 2..8
@@ -112,6 +116,11 @@ struct AggParams {
     uint32_t lds_ok;            // 1: no byte-wise OR values (wave results may be combined in LDS)
     uint32_t packed;            // 1: the whole group key packs into 63 bits (exact tag)
     uint64_t hash_mask;         // hashed keys: bits of the hash kept (tests force collisions with NGZ_AGG_HASH_BITS)
+    uint32_t own;               // 1: one record per group and push (its owner) reduces with plain stores
+    uint32_t kw_n;              // hashed keys of at most 8 words: their count (key words held in registers), else 0
+    uint8_t kw_key[8], kw_idx[8];  // key word j: its key field and its word within the field
+    uint64_t unit_op[2];        // owner path: 4-bit op of each 8-byte unit of the row (units 0-15, 16-31)
+    uint64_t unit_src[2];       // ... and its operand (U_SRC_*)
 };
 
 __device__ __forceinline__ uint64_t mix64(uint64_t h, uint64_t v) {
@@ -157,8 +166,31 @@ struct KeyWords {
     }
 };
 
+// Canonical key words of a record held in registers (hashed keys of at most 8 words): the
+// record's columns are read once, and the slot's key is compared with a few wide loads
+struct KeyVal {
+    uint32_t w[8];
+};
+
+__device__ __forceinline__ void key_words(const AggSlotPlan &sp, const AggParams &P, uint64_t row, KeyVal &kv) {
+    bool nul = false;
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) {
+        kv.w[j] = 0;
+        if (j >= P.kw_n) continue;
+        const uint32_t k = P.kw_key[j], i = P.kw_idx[j];
+        const uint8_t *c = sp.key_col[k];
+        if (!c) continue;
+        const uint32_t w = sp.key_w[k];
+        if (i == 0) nul = false;
+        const uint8_t *q = c + row * w;
+        if (P.key_kind[k] == KK_OCTETS) kv.w[j] = i == 0 ? w : cell_word(q, w, i - 1, false, nul);
+        else kv.w[j] = cell_word(q, w, i, P.key_kind[k] == KK_STR, nul);
+    }
+}
+
 __device__ __forceinline__ uint64_t key_tag(const AggSlotPlan &sp, const AggParams &P, uint64_t row, uint32_t win,
-                                            uint32_t &present) {
+                                            uint32_t &present, KeyVal &kv) {
     present = 0;
     if (P.packed) {  // exact tag: bit 63 | window/60 | flow type | per key: presence bit + value bits
         uint64_t x = ((uint64_t)(win / 60) << 1) | (sp.proto == 9);
@@ -176,20 +208,49 @@ __device__ __forceinline__ uint64_t key_tag(const AggSlotPlan &sp, const AggPara
         return x | (1ull << 63);
     }
     uint64_t h = mix64(0x4E475A41474731ull, ((uint64_t)win << 8) | sp.proto);
-    for (uint32_t k = 0; k < P.n_keys; ++k) {
-        const uint8_t *c = sp.key_col[k];
-        h = mix64(h, c ? 0x100u : 0u);
-        if (!c) continue;
-        present |= 1u << k;
-        KeyWords kw{c + row * sp.key_w[k], sp.key_w[k], P.key_kind[k]};
-        for (uint32_t j = 0; j < P.key_slot[k] / 4; ++j) h = mix64(h, kw(j));
+    if (P.kw_n) {
+        key_words(sp, P, row, kv);
+#pragma unroll
+        for (uint32_t j = 0; j < 8; ++j) {
+            if (j >= P.kw_n) continue;
+            const uint32_t k = P.kw_key[j];
+            const bool has = sp.key_col[k] != nullptr;
+            if (P.kw_idx[j] == 0) {
+                h = mix64(h, has ? 0x100u : 0u);
+                if (has) present |= 1u << k;
+            }
+            if (has) h = mix64(h, kv.w[j]);
+        }
+    } else {
+        for (uint32_t k = 0; k < P.n_keys; ++k) {
+            const uint8_t *c = sp.key_col[k];
+            h = mix64(h, c ? 0x100u : 0u);
+            if (!c) continue;
+            present |= 1u << k;
+            KeyWords kw{c + row * sp.key_w[k], sp.key_w[k], P.key_kind[k]};
+            for (uint32_t j = 0; j < P.key_slot[k] / 4; ++j) h = mix64(h, kw(j));
+        }
     }
     h &= P.hash_mask;
     return h < 2 ? h + 2 : h;  // 0 / 1 are the empty and tombstone tags
 }
 
 __device__ __forceinline__ bool key_equal(const uint8_t *R, const AggSlotPlan &sp, const AggParams &P, uint64_t row,
-                                          uint32_t win, uint32_t kp) {
+                                          uint32_t win, uint32_t kp, const KeyVal &kv) {
+    if (P.kw_n) {
+        // header and key words with independent wide loads (keys start at KEY0, 16-byte aligned;
+        // an absent key's words are zero in the row and in kv)
+        const uint4 h0 = *(const uint4 *)R;
+        const uint4 k0 = *(const uint4 *)(R + KEY0);
+        uint4 k1 = make_uint4(0, 0, 0, 0);
+        if (P.kw_n > 4) k1 = *(const uint4 *)(R + KEY0 + 16);
+        const uint32_t rw[8] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w};
+        bool same = h0.x == win && h0.y == sp.proto && h0.z == kp;
+#pragma unroll
+        for (uint32_t j = 0; j < 8; ++j)
+            if (j < P.kw_n) same = same && rw[j] == kv.w[j];
+        return same;
+    }
     bool same = *(const uint32_t *)(R + 0) == win && *(const uint32_t *)(R + 4) == sp.proto &&
                 *(const uint32_t *)(R + 8) == kp;
     for (uint32_t k = 0; k < P.n_keys && same; ++k) {
@@ -203,10 +264,16 @@ __device__ __forceinline__ bool key_equal(const uint8_t *R, const AggSlotPlan &s
 }
 
 __device__ __forceinline__ void key_write(uint8_t *R, const AggSlotPlan &sp, const AggParams &P, uint64_t row,
-                                          uint32_t win, uint32_t kp) {
+                                          uint32_t win, uint32_t kp, const KeyVal &kv) {
     *(uint32_t *)(R + 0) = win;
     *(uint32_t *)(R + 4) = sp.proto;
     *(uint32_t *)(R + 8) = kp;
+    if (P.kw_n) {
+#pragma unroll
+        for (uint32_t j = 0; j < 8; ++j)
+            if (j < P.kw_n) ((uint32_t *)(R + KEY0))[j] = kv.w[j];
+        return;
+    }
     for (uint32_t k = 0; k < P.n_keys; ++k) {
         uint32_t *dst = (uint32_t *)(R + P.key_off[k]);
         const uint8_t *c = sp.key_col[k];
@@ -339,51 +406,80 @@ __global__ void k_agg_domfix(const ngz_dgram_hdr *__restrict__ hdr, const unsign
     }
 }
 
-__global__ void k_agg_setidx(const ngz_set_info *__restrict__ sets, const uint32_t *__restrict__ rstart,
-                             uint32_t n_sets, uint32_t *__restrict__ setidx) {
-    // one wave per set writes the set index of each of its records
+// Per-record context, 16 bytes, written once per push so the record kernels reach a record's
+// row, times, plan and datagram info with one coalesced load instead of a chain of lookups
+// (set index -> set -> datagram header / info -> plan):
+//   x: row in the slot's columns   y: export time   z: sys-up time (NetFlow v9, else 0)
+//   w: slot (bits 0-15) | datagram info (bits 16-31, DG_VALID: aggregated)
+constexpr uint16_t DG_VALID = 0x8000;
+__global__ void k_agg_recinfo(const ngz_set_info *__restrict__ sets, const uint32_t *__restrict__ rstart,
+                              uint32_t n_sets, const ngz_dgram_hdr *__restrict__ hdr,
+                              const uint16_t *__restrict__ dginfo, const AggSlotPlan *__restrict__ plans,
+                              uint32_t n_dgrams, uint32_t n_slots, uint4 *__restrict__ rinfo,
+                              unsigned int *__restrict__ err) {
+    // one wave per set writes the context of each of its records
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t n_waves = (gridDim.x * blockDim.x) >> 6;
     for (uint32_t s = wave; s < n_sets; s += n_waves) {
-        const uint32_t n = sets[s].n, r0 = rstart[s];
-        for (uint32_t i = lane; i < n; i += 64) setidx[r0 + i] = s;
+        const ngz_set_info si = sets[s];
+        const uint32_t n = si.n, r0 = rstart[s];
+        if (!n) continue;
+        uint32_t ts = 0, sysup = 0, w = 0;
+        if (si.dgram >= n_dgrams || si.slot >= n_slots) {
+            if (lane == 0) atomicOr(err, 16u);
+        } else {
+            const ngz_dgram_hdr &h = hdr[si.dgram];
+            ts = h.time;
+            sysup = h.version == 9 ? h.sys_up_time : 0u;
+            uint16_t info = dginfo[si.dgram];
+            if ((info & DG_USE) && plans[si.slot].usable) info |= DG_VALID;
+            w = si.slot | ((uint32_t)info << 16);
+        }
+        for (uint32_t i = lane; i < n; i += 64) rinfo[r0 + i] = make_uint4(si.rec0 + i, ts, sysup, w);
     }
 }
 
-// Everything the record kernels share: record t -> its set, datagram, row and plan
+// Everything the record kernels share
 struct RecCtx {
-    const ngz_dgram_hdr *hdr;
-    const ngz_set_info *sets;
-    const uint32_t *rstart;
-    const uint32_t *setidx;
+    const uint4 *rinfo;
     uint64_t n_rec;
-    uint32_t n_dgrams, n_slots;
-    const uint16_t *dginfo;
     const AggSlotPlan *plans;
 };
 
 struct Rec {
     bool valid = false, late = false;
-    ngz_set_info si{};
+    uint32_t slot = 0, ts = 0, sysup = 0;
     uint16_t info = 0;
     uint64_t row = 0;
 };
 
-__device__ __forceinline__ Rec rec_of(const RecCtx &C, uint64_t t, unsigned int *err) {
+__device__ __forceinline__ Rec rec_of(const RecCtx &C, uint64_t t, unsigned int *) {
     Rec r;
     if (t >= C.n_rec) return r;
-    const uint32_t s = C.setidx[t];
-    r.si = C.sets[s];
-    if (r.si.dgram >= C.n_dgrams || r.si.slot >= C.n_slots) {
-        atomicOr(err, 16u);
-        return r;
-    }
-    r.info = C.dginfo[r.si.dgram];
+    const uint4 p = C.rinfo[t];
+    r.row = p.x;
+    r.ts = p.y;
+    r.sysup = p.z;
+    r.slot = p.w & 0xFFFF;
+    r.info = (uint16_t)(p.w >> 16);
     r.late = (r.info & DG_LATE) != 0;
-    r.valid = (r.info & DG_USE) && C.plans[r.si.slot].usable;
-    r.row = r.si.rec0 + (uint32_t)(t - C.rstart[s]);
+    r.valid = (r.info & DG_VALID) != 0;
     return r;
+}
+
+// Appends v to list for every lane that wants to, with one counter atomic per wave (the
+// counters are single words: one atomic per record would serialise on them)
+template <class CT>
+__device__ __forceinline__ void wave_append(uint32_t *__restrict__ list, CT *__restrict__ counter, bool want,
+                                            uint32_t v) {
+    const uint64_t m = __ballot(want);
+    if (!m) return;
+    const int lane = (int)__lane_id(), l0 = __ffsll((unsigned long long)m) - 1;
+    uint32_t base = 0;
+    if (lane == l0) base = (uint32_t)atomicAdd(counter, (CT)__popcll(m));
+    base = (uint32_t)__shfl((int)base, l0);
+    if (want) list[base + __popcll(m & ((1ull << lane) - 1))] = v;
 }
 
 // Open-addressing probe for one record's group.  Claiming a free slot: CAS on the tag, then
@@ -394,27 +490,29 @@ __device__ __forceinline__ Rec rec_of(const RecCtx &C, uint64_t t, unsigned int 
 // tentatively (*tentative): k_agg_check compares the keys once the pass is over.
 template <bool EXACT>
 __device__ __forceinline__ uint32_t probe(const AggSlotPlan &sp, const AggParams &P, uint64_t row, uint32_t win,
-                                          uint32_t kp, uint64_t h, unsigned long long *__restrict__ tags,
-                                          uint8_t *__restrict__ rows, uint32_t *__restrict__ claims,
-                                          unsigned long long *__restrict__ n_claims, unsigned int *__restrict__ err,
-                                          bool *tentative) {
+                                          uint32_t kp, const KeyVal &kv, uint64_t h,
+                                          unsigned long long *__restrict__ tags, uint8_t *__restrict__ rows,
+                                          unsigned int *__restrict__ err, bool *tentative, bool *claimed) {
     uint64_t g = slot_of(h) & P.mask;
-    *tentative = false;
+    *tentative = *claimed = false;
     for (uint64_t probes = 0; probes <= P.mask; ++probes, g = (g + 1) & P.mask) {
         unsigned long long cur = tags[g];
         if (cur == TAG_EMPTY) {
             cur = atomicCAS(&tags[g], TAG_EMPTY, (unsigned long long)h);
             if (cur == TAG_EMPTY) {
-                key_write(rows + g * P.row_bytes, sp, P, row, win, kp);
-                claims[atomicAdd(n_claims, 1ull)] = (uint32_t)g;
+                key_write(rows + g * P.row_bytes, sp, P, row, win, kp, kv);
+                *claimed = true;
                 return (uint32_t)g;
             }
         }
         if (cur != h) continue;
         if (P.packed) return (uint32_t)g;
         const uint8_t *R = rows + g * P.row_bytes;
-        if (EXACT || *(const volatile uint32_t *)(R + 36) != 0) {
-            if (key_equal(R, sp, P, row, win, kp)) return (uint32_t)g;
+        // the marker is written by k_agg_apply* only: stable during this pass (loaded with the key)
+        const uint32_t mark = EXACT ? 1u : *(const uint32_t *)(R + 36);
+        const bool eq = key_equal(R, sp, P, row, win, kp, kv);
+        if (mark != 0) {
+            if (eq) return (uint32_t)g;
             continue;
         }
         *tentative = true;
@@ -439,15 +537,19 @@ __global__ __launch_bounds__(256) void k_agg_claim(const RecCtx C, const AggPara
         if ((threadIdx.x & 63) == 0 && late_mask) atomicAdd(late_count, (unsigned long long)__popcll(late_mask));
         if (t >= C.n_rec) continue;
         uint32_t g = NONE;
+        bool tentative = false, claimed = false;
         if (r.valid) {
-            const AggSlotPlan &sp = C.plans[r.si.slot];
-            const uint32_t ts = C.hdr[r.si.dgram].time, win = ts - ts % 60;  // get_window_start
+            const AggSlotPlan &sp = C.plans[r.slot];
+            const uint32_t ts = r.ts, win = ts - ts % 60;  // get_window_start
             uint32_t kp;
-            const uint64_t h = key_tag(sp, P, r.row, win, kp);
-            bool tentative;
-            g = probe<false>(sp, P, r.row, win, kp, h, tags, rows, claims, n_claims, err, &tentative);
-            if (tentative) tent[atomicAdd(n_tent, 1u)] = (uint32_t)t;
+            KeyVal kv;
+            const uint64_t h = key_tag(sp, P, r.row, win, kp, kv);
+            g = probe<false>(sp, P, r.row, win, kp, kv, h, tags, rows, err, &tentative, &claimed);
+            // every record of the group writes itself as the owner; the last store wins
+            if (P.own && g != NONE) *(uint32_t *)(rows + (uint64_t)g * P.row_bytes + OWN_OFF) = (uint32_t)t;
         }
+        wave_append(tent, n_tent, tentative, (uint32_t)t);
+        wave_append(claims, n_claims, claimed, g);
         rec_g[t] = g;
     }
 }
@@ -467,13 +569,14 @@ __global__ __launch_bounds__(256) void k_agg_check(const RecCtx C, const AggPara
         if (g == NONE) continue;
         const Rec r = rec_of(C, t, err);
         if (!r.valid) continue;
-        const AggSlotPlan &sp = C.plans[r.si.slot];
-        const uint32_t ts = C.hdr[r.si.dgram].time, win = ts - ts % 60;
+        const AggSlotPlan &sp = C.plans[r.slot];
+        const uint32_t ts = r.ts, win = ts - ts % 60;
         uint32_t kp;
-        (void)key_tag(sp, P, r.row, win, kp);
-        if (!key_equal(rows + (uint64_t)g * P.row_bytes, sp, P, r.row, win, kp)) {
+        KeyVal kv;
+        (void)key_tag(sp, P, r.row, win, kp, kv);
+        if (!key_equal(rows + (uint64_t)g * P.row_bytes, sp, P, r.row, win, kp, kv)) {
             rec_g[t] = NONE;
-            collided[atomicAdd(n_collided, 1u)] = (uint32_t)t;
+            collided[atomicAdd(n_collided, 1u)] = (uint32_t)t;  // rare (64-bit tag collisions)
         }
     }
 }
@@ -488,13 +591,18 @@ __global__ __launch_bounds__(256) void k_agg_reprobe(const RecCtx C, const AggPa
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n_list; i += gridDim.x * blockDim.x) {
         const uint64_t t = list[i];
         const Rec r = rec_of(C, t, err);
-        if (!r.valid) continue;
-        const AggSlotPlan &sp = C.plans[r.si.slot];
-        const uint32_t ts = C.hdr[r.si.dgram].time, win = ts - ts % 60;
-        uint32_t kp;
-        const uint64_t h = key_tag(sp, P, r.row, win, kp);
-        bool tentative;
-        rec_g[t] = probe<true>(sp, P, r.row, win, kp, h, tags, rows, claims, n_claims, err, &tentative);
+        bool tentative = false, claimed = false;
+        uint32_t g = NONE;
+        if (r.valid) {
+            const AggSlotPlan &sp = C.plans[r.slot];
+            const uint32_t ts = r.ts, win = ts - ts % 60;
+            uint32_t kp;
+            KeyVal kv;
+            const uint64_t h = key_tag(sp, P, r.row, win, kp, kv);
+            g = probe<true>(sp, P, r.row, win, kp, kv, h, tags, rows, err, &tentative, &claimed);
+            rec_g[t] = g;
+        }
+        wave_append(claims, n_claims, claimed, g);
     }
 }
 
@@ -575,7 +683,7 @@ __device__ __forceinline__ void apply_push_constants(uint8_t *R, const AggParams
 constexpr int CN = 64;
 template <int MAXV>  // aggregated fields held in registers (value loads issued together, before any atomic)
 __global__ __launch_bounds__(256, 4) void k_agg_apply(const RecCtx C, const AggParams P,
-                                                    const uint32_t *__restrict__ rec_g, uint8_t *__restrict__ rows,
+                                                    uint32_t *__restrict__ rec_g, uint8_t *__restrict__ rows,
                                                     unsigned int *__restrict__ err) {
     __shared__ uint32_t c_g[CN];
     __shared__ unsigned long long c_cnt[CN], c_tpl[CN], c_d0[CN], c_d1[CN];
@@ -595,15 +703,21 @@ __global__ __launch_bounds__(256, 4) void k_agg_apply(const RecCtx C, const AggP
         uint32_t g = t < C.n_rec ? rec_g[t] : NONE;
         Rec r;
         if (g != NONE) r = rec_of(C, t, err);
+        if (g != NONE && P.own && r.valid &&
+            *(const uint32_t *)(rows + (uint64_t)g * P.row_bytes + OWN_OFF) == (uint32_t)t) {
+            // the group's owner record is left to k_agg_apply_own, which runs after this kernel
+            rec_g[t] = g | OWN_BIT;
+            g = NONE;
+        }
         const bool valid = g != NONE && r.valid;
         if (!valid) g = NONE;
-        const AggSlotPlan &sp = C.plans[valid ? r.si.slot : 0];
+        const AggSlotPlan &sp = C.plans[valid ? r.slot : 0];
         const uint64_t row = r.row;
         uint32_t ts = 0, sysup = 0;
         uint64_t tpl = 0, dom0 = 0, dom1 = 0;
         if (valid) {
-            ts = C.hdr[r.si.dgram].time;
-            sysup = C.hdr[r.si.dgram].version == 9 ? C.hdr[r.si.dgram].sys_up_time : 0u;
+            ts = r.ts;
+            sysup = r.sysup;
             tpl = sp.tpl_bit;
             const uint32_t db = (r.info >> 2) & 0x7F;
             (db < 64 ? dom0 : dom1) = 1ull << (db & 63);
@@ -776,6 +890,122 @@ __global__ __launch_bounds__(256, 4) void k_agg_apply(const RecCtx C, const AggP
     }
 }
 
+// Owner path ops, one per 8-byte unit of the row (AggParams::unit_op / unit_src)
+enum : uint8_t { U_KEEP = 0, U_ADD = 1, U_MIN = 2, U_MAX = 3, U_OR = 4, U_VP = 5, U_TS = 6, U_SYS = 7 };
+constexpr int OWN_ROUNDS = 2;  // k_agg_apply_own: rounds of eight owners whose rows are in flight together
+enum : uint8_t { U_SRC_ONE = 8, U_SRC_COLL = 9, U_SRC_PORT = 10, U_SRC_TPL = 11, U_SRC_DOM0 = 12, U_SRC_DOM1 = 13 };
+
+// The owner record of each group (listed by k_agg_apply, which has applied every other record
+// of the push with atomics by now): its whole reduction with plain loads and stores, eight
+// lanes per record, each lane one 16-byte piece of the row (two with rows over 128 bytes), so
+// one wave instruction moves eight rows.  A row is touched by no other lane in this kernel.
+__global__ __launch_bounds__(256) void k_agg_apply_own(const RecCtx C, const AggParams P,
+                                                       uint32_t *__restrict__ rec_g, uint8_t *__restrict__ rows,
+                                                       unsigned int *__restrict__ err) {
+    const uint32_t lane = threadIdx.x & 63, piece = lane & 7, np = P.row_bytes / 16;
+    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint64_t n_waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    // 64 records per wave step.  Every lane first loads its own record's operands (coalesced,
+    // all in flight together); the owners among them are then taken eight at a time, one per
+    // lane octet, their operands handed over by lane shuffles, so each round waits on its
+    // rows only.
+    for (uint64_t base = wave * 64; base < C.n_rec; base += n_waves * 64) {
+        const uint32_t mine = base + lane < C.n_rec ? rec_g[base + lane] : NONE;
+        const bool owner = mine != NONE && (mine & OWN_BIT);
+        uint64_t m = __ballot(owner);
+        if (!m) continue;
+        if (owner) rec_g[base + lane] = mine & ~OWN_BIT;  // plain group index again (k_agg_ordered sorts on it)
+        Rec r;
+        if (owner) r = rec_of(C, base + lane, err);
+        const AggSlotPlan &sp = C.plans[r.slot];
+        const uint32_t db = (r.info >> 2) & 0x7F;
+        const uint64_t dom0 = db < 64 ? 1ull << db : 0ull, dom1 = db < 64 ? 0ull : 1ull << (db & 63);
+        const uint64_t tpl = r.valid ? sp.tpl_bit : 0ull;
+        uint64_t xv[8];
+        uint32_t hv = 0;
+#pragma unroll
+        for (int v = 0; v < 8; ++v) {
+            xv[v] = 0;
+            if (r.valid && v < (int)P.n_vals && sp.val_col[v] && !vc_ordered(P.val_vc[v])) {
+                xv[v] = value_operand(sp, P, v, r.row);
+                hv |= 1u << v;
+            }
+        }
+        const uint32_t vmask = r.valid ? 1u : 0u;
+        while (m) {
+            // up to OWN_ROUNDS rounds of eight owners: every round's rows are loaded before any
+            // is reduced, so OWN_ROUNDS x 8 rows per wave are in flight
+            int src[OWN_ROUNDS];
+            bool one[OWN_ROUNDS], two[OWN_ROUNDS];
+            uint4 *q[OWN_ROUNDS];
+            uint4 w0[OWN_ROUNDS], w1[OWN_ROUNDS];
+#pragma unroll
+            for (int k = 0; k < OWN_ROUNDS; ++k) {
+                // octet o takes the o-th lowest owner left in m
+                uint64_t mm = m;
+                for (uint32_t o = lane >> 3; o > 0 && mm; --o) mm &= mm - 1;
+                const bool act = mm != 0;
+                src[k] = act ? __ffsll((unsigned long long)mm) - 1 : 0;
+                for (int j = 0; j < 8 && m; ++j) m &= m - 1;
+                // every lane takes part in the shuffles (a lane left out by a short-circuit
+                // would read 0 from an inactive source lane)
+                const uint32_t g = (uint32_t)__shfl((int)mine, src[k]) & ~OWN_BIT;
+                const uint32_t s_valid = (uint32_t)__shfl((int)vmask, src[k]);
+                const bool ok = act && s_valid != 0;
+                q[k] = (uint4 *)(rows + (uint64_t)g * P.row_bytes);
+                one[k] = ok && piece < np;
+                two[k] = ok && piece + 8 < np;
+                w0[k] = w1[k] = make_uint4(0, 0, 0, 0);
+                if (one[k]) w0[k] = q[k][piece];
+                if (two[k]) w1[k] = q[k][piece + 8];
+            }
+#pragma unroll
+            for (int k = 0; k < OWN_ROUNDS; ++k) {
+                const int sl = src[k];
+                const uint32_t s_ts = (uint32_t)__shfl((int)r.ts, sl), s_sys = (uint32_t)__shfl((int)r.sysup, sl);
+                const uint32_t s_hv = (uint32_t)__shfl((int)hv, sl);
+                const uint64_t s_d0 = readlane64(dom0, sl), s_d1 = readlane64(dom1, sl), s_tpl = readlane64(tpl, sl);
+                uint64_t s_xv[8];
+#pragma unroll
+                for (int v = 0; v < 8; ++v) s_xv[v] = v < (int)P.n_vals ? readlane64(xv[v], sl) : 0ull;
+                auto unit = [&](uint32_t u, uint32_t &lo, uint32_t &hi) {
+                    const uint32_t op = (uint32_t)(P.unit_op[u >> 4] >> (4 * (u & 15))) & 15;
+                    if (op == U_KEEP) return;
+                    if (op == U_VP) { hi |= s_hv; return; }
+                    if (op == U_TS) { lo = min(lo, s_ts); hi = max(hi, s_ts); return; }
+                    if (op == U_SYS) { lo = max(lo, s_sys); hi = P.push_id; return; }
+                    const uint32_t sv = (uint32_t)(P.unit_src[u >> 4] >> (4 * (u & 15))) & 15;
+                    uint64_t x = 0;
+                    if (sv < 8) {
+                        if (!((s_hv >> sv) & 1)) return;
+#pragma unroll
+                        for (int v = 0; v < 8; ++v)
+                            if (sv == (uint32_t)v) x = s_xv[v];
+                    } else {
+                        x = sv == U_SRC_ONE ? 1ull : sv == U_SRC_COLL ? P.coll_flip
+                          : sv == U_SRC_PORT ? 1ull << P.port_bit : sv == U_SRC_TPL ? s_tpl
+                          : sv == U_SRC_DOM0 ? s_d0 : s_d1;
+                    }
+                    uint64_t c = ((uint64_t)hi << 32) | lo;
+                    c = op == U_ADD ? c + x : op == U_MIN ? (x < c ? x : c) : op == U_MAX ? (x > c ? x : c) : (c | x);
+                    lo = (uint32_t)c;
+                    hi = (uint32_t)(c >> 32);
+                };
+                if (one[k]) {
+                    unit(2 * piece, w0[k].x, w0[k].y);
+                    unit(2 * piece + 1, w0[k].z, w0[k].w);
+                    q[k][piece] = w0[k];
+                }
+                if (two[k]) {
+                    unit(2 * piece + 16, w1[k].x, w1[k].y);
+                    unit(2 * piece + 17, w1[k].z, w1[k].w);
+                    q[k][piece + 8] = w1[k];
+                }
+            }
+        }
+    }
+}
+
 __global__ void k_agg_iota(uint32_t *__restrict__ x, uint64_t n) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
         x[i] = (uint32_t)i;
@@ -823,7 +1053,7 @@ __global__ __launch_bounds__(256) void k_agg_ordered(const RecCtx C, const AggPa
             for (uint64_t j = i; j < n && sg[j] == g; ++j) {
                 const Rec r = rec_of(C, sr[j], err);
                 if (!r.valid) continue;
-                const AggSlotPlan &sp = C.plans[r.si.slot];
+                const AggSlotPlan &sp = C.plans[r.slot];
                 if (!sp.val_col[v]) continue;
                 const uint8_t *cell = sp.val_col[v] + r.row * sp.val_w[v];
                 if (vc == VC_F64) {
@@ -980,7 +1210,7 @@ struct ngz_agg {
     // scratch, grown on demand
     void *scratch = nullptr;
     size_t scratch_cap = 0;
-    uint8_t *rec_buf = nullptr;  // setidx, rec_g, claims, collided lists, sort buffers
+    uint8_t *rec_buf = nullptr;  // record contexts, rec_g, claims, collided lists, sort buffers
     size_t rec_cap = 0;
 };
 
@@ -1246,7 +1476,7 @@ int ngz_agg_create(int device, const ngz_agg_field *fields, uint32_t n_fields, u
     a->val_kind_seen.assign(a->vals.size(), -1);
     // row layout: header, keys (canonical bytes, slot a multiple of 4), values (8 B; IPv6 16 B;
     // byte ORs up to 32 B)
-    uint32_t off = ROW_HDR;
+    uint32_t off = KEY0;
     AggParams &P = a->P;
     P.n_keys = (uint32_t)a->keys.size();
     P.n_vals = (uint32_t)a->vals.size();
@@ -1282,7 +1512,7 @@ int ngz_agg_create(int device, const ngz_agg_field *fields, uint32_t n_fields, u
         P.key_pw[k] = (uint32_t)fw;
         off += slot;
     }
-    if (off - ROW_HDR > NGZ_AGG_MAX_KEY_BYTES + 64) { delete a; return NGZ_E_LIMIT; }
+    if (off - KEY0 > NGZ_AGG_MAX_KEY_BYTES + 64) { delete a; return NGZ_E_LIMIT; }
     off = (off + 7) & ~7u;
     bool ranks = false;
     for (uint32_t v = 0; v < P.n_vals; ++v) {
@@ -1294,7 +1524,7 @@ int ngz_agg_create(int device, const ngz_agg_field *fields, uint32_t n_fields, u
         ranks = ranks || (vcs[v] == VC_RANK && !P.val_tcp[v]);
         off += value_slot_bytes(vcs[v]);
     }
-    P.row_bytes = (off + 7) & ~7u;
+    P.row_bytes = (off + 15) & ~15u;  // whole 16-byte pieces (k_agg_apply_own)
     {
         uint32_t bits = 28;  // window/60 + flow type
         bool ok = true;
@@ -1307,11 +1537,54 @@ int ngz_agg_create(int device, const ngz_agg_field *fields, uint32_t n_fields, u
     P.lds_ok = 1;
     for (uint32_t v = 0; v < P.n_vals; ++v)
         if (P.val_vc[v] == VC_BYTES) P.lds_ok = 0;
+    // hashed keys of at most 8 words: key words in registers (KeyVal)
+    {
+        uint32_t nw = 0;
+        for (uint32_t k = 0; k < P.n_keys; ++k) nw += P.key_slot[k] / 4;
+        P.kw_n = 0;
+        if (!P.packed && nw <= 8 && getenv("NGZ_AGG_NO_KW") == nullptr) {
+            uint32_t j = 0;
+            for (uint32_t k = 0; k < P.n_keys; ++k)
+                for (uint32_t i = 0; i < P.key_slot[k] / 4; ++i, ++j) {
+                    P.kw_key[j] = (uint8_t)k;
+                    P.kw_idx[j] = (uint8_t)i;
+                }
+            P.kw_n = nw;
+        }
+    }
+    // owner path: rows of up to 256 bytes, no byte-wise ORs, aggregated fields 0-7
+    P.own = P.lds_ok && P.row_bytes <= 256 && P.n_vals <= 8 && getenv("NGZ_AGG_NO_OWN") == nullptr;
+    {
+        uint8_t op[32] = {}, src[32] = {};
+        op[1] = U_VP;                                   // val_present (high word of key_present's unit)
+        op[2] = U_ADD, src[2] = U_SRC_ONE;              // record_count
+        op[3] = U_TS;                                   // min / max export time
+        op[4] = U_SYS;                                  // max sys-up time, push marker
+        op[5] = U_MIN, src[5] = U_SRC_COLL;             // min / max collection time (flipped)
+        op[6] = U_MAX, src[6] = U_SRC_COLL;
+        op[7] = U_OR, src[7] = U_SRC_TPL;               // template, peer port, domain sets
+        op[8] = U_OR, src[8] = U_SRC_PORT;
+        op[9] = U_OR, src[9] = U_SRC_DOM0;
+        op[10] = U_OR, src[10] = U_SRC_DOM1;
+        for (uint32_t v = 0; v < P.n_vals && v < 8; ++v) {
+            if (vc_ordered(P.val_vc[v])) continue;      // k_agg_ordered
+            const uint32_t u = P.val_off[v] / 8;
+            op[u] = P.val_op[v] == NGZ_AGG_ADD ? U_ADD : P.val_op[v] == NGZ_AGG_MIN ? U_MIN
+                  : P.val_op[v] == NGZ_AGG_MAX ? U_MAX : U_OR;
+            src[u] = (uint8_t)v;
+        }
+        P.unit_op[0] = P.unit_op[1] = P.unit_src[0] = P.unit_src[1] = 0;
+        for (uint32_t u = 0; u < 32; ++u) {
+            P.unit_op[u >> 4] |= (uint64_t)op[u] << (4 * (u & 15));
+            P.unit_src[u >> 4] |= (uint64_t)src[u] << (4 * (u & 15));
+        }
+    }
     P.hash_mask = ~0ull;
     if (const char *hb = getenv("NGZ_AGG_HASH_BITS")) {  // test knob: a narrow hash makes distinct keys collide
         const int b = atoi(hb);
         if (b > 0 && b < 64) P.hash_mask = (1ull << b) - 1;
     }
+    if (capacity > (1ull << 30)) { delete a; return NGZ_E_LIMIT; }  // slot indexes stay below OWN_BIT
     uint64_t slots = 1024;
     while (slots < 2 * std::max<uint64_t>(capacity, 1)) slots <<= 1;
     a->slots = slots;
@@ -1554,6 +1827,11 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, uint16_t pe
     P.push_id = ++a->push_id;
     P.port_bit = (uint32_t)port_bit;
     P.coll_flip = (uint64_t)collection_time_ms ^ (1ull << 63);
+    // owner path only where groups get few records per push (many groups per record): with
+    // few, hot groups the wave / workgroup pre-aggregation of k_agg_apply serves them better
+    // and the owner stores and checks would only add traffic.  Decided from the groups held
+    // before the push (an empty table: the first push of any key).
+    P.own = P.own && (a->live == 0 || a->live * 8 > (uint64_t)out->n_records);
     AGG_HIP(a, hipEventRecord(a->ev0, st));
     AGG_HIP(a, hipMemsetAsync(has_rec, 0, 4ull * D, st));
     AGG_HIP(a, hipMemsetAsync(a->late, 0, 8, st));
@@ -1599,7 +1877,7 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, uint16_t pe
         if (int r = upload_domains(a)) { restore(); return r; }
         hipLaunchKernelGGL(k_agg_domfix, dim3(grid_for(D)), dim3(256), 0, st, hdr, a->dom_dict, dginfo, D, a->err);
     }
-    // per-record buffers: setidx, rec_g, claims, two record lists, sort keys / values (x2)
+    // per-record buffers: contexts (16 B), rec_g, claims, two record lists, sort keys / values (x2)
     const uint64_t R4 = al(4ull * std::max<uint32_t>(n_rec, 1));
     const bool ordered = [&] {
         for (uint32_t v = 0; v < P.n_vals; ++v)
@@ -1611,7 +1889,7 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, uint16_t pe
         hipcub::DeviceRadixSort::SortPairs(nullptr, sort_tmp, (uint32_t *)nullptr, (uint32_t *)nullptr,
                                            (uint32_t *)nullptr, (uint32_t *)nullptr, (int)std::max<uint32_t>(n_rec, 1),
                                            0, 32, st);
-    const size_t rec_need = 5 * R4 + (ordered ? 4 * R4 + al(sort_tmp) : 0);
+    const size_t rec_need = 8 * R4 + (ordered ? 4 * R4 + al(sort_tmp) : 0);
     if (rec_need > a->rec_cap) {
         hipFree(a->rec_buf);
         a->rec_buf = nullptr;
@@ -1619,12 +1897,13 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, uint16_t pe
         if (hipMalloc(&a->rec_buf, rec_need) != hipSuccess) { restore(); upload_domains(a); return fail(a, NGZ_E_NOMEM, "record buffers"); }
         a->rec_cap = rec_need;
     }
-    uint32_t *setidx = (uint32_t *)a->rec_buf, *rec_g = (uint32_t *)(a->rec_buf + R4),
-             *claims = (uint32_t *)(a->rec_buf + 2 * R4), *list_a = (uint32_t *)(a->rec_buf + 3 * R4),
-             *list_b = (uint32_t *)(a->rec_buf + 4 * R4);
-    hipLaunchKernelGGL(k_agg_setidx, dim3(grid_for(64ull * NS, 256, 4096)), dim3(256), 0, st, sets, rstart, NS, setidx);
+    uint4 *rinfo = (uint4 *)a->rec_buf;
+    uint32_t *rec_g = (uint32_t *)(a->rec_buf + 4 * R4), *claims = (uint32_t *)(a->rec_buf + 5 * R4),
+             *list_a = (uint32_t *)(a->rec_buf + 6 * R4), *list_b = (uint32_t *)(a->rec_buf + 7 * R4);
+    hipLaunchKernelGGL(k_agg_recinfo, dim3(grid_for(64ull * NS, 256, 4096)), dim3(256), 0, st, sets, rstart, NS, hdr,
+                       dginfo, a->plans, D, S, rinfo, a->err);
     AGG_HIP(a, hipGetLastError());
-    const RecCtx C{hdr, sets, rstart, setidx, (uint64_t)n_rec, D, S, dginfo, a->plans};
+    const RecCtx C{rinfo, (uint64_t)n_rec, a->plans};
     const uint32_t blocks = (uint32_t)((n_rec + 255) / 256);
     static const uint32_t grid_cap = getenv("NGZ_AGG_GRID") ? (uint32_t)std::max(1, atoi(getenv("NGZ_AGG_GRID"))) : 4096u;
     const uint32_t ig = std::max<uint32_t>(1, std::min<uint32_t>(blocks, grid_cap));
@@ -1685,14 +1964,16 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, uint16_t pe
     // groups (about one record per group and push): one tile per workgroup, all records in flight
     if (n_rec) {
         const uint32_t ag = (a->live + n_claims) * 8 > n_rec ? fg : ig;
+        // owner records (marked in rec_g) reduced after every other record
         if (P.n_vals <= 8)
             hipLaunchKernelGGL(k_agg_apply<8>, dim3(ag), dim3(256), 0, st, C, P, rec_g, a->rows, a->err);
         else
             hipLaunchKernelGGL(k_agg_apply<NGZ_AGG_MAX_VALUES>, dim3(ag), dim3(256), 0, st, C, P, rec_g, a->rows, a->err);
+        if (P.own) hipLaunchKernelGGL(k_agg_apply_own, dim3(fg), dim3(256), 0, st, C, P, rec_g, a->rows, a->err);
         if (ordered) {
-            uint32_t *sk = (uint32_t *)(a->rec_buf + 5 * R4), *sv = (uint32_t *)(a->rec_buf + 6 * R4),
-                     *sk2 = (uint32_t *)(a->rec_buf + 7 * R4), *sv2 = (uint32_t *)(a->rec_buf + 8 * R4);
-            void *stmp = a->rec_buf + 9 * R4;
+            uint32_t *sk = (uint32_t *)(a->rec_buf + 8 * R4), *sv = (uint32_t *)(a->rec_buf + 9 * R4),
+                     *sk2 = (uint32_t *)(a->rec_buf + 10 * R4), *sv2 = (uint32_t *)(a->rec_buf + 11 * R4);
+            void *stmp = a->rec_buf + 12 * R4;
             AGG_HIP(a, hipMemcpyAsync(sk, rec_g, 4ull * n_rec, hipMemcpyDeviceToDevice, st));
             hipLaunchKernelGGL(k_agg_iota, dim3(grid_for(n_rec)), dim3(256), 0, st, sv, (uint64_t)n_rec);
             int end_bit = 1;
