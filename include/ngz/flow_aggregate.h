@@ -112,7 +112,8 @@ typedef struct {
 } ngz_agg_row;
 
 /* Row layout of ngz_agg_flush output: row_bytes per group (a multiple of 16); the
- * ngz_agg_row header, 8 bytes of device bookkeeping, then key field k at key_off[k] (column width of the IE, rounded to 4; width in key_width[k]: 0 if the
+ * ngz_agg_row header, 8 bytes of device bookkeeping, then key field k at key_off[k]
+ * (column width of the IE, rounded to 4; width in key_width[k]: 0 if the
  * field never appeared), value v at val_off[v] (8 bytes; OR of byte fields: width
  * rounded to 4, in val_width[v]).  Integer values are little-endian at the IE's
  * Rust width (adds wrap at that width, as release-mode `+=`). */
