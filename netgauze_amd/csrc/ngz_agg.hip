@@ -235,22 +235,34 @@ __device__ __forceinline__ uint64_t key_tag(const AggSlotPlan &sp, const AggPara
     return h < 2 ? h + 2 : h;  // 0 / 1 are the empty and tombstone tags
 }
 
+// A slot's header and first 8 key words (KeyVal keys), loaded with three 16-byte loads
+struct KeyRow {
+    uint4 h0, k0, k1;
+};
+
+__device__ __forceinline__ KeyRow key_row_load(const uint8_t *R, const AggParams &P) {
+    KeyRow kr;
+    kr.h0 = *(const uint4 *)R;
+    kr.k0 = *(const uint4 *)(R + KEY0);
+    kr.k1 = make_uint4(0, 0, 0, 0);
+    if (P.kw_n > 4) kr.k1 = *(const uint4 *)(R + KEY0 + 16);
+    return kr;
+}
+
+__device__ __forceinline__ bool key_row_equal(const KeyRow &kr, const AggSlotPlan &sp, const AggParams &P,
+                                              uint32_t win, uint32_t kp, const KeyVal &kv) {
+    // an absent key's words are zero in the row and in kv
+    const uint32_t rw[8] = {kr.k0.x, kr.k0.y, kr.k0.z, kr.k0.w, kr.k1.x, kr.k1.y, kr.k1.z, kr.k1.w};
+    bool same = kr.h0.x == win && kr.h0.y == sp.proto && kr.h0.z == kp;
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j)
+        if (j < P.kw_n) same = same && rw[j] == kv.w[j];
+    return same;
+}
+
 __device__ __forceinline__ bool key_equal(const uint8_t *R, const AggSlotPlan &sp, const AggParams &P, uint64_t row,
                                           uint32_t win, uint32_t kp, const KeyVal &kv) {
-    if (P.kw_n) {
-        // header and key words with independent wide loads (keys start at KEY0, 16-byte aligned;
-        // an absent key's words are zero in the row and in kv)
-        const uint4 h0 = *(const uint4 *)R;
-        const uint4 k0 = *(const uint4 *)(R + KEY0);
-        uint4 k1 = make_uint4(0, 0, 0, 0);
-        if (P.kw_n > 4) k1 = *(const uint4 *)(R + KEY0 + 16);
-        const uint32_t rw[8] = {k0.x, k0.y, k0.z, k0.w, k1.x, k1.y, k1.z, k1.w};
-        bool same = h0.x == win && h0.y == sp.proto && h0.z == kp;
-#pragma unroll
-        for (uint32_t j = 0; j < 8; ++j)
-            if (j < P.kw_n) same = same && rw[j] == kv.w[j];
-        return same;
-    }
+    if (P.kw_n) return key_row_equal(key_row_load(R, P), sp, P, win, kp, kv);
     bool same = *(const uint32_t *)(R + 0) == win && *(const uint32_t *)(R + 4) == sp.proto &&
                 *(const uint32_t *)(R + 8) == kp;
     for (uint32_t k = 0; k < P.n_keys && same; ++k) {
