@@ -910,6 +910,12 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
     B.proc_counts = d_proc;
     B.cap_pad_windows = ctx->cap_pad_windows;
     B.recmap = nullptr;
+    B.dsum = nullptr;
+    static const bool dsum_on = !getenv("NGZ_DSUM") || atoi(getenv("NGZ_DSUM")) != 0;
+    if (dsum_on && N) {
+        if (ctx->d_dsum.ensure(N)) return fail(ctx, NGZ_E_NOMEM, "device alloc (datagram summaries)");
+        B.dsum = ctx->d_dsum.p;
+    }
     bool any_vlen = false;
     for (uint32_t s = 0; s < S; ++s) {
         const DevPlan &P = ctx->versions[ctx->slot_version[s]].plan;
@@ -1237,7 +1243,7 @@ void ngz_ctx_destroy(ngz_ctx *ctx) {
     ctx->d_tl_slot.release(); ctx->d_hf_flag.release(); ctx->d_hf_hdr.release(); ctx->d_hf_first.release(); ctx->d_hf_sets.release();
     ctx->d_hdr.release(); ctx->d_counts.release(); ctx->d_scan.release(); ctx->d_scan_tmp.release();
     ctx->d_slots.release(); ctx->d_chunks.release(); ctx->d_sets.release(); ctx->d_arena.release();
-    ctx->d_proc.release(); ctx->d_summary.release(); ctx->d_recmap.release(); ctx->d_in_bytes.release(); ctx->d_in_off.release();
+    ctx->d_proc.release(); ctx->d_summary.release(); ctx->d_recmap.release(); ctx->d_dsum.release(); ctx->d_in_bytes.release(); ctx->d_in_off.release();
     ctx->d_in_len.release();
     for (auto &e : ctx->ev) hipEventDestroy(e);
     for (uint32_t i = 0; i < ctx->n_aux; ++i) {

@@ -294,5 +294,6 @@ struct BatchDev {        // device pointers of one batch
     uint32_t cap_pad_windows;  // extra workgroup windows of capacity per slot (column placement tuning)
     uint32_t reserved_b;
     uint32_t *recmap;          // variable-length slots: 1 bit per batch byte, set at every complete record
+    unsigned long long *dsum;  // per datagram: its one data set (k_frame -> k_emit), 0 = walk it again
                                // start by k_frame's walk, read by k_emit instead of walking again (or null)
 };

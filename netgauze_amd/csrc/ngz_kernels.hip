@@ -213,7 +213,9 @@ struct CountVis {
     const DevPlan *plans;
     uint32_t *recmap;
     uint64_t dg_off;
+    uint64_t sum = 0;  // the first data set: set_pos | slot << 16 | n << 32 | (end - set_pos, or 1) << 48
     __device__ uint32_t vlen(const uint8_t *p, uint32_t pos, uint32_t end, uint32_t, const DevPlan &pl, uint64_t *err) {
+        if (!sets) sum = (uint64_t)(end - (pos - 4)) << 48;
         uint32_t *rm = recmap;
         const uint64_t g = dg_off;
         return ngz_vlen_walk(p, pos, end, pl, err, [rm, g](uint32_t, uint32_t at) {
@@ -223,7 +225,8 @@ struct CountVis {
             }
         });
     }
-    __device__ void on_set(uint32_t, uint32_t slot, uint32_t n, uint32_t, uint32_t) {
+    __device__ void on_set(uint32_t set_pos, uint32_t slot, uint32_t n, uint32_t, uint32_t) {
+        if (!sets) sum = (sum ? sum : 1ull << 48) | set_pos | ((uint64_t)slot << 16) | ((uint64_t)(n & 0xFFFF) << 32);
         counts[(uint64_t)slot * N + d] += n;
         if (n) counts[(uint64_t)(S + slot) * N + d] += (n + plans[slot].window - 1) / plans[slot].window + 1;
         sets += 1;
@@ -244,6 +247,12 @@ __global__ void __launch_bounds__(kFrameBlock) k_frame(BatchDev B, const uint32_
         o.status = NGZ_FR_HOST;
     const uint64_t N = B.n;
     B.counts[(uint64_t)(2 * B.n_slots) * N + d] = vis.sets;
+    // one data set, parsed cleanly: k_emit takes it from here instead of walking the datagram again
+    if (B.dsum)
+        B.dsum[d] = (o.status == NGZ_FR_OK && o.err == NGZ_NO_ERR && vis.sets == 1 && !(hf_flag && hf_flag[d]) &&
+                     ((vis.sum >> 32) & 0xFFFF) < 0xFFFF)
+                        ? vis.sum
+                        : 0ull;
     ngz_dgram_hdr h;
     h.status = (uint8_t)o.status;
     h.version = (uint8_t)o.version;
@@ -506,8 +515,21 @@ __global__ void __launch_bounds__(256) k_emit(BatchDev B, const uint32_t *hf_fla
         vis.ntab = ntab;
         vis.lrs = st_rs;
         vis.lrd = st_rd;
-        WalkOut o;
-        walk_datagram(B, hf_flag, hf_first, d, o, vis);
+        const unsigned long long sm = B.dsum ? B.dsum[d] : 0ull;
+        if (sm) {
+            // k_frame's summary of the datagram's one data set (same calls as walk_datagram)
+            const uint32_t set_pos = (uint32_t)(sm & 0xFFFF), slot = (uint32_t)(sm >> 16) & 0xFFFF;
+            const uint32_t n = (uint32_t)(sm >> 32) & 0xFFFF, sl = (uint32_t)(sm >> 48);
+            const DevPlan &pl = B.plans[slot];
+            if (pl.has_vlen && pl.rpl) {
+                uint64_t e = NGZ_NO_ERR;
+                vis.vlen(B.bytes + vis.dg_off, set_pos + 4, set_pos + sl, slot, pl, &e);
+            }
+            vis.on_set(set_pos, slot, n, set_pos + 4, pl.rec_len);
+        } else {
+            WalkOut o;
+            walk_datagram(B, hf_flag, hf_first, d, o, vis);
+        }
     }
     if (!ntab) return;
     __syncthreads();
