@@ -111,7 +111,8 @@ typedef struct {
     uint64_t domain_bits[2];    /* observation_domain_ids set */
 } ngz_agg_row;
 
-/* Row layout of ngz_agg_flush output: row_bytes per group (a multiple of 16); the
+/* Row layout of ngz_agg_flush output: row_bytes per group (a multiple of 128: whole
+ * cache lines in the device table; 16 with NGZ_AGG_ROW_PACK set); the
  * ngz_agg_row header, 8 bytes of device bookkeeping, then key field k at key_off[k]
  * (column width of the IE, rounded to 4; width in key_width[k]: 0 if the
  * field never appeared), value v at val_off[v] (8 bytes; OR of byte fields: width

@@ -1536,7 +1536,10 @@ int ngz_agg_create(int device, const ngz_agg_field *fields, uint32_t n_fields, u
         ranks = ranks || (vcs[v] == VC_RANK && !P.val_tcp[v]);
         off += value_slot_bytes(vcs[v]);
     }
-    P.row_bytes = (off + 15) & ~15u;  // whole 16-byte pieces (k_agg_apply_own)
+    // whole 128-byte lines: a row at a random slot then touches ceil(row/128) lines, not one
+    // more when it straddles (176-byte rows at a 176-byte stride cover 2.4 lines on average);
+    // NGZ_AGG_ROW_PACK keeps whole 16-byte pieces only (k_agg_apply_own's unit)
+    P.row_bytes = getenv("NGZ_AGG_ROW_PACK") ? (off + 15) & ~15u : (off + 127) & ~127u;
     {
         uint32_t bits = 28;  // window/60 + flow type
         bool ok = true;
