@@ -693,6 +693,7 @@ __device__ __forceinline__ void apply_push_constants(uint8_t *R, const AggParams
 // all the tiles the workgroup walks, and applied to HBM once per workgroup.  Values of the
 // ordered classes are left to k_agg_ordered.
 constexpr int CN = 64;
+constexpr int CN_PROBES = 8;  // a group's entry sits within this many slots of its home slot
 template <int MAXV>  // aggregated fields held in registers (value loads issued together, before any atomic)
 __global__ __launch_bounds__(256, 4) void k_agg_apply(const RecCtx C, const AggParams P,
                                                     uint32_t *__restrict__ rec_g, uint8_t *__restrict__ rows,
@@ -702,9 +703,10 @@ __global__ __launch_bounds__(256, 4) void k_agg_apply(const RecCtx C, const AggP
     __shared__ uint32_t c_g[CN];
     __shared__ unsigned long long c_cnt[CN], c_tpl[CN], c_d0[CN], c_d1[CN];
     __shared__ unsigned long long c_val[CN][NGZ_AGG_MAX_VALUES];
-    __shared__ uint32_t c_tmin[CN], c_tmax[CN], c_smax[CN], c_vp[CN];
+    __shared__ uint32_t c_tmin[CN], c_tmax[CN], c_smax[CN], c_vp[CN], c_wt[CN];
     for (int e = threadIdx.x; e < CN; e += blockDim.x) {
         c_g[e] = NONE;
+        c_wt[e] = NONE;
         c_cnt[e] = c_tpl[e] = c_d0[e] = c_d1[e] = 0;
         c_tmin[e] = 0xFFFFFFFFu;
         c_tmax[e] = c_smax[e] = c_vp[e] = 0;
@@ -717,6 +719,7 @@ __global__ __launch_bounds__(256, 4) void k_agg_apply(const RecCtx C, const AggP
     for (uint64_t tile = blockIdx.x; tile * blockDim.x < n; tile += gridDim.x) {
         const uint64_t i = tile * blockDim.x + threadIdx.x;
         const uint64_t t = i < n ? (list ? list[i] : i) : C.n_rec;
+        const uint32_t wave_tile = (uint32_t)(tile * (blockDim.x / 64) + threadIdx.x / 64);  // unique per block
         uint32_t g = t < C.n_rec ? rec_g[t] : NONE;
         Rec r;
         if (g != NONE) r = rec_of(C, t, err);
@@ -761,6 +764,51 @@ __global__ __launch_bounds__(256, 4) void k_agg_apply(const RecCtx C, const AggP
                                          (dom0 | (dom1 ? (1ull << 63) | dom1 : 0ull)) == u2);
             hdr_uniform = __ballot(!same) == 0;
         }
+        if (P.lds_ok && todo) {
+            // lanes whose group already has an entry in the workgroup's table apply their own
+            // record there, all lanes at once (one LDS atomic per field and lane; lanes of one
+            // group collide on its entry, which the LDS serialises far faster than the leader
+            // loop below walks the groups one by one); the loop is left with the other lanes
+            int e = -1;
+            if (valid) {
+                int i = (int)(slot_of(g) & (CN - 1));
+                for (int probes = 0; probes < CN_PROBES; ++probes, i = (i + 1) & (CN - 1)) {
+                    const uint32_t cur = c_g[i];
+                    if (cur == g) { e = i; break; }
+                    if (cur == NONE) break;
+                }
+            }
+            const uint64_t hits = __ballot(e >= 0);
+            if (hits) {
+                todo &= ~hits;
+                if (e >= 0) {
+                    atomicAdd(&c_cnt[e], 1ull);
+                    // the header fields once per (entry, wave tile) when the wave shares them
+                    const bool hdr = !hdr_uniform || atomicExch(&c_wt[e], wave_tile) != wave_tile;
+                    if (hdr) {
+                        atomicMin(&c_tmin[e], ts);
+                        atomicMax(&c_tmax[e], ts);
+                        if (sysup) atomicMax(&c_smax[e], sysup);
+                        atomicOr(&c_tpl[e], (unsigned long long)tpl);
+                        if (dom0) atomicOr(&c_d0[e], (unsigned long long)dom0);
+                        if (dom1) atomicOr(&c_d1[e], (unsigned long long)dom1);
+                    }
+#pragma unroll
+                    for (int v = 0; v < MAXV; ++v) {
+                        if (v >= (int)P.n_vals) break;
+                        if (!((hv >> v) & 1)) continue;
+                        unsigned long long *c = &c_val[e][v];
+                        switch (P.val_op[v]) {
+                        case NGZ_AGG_ADD: if (xv[v]) atomicAdd(c, (unsigned long long)xv[v]); break;
+                        case NGZ_AGG_MIN: atomicMin(c, (unsigned long long)xv[v]); break;
+                        case NGZ_AGG_MAX: atomicMax(c, (unsigned long long)xv[v]); break;
+                        default: atomicOr(c, (unsigned long long)xv[v]); break;
+                        }
+                    }
+                    if (hv) atomicOr(&c_vp[e], hv);
+                }
+            }
+        }
         while (todo) {
             const int leader = __ffsll((unsigned long long)todo) - 1;
             const uint32_t lg = (uint32_t)__shfl((int)g, leader);
@@ -776,7 +824,7 @@ __global__ __launch_bounds__(256, 4) void k_agg_apply(const RecCtx C, const AggP
                 int e0 = -1;
                 if (lane == leader) {
                     int i = (int)(slot_of(lg) & (CN - 1));
-                    for (int probes = 0; probes < CN; ++probes, i = (i + 1) & (CN - 1)) {
+                    for (int probes = 0; probes < CN_PROBES; ++probes, i = (i + 1) & (CN - 1)) {
                         uint32_t cur = c_g[i];
                         if (cur == NONE) {
                             cur = atomicCAS(&c_g[i], NONE, lg);
@@ -2006,8 +2054,13 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, uint16_t pe
     // groups (about one record per group and push): one tile per workgroup, all records in flight
     if (n_rec) {
         const uint32_t ag = (a->live + n_claims) * 8 > n_rec ? fg : ig;
+        // fused owner test (k_agg_apply_own first) only when the table already holds many groups
+        // per record: then nearly every record is its group's owner.  An empty table (the first
+        // push of any key) may hold few, hot groups: almost every record would then be listed
+        // for k_agg_apply, one counter atomic per wave on a single word (142 ms for 12 groups
+        // and 10^8 records), so the owner test stays in k_agg_apply there.
         static const bool split = getenv("NGZ_AGG_OWN_SPLIT") != nullptr;  // A/B: the owner test in k_agg_apply
-        if (P.own && !split) {
+        if (P.own && !split && a->live * 8 > (uint64_t)n_rec) {
             // owners reduce their rows first, the records k_agg_apply_own lists apply atomics after
             AGG_HIP(a, hipMemsetAsync(a->n_coll, 0, 4, st));
             hipLaunchKernelGGL(k_agg_apply_own<true>, dim3(fg), dim3(256), 0, st, C, P, rec_g, a->rows, list_a, a->n_coll,

@@ -1,24 +1,35 @@
 #!/bin/bash
-# PMC passes (one per run) over the aggregation bench: wave-cycle breakdown and atomic traffic.
+# PMC passes (one per run) over the aggregation bench: wave-cycle breakdown, HBM bytes,
+# per record kernel (averaged over its dispatches).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-aggpmc}
 mkdir -p $OUT
-K=${AGG_KEY:-proto_dir}
-timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAVES --output-format csv -d $OUT/sq -o run -- python3 bench.py --agg $K --steps 2 --warmup 1 --records 20000000 > $OUT/sq.json 2> $OUT/sq.err || { tail -5 $OUT/sq.err; exit 1; }
-timeout -s KILL 120 rocprofv3 --pmc TCC_EA0_ATOMIC_sum TCC_HIT_sum TCC_MISS_sum --output-format csv -d $OUT/tcc -o run -- python3 bench.py --agg $K --steps 2 --warmup 1 --records 20000000 > $OUT/tcc.json 2> $OUT/tcc.err || { tail -5 $OUT/tcc.err; exit 2; }
-python3 - <<'PY'
-import csv, glob, os, collections
-out = os.environ.get("TAG", "aggpmc")
-for sub in ("sq", "tcc"):
-    for f in glob.glob("gpurun_out/%s/%s/*counter_collection.csv" % (out, sub)):
-        agg = collections.defaultdict(float)
-        n = collections.Counter()
+K=${AGG_KEY:-5tuple}
+N=${RECORDS:-20000000}
+run() {  # name counters...
+  local name=$1; shift
+  timeout -s KILL 120 rocprofv3 --pmc "$@" --output-format csv -d $OUT/$name -o run -- python3 bench.py --agg $K --steps 2 --warmup 1 --records $N > $OUT/$name.json 2> $OUT/$name.err || { tail -5 $OUT/$name.err; exit 1; }
+}
+run sq SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVES SQ_BUSY_CYCLES
+run fetch FETCH_SIZE
+run write WRITE_SIZE
+run tcc TCC_HIT_sum TCC_MISS_sum TCC_EA0_ATOMIC_sum
+python3 - $OUT <<'PY'
+import csv, glob, sys, collections
+out = sys.argv[1]
+res = collections.defaultdict(lambda: collections.defaultdict(list))
+for sub in ("sq", "fetch", "write", "tcc"):
+    for f in glob.glob("%s/%s/*counter_collection.csv" % (out, sub)):
+        per = collections.defaultdict(float)
         for r in csv.DictReader(open(f)):
-            if "k_agg_insert" in r["Kernel_Name"]:
-                agg[r["Counter_Name"]] += float(r["Counter_Value"])
-                n[r["Counter_Name"]] += 1
-        for k, v in sorted(agg.items()):
-            print(sub, k, v / max(1, n[k]) * 1.0, "(per dispatch-row avg over %d rows)" % n[k])
+            k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
+            if "k_agg" not in k:
+                continue
+            per[(k, r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
+        for (k, d, c), v in per.items():
+            res[k][c].append(v)
+for k in sorted(res):
+    print(k, " ".join("%s=%.4g" % (c, sum(v) / len(v)) for c, v in sorted(res[k].items())))
 PY
