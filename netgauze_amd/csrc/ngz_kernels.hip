@@ -214,15 +214,28 @@ struct CountVis {
     uint32_t *recmap;
     uint64_t dg_off;
     uint64_t sum = 0;  // the first data set: set_pos | slot << 16 | n << 32 | (end - set_pos, or 1) << 48
+    uint64_t dg_end = 0;  // batch offset past the datagram
+    // record-start marks of the word being filled (record starts only ever move forward)
+    uint64_t mw = ~0ull;
+    uint32_t mbits = 0;
+    __device__ void mark_flush() {
+        if (mw == ~0ull) return;
+        // a word wholly inside this datagram is this thread's alone: a plain store (the map
+        // is zeroed per batch); a word shared with a neighbouring datagram takes an atomicOr
+        if (32 * mw >= dg_off && 32 * mw + 32 <= dg_end) recmap[mw] = mbits;
+        else atomicOr(&recmap[mw], mbits);
+    }
     __device__ uint32_t vlen(const uint8_t *p, uint32_t pos, uint32_t end, uint32_t, const DevPlan &pl, uint64_t *err) {
         if (!sets) sum = (uint64_t)(end - (pos - 4)) << 48;
-        uint32_t *rm = recmap;
-        const uint64_t g = dg_off;
-        return ngz_vlen_walk(p, pos, end, pl, err, [rm, g](uint32_t, uint32_t at) {
-            if (rm) {
-                const uint64_t b = g + at;
-                atomicOr(&rm[b >> 5], 1u << (b & 31));
+        return ngz_vlen_walk(p, pos, end, pl, err, [this](uint32_t, uint32_t at) {
+            if (!recmap) return;
+            const uint64_t b = dg_off + at;
+            if ((b >> 5) != mw) {
+                mark_flush();
+                mw = b >> 5;
+                mbits = 0;
             }
+            mbits |= 1u << (b & 31);
         });
     }
     __device__ void on_set(uint32_t set_pos, uint32_t slot, uint32_t n, uint32_t, uint32_t) {
@@ -240,8 +253,10 @@ __global__ void __launch_bounds__(kFrameBlock) k_frame(BatchDev B, const uint32_
     for (uint32_t r = 0; r < 2 * B.n_slots; ++r) B.counts[(uint64_t)r * B.n + d] = 0;
     if (d == 0) B.counts[(uint64_t)(2 * B.n_slots + 1) * B.n] = 0;  // the scan's trailing element
     CountVis vis{B.counts, B.n, B.n_slots, d, 0, B.plans, B.recmap, B.offsets[d]};
+    vis.dg_end = vis.dg_off + B.lengths[d];
     WalkOut o;
     walk_datagram(B, hf_flag, hf_first, d, o, vis);
+    vis.mark_flush();
     // a walk that ended OK visited every set (template sets end it with HOST)
     if (o.status != NGZ_FR_HOST && o.status != NGZ_FR_OK && !(hf_flag && hf_flag[d]) && has_template_sets(B, d))
         o.status = NGZ_FR_HOST;
