@@ -1174,6 +1174,155 @@ __global__ __launch_bounds__(256) void k_agg_ordered(const RecCtx C, const AggPa
     }
 }
 
+// ---- Partitioned reduction: many groups, several records each per push ----
+// Groups far beyond a workgroup's LDS table (protocol + port: 393 216 groups of ~250 records per
+// push) leave k_agg_apply with ~3 device atomics per record, each a memory round trip.  Instead
+// the records are partitioned by table slot range: partition p is slots [p, p + 1) * PART_SLOTS,
+// so its groups fit one workgroup's LDS table indexed by slot.  A histogram pass (partition-major
+// counts per tile of records), one scan and a scatter pass copy every record's operands into its
+// partition's run; one workgroup per partition then reduces its run in LDS and updates its rows
+// with plain loads and stores (no other workgroup touches them).  Per record: its operands read
+// once, a payload written and read once, instead of ~3 atomics and ~8 row peeks.  The order of
+// records within a run is not kept: only order-free reductions run here (ordered classes are
+// k_agg_ordered's).
+constexpr uint32_t PART_SLOTS = 512, PART_SHIFT = 9;
+constexpr uint32_t PART_TILE = 65536;  // records per histogram / scatter workgroup (4x larger tiles
+                                       // of 1024-thread workgroups: scatter 8.0 -> 10.9 ms)
+
+// counts[p * n_tiles + tile]: the tile's records headed for partition p (a record has a group
+// only if the claim found it valid)
+__global__ __launch_bounds__(256) void k_agg_part_hist(const RecCtx C, const uint32_t *__restrict__ rec_g, uint32_t n_part,
+                                                       uint32_t *__restrict__ counts) {
+    extern __shared__ uint32_t h[];
+    for (uint32_t i = threadIdx.x; i < n_part; i += blockDim.x) h[i] = 0;
+    __syncthreads();
+    const uint64_t t0 = (uint64_t)blockIdx.x * PART_TILE, t1 = min(t0 + PART_TILE, C.n_rec);
+    for (uint64_t t = t0 + threadIdx.x; t < t1; t += blockDim.x) {
+        const uint32_t g = rec_g[t];
+        if (g != NONE) atomicAdd(&h[g >> PART_SHIFT], 1u);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n_part; i += blockDim.x) counts[(uint64_t)i * gridDim.x + blockIdx.x] = h[i];
+}
+
+// Payload of one record (pb bytes): {group, export time, sys-up time, slot | info << 16}, then
+// the operands of aggregated fields 0..n_vals-1 (u64 each; zero when absent or ordered)
+__global__ __launch_bounds__(256) void k_agg_part_scatter(const RecCtx C, const AggParams P, const uint32_t *__restrict__ rec_g,
+                                                          uint32_t n_part, const uint32_t *__restrict__ offs,
+                                                          uint8_t *__restrict__ pay, uint32_t pb) {
+    extern __shared__ uint32_t cur[];
+    for (uint32_t i = threadIdx.x; i < n_part; i += blockDim.x) cur[i] = offs[(uint64_t)i * gridDim.x + blockIdx.x];
+    __syncthreads();
+    const uint64_t t0 = (uint64_t)blockIdx.x * PART_TILE, t1 = min(t0 + PART_TILE, C.n_rec);
+    for (uint64_t t = t0 + threadIdx.x; t < t1; t += blockDim.x) {
+        const uint32_t g = rec_g[t];
+        if (g == NONE) continue;
+        const Rec r = rec_of(C, t, nullptr);
+        const uint32_t pos = atomicAdd(&cur[g >> PART_SHIFT], 1u);
+        uint4 *d = (uint4 *)(pay + (uint64_t)pos * pb);
+        d[0] = make_uint4(g, r.ts, r.sysup, r.slot | ((uint32_t)r.info << 16));
+        const AggSlotPlan &sp = C.plans[r.slot];
+        uint64_t x[8];
+#pragma unroll
+        for (int v = 0; v < 8; ++v)
+            x[v] = v < (int)P.n_vals && sp.val_col[v] && !vc_ordered(P.val_vc[v]) ? value_operand(sp, P, v, r.row) : 0ull;
+#pragma unroll
+        for (int v = 0; v < 8; v += 2)
+            if (v < (int)P.n_vals)
+                d[1 + v / 2] = make_uint4((uint32_t)x[v], (uint32_t)(x[v] >> 32), (uint32_t)x[v + 1], (uint32_t)(x[v + 1] >> 32));
+    }
+}
+
+// One workgroup per partition: its run reduced into an LDS table indexed by slot, then every
+// touched row updated in place (the reductions of FlowCacheRecord::reduce, aggregator.rs:159-198)
+__global__ __launch_bounds__(256) void k_agg_part_reduce(const AggParams P, const AggSlotPlan *__restrict__ plans,
+                                                         const uint32_t *__restrict__ offs, uint32_t n_tiles,
+                                                         const uint8_t *__restrict__ pay, uint32_t pb,
+                                                         uint8_t *__restrict__ rows) {
+    __shared__ uint32_t e_cnt[PART_SLOTS], e_tmin[PART_SLOTS], e_tmax[PART_SLOTS], e_smax[PART_SLOTS], e_vp[PART_SLOTS];
+    __shared__ unsigned long long e_tpl[PART_SLOTS], e_d0[PART_SLOTS], e_d1[PART_SLOTS];
+    __shared__ unsigned long long e_val[8][PART_SLOTS];
+    for (uint32_t e = threadIdx.x; e < PART_SLOTS; e += blockDim.x) {
+        e_cnt[e] = e_smax[e] = e_vp[e] = e_tmax[e] = 0;
+        e_tmin[e] = 0xFFFFFFFFu;
+        e_tpl[e] = e_d0[e] = e_d1[e] = 0;
+#pragma unroll
+        for (int v = 0; v < 8; ++v) e_val[v][e] = v < (int)P.n_vals && P.val_op[v] == NGZ_AGG_MIN ? ~0ull : 0ull;
+    }
+    __syncthreads();
+    const uint32_t p = blockIdx.x;
+    const uint64_t beg = offs[(uint64_t)p * n_tiles], end = offs[(uint64_t)(p + 1) * n_tiles];
+    for (uint64_t i = beg + threadIdx.x; i < end; i += blockDim.x) {
+        const uint4 *q = (const uint4 *)(pay + i * pb);
+        const uint4 h = q[0];
+        uint64_t x[8];
+#pragma unroll
+        for (int v = 0; v < 8; v += 2) {
+            x[v] = x[v + 1] = 0;
+            if (v < (int)P.n_vals) {
+                const uint4 w = q[1 + v / 2];
+                x[v] = ((uint64_t)w.y << 32) | w.x;
+                x[v + 1] = ((uint64_t)w.w << 32) | w.z;
+            }
+        }
+        const uint32_t e = h.x & (PART_SLOTS - 1), ts = h.y, sysup = h.z, slot = h.w & 0xFFFF, info = h.w >> 16;
+        const AggSlotPlan &sp = plans[slot];
+        const uint32_t db = (info >> 2) & 0x7F;
+        atomicAdd(&e_cnt[e], 1u);
+        atomicMin(&e_tmin[e], ts);
+        atomicMax(&e_tmax[e], ts);
+        if (sysup) atomicMax(&e_smax[e], sysup);
+        atomicOr(&e_tpl[e], (unsigned long long)sp.tpl_bit);
+        atomicOr(db < 64 ? &e_d0[e] : &e_d1[e], 1ull << (db & 63));
+        uint32_t hv = 0;
+#pragma unroll
+        for (int v = 0; v < 8; ++v) {
+            if (v >= (int)P.n_vals || !sp.val_col[v] || vc_ordered(P.val_vc[v])) continue;
+            hv |= 1u << v;
+            unsigned long long *c = &e_val[v][e];
+            switch (P.val_op[v]) {
+            case NGZ_AGG_ADD: if (x[v]) atomicAdd(c, (unsigned long long)x[v]); break;
+            case NGZ_AGG_MIN: atomicMin(c, (unsigned long long)x[v]); break;
+            case NGZ_AGG_MAX: atomicMax(c, (unsigned long long)x[v]); break;
+            default: atomicOr(c, (unsigned long long)x[v]); break;
+            }
+        }
+        if (hv) atomicOr(&e_vp[e], hv);
+    }
+    __syncthreads();
+    for (uint32_t e = threadIdx.x; e < PART_SLOTS; e += blockDim.x) {
+        const uint32_t cnt = e_cnt[e];
+        if (!cnt) continue;
+        uint8_t *R = rows + (uint64_t)(p * PART_SLOTS + e) * P.row_bytes;
+        uint32_t *u = (uint32_t *)R;
+        uint64_t *w = (uint64_t *)R;
+        w[2] += cnt;                      // record_count (16)
+        u[6] = min(u[6], e_tmin[e]);      // min / max export time (24, 28)
+        u[7] = max(u[7], e_tmax[e]);
+        u[8] = max(u[8], e_smax[e]);      // max sys-up time (32)
+        u[9] = P.push_id;                 // per-push marker (36): the push constants are applied here
+        w[5] = min(w[5], P.coll_flip);    // min / max collection time, flipped (40, 48)
+        w[6] = max(w[6], P.coll_flip);
+        w[7] |= e_tpl[e];                 // template, peer port, domain sets (56, 64, 72, 80)
+        w[8] |= 1ull << P.port_bit;
+        w[9] |= e_d0[e];
+        w[10] |= e_d1[e];
+        const uint32_t vp = e_vp[e];
+        u[3] |= vp;                       // val_present (12)
+        for (uint32_t v = 0; v < P.n_vals && v < 8; ++v) {
+            if (!((vp >> v) & 1)) continue;
+            uint64_t *dst = (uint64_t *)(R + P.val_off[v]);
+            const uint64_t xv = e_val[v][e], c = *dst;
+            switch (P.val_op[v]) {
+            case NGZ_AGG_ADD: *dst = c + xv; break;
+            case NGZ_AGG_MIN: *dst = xv < c ? xv : c; break;
+            case NGZ_AGG_MAX: *dst = xv > c ? xv : c; break;
+            default: *dst = c | xv; break;
+            }
+        }
+    }
+}
+
 __global__ void k_agg_init(uint8_t *__restrict__ rows, uint64_t n_groups, uint32_t row_bytes,
                            const uint32_t *__restrict__ ident, uint32_t ident_words) {
     // every row <- the identity row (min fields at their maximum)
@@ -1299,6 +1448,8 @@ struct ngz_agg {
     size_t scratch_cap = 0;
     uint8_t *rec_buf = nullptr;  // record contexts, rec_g, claims, collided lists, sort buffers
     size_t rec_cap = 0;
+    uint8_t *part_buf = nullptr;  // partitioned reduction: counts, offsets, scan scratch, payloads
+    size_t part_cap = 0;
 };
 
 namespace {
@@ -1745,6 +1896,7 @@ void ngz_agg_destroy(ngz_agg *a) {
     hipFree(a->plans);
     hipFree(a->scratch);
     hipFree(a->rec_buf);
+    hipFree(a->part_buf);
     if (a->ev0) hipEventDestroy(a->ev0);
     if (a->ev1) hipEventDestroy(a->ev1);
     if (a->stream) hipStreamDestroy(a->stream);
@@ -2060,7 +2212,40 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, uint16_t pe
         // for k_agg_apply, one counter atomic per wave on a single word (142 ms for 12 groups
         // and 10^8 records), so the owner test stays in k_agg_apply there.
         static const bool split = getenv("NGZ_AGG_OWN_SPLIT") != nullptr;  // A/B: the owner test in k_agg_apply
-        if (P.own && !split && a->live * 8 > (uint64_t)n_rec) {
+        // partitioned reduction: more groups than LDS tables hold, at least 8 records per group
+        // (NGZ_AGG_PART: 0 never, 1 whenever the config allows it)
+        const int part_env = getenv("NGZ_AGG_PART") ? atoi(getenv("NGZ_AGG_PART")) : -1;  // read per push (tests)
+        const uint64_t groups = a->live + n_claims, n_part = a->slots / PART_SLOTS;
+        const bool part_ok = P.lds_ok && P.n_vals <= 8 && a->slots >= PART_SLOTS && n_part <= 8192;
+        const bool part = part_ok && (part_env == 1 || (part_env != 0 && n_rec >= (1u << 20) && groups > 4096 &&
+                                                         groups * 8 <= (uint64_t)n_rec));
+        if (part) {
+            const uint32_t nt = (uint32_t)((n_rec + PART_TILE - 1) / PART_TILE), np = (uint32_t)n_part;
+            const uint32_t pb = 16 + 16 * ((P.n_vals + 1) / 2);
+            const uint64_t nc = (uint64_t)np * nt + 1;
+            size_t stb = 0;
+            hipcub::DeviceScan::ExclusiveSum(nullptr, stb, (uint32_t *)nullptr, (uint32_t *)nullptr, (int)nc, st);
+            const size_t need = 2 * al(4 * nc) + al(stb) + (size_t)n_rec * pb;
+            if (need > a->part_cap) {
+                hipFree(a->part_buf);
+                a->part_buf = nullptr;
+                a->part_cap = 0;
+                if (hipMalloc(&a->part_buf, need) != hipSuccess) {
+                    a->poisoned = true;  // the claims are committed: this push cannot be undone here
+                    return fail(a, NGZ_E_NOMEM, "partition buffers");
+                }
+                a->part_cap = need;
+            }
+            uint32_t *counts = (uint32_t *)a->part_buf, *offs = (uint32_t *)(a->part_buf + al(4 * nc));
+            void *stmp = a->part_buf + 2 * al(4 * nc);
+            uint8_t *pay = a->part_buf + 2 * al(4 * nc) + al(stb);
+            AGG_HIP(a, hipMemsetAsync(counts + nc - 1, 0, 4, st));
+            hipLaunchKernelGGL(k_agg_part_hist, dim3(nt), dim3(256), 4 * np, st, C, rec_g, np, counts);
+            AGG_HIP(a, hipcub::DeviceScan::ExclusiveSum(stmp, stb, counts, offs, (int)nc, st));
+            hipLaunchKernelGGL(k_agg_part_scatter, dim3(nt), dim3(256), 4 * np, st, C, P, rec_g, np, offs, pay, pb);
+            hipLaunchKernelGGL(k_agg_part_reduce, dim3(np), dim3(256), 0, st, P, a->plans, offs, nt, pay, pb, a->rows);
+        } else if (P.own && !split && a->live * 8 > (uint64_t)n_rec) {
+
             // owners reduce their rows first, the records k_agg_apply_own lists apply atomics after
             AGG_HIP(a, hipMemsetAsync(a->n_coll, 0, 4, st));
             hipLaunchKernelGGL(k_agg_apply_own<true>, dim3(fg), dim3(256), 0, st, C, P, rec_g, a->rows, list_a, a->n_coll,

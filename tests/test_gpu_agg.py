@@ -467,3 +467,31 @@ def test_stale_batch_is_refused(dev):
     agg = FlowAggregator([(0, 4, 0, OK), (0, 1, 0, ADD)])
     with pytest.raises(AggError, match="stale"):
         agg.push(old)
+
+
+@pytest.mark.parametrize("keys", [
+    [(0, 4, 0, OK), (0, 61, 0, OK)],
+    [(0, 4, 0, OK), (0, 11, 0, OK)],                    # protocol + destination port (bench key dport)
+    [(0, 8, 0, OK), (0, 12, 0, OK), (0, 7, 0, OK), (0, 11, 0, OK), (0, 4, 0, OK)],
+])
+def test_partitioned_reduction(dev, keys, monkeypatch):
+    """The partitioned reduction (slot-range partitions reduced in LDS, rows updated in place),
+    forced with NGZ_AGG_PART=1, on the T20 streams with late messages and closing windows."""
+    monkeypatch.setenv("NGZ_AGG_PART", "1")
+    times = [1_700_000_010, 1_700_000_030, 1_700_000_015, 1_700_000_045, 1_700_000_020, 1_700_000_050,
+             1_700_000_061, 1_700_000_049]
+    d = t20_datagrams(6000, 100, times)
+    check(keys + T20_AGG, [d[:25], d[25:]])
+
+
+def test_partitioned_reduction_ports_captures_orders(dev, monkeypatch):
+    """Forced partitioned reduction: peer ports and collection times over two pushes, every
+    reference capture (wide and packed keys), wrapping adds / signed min-max, and the ordered
+    reductions that run after it."""
+    monkeypatch.setenv("NGZ_AGG_PART", "1")
+    test_t20_multi_port_collection_times(dev)
+    test_wrapping_add_and_signed_min_max(dev)
+    test_ordered_reductions(dev)
+    for name in [c[0] for c in golden_io.cases()]:
+        for fields in ("wide", "packed"):
+            test_reference_captures(dev, name, fields)
