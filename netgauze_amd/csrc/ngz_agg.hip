@@ -979,6 +979,9 @@ __global__ __launch_bounds__(256, 4) void k_agg_apply(const RecCtx C, const AggP
 // Owner path ops, one per 8-byte unit of the row (AggParams::unit_op / unit_src)
 enum : uint8_t { U_KEEP = 0, U_ADD = 1, U_MIN = 2, U_MAX = 3, U_OR = 4, U_VP = 5, U_TS = 6, U_SYS = 7 };
 constexpr int OWN_ROUNDS = 2;  // k_agg_apply_own: rounds of eight owners whose rows are in flight together
+// k_agg_apply_own's LDS row per record: aggregated-field operands 0-7, then export | sys-up time,
+// template bit, domain bits, present-value bits
+enum : uint32_t { OP_TS = 8, OP_TPL = 9, OP_D0 = 10, OP_D1 = 11, OP_HV = 12, OPW = 13 };
 enum : uint8_t { U_SRC_ONE = 8, U_SRC_COLL = 9, U_SRC_PORT = 10, U_SRC_TPL = 11, U_SRC_DOM0 = 12, U_SRC_DOM1 = 13 };
 
 // The owner record of each group: its whole reduction with plain loads and stores, eight
@@ -999,9 +1002,24 @@ __global__ __launch_bounds__(256) void k_agg_apply_own(const RecCtx C, const Agg
     const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint64_t n_waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
     // 64 records per wave step.  Every lane first loads its own record's operands (coalesced,
-    // all in flight together); the owners among them are then taken eight at a time, one per
-    // lane octet, their operands handed over by lane shuffles, so each round waits on its
-    // rows only.
+    // all in flight together) and puts them in the wave's LDS rows; the owners among them are
+    // then taken eight at a time, one per lane octet, and each lane reads from LDS just the
+    // operands of its own row piece's units (the op table is per lane), so each round waits on
+    // its rows only.  (Handing all operands over by lane shuffles took ~25 bpermutes per round
+    // and 16 more VGPRs.)
+    __shared__ unsigned long long opnd[4][64][OPW];
+    unsigned long long (*ops)[OPW] = opnd[(threadIdx.x >> 6) & 3];
+    // the lane's four 8-byte units (2p, 2p+1 in the first line, 2p+16, 2p+17 in the second):
+    // op, and the operand column of the LDS row (OPW: none)
+    uint32_t uop[4], ucol[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t u = 2 * piece + (j & 1) + (j >= 2 ? 16 : 0);
+        uop[j] = (uint32_t)(P.unit_op[u >> 4] >> (4 * (u & 15))) & 15;
+        const uint32_t sv = (uint32_t)(P.unit_src[u >> 4] >> (4 * (u & 15))) & 15;
+        ucol[j] = uop[j] == U_KEEP ? OPW : uop[j] == U_VP ? OP_HV : (uop[j] == U_TS || uop[j] == U_SYS) ? OP_TS
+                : sv < 8 ? sv : sv == U_SRC_TPL ? OP_TPL : sv == U_SRC_DOM0 ? OP_D0 : sv == U_SRC_DOM1 ? OP_D1 : OPW;
+    }
     for (uint64_t base = wave * 64; base < C.n_rec; base += n_waves * 64) {
         const uint32_t mine = base + lane < C.n_rec ? rec_g[base + lane] : NONE;
         Rec r;
@@ -1011,20 +1029,26 @@ __global__ __launch_bounds__(256) void k_agg_apply_own(const RecCtx C, const Agg
         if (!m) continue;
         if (!FUSED && owner) rec_g[base + lane] = mine & ~OWN_BIT;  // plain group index again (k_agg_ordered sorts on it)
         if (!FUSED && owner) r = rec_of(C, base + lane, err);
-        const AggSlotPlan &sp = C.plans[r.slot];
-        const uint32_t db = (r.info >> 2) & 0x7F;
-        const uint64_t dom0 = db < 64 ? 1ull << db : 0ull, dom1 = db < 64 ? 0ull : 1ull << (db & 63);
-        const uint64_t tpl = r.valid ? sp.tpl_bit : 0ull;
-        uint64_t xv[8];
-        uint32_t hv = 0;
+        {
+            const AggSlotPlan &sp = C.plans[r.slot];
+            const uint32_t db = (r.info >> 2) & 0x7F;
+            uint32_t hv = 0;
 #pragma unroll
-        for (int v = 0; v < 8; ++v) {
-            xv[v] = 0;
-            if (r.valid && v < (int)P.n_vals && sp.val_col[v] && !vc_ordered(P.val_vc[v])) {
-                xv[v] = value_operand(sp, P, v, r.row);
-                hv |= 1u << v;
+            for (int v = 0; v < 8; ++v) {
+                uint64_t x = 0;
+                if (r.valid && v < (int)P.n_vals && sp.val_col[v] && !vc_ordered(P.val_vc[v])) {
+                    x = value_operand(sp, P, v, r.row);
+                    hv |= 1u << v;
+                }
+                ops[lane][v] = x;
             }
+            ops[lane][OP_TS] = ((uint64_t)r.sysup << 32) | r.ts;
+            ops[lane][OP_TPL] = r.valid ? sp.tpl_bit : 0ull;
+            ops[lane][OP_D0] = db < 64 ? 1ull << db : 0ull;
+            ops[lane][OP_D1] = db < 64 ? 0ull : 1ull << (db & 63);
+            ops[lane][OP_HV] = hv;
         }
+        __builtin_amdgcn_wave_barrier();
         const uint32_t vmask = r.valid ? 1u : 0u;
         while (m) {
             // up to OWN_ROUNDS rounds of eight owners: every round's rows are loaded before any
@@ -1069,48 +1093,46 @@ __global__ __launch_bounds__(256) void k_agg_apply_own(const RecCtx C, const Agg
             }
 #pragma unroll
             for (int k = 0; k < OWN_ROUNDS; ++k) {
-                const int sl = src[k];
-                const uint32_t s_ts = (uint32_t)__shfl((int)r.ts, sl), s_sys = (uint32_t)__shfl((int)r.sysup, sl);
-                const uint32_t s_hv = (uint32_t)__shfl((int)hv, sl);
-                const uint64_t s_d0 = readlane64(dom0, sl), s_d1 = readlane64(dom1, sl), s_tpl = readlane64(tpl, sl);
-                uint64_t s_xv[8];
+                const unsigned long long *o = ops[src[k]];
+                const uint32_t s_hv = (uint32_t)o[OP_HV];
 #pragma unroll
-                for (int v = 0; v < 8; ++v) s_xv[v] = v < (int)P.n_vals ? readlane64(xv[v], sl) : 0ull;
-                auto unit = [&](uint32_t u, uint32_t &lo, uint32_t &hi) {
-                    const uint32_t op = (uint32_t)(P.unit_op[u >> 4] >> (4 * (u & 15))) & 15;
-                    if (op == U_KEEP) return;
-                    if (op == U_VP) { hi |= s_hv; return; }
-                    if (op == U_TS) { lo = min(lo, s_ts); hi = max(hi, s_ts); return; }
-                    if (op == U_SYS) { lo = max(lo, s_sys); hi = P.push_id; return; }
-                    const uint32_t sv = (uint32_t)(P.unit_src[u >> 4] >> (4 * (u & 15))) & 15;
-                    uint64_t x = 0;
-                    if (sv < 8) {
-                        if (!((s_hv >> sv) & 1)) return;
+                for (int h = 0; h < 2; ++h) {
+                    if (!(h ? two[k] : one[k])) continue;
+                    uint4 &wv = h ? w1[k] : w0[k];
+                    uint32_t *c = (uint32_t *)&wv;
 #pragma unroll
-                        for (int v = 0; v < 8; ++v)
-                            if (sv == (uint32_t)v) x = s_xv[v];
-                    } else {
-                        x = sv == U_SRC_ONE ? 1ull : sv == U_SRC_COLL ? P.coll_flip
-                          : sv == U_SRC_PORT ? 1ull << P.port_bit : sv == U_SRC_TPL ? s_tpl
-                          : sv == U_SRC_DOM0 ? s_d0 : s_d1;
+                    for (int e = 0; e < 2; ++e) {
+                        const int j = 2 * h + e;
+                        const uint32_t op = uop[j];
+                        if (op == U_KEEP) continue;
+                        uint32_t &lo = c[2 * e], &hi = c[2 * e + 1];
+                        const uint32_t col = ucol[j];
+                        const uint64_t x = col < OPW ? o[col] : 0ull;
+                        if (op == U_VP) { hi |= s_hv; continue; }
+                        if (op == U_TS) { lo = min(lo, (uint32_t)x); hi = max(hi, (uint32_t)x); continue; }
+                        if (op == U_SYS) { lo = max(lo, (uint32_t)(x >> 32)); hi = P.push_id; continue; }
+                        uint64_t y;
+                        if (col < 8) {
+                            if (!((s_hv >> col) & 1)) continue;  // the record lacks the field (None)
+                            y = x;
+                        } else if (col < OPW) {
+                            y = x;
+                        } else {  // per-push constants
+                            const uint32_t u = 2 * piece + (j & 1) + (j >= 2 ? 16 : 0);
+                            const uint32_t sv = (uint32_t)(P.unit_src[u >> 4] >> (4 * (u & 15))) & 15;
+                            y = sv == U_SRC_ONE ? 1ull : sv == U_SRC_COLL ? P.coll_flip : 1ull << P.port_bit;
+                        }
+                        uint64_t cur = ((uint64_t)hi << 32) | lo;
+                        cur = op == U_ADD ? cur + y : op == U_MIN ? (y < cur ? y : cur) : op == U_MAX ? (y > cur ? y : cur)
+                                                                                                       : (cur | y);
+                        lo = (uint32_t)cur;
+                        hi = (uint32_t)(cur >> 32);
                     }
-                    uint64_t c = ((uint64_t)hi << 32) | lo;
-                    c = op == U_ADD ? c + x : op == U_MIN ? (x < c ? x : c) : op == U_MAX ? (x > c ? x : c) : (c | x);
-                    lo = (uint32_t)c;
-                    hi = (uint32_t)(c >> 32);
-                };
-                if (one[k]) {
-                    unit(2 * piece, w0[k].x, w0[k].y);
-                    unit(2 * piece + 1, w0[k].z, w0[k].w);
-                    q[k][piece] = w0[k];
-                }
-                if (two[k]) {
-                    unit(2 * piece + 16, w1[k].x, w1[k].y);
-                    unit(2 * piece + 17, w1[k].z, w1[k].w);
-                    q[k][piece + 8] = w1[k];
+                    q[k][piece + 8 * h] = wv;
                 }
             }
         }
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
