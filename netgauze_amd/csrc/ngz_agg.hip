@@ -2249,9 +2249,9 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, uint16_t pe
     // groups (about one record per group and push): one tile per workgroup, all records in flight
     if (n_rec) {
         const uint32_t ag = (a->live + n_claims) * 8 > n_rec ? fg : ig;
-        // fused owner test (k_agg_apply_own first) only when the table already holds many groups
-        // per record: then nearly every record is its group's owner.  An empty table (the first
-        // push of any key) may hold few, hot groups: almost every record would then be listed
+        // fused owner test (k_agg_apply_own first) only when the table holds many groups per
+        // record after the claims: then nearly every record is its group's owner.  Few, hot
+        // groups (a first push of a low-cardinality key included) would list almost every record
         // for k_agg_apply, one counter atomic per wave on a single word (142 ms for 12 groups
         // and 10^8 records), so the owner test stays in k_agg_apply there.
         static const bool split = getenv("NGZ_AGG_OWN_SPLIT") != nullptr;  // A/B: the owner test in k_agg_apply
@@ -2287,7 +2287,7 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, uint16_t pe
             AGG_HIP(a, hipcub::DeviceScan::ExclusiveSum(stmp, stb, counts, offs, (int)nc, st));
             hipLaunchKernelGGL(k_agg_part_scatter, dim3(nt), dim3(256), 4 * np, st, C, P, rec_g, np, offs, pay, pb);
             hipLaunchKernelGGL(k_agg_part_reduce, dim3(np), dim3(256), 0, st, P, a->plans, offs, nt, pay, pb, a->rows);
-        } else if (P.own && !split && a->live * 8 > (uint64_t)n_rec) {
+        } else if (P.own && !split && groups * 8 > (uint64_t)n_rec) {
 
             // owners reduce their rows first, the records k_agg_apply_own lists apply atomics after
             AGG_HIP(a, hipMemsetAsync(a->n_coll, 0, 4, st));
