@@ -495,3 +495,43 @@ def test_partitioned_reduction_ports_captures_orders(dev, monkeypatch):
     for name in [c[0] for c in golden_io.cases()]:
         for fields in ("wide", "packed"):
             test_reference_captures(dev, name, fields)
+
+
+def test_partitioned_equals_atomic_at_full_size(dev, monkeypatch):
+    """Full size: 10^8 T20 records (the bench batch) by protocol + destination port, 393 216
+    groups, two pushes (the first creates the groups, the second reduces into them).  The
+    partitioned reduction and the LDS / atomic one give byte-identical rows (every reduction
+    there is order-free); only the owner word, device bookkeeping whose last writer varies
+    from run to run, is left out."""
+    import numpy as np
+    from netgauze_amd import synth
+    from netgauze_amd.aggregate import FlowAggregator
+    from netgauze_amd.flow import FlowInfoCodec
+    n = 100_000_000
+    codec = FlowInfoCodec(0, rtc_sync=True)
+    codec.decode_datagrams([synth.template_message()])
+    rec = synth.t20_records(n, device=dev)
+    buf, offs, lens = synth.ipfix_data_stream(rec, 64)
+    del rec
+    m = torch.arange(offs.numel(), device=dev, dtype=torch.int64)
+    t = 1_700_000_010 + (m * 60) // offs.numel()  # two minute windows
+    for b in range(4):
+        buf[offs + 4 + b] = ((t >> (8 * (3 - b))) & 0xFF).to(torch.uint8)
+    del m, t
+    batch = codec.decode_batch(buf, offs, lens)
+    assert batch.n_records == n
+    fields = [(0, 4, 0, OK), (0, 11, 0, OK)] + T20_AGG
+    rows = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("NGZ_AGG_PART", mode)
+        agg = FlowAggregator(fields, capacity=1 << 20, lateness_s=60)
+        for _ in range(2):
+            assert agg.push(batch, 4739, 0) == 0
+        _, raw = agg.flush_raw()
+        agg.close()
+        raw = np.array(raw)
+        raw[:, 88:92] = 0  # owner word
+        rows[mode] = sorted(bytes(r) for r in raw)
+    assert len(rows["1"]) > 300_000
+    assert rows["0"] == rows["1"]
+    codec.close()
