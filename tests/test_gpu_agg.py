@@ -535,3 +535,42 @@ def test_partitioned_equals_atomic_at_full_size(dev, monkeypatch):
     assert len(rows["1"]) > 300_000
     assert rows["0"] == rows["1"]
     codec.close()
+
+
+def test_owner_path_equals_atomic_5tuple(dev, monkeypatch):
+    """10^7 T20 records by the 5-tuple (about one group per record), two pushes: the owner
+    path (each group's owner record reduces its row with plain stores, k_agg_apply_own) and
+    the per-record atomics (NGZ_AGG_NO_OWN) give byte-identical rows, owner word aside."""
+    import numpy as np
+    from netgauze_amd import synth
+    from netgauze_amd.aggregate import FlowAggregator
+    from netgauze_amd.flow import FlowInfoCodec
+    n = 10_000_000
+    codec = FlowInfoCodec(0, rtc_sync=True)
+    codec.decode_datagrams([synth.template_message()])
+    rec = synth.t20_records(n, device=dev)
+    buf, offs, lens = synth.ipfix_data_stream(rec, 64)
+    del rec
+    m = torch.arange(offs.numel(), device=dev, dtype=torch.int64)
+    t = 1_700_000_010 + (m * 60) // offs.numel()  # two minute windows, nothing late
+    for b in range(4):
+        buf[offs + 4 + b] = ((t >> (8 * (3 - b))) & 0xFF).to(torch.uint8)
+    del m, t
+    batch = codec.decode_batch(buf, offs, lens)
+    assert batch.n_records == n
+    fields = [(0, 8, 0, OK), (0, 12, 0, OK), (0, 7, 0, OK), (0, 11, 0, OK), (0, 4, 0, OK)] + T20_AGG
+    rows = {}
+    for mode in ("own", "atomic"):
+        if mode == "atomic":
+            monkeypatch.setenv("NGZ_AGG_NO_OWN", "1")
+        agg = FlowAggregator(fields, capacity=n, lateness_s=60)
+        for _ in range(2):
+            assert agg.push(batch, 4739, 0) == 0
+        _, raw = agg.flush_raw()
+        agg.close()
+        raw = np.array(raw)
+        raw[:, 88:92] = 0  # owner word
+        rows[mode] = np.sort(np.ascontiguousarray(raw).view(np.dtype((np.void, raw.shape[1]))).ravel())
+    assert len(rows["own"]) > n // 2
+    assert np.array_equal(rows["own"], rows["atomic"])
+    codec.close()
