@@ -92,20 +92,22 @@ def cpu_baseline(workload="t20", seconds_budget=10.0, single_budget=4.0):
 
 def committed_traffic(records, workload):
     """Per-launch HBM bytes of the decode kernel from a committed rocprofv3 PMC
-    profile of this same workload (profiles/*/traffic.json, written by
-    tools/summarize_profile.py) taken of THIS source tree (its source hash,
-    netgauze_amd/buildinfo.py), or None: a profile of an older build is never
-    reported as this build's traffic."""
+    profile of this same workload (profiles/**/traffic.json at any depth, written
+    by tools/summarize_profile.py) taken of THIS build's decode sources (their
+    hash, netgauze_amd/buildinfo.decode_source_hash), or None: a profile of an
+    older decode build is never reported as this build's traffic.  The newest
+    matching profile (by path: profiles/<round><letter>/...) wins."""
     import glob
     from netgauze_amd import buildinfo
-    want = buildinfo.source_hash()
+    want, whole = buildinfo.decode_source_hash(), buildinfo.source_hash()
     best = None
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*", "traffic.json"))):
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "traffic.json"), recursive=True)):
         try:
             t = json.load(open(f))
         except (OSError, ValueError):
             continue
-        if t.get("records") == records and t.get("workload") == workload and t.get("source_hash") == want:
+        if t.get("records") == records and t.get("workload") == workload and \
+                (t.get("decode_source_hash") == want or t.get("source_hash") == whole):
             best = (t["traffic_bytes"], os.path.relpath(f, ROOT))
     return best
 

@@ -1,7 +1,8 @@
 /* MI355X flow aggregation over decoded IPFIX / NetFlow v9 columns (C ABI).
  *
  * the step after the decode path.  One ngz_agg
- * replaces the collector's per-peer windowed FlowAggregator:
+ * replaces one collector shard's windowed aggregation (the AggregationActor's
+ * window_aggregate over every exporter peer the shard sees, actor.rs:151-181):
  *
  *   FlowAggregator::push / flush     crates/collector/src/flow/aggregation/aggregator.rs:68-95
  *   FlowCacheRecord::reduce          aggregator.rs:159-198   (Add / Min / Max / BoolMapOr; None + Some -> Some)
@@ -12,20 +13,23 @@
  *   get_window_start                 aggregation.rs:79-89    (timestamp floored to the minute)
  *   validate_operation_compatibility aggregation/config.rs:212-250, generator.rs:580-629
  *
- *   AggFlowInfo::into_flowinfo_with_extra_fields  aggregator.rs:203-277 (ngz_agg_flowinfo_json)
+ *   AggFlowInfo::into_flowinfo_with_extra_fields  aggregator.rs:203-277 + actor.rs:222-240 (ngz_agg_flowinfo_json)
  *
  * The group table lives in HBM and persists across ngz_agg_push calls; one
- * aggregator serves one exporter peer IP (the window key, aggregator.rs:109-117).
- * Records are grouped by (window start, flow type, key fields) exactly: keys are
- * compared, never identified by a hash.  A record whose message export time is
- * more than `lateness` behind the peer's event time is late and is counted, not
- * aggregated (aggregation.rs:139-141).  Windows whose start is at or before
- * get_window_start(event time - lateness) - window_duration are closed
- * (aggregation.rs:154-160): ngz_agg_emit hands their groups out and frees their
- * room; ngz_agg_flush hands out every group (WindowAggregator::flush).
+ * aggregator serves every exporter peer of a shard.  Records are grouped by
+ * (peer IP, window start, flow type, key fields) exactly -- FlowCacheKey is
+ * (peer_ip, flow_type, key_fields) and the window aggregator keys its windows by
+ * peer IP (aggregator.rs:109-124, aggregation.rs:96-108): keys are compared,
+ * never identified by a hash.  Each peer IP has its own event time: a record
+ * whose message export time is more than `lateness` behind its peer's event time
+ * is late and is counted, not aggregated (aggregation.rs:139-141), and a peer's
+ * windows whose start is at or before get_window_start(its event time -
+ * lateness) - window_duration are closed (aggregation.rs:154-160), independently
+ * of the other peers: ngz_agg_emit hands the groups of closed windows out and
+ * frees their room; ngz_agg_flush hands out every group (WindowAggregator::flush).
  *
  * A push is all-or-nothing: when it fails (NGZ_AGG_E_OVERFLOW, NGZ_E_LIMIT, ...)
- * the groups, the set dictionaries and the event time are as they were before
+ * the groups, the set dictionaries and the event times are as they were before
  * it.  Only a device error or an internal inconsistency poisons the aggregator
  * (NGZ_AGG_E_POISONED from then on, until ngz_agg_reset).
  */
@@ -53,8 +57,10 @@ extern "C" {
 #define NGZ_AGG_MAX_KEY_BYTES 128   /* sum of key row slots (see ngz_agg_key_desc) */
 #define NGZ_AGG_SET_BITS 64         /* distinct template ids / peer ports among the live groups; 128 observation
                                        domains (entries no live group uses are reused) */
+#define NGZ_AGG_MAX_PEERS 65536     /* distinct exporter peer IPs between two flushes */
 
-#define NGZ_AGG_E_OVERFLOW (-10)    /* more groups than the capacity, or a set dictionary full of live entries */
+#define NGZ_AGG_E_OVERFLOW (-10)    /* more groups than the capacity, a set dictionary full of live entries, or
+                                       more peer IPs than max_peers */
 #define NGZ_AGG_E_COLLISION (-11)   /* no longer returned: hash collisions are resolved by comparing keys */
 #define NGZ_AGG_E_POISONED (-12)    /* an earlier device error / internal inconsistency; ngz_agg_reset clears it */
 
@@ -69,6 +75,15 @@ typedef struct {
 
 typedef struct ngz_agg ngz_agg;
 
+/* An exporter peer (std::net::SocketAddr, the `peer` of explode, aggregator.rs:286-292):
+ * the IP keys the groups and the windows, the port joins the groups' peer_ports set. */
+typedef struct {
+    uint8_t family;      /* 4 or 6 */
+    uint8_t reserved;
+    uint16_t port;
+    uint8_t addr[16];    /* network order; IPv4 in addr[0..3] */
+} ngz_peer;
+
 /* Validates the config like AggregationConfig::validate + validate_operation_compatibility
  * (window > 0, lateness <= window; the op allowed by IE::supports_{arithmetic,comparison,
  * bitwise}_ops, generator.rs:1176-1272 -- data type, sub-registry and dataTypeSemantics
@@ -76,19 +91,23 @@ typedef struct ngz_agg ngz_agg;
  * it accepts one the device does not run (Min/Max over list types or the nested reason-code
  * sub-registry of forwardingStatus).  Key fields keep their order (key_select), aggregated
  * fields theirs (agg_select).  capacity: live groups held at most, up to 2^30 (the HBM table
- * has at least twice as many slots). */
+ * has at least twice as many slots).  max_peers: distinct peer IPs the aggregator takes
+ * between flushes (0 = NGZ_AGG_MAX_PEERS); a small bound leaves more bits of the exact
+ * 63-bit group tag to the key fields. */
 int ngz_agg_create(int device, const ngz_agg_field *fields, uint32_t n_fields, uint64_t window_ms,
-                   uint64_t lateness_ms, uint64_t capacity, ngz_agg **out);
+                   uint64_t lateness_ms, uint64_t capacity, uint32_t max_peers, ngz_agg **out);
 void ngz_agg_destroy(ngz_agg *a);
 const char *ngz_agg_last_error(ngz_agg *a);
 
 /* Explode + push every data record of the batch last decoded on ctx (out from
- * ngz_decode_batch), in datagram order.  peer_port joins peer_ports; collection_time_ms
- * is the batch's collection time (min/max_collection_time).  Records of failed
- * messages are not pushed (they yield no FlowInfo).  *late_records (may be NULL)
- * receives the records dropped as late.  hip_stream: the stream the batch was decoded
- * on (NULL = the context's stream is synchronised by ngz_decode_batch already). */
-int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, uint16_t peer_port,
+ * ngz_decode_batch), in datagram order: the FlowInfos one peer sent (a context is one
+ * peer's FlowInfoCodec).  peer: its address (a new IP beyond max_peers is
+ * NGZ_AGG_E_OVERFLOW); collection_time_ms is the batch's collection time
+ * (min/max_collection_time).  Records of failed messages are not pushed (they yield no
+ * FlowInfo).  *late_records (may be NULL) receives the records dropped as late.
+ * hip_stream: the stream the batch was decoded on (NULL = the context's stream is
+ * synchronised by ngz_decode_batch already). */
+int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, const ngz_peer *peer,
                  int64_t collection_time_ms, uint64_t *late_records, void *hip_stream);
 
 /* One flushed group (host).  Key and value bytes follow at key_off / val_off of the row
@@ -96,7 +115,8 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, uint16_t pe
 typedef struct {
     uint32_t window_start;      /* seconds, minute-floored (get_window_start) */
     uint8_t flow_type;          /* 10 IPFIX / 9 NetFlow v9 */
-    uint8_t reserved0[3];
+    uint8_t reserved0;
+    uint16_t peer;              /* the group's peer IP: entry of ngz_agg_peer */
     uint32_t key_present;       /* bit k: key field k is Some */
     uint32_t val_present;       /* bit v: aggregated field v is Some */
     uint64_t record_count;
@@ -125,16 +145,18 @@ int ngz_agg_layout(ngz_agg *a, uint32_t *row_bytes, uint32_t *key_off, uint16_t 
 int64_t ngz_agg_groups(ngz_agg *a);
 
 /* Copies every group (unordered) into dst (cap bytes, row_bytes each), then empties
- * the table, the set dictionaries and forgets the peer's event time
+ * the table, the set dictionaries, and forgets every peer and its event time
  * (WindowAggregator::flush).  Returns the groups written or <0 (NGZ_E_INVALID: cap too
  * small; nothing is emptied). */
 int64_t ngz_agg_flush(ngz_agg *a, void *dst, uint64_t cap);
 
-/* Groups of the windows the event time has closed (aggregation.rs:154-160), and the
- * emission of those groups: copied into dst like ngz_agg_flush, then removed.  The
+/* Groups of the windows their peer's event time has closed (aggregation.rs:154-160), and
+ * the emission of those groups: copied into dst like ngz_agg_flush, then removed.  The
  * reference emits a closed window from the process_item call that closes it; here the
  * windows closed by a push are emitted after it, with the same contents (an item is
- * never late for a window that is still open, and never lands in a closed one). */
+ * never late for a window that is still open, and never lands in a closed one).
+ * ngz_agg_emit returns the groups handed out; if rebuilding the table afterwards fails,
+ * the aggregator is poisoned (the next call reports it), the groups are still out. */
 int64_t ngz_agg_closed(ngz_agg *a);
 int64_t ngz_agg_emit(ngz_agg *a, void *dst, uint64_t cap);
 
@@ -146,6 +168,11 @@ int ngz_agg_reset(ngz_agg *a);
  * entries read all-ones).  Each array receives up to cap entries; returns 0. */
 int ngz_agg_sets(ngz_agg *a, uint32_t *templates, uint32_t *n_templates, uint16_t *ports, uint32_t *n_ports,
                  uint32_t *domains, uint32_t *n_domains, uint32_t cap);
+
+/* The peer IP of output rows (ngz_agg_row.peer) last returned by ngz_agg_flush /
+ * ngz_agg_emit (port: that of the push that first brought the IP).  out may be NULL.
+ * Returns the number of peers, or NGZ_E_INVALID for an index beyond them. */
+int ngz_agg_peer(ngz_agg *a, uint32_t index, ngz_peer *out);
 
 /* How a key / value is stored in an output row.
  * Key kkind: 0 the decoded column cell (width bytes), 1 a fixed string up to its first
@@ -171,18 +198,22 @@ typedef struct {
 int ngz_agg_key_info(ngz_agg *a, uint32_t k, ngz_agg_key_desc *out);
 int ngz_agg_value_info(ngz_agg *a, uint32_t v, ngz_agg_value_desc *out);
 
-/* AggFlowInfo::into_flowinfo_with_extra_fields (aggregator.rs:203-277) of output rows
- * (n rows of ngz_agg_flush / ngz_agg_emit, read with the dictionaries of that call):
+/* AggFlowInfo::into_flowinfo_with_extra_fields (aggregator.rs:203-277) of output rows,
+ * with the extra fields the aggregation actor always passes (actor.rs:222-240), for the
+ * n rows of one ngz_agg_flush / ngz_agg_emit call, read with that call's dictionaries:
  * one FlowInfo per group, as the serde JSON text of the decode path (ngz_batch_json):
  * an IPFIX or NetFlow v9 packet whose one data set (id 65535) holds one record: the
  * present key fields, the present aggregated fields, originalFlowsPresent,
- * minExportSeconds, maxExportSeconds, collectionTimeMilliseconds (the max), then one
- * NetGauze originalExporterTransportPort per peer port, one originalObservationDomainId
- * per domain and one NetGauze originalTemplateId per template id, each set in ascending
- * order (the reference iterates HashSets: unspecified order).  Packet header: export
- * time export_time_ms (the reference uses Utc::now()), sequence numbers seq0, seq0+1, ...,
- * observation domain / source id shard_id, NetFlow v9 sys_up_time = the group's max.
- * fn gets (row index, NGZ_DG_OK, text, length).  Returns rows rendered or <0. */
+ * minExportSeconds, maxExportSeconds, collectionTimeMilliseconds (the max), NetGauze
+ * windowStart and windowEnd (window start + window duration),
+ * originalExporterIPv4Address / originalExporterIPv6Address (the group's peer IP), then
+ * one NetGauze originalExporterTransportPort per peer port, one
+ * originalObservationDomainId per domain and one NetGauze originalTemplateId per template
+ * id, each set in ascending order (the reference iterates HashSets: unspecified order).
+ * Packet header: export time export_time_ms (the reference uses Utc::now()), sequence
+ * numbers seq0, seq0+1, ..., observation domain / source id shard_id, NetFlow v9
+ * sys_up_time = the group's max.  fn gets (row index, NGZ_DG_OK, text, length).  Returns
+ * rows rendered or <0. */
 int64_t ngz_agg_flowinfo_json(ngz_agg *a, const void *rows, uint64_t n, uint32_t shard_id, uint32_t seq0,
                               int64_t export_time_ms, ngz_json_line_fn fn, void *user);
 

@@ -40,7 +40,7 @@ INGEST_FUNCTIONS = [
 AGG_FUNCTIONS = [
     "ngz_agg_create", "ngz_agg_destroy", "ngz_agg_last_error", "ngz_agg_push", "ngz_agg_layout",
     "ngz_agg_groups", "ngz_agg_flush", "ngz_agg_closed", "ngz_agg_emit", "ngz_agg_reset", "ngz_agg_sets",
-    "ngz_agg_key_info", "ngz_agg_value_info", "ngz_agg_flowinfo_json", "ngz_agg_last_timing",
+    "ngz_agg_key_info", "ngz_agg_value_info", "ngz_agg_flowinfo_json", "ngz_agg_last_timing", "ngz_agg_peer",
 ]
 NGZ_AGG_KEY, NGZ_AGG_ADD, NGZ_AGG_MIN, NGZ_AGG_MAX, NGZ_AGG_OR = range(5)
 NGZ_AGG_E_OVERFLOW, NGZ_AGG_E_COLLISION, NGZ_AGG_E_POISONED = -10, -11, -12
@@ -120,7 +120,33 @@ class AggValueDesc(ctypes.Structure):
 
 assert ctypes.sizeof(AggKeyDesc) == 8 and ctypes.sizeof(AggValueDesc) == 8
 
-AGG_ROW_DTYPE = np.dtype([("window_start", "<u4"), ("flow_type", "u1"), ("reserved0", "u1", 3),
+
+class Peer(ctypes.Structure):
+    """ngz_peer: an exporter's SocketAddr."""
+    _fields_ = [("family", ctypes.c_uint8), ("reserved", ctypes.c_uint8), ("port", ctypes.c_uint16),
+                ("addr", ctypes.c_uint8 * 16)]
+
+    @classmethod
+    def of(cls, ip, port):
+        import ipaddress
+        a = ipaddress.ip_address(ip)
+        p = cls()
+        p.family = a.version
+        p.port = port
+        b = a.packed
+        for i, x in enumerate(b):
+            p.addr[i] = x
+        return p
+
+    def ip(self):
+        import ipaddress
+        b = bytes(self.addr)
+        return str(ipaddress.ip_address(b[:4] if self.family == 4 else b))
+
+
+assert ctypes.sizeof(Peer) == 20
+
+AGG_ROW_DTYPE = np.dtype([("window_start", "<u4"), ("flow_type", "u1"), ("reserved0", "u1"), ("peer", "<u2"),
                           ("key_present", "<u4"), ("val_present", "<u4"), ("record_count", "<u8"),
                           ("min_export_time", "<u4"), ("max_export_time", "<u4"), ("max_sys_up_time", "<u4"),
                           ("reserved1", "<u4"), ("min_collection_ms", "<i8"), ("max_collection_ms", "<i8"),
@@ -178,13 +204,13 @@ def load():
     lib.ngz_template_counts_device.argtypes = [P, I, P, U32, I, P]
     lib.ngz_template_counts_device.restype = I
     # aggregation (flow_aggregate.h)
-    lib.ngz_agg_create.argtypes = [I, ctypes.POINTER(AggField), U32, U64, U64, U64, ctypes.POINTER(P)]
+    lib.ngz_agg_create.argtypes = [I, ctypes.POINTER(AggField), U32, U64, U64, U64, U32, ctypes.POINTER(P)]
     lib.ngz_agg_create.restype = I
     lib.ngz_agg_destroy.argtypes = [P]
     lib.ngz_agg_destroy.restype = None
     lib.ngz_agg_last_error.argtypes = [P]
     lib.ngz_agg_last_error.restype = ctypes.c_char_p
-    lib.ngz_agg_push.argtypes = [P, P, ctypes.POINTER(BatchOut), ctypes.c_uint16, ctypes.c_int64,
+    lib.ngz_agg_push.argtypes = [P, P, ctypes.POINTER(BatchOut), ctypes.POINTER(Peer), ctypes.c_int64,
                                  ctypes.POINTER(ctypes.c_uint64), P]
     lib.ngz_agg_push.restype = I
     lib.ngz_agg_layout.argtypes = [P, ctypes.POINTER(U32), ctypes.POINTER(U32), ctypes.POINTER(ctypes.c_uint16),
@@ -211,6 +237,8 @@ def load():
     lib.ngz_agg_value_info.restype = I
     lib.ngz_agg_flowinfo_json.argtypes = [P, P, U64, U32, U32, ctypes.c_int64, JSON_LINE_FN, P]
     lib.ngz_agg_flowinfo_json.restype = ctypes.c_int64
+    lib.ngz_agg_peer.argtypes = [P, U32, ctypes.POINTER(Peer)]
+    lib.ngz_agg_peer.restype = I
     # ingest (flow_ingest.h)
     lib.ngz_pcap_open.argtypes = [ctypes.c_char_p, ctypes.POINTER(P)]
     lib.ngz_pcap_open.restype = I

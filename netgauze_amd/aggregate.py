@@ -4,10 +4,12 @@ in include/ngz/flow_aggregate.h (libngz.so; the group table lives in HBM).
 `FlowAggregator(transform, window, lateness)` takes the reference's
 AggregationConfig.transform shape (crates/collector/src/flow/aggregation/config.rs:
 152-176, 252-335): an ordered mapping IE -> Op, or IE -> {index: Op}, where IE is
-(pen, ie_id).  `push(batch, peer_port, collection_ms)` explodes and reduces every
-data record of a decoded batch (aggregator.rs:78-90, 159-198, 286-354);
-`emit()` returns the groups of the windows the event time has closed
-(analytics/src/aggregation.rs:154-160) and `flush()` every group
+(pen, ie_id).  One aggregator serves a collector shard: every exporter peer.
+`push(batch, peer_port, collection_ms, peer_ip)` explodes and reduces every data
+record of a batch one peer sent (aggregator.rs:78-90, 159-198, 286-354), grouped
+by (peer IP, window, flow type, key); `emit()` returns the groups of the windows
+each peer's event time has closed (analytics/src/aggregation.rs:154-160) and
+`flush()` every group
 (WindowAggregator::flush, :175-185), as dicts with canonical values: ints for
 integer-like fields, bytes for byte-like ones, str for strings, floats, and
 (secs, nanos) for date-times -- each field rendered from its IE's data type in
@@ -74,14 +76,16 @@ def _datetime_ms(ms):
 
 
 class FlowAggregator:
-    def __init__(self, transform, window_s=60, lateness_s=10, capacity=1 << 20, device=0, kinds=None):
+    DEFAULT_PEER = "192.0.2.1"  # TEST-NET-1: the exporter of pushes that name none
+
+    def __init__(self, transform, window_s=60, lateness_s=10, capacity=1 << 20, device=0, kinds=None, max_peers=0):
         self.fields = unify(transform) if isinstance(transform, dict) else list(transform)
         self.key_fields = [f for f in self.fields if f[3] == _lib.NGZ_AGG_KEY]
         self.val_fields = [f for f in self.fields if f[3] != _lib.NGZ_AGG_KEY]
         arr = (_lib.AggField * max(len(self.fields), 1))(*[_lib.AggField(p, i, x, o) for p, i, x, o in self.fields])
         h = ctypes.c_void_p()
         rc = lib().ngz_agg_create(device, arr, len(self.fields), int(window_s * 1000), int(lateness_s * 1000),
-                                  capacity, ctypes.byref(h))
+                                  capacity, max_peers, ctypes.byref(h))
         if rc != 0:
             raise AggError("ngz_agg_create failed (%d)" % rc)
         self._h = h
@@ -106,16 +110,27 @@ class FlowAggregator:
             raise AggError("%s (%d)" % (lib().ngz_agg_last_error(self._h).decode(), rc))
         return rc
 
-    def push(self, batch, peer_port=4739, collection_ms=0):
-        """Aggregate every data record of a DecodedBatch; returns the late records.
-        The batch must be the latest one its codec decoded (its device arrays are
-        reused by the next decode)."""
+    def push(self, batch, peer_port=4739, collection_ms=0, peer_ip=DEFAULT_PEER):
+        """Aggregate every data record of a DecodedBatch the peer (peer_ip, peer_port)
+        sent; returns the late records.  The batch must be the latest one its codec
+        decoded (its device arrays are reused by the next decode)."""
         if batch.generation != batch._codec.generation:
             raise AggError("stale DecodedBatch: its codec has decoded another batch since")
         late = ctypes.c_uint64()
-        self._check(lib().ngz_agg_push(self._h, batch._codec._ctx, ctypes.byref(batch.out), peer_port,
+        peer = _lib.Peer.of(peer_ip, peer_port)
+        self._check(lib().ngz_agg_push(self._h, batch._codec._ctx, ctypes.byref(batch.out), ctypes.byref(peer),
                                        collection_ms, ctypes.byref(late), None))
         return late.value
+
+    def peers(self):
+        """Peer IPs of the rows last returned by flush / emit (row field `peer`)."""
+        out = []
+        p = _lib.Peer()
+        n = lib().ngz_agg_peer(self._h, 0, ctypes.byref(p))
+        for i in range(max(n, 0)):
+            lib().ngz_agg_peer(self._h, i, ctypes.byref(p))
+            out.append(p.ip())
+        return out
 
     def push_ms(self):
         t = ctypes.c_float()
@@ -197,6 +212,7 @@ class FlowAggregator:
         rb, ko, kw, vo, vw = self.layout()
         kd, vd = self.descs()
         tpl, ports, doms = self.sets()
+        peers = self.peers() if len(hdr) else []
 
         def bits(x, dictionary):
             return {dictionary[i] for i in range(len(dictionary)) if (int(x) >> i) & 1}
@@ -217,7 +233,8 @@ class FlowAggregator:
                     continue
                 vals.append(self._render_value(pen, ie, vd[v], bytes(r[vo[v]:vo[v] + 32])))
             dom_bits = int(h["domain_bits"][0]) | (int(h["domain_bits"][1]) << 64)
-            out.append(dict(window_start=int(h["window_start"]), flow_type=int(h["flow_type"]), key=tuple(key),
+            out.append(dict(peer=peers[int(h["peer"])], window_start=int(h["window_start"]),
+                            flow_type=int(h["flow_type"]), key=tuple(key),
                             vals=tuple(vals), record_count=int(h["record_count"]),
                             min_export=int(h["min_export_time"]), max_export=int(h["max_export_time"]),
                             max_sysup=int(h["max_sys_up_time"]), min_coll=int(h["min_collection_ms"]),

@@ -44,6 +44,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -112,6 +113,8 @@ struct AggParams {
     uint64_t mask;              // table slots - 1
     uint32_t push_id;
     uint32_t port_bit;
+    uint32_t peer;              // the push's peer IP (entry of the aggregator's peer dictionary)
+    uint32_t peer_bits;         // packed tags: bits of the peer entry (log2 of max_peers)
     uint64_t coll_flip;         // collection time ms, sign bit flipped (unsigned order == signed order)
     uint32_t lds_ok;            // 1: no byte-wise OR values (wave results may be combined in LDS)
     uint32_t packed;            // 1: the whole group key packs into 63 bits (exact tag)
@@ -189,11 +192,16 @@ __device__ __forceinline__ void key_words(const AggSlotPlan &sp, const AggParams
     }
 }
 
+// row header word 1 (ngz_agg_row bytes 4-7): flow type, reserved byte, peer entry
+__device__ __forceinline__ uint32_t hdr_word(const AggSlotPlan &sp, const AggParams &P) {
+    return sp.proto | (P.peer << 16);
+}
+
 __device__ __forceinline__ uint64_t key_tag(const AggSlotPlan &sp, const AggParams &P, uint64_t row, uint32_t win,
                                             uint32_t &present, KeyVal &kv) {
     present = 0;
-    if (P.packed) {  // exact tag: bit 63 | window/60 | flow type | per key: presence bit + value bits
-        uint64_t x = ((uint64_t)(win / 60) << 1) | (sp.proto == 9);
+    if (P.packed) {  // exact tag: bit 63 | window/60 | flow type | peer | per key: presence bit + value bits
+        uint64_t x = ((((uint64_t)(win / 60) << 1) | (sp.proto == 9)) << P.peer_bits) | P.peer;
         for (uint32_t k = 0; k < P.n_keys; ++k) {
             const uint8_t *c = sp.key_col[k];
             const uint32_t w = sp.key_w[k];
@@ -207,7 +215,7 @@ __device__ __forceinline__ uint64_t key_tag(const AggSlotPlan &sp, const AggPara
         }
         return x | (1ull << 63);
     }
-    uint64_t h = mix64(0x4E475A41474731ull, ((uint64_t)win << 8) | sp.proto);
+    uint64_t h = mix64(0x4E475A41474731ull, ((uint64_t)win << 32) | hdr_word(sp, P));
     if (P.kw_n) {
         key_words(sp, P, row, kv);
 #pragma unroll
@@ -253,7 +261,7 @@ __device__ __forceinline__ bool key_row_equal(const KeyRow &kr, const AggSlotPla
                                               uint32_t win, uint32_t kp, const KeyVal &kv) {
     // an absent key's words are zero in the row and in kv
     const uint32_t rw[8] = {kr.k0.x, kr.k0.y, kr.k0.z, kr.k0.w, kr.k1.x, kr.k1.y, kr.k1.z, kr.k1.w};
-    bool same = kr.h0.x == win && kr.h0.y == sp.proto && kr.h0.z == kp;
+    bool same = kr.h0.x == win && kr.h0.y == hdr_word(sp, P) && kr.h0.z == kp;
 #pragma unroll
     for (uint32_t j = 0; j < 8; ++j)
         if (j < P.kw_n) same = same && rw[j] == kv.w[j];
@@ -263,7 +271,7 @@ __device__ __forceinline__ bool key_row_equal(const KeyRow &kr, const AggSlotPla
 __device__ __forceinline__ bool key_equal(const uint8_t *R, const AggSlotPlan &sp, const AggParams &P, uint64_t row,
                                           uint32_t win, uint32_t kp, const KeyVal &kv) {
     if (P.kw_n) return key_row_equal(key_row_load(R, P), sp, P, win, kp, kv);
-    bool same = *(const uint32_t *)(R + 0) == win && *(const uint32_t *)(R + 4) == sp.proto &&
+    bool same = *(const uint32_t *)(R + 0) == win && *(const uint32_t *)(R + 4) == hdr_word(sp, P) &&
                 *(const uint32_t *)(R + 8) == kp;
     for (uint32_t k = 0; k < P.n_keys && same; ++k) {
         const uint8_t *c = sp.key_col[k];
@@ -278,7 +286,7 @@ __device__ __forceinline__ bool key_equal(const uint8_t *R, const AggSlotPlan &s
 __device__ __forceinline__ void key_write(uint8_t *R, const AggSlotPlan &sp, const AggParams &P, uint64_t row,
                                           uint32_t win, uint32_t kp, const KeyVal &kv) {
     *(uint32_t *)(R + 0) = win;
-    *(uint32_t *)(R + 4) = sp.proto;
+    *(uint32_t *)(R + 4) = hdr_word(sp, P);
     *(uint32_t *)(R + 8) = kp;
     if (P.kw_n) {
 #pragma unroll
@@ -1375,29 +1383,33 @@ __global__ void k_agg_init(uint8_t *__restrict__ rows, uint64_t n_groups, uint32
         ((uint32_t *)rows)[i] = ident[i % ident_words];
 }
 
-// groups selected for output: every live group (cutoff == INT64_MAX) or the closed windows
-__device__ __forceinline__ bool selected(uint64_t tag, const uint8_t *R, int64_t cutoff_s) {
-    return tag_live(tag) && (int64_t)*(const uint32_t *)R <= cutoff_s;
+// groups selected for output: every live group (cut == nullptr) or the closed windows, each
+// group against its own peer's cutoff (cut[peer], INT64_MIN: the peer closed nothing)
+__device__ __forceinline__ bool selected(uint64_t tag, const uint8_t *R, const int64_t *__restrict__ cut) {
+    if (!tag_live(tag)) return false;
+    if (!cut) return true;
+    const uint32_t peer = *(const uint16_t *)(R + 6);
+    return (int64_t)*(const uint32_t *)R <= cut[peer];
 }
 
 __global__ void k_agg_count(const unsigned long long *__restrict__ tags, const uint8_t *__restrict__ rows,
-                            uint64_t n_slots, uint32_t row_bytes, int64_t cutoff_s,
+                            uint64_t n_slots, uint32_t row_bytes, const int64_t *__restrict__ cut,
                             unsigned long long *__restrict__ cursor) {
     uint32_t c = 0;
     for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n_slots;
          g += (uint64_t)gridDim.x * blockDim.x)
-        c += selected(tags[g], rows + g * row_bytes, cutoff_s);
+        c += selected(tags[g], rows + g * row_bytes, cut);
     if (c) atomicAdd(cursor, (unsigned long long)c);
 }
 
 // copies the selected groups to out; tomb: their slots become tombstones (closed windows)
 __global__ void k_agg_take(unsigned long long *__restrict__ tags, const uint8_t *__restrict__ rows, uint64_t n_slots,
-                           uint32_t row_bytes, int64_t cutoff_s, int tomb, uint8_t *__restrict__ out,
+                           uint32_t row_bytes, const int64_t *__restrict__ cut, int tomb, uint8_t *__restrict__ out,
                            unsigned long long *__restrict__ cursor) {
     for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n_slots;
          g += (uint64_t)gridDim.x * blockDim.x) {
         const uint8_t *R = rows + g * row_bytes;
-        if (!selected(tags[g], R, cutoff_s)) continue;
+        if (!selected(tags[g], R, cut)) continue;
         const uint64_t o = atomicAdd(cursor, 1ull);
         const uint32_t *src = (const uint32_t *)R;
         uint32_t *dst = (uint32_t *)(out + o * row_bytes);
@@ -1468,7 +1480,12 @@ struct ngz_agg {
     std::vector<int64_t> templates, ports, domains;
     // the dictionaries as of the last flush / emit (the rows it returned refer to them)
     std::vector<int64_t> out_templates, out_ports, out_domains;
-    uint32_t current_time = 0;  // the peer's event time (seconds), 0 = none yet
+    // exporter peers: the IP keys groups and windows (aggregator.rs:119-124, aggregation.rs:96-108);
+    // entry i is the rows' peer field.  Each peer has its own event time (seconds, 0 = none yet)
+    uint32_t max_peers = NGZ_AGG_MAX_PEERS;
+    std::vector<ngz_peer> peers, out_peers;
+    std::vector<uint32_t> peer_time;
+    std::map<std::string, uint32_t> peer_index;
     uint32_t push_id = 0;
     float t_push = 0;
     // device
@@ -1483,6 +1500,8 @@ struct ngz_agg {
     unsigned long long *n_claims = nullptr;
     unsigned int *n_coll = nullptr;
     unsigned long long *used = nullptr;
+    int64_t *cut = nullptr;         // per-peer window cutoffs of ngz_agg_closed / ngz_agg_emit
+    uint32_t cut_cap = 0;
     uint32_t *rank_maps = nullptr;  // one 65536-bit map per VC_RANK sub-registry value
     AggSlotPlan *plans = nullptr;
     uint32_t plans_cap = 0;
@@ -1685,13 +1704,14 @@ void finish_rows(ngz_agg *a, uint8_t *dst, int64_t n) {
     }
 }
 
-// groups selected by cutoff (INT64_MAX: all) -> dst (host); tomb: free their slots
-int64_t take_rows(ngz_agg *a, void *dst, uint64_t cap, int64_t cutoff_s, bool tomb) {
+// groups selected by per-peer cutoffs (device array; nullptr: every group) -> dst (host);
+// tomb: free their slots
+int64_t take_rows(ngz_agg *a, void *dst, uint64_t cap, const int64_t *cut, bool tomb) {
     AGG_HIP(a, hipSetDevice(a->device));
     unsigned long long n = 0;
     AGG_HIP(a, hipMemsetAsync(a->cursor, 0, 8, a->stream));
     hipLaunchKernelGGL(k_agg_count, dim3(grid_for(a->slots)), dim3(256), 0, a->stream, a->tags, a->rows, a->slots,
-                       a->P.row_bytes, cutoff_s, a->cursor);
+                       a->P.row_bytes, cut, a->cursor);
     AGG_HIP(a, hipMemcpyAsync(&n, a->cursor, 8, hipMemcpyDeviceToHost, a->stream));
     AGG_HIP(a, hipStreamSynchronize(a->stream));
     const uint32_t RB = a->P.row_bytes;
@@ -1701,7 +1721,7 @@ int64_t take_rows(ngz_agg *a, void *dst, uint64_t cap, int64_t cutoff_s, bool to
         if (hipMalloc(&tmp, (uint64_t)n * RB) != hipSuccess) return fail(a, NGZ_E_NOMEM, "output staging");
         AGG_HIP(a, hipMemsetAsync(a->cursor, 0, 8, a->stream));
         hipLaunchKernelGGL(k_agg_take, dim3(grid_for(a->slots)), dim3(256), 0, a->stream, a->tags, a->rows, a->slots, RB,
-                           cutoff_s, tomb ? 1 : 0, tmp, a->cursor);
+                           cut, tomb ? 1 : 0, tmp, a->cursor);
         hipError_t e = hipMemcpyAsync(dst, tmp, (uint64_t)n * RB, hipMemcpyDeviceToHost, a->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(a->stream);
         hipFree(tmp);
@@ -1711,18 +1731,52 @@ int64_t take_rows(ngz_agg *a, void *dst, uint64_t cap, int64_t cutoff_s, bool to
     a->out_templates = a->templates;
     a->out_ports = a->ports;
     a->out_domains = a->domains;
+    a->out_peers = a->peers;
     return (int64_t)n;
 }
 
 int64_t floordiv64(int64_t x, int64_t d) { return x / d - ((x % d != 0) && ((x < 0) != (d < 0))); }
 
-// Windows closed by the current event time (aggregation.rs:154-160): starts <= cutoff =
+// Windows a peer's event time has closed (aggregation.rs:154-160): starts <= cutoff =
 // get_window_start(current_time - lateness) - window_duration, in seconds (floored).
-int64_t cutoff_s(const ngz_agg *a) {
-    if (!a->current_time) return INT64_MIN;
-    const int64_t t = (int64_t)a->current_time * 1000 - (int64_t)a->lateness_ms;
+int64_t cutoff_s(const ngz_agg *a, uint32_t peer) {
+    const uint32_t ct = a->peer_time[peer];
+    if (!ct) return INT64_MIN;
+    const int64_t t = (int64_t)ct * 1000 - (int64_t)a->lateness_ms;
     const int64_t cut_ms = floordiv64(t, 60000) * 60000 - (int64_t)a->window_ms;
     return floordiv64(cut_ms, 1000);
+}
+
+// every peer's cutoff into the device array a->cut; false: no peer has an event time
+int upload_cutoffs(ngz_agg *a, bool *any) {
+    *any = false;
+    const uint32_t n = (uint32_t)a->peers.size();
+    std::vector<int64_t> c(std::max<uint32_t>(n, 1), INT64_MIN);
+    for (uint32_t i = 0; i < n; ++i) {
+        c[i] = cutoff_s(a, i);
+        *any = *any || c[i] != INT64_MIN;
+    }
+    if (!*any) return NGZ_OK;
+    if (n > a->cut_cap) {
+        hipFree(a->cut);
+        a->cut = nullptr;
+        a->cut_cap = 0;
+        const uint32_t want = std::max<uint32_t>(n, 64);
+        if (hipMalloc(&a->cut, 8ull * want) != hipSuccess) return fail(a, NGZ_E_NOMEM, "cutoff table");
+        a->cut_cap = want;
+    }
+    AGG_HIP(a, hipMemcpyAsync(a->cut, c.data(), 8ull * n, hipMemcpyHostToDevice, a->stream));
+    return NGZ_OK;
+}
+
+void forget_peers(ngz_agg *a) {
+    a->peers.clear();
+    a->peer_time.clear();
+    a->peer_index.clear();
+}
+
+std::string peer_key(const ngz_peer &p) {
+    return std::string(1, (char)p.family) + std::string((const char *)p.addr, p.family == 4 ? 4 : 16);
 }
 
 }  // namespace
@@ -1730,12 +1784,14 @@ int64_t cutoff_s(const ngz_agg *a) {
 extern "C" {
 
 int ngz_agg_create(int device, const ngz_agg_field *fields, uint32_t n_fields, uint64_t window_ms,
-                   uint64_t lateness_ms, uint64_t capacity, ngz_agg **out) {
+                   uint64_t lateness_ms, uint64_t capacity, uint32_t max_peers, ngz_agg **out) {
     if (!out || (n_fields && !fields)) return NGZ_E_INVALID;
     *out = nullptr;
     if (window_ms == 0 || lateness_ms > window_ms) return NGZ_E_INVALID;  // AggregationConfig::validate
+    if (max_peers > NGZ_AGG_MAX_PEERS) return NGZ_E_LIMIT;
     ngz_agg *a = new ngz_agg();
     a->device = device;
+    a->max_peers = max_peers ? max_peers : NGZ_AGG_MAX_PEERS;
     a->window_ms = window_ms;
     a->lateness_ms = lateness_ms;
     std::vector<int> vcs;
@@ -1809,8 +1865,10 @@ int ngz_agg_create(int device, const ngz_agg_field *fields, uint32_t n_fields, u
     // more when it straddles (176-byte rows at a 176-byte stride cover 2.4 lines on average);
     // NGZ_AGG_ROW_PACK keeps whole 16-byte pieces only (k_agg_apply_own's unit)
     P.row_bytes = getenv("NGZ_AGG_ROW_PACK") ? (off + 15) & ~15u : (off + 127) & ~127u;
+    P.peer_bits = 0;
+    while ((1u << P.peer_bits) < a->max_peers) ++P.peer_bits;
     {
-        uint32_t bits = 28;  // window/60 + flow type
+        uint32_t bits = 28 + P.peer_bits;  // window/60 + flow type + peer entry
         bool ok = true;
         for (uint32_t k = 0; k < P.n_keys; ++k) {
             ok = ok && P.key_pw[k] != 0;
@@ -1935,6 +1993,7 @@ void ngz_agg_destroy(ngz_agg *a) {
     hipFree(a->n_claims);
     hipFree(a->n_coll);
     hipFree(a->used);
+    hipFree(a->cut);
     hipFree(a->rank_maps);
     hipFree(a->plans);
     hipFree(a->scratch);
@@ -1966,18 +2025,55 @@ int ngz_agg_layout(ngz_agg *a, uint32_t *row_bytes, uint32_t *key_off, uint16_t 
     return NGZ_OK;
 }
 
-int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, uint16_t peer_port, int64_t collection_time_ms,
-                 uint64_t *late_records, void *hip_stream) {
-    if (!a || !ctx || !out) return NGZ_E_INVALID;
+int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, const ngz_peer *peer,
+                 int64_t collection_time_ms, uint64_t *late_records, void *hip_stream) {
+    if (!a || !ctx || !out || !peer || (peer->family != 4 && peer->family != 6)) return NGZ_E_INVALID;
     if (late_records) *late_records = 0;
     if (a->poisoned) return fail(a, NGZ_AGG_E_POISONED, "aggregator failed earlier: ngz_agg_reset it");
     AGG_HIP(a, hipSetDevice(a->device));
     if (hip_stream) AGG_HIP(a, hipStreamSynchronize((hipStream_t)hip_stream));
+    const uint16_t peer_port = peer->port;
+    // the peer IP's entry (a new IP gets the next one; taken back if the push fails)
+    const std::string pk = peer_key(*peer);
+    bool new_peer = false;
+    uint32_t pi;
+    {
+        auto it = a->peer_index.find(pk);
+        if (it != a->peer_index.end()) {
+            pi = it->second;
+        } else {
+            if (a->peers.size() >= a->max_peers)
+                return fail(a, NGZ_AGG_E_OVERFLOW, "more peer IPs than the aggregator's max_peers");
+            pi = (uint32_t)a->peers.size();
+            ngz_peer p = *peer;
+            if (p.family == 4) memset(p.addr + 4, 0, 12);
+            p.reserved = 0;
+            a->peers.push_back(p);
+            a->peer_time.push_back(0);
+            a->peer_index.emplace(pk, pi);
+            new_peer = true;
+        }
+    }
+    // tombstones of emitted windows are not reused by the probes: rebuild the table first when
+    // they and the most groups this push can add would crowd it
+    if (a->tombs && a->live + a->tombs + std::min<uint64_t>(out->n_records, a->limit - std::min(a->live, a->limit)) >
+                        a->slots / 4 * 3) {
+        if (int r = rehash(a)) {
+            if (new_peer) { a->peers.pop_back(); a->peer_time.pop_back(); a->peer_index.erase(pk); }
+            return r;
+        }
+    }
     // dictionaries as they were: a failed push puts them back
     const std::vector<int64_t> keep_t = a->templates, keep_p = a->ports, keep_d = a->domains;
     const std::vector<int> keep_vw = a->val_w, keep_kw = a->key_w, keep_kk = a->key_kind_seen, keep_vk = a->val_kind_seen;
     bool gc_done = false;
     auto restore = [&]() {
+        if (new_peer) {
+            a->peers.pop_back();
+            a->peer_time.pop_back();
+            a->peer_index.erase(pk);
+            new_peer = false;
+        }
         a->templates = keep_t;
         a->ports = keep_p;
         a->domains = keep_d;
@@ -2111,6 +2207,7 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, uint16_t pe
     AggParams P = a->P;
     P.push_id = ++a->push_id;
     P.port_bit = (uint32_t)port_bit;
+    P.peer = pi;
     P.coll_flip = (uint64_t)collection_time_ms ^ (1ull << 63);
     // owner path only where groups get few records per push (many groups per record): with
     // few, hot groups the wave / workgroup pre-aggregation of k_agg_apply serves them better
@@ -2129,7 +2226,7 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, uint16_t pe
     hipLaunchKernelGGL(k_agg_ts, dim3(grid_for(D)), dim3(256), 0, st, hdr, has_rec, D, ts);
     size_t tmp = cub_max;
     AGG_HIP(a, hipcub::DeviceScan::InclusiveScan(cub_tmp, tmp, ts, pm, hipcub::Max(), D, st));
-    hipLaunchKernelGGL(k_agg_late, dim3(grid_for(D)), dim3(256), 0, st, hdr, has_rec, pm, D, a->current_time,
+    hipLaunchKernelGGL(k_agg_late, dim3(grid_for(D)), dim3(256), 0, st, hdr, has_rec, pm, D, a->peer_time[pi],
                        a->lateness_ms, a->dom_dict, dginfo, a->newdom, a->err);
     // record starts of every set: n copied out of the set table (stride 16 B) then scanned
     AGG_HIP(a, hipMemsetAsync(cnt + NS, 0, 4, st));
@@ -2333,7 +2430,7 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, uint16_t pe
     AGG_HIP(a, hipStreamSynchronize(st));
     hipEventElapsedTime(&a->t_push, a->ev0, a->ev1);
     a->live += n_claims;
-    if (last_pm > a->current_time) a->current_time = last_pm;
+    if (last_pm > a->peer_time[pi]) a->peer_time[pi] = last_pm;
     if (late_records) *late_records = late;
     return NGZ_OK;
 }
@@ -2346,11 +2443,11 @@ int64_t ngz_agg_groups(ngz_agg *a) {
 int64_t ngz_agg_flush(ngz_agg *a, void *dst, uint64_t cap) {
     if (!a) return NGZ_E_INVALID;
     if (a->poisoned) return fail(a, NGZ_AGG_E_POISONED, "aggregator failed earlier: ngz_agg_reset it");
-    const int64_t n = take_rows(a, dst, cap, INT64_MAX, false);
+    const int64_t n = take_rows(a, dst, cap, nullptr, false);
     if (n < 0) return n;
-    // WindowAggregator::flush: every window out, the event time forgotten; the set
-    // dictionaries start over (the rows just returned refer to out_*)
-    a->current_time = 0;
+    // WindowAggregator::flush: every window out, the event times forgotten; the set and
+    // peer dictionaries start over (the rows just returned refer to out_*)
+    forget_peers(a);
     a->templates.clear();
     a->ports.clear();
     a->domains.clear();
@@ -2365,13 +2462,14 @@ int64_t ngz_agg_flush(ngz_agg *a, void *dst, uint64_t cap) {
 int64_t ngz_agg_closed(ngz_agg *a) {
     if (!a) return NGZ_E_INVALID;
     if (a->poisoned) return fail(a, NGZ_AGG_E_POISONED, "aggregator failed earlier: ngz_agg_reset it");
-    const int64_t cut = cutoff_s(a);
-    if (cut == INT64_MIN) return 0;
     AGG_HIP(a, hipSetDevice(a->device));
+    bool any = false;
+    if (int r = upload_cutoffs(a, &any)) return r;
+    if (!any) return 0;
     unsigned long long n = 0;
     AGG_HIP(a, hipMemsetAsync(a->cursor, 0, 8, a->stream));
     hipLaunchKernelGGL(k_agg_count, dim3(grid_for(a->slots)), dim3(256), 0, a->stream, a->tags, a->rows, a->slots,
-                       a->P.row_bytes, cut, a->cursor);
+                       a->P.row_bytes, a->cut, a->cursor);
     AGG_HIP(a, hipMemcpyAsync(&n, a->cursor, 8, hipMemcpyDeviceToHost, a->stream));
     AGG_HIP(a, hipStreamSynchronize(a->stream));
     return (int64_t)n;
@@ -2380,21 +2478,23 @@ int64_t ngz_agg_closed(ngz_agg *a) {
 int64_t ngz_agg_emit(ngz_agg *a, void *dst, uint64_t cap) {
     if (!a) return NGZ_E_INVALID;
     if (a->poisoned) return fail(a, NGZ_AGG_E_POISONED, "aggregator failed earlier: ngz_agg_reset it");
-    const int64_t cut = cutoff_s(a);
-    if (cut == INT64_MIN) {
+    AGG_HIP(a, hipSetDevice(a->device));
+    bool any = false;
+    if (int r = upload_cutoffs(a, &any)) return r;
+    if (!any) {
         a->out_templates = a->templates;
         a->out_ports = a->ports;
         a->out_domains = a->domains;
+        a->out_peers = a->peers;
         return 0;
     }
-    const int64_t n = take_rows(a, dst, cap, cut, true);
+    const int64_t n = take_rows(a, dst, cap, a->cut, true);
     if (n <= 0) return n;
     a->live -= (uint64_t)n;
     a->tombs += (uint64_t)n;
-    if (a->live + a->tombs > a->slots / 2) {
-        const int rc = rehash(a);
-        if (rc) return rc;
-    }
+    // the n groups are handed out and their slots freed whatever happens next: a failed
+    // rebuild poisons the aggregator (reported by the next call), it does not lose them
+    if (a->live + a->tombs > a->slots / 2) rehash(a);
     return n;
 }
 
@@ -2402,7 +2502,7 @@ int ngz_agg_reset(ngz_agg *a) {
     if (!a) return NGZ_E_INVALID;
     AGG_HIP(a, hipSetDevice(a->device));
     a->poisoned = false;
-    a->current_time = 0;
+    forget_peers(a);
     a->templates.clear();
     a->ports.clear();
     a->domains.clear();
@@ -2427,6 +2527,12 @@ int ngz_agg_sets(ngz_agg *a, uint32_t *templates, uint32_t *n_templates, uint16_
     out(a->out_ports, ports, n_ports, (uint16_t)0xFFFF);
     out(a->out_domains, domains, n_domains, 0xFFFFFFFFu);
     return NGZ_OK;
+}
+
+int ngz_agg_peer(ngz_agg *a, uint32_t index, ngz_peer *out) {
+    if (!a || index >= a->out_peers.size()) return NGZ_E_INVALID;
+    if (out) *out = a->out_peers[index];
+    return (int)a->out_peers.size();
 }
 
 int ngz_agg_last_timing(ngz_agg *a, float *push_ms) {
@@ -2467,4 +2573,6 @@ void agg_out_dicts(const ngz_agg *a, const std::vector<int64_t> **t, const std::
     *p = &a->out_ports;
     *d = &a->out_domains;
 }
+const std::vector<ngz_peer> &agg_out_peers(const ngz_agg *a) { return a->out_peers; }
+uint64_t agg_window_ms(const ngz_agg *a) { return a->window_ms; }
 }  // namespace ngzh

@@ -1256,8 +1256,10 @@ void ngz_ctx_destroy(ngz_ctx *ctx) {
     if (ctx->h_slots) hipHostFree(ctx->h_slots);
     if (ctx->h_proc) hipHostFree(ctx->h_proc);
     if (ctx->h_done) hipHostFree(ctx->h_done);
-    if (ctx->counts_ev) { hipEventSynchronize(ctx->counts_ev); hipEventDestroy(ctx->counts_ev); }
-    if (ctx->h_counts_stage) hipHostFree(ctx->h_counts_stage);
+    for (int i = 0; i < ngz_ctx::COUNTS_RING; ++i) {
+        if (ctx->counts_ev[i]) { hipEventSynchronize(ctx->counts_ev[i]); hipEventDestroy(ctx->counts_ev[i]); }
+        if (ctx->h_counts_stage[i]) hipHostFree(ctx->h_counts_stage[i]);
+    }
     hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -1551,28 +1553,31 @@ int ngz_template_counts_device(ngz_ctx *ctx, int proto, uint64_t *dev_table, uin
     if (!ctx || (proto != 9 && proto != 10) || (cap && !dev_table)) return NGZ_E_INVALID;
     HIPCHK(hipSetDevice(ctx->device));
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : ctx->stream;
-    // the staging buffer is reused: the previous table's copy must have left it
-    if (ctx->counts_ev) HIPCHK(hipEventSynchronize(ctx->counts_ev));
-    else HIPCHK(hipEventCreateWithFlags(&ctx->counts_ev, hipEventDisableTiming));
-    if (cap > ctx->h_counts_cap) {
-        if (ctx->h_counts_stage) hipHostFree(ctx->h_counts_stage);
-        ctx->h_counts_stage = nullptr;
-        ctx->h_counts_cap = 0;
-        HIPCHK(hipHostMalloc((void **)&ctx->h_counts_stage, 16ull * cap, hipHostMallocDefault));
-        ctx->h_counts_cap = cap;
+    // staging table of this call: the ring slot whose last copy is the oldest (queued
+    // COUNTS_RING calls ago, long complete in a per-step exchange: no host wait in practice)
+    const int slot = (int)(ctx->counts_next++ % ngz_ctx::COUNTS_RING);
+    if (ctx->counts_ev[slot]) HIPCHK(hipEventSynchronize(ctx->counts_ev[slot]));
+    else HIPCHK(hipEventCreateWithFlags(&ctx->counts_ev[slot], hipEventDisableTiming));
+    if (cap > ctx->h_counts_cap[slot]) {
+        if (ctx->h_counts_stage[slot]) hipHostFree(ctx->h_counts_stage[slot]);
+        ctx->h_counts_stage[slot] = nullptr;
+        ctx->h_counts_cap[slot] = 0;
+        HIPCHK(hipHostMalloc((void **)&ctx->h_counts_stage[slot], 16ull * cap, hipHostMallocDefault));
+        ctx->h_counts_cap[slot] = cap;
     }
+    uint64_t *stage = ctx->h_counts_stage[slot];
     const int n = ngz_template_counts(ctx, proto, nullptr, nullptr, 0, 0);
     std::vector<uint16_t> ids(std::max(n, 1));
     std::vector<uint64_t> cnt(std::max(n, 1));
     // a table too small resets nothing: the counts carry over to the call that has room for them
     ngz_template_counts(ctx, proto, ids.data(), cnt.data(), (uint32_t)n, reset && (uint32_t)n <= cap);
     for (uint32_t i = 0; i < cap; ++i) {
-        ctx->h_counts_stage[2 * i] = (int)i < n ? ids[i] : 0;
-        ctx->h_counts_stage[2 * i + 1] = (int)i < n ? cnt[i] : 0;
+        stage[2 * i] = (int)i < n ? ids[i] : 0;
+        stage[2 * i + 1] = (int)i < n ? cnt[i] : 0;
     }
     if (cap) {
-        HIPCHK(hipMemcpyAsync(dev_table, ctx->h_counts_stage, 16ull * cap, hipMemcpyHostToDevice, st));
-        HIPCHK(hipEventRecord(ctx->counts_ev, st));
+        HIPCHK(hipMemcpyAsync(dev_table, stage, 16ull * cap, hipMemcpyHostToDevice, st));
+        HIPCHK(hipEventRecord(ctx->counts_ev[slot], st));
     }
     return n;
 }

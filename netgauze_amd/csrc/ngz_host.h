@@ -193,6 +193,8 @@ const std::vector<ngz_agg_field> &agg_keys(const ngz_agg *a);
 const std::vector<ngz_agg_field> &agg_vals(const ngz_agg *a);
 void agg_out_dicts(const ngz_agg *a, const std::vector<int64_t> **t, const std::vector<int64_t> **p,
                    const std::vector<int64_t> **d);
+const std::vector<ngz_peer> &agg_out_peers(const ngz_agg *a);
+uint64_t agg_window_ms(const ngz_agg *a);
 // Host template state of a context (both TemplatesMaps): saved before a
 // speculative batch and restored when its framing guess was wrong (ngz_collector.cpp)
 struct TemplateState {
@@ -291,7 +293,12 @@ struct ngz_ctx {
     uint64_t batch_serial = 0;                      // bumped by every ngz_decode_batch
     std::shared_ptr<ngzh::JsonView> json_view;      // ngz_dgram_json cache of the last batch
     // ngz_template_counts_device: pinned staging of the count table and the event of its last copy
-    uint64_t *h_counts_stage = nullptr;
-    uint32_t h_counts_cap = 0;
-    hipEvent_t counts_ev = nullptr;
+    // ngz_template_counts_device staging: a ring of pinned tables, each reused only after
+    // the copy that last read it has completed (its event), so no call waits on the copy
+    // it or the previous call just queued
+    static constexpr int COUNTS_RING = 4;
+    uint64_t *h_counts_stage[COUNTS_RING] = {};
+    uint32_t h_counts_cap[COUNTS_RING] = {};
+    hipEvent_t counts_ev[COUNTS_RING] = {};
+    uint32_t counts_next = 0;
 };

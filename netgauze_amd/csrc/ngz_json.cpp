@@ -537,6 +537,8 @@ extern "C" int64_t ngz_agg_flowinfo_json(ngz_agg *a, const void *rows, uint64_t 
     for (uint32_t v = 0; v < vals.size(); ++v) ngz_agg_value_info(a, v, &vd[v]);
     const std::vector<int64_t> *dt, *dp, *dd;
     agg_out_dicts(a, &dt, &dp, &dd);
+    const std::vector<ngz_peer> &peers = agg_out_peers(a);
+    const uint64_t win_ms = agg_window_ms(a);
     const int64_t es = floordiv(export_time_ms, 1000);
     const uint32_t ens = (uint32_t)(export_time_ms - es * 1000) * 1000000u;
     std::string o;
@@ -609,6 +611,29 @@ extern "C" int64_t ngz_agg_flowinfo_json(ngz_agg *a, const void *rows, uint64_t 
         sep();
         memcpy(cell, &h.max_collection_ms, 8);
         put_cell(o, 0, 258, NGZ_K_DTMS, 8, cell);  // collectionTimeMilliseconds
+        // the actor's extra fields (actor.rs:222-240): NetGauze windowStart / windowEnd of the
+        // emitted window ((start, start + window_duration), aggregation.rs:163-168), then the
+        // peer IP as originalExporterIPv4Address / originalExporterIPv6Address
+        const int64_t ws_ms = (int64_t)h.window_start * 1000;
+        const int64_t we_ms = ws_ms + (int64_t)win_ms;
+        sep();
+        memcpy(cell, &ws_ms, 8);
+        put_cell(o, 3746, 1, NGZ_K_DTMS, 8, cell);  // NetGauze windowStart
+        sep();
+        memcpy(cell, &we_ms, 8);
+        put_cell(o, 3746, 2, NGZ_K_DTMS, 8, cell);  // NetGauze windowEnd
+        if (h.peer >= peers.size()) return NGZ_E_INVALID;
+        const ngz_peer &pe = peers[h.peer];
+        sep();
+        if (pe.family == 4) {
+            const uint32_t ip = ((uint32_t)pe.addr[0] << 24) | ((uint32_t)pe.addr[1] << 16) |
+                                ((uint32_t)pe.addr[2] << 8) | pe.addr[3];
+            uint8_t c4[4];
+            memcpy(c4, &ip, 4);
+            put_cell(o, 0, 403, NGZ_K_UINT, 4, c4);  // originalExporterIPv4Address
+        } else {
+            put_cell(o, 0, 404, NGZ_K_BYTES, 16, pe.addr);  // originalExporterIPv6Address
+        }
         auto bits_sorted = [](const std::vector<int64_t> &d, const uint64_t *bits, int words) {
             std::vector<int64_t> out;
             for (size_t i = 0; i < d.size() && (int)(i / 64) < words; ++i)

@@ -21,6 +21,7 @@
 // across a compile, so a new template on one exporter's context never stalls
 // another context.  Each entry compiles once; concurrent askers wait on it
 // (ngz_rtc_kernel, synchronous) or poll it (async).
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 
@@ -501,11 +502,18 @@ struct Entry {
 std::mutex g_mu;  // the map only; never held across a compile
 std::map<std::pair<int, std::string>, std::unique_ptr<Entry>> g_cache;
 
-// Background compiles never outlive the runtime they load modules into.
-// They are joined by an atexit handler registered when the first one starts:
-// it runs before every exit handler registered earlier -- those of the host
-// runtime (torch, HIP) included, which would otherwise tear the device state
-// down under a compile still loading its module.
+// Background compiles never outlive the runtime they compile and load modules
+// with.  They are joined by an exit handler, and exit handlers run in the
+// reverse order of their registration -- static destructors of a library
+// included, registered when the library is loaded.  The compiler hiprtc drives
+// (libamd_comgr, LLVM) is not linked in: hiprtc dlopens it on its first
+// program, i.e. on the first worker thread, after a handler registered when
+// that worker started.  Exit then ran comgr's / LLVM's static destructors
+// first, under a compile still inside them, and the join waited on a thread
+// that could not finish (the exit hang of a dist rank in r2).  So the handler
+// is registered once hiprtc and comgr are loaded and initialised
+// (prime_rtc_runtime): every destructor they register comes before it and
+// runs after the join.
 struct Workers {
     std::mutex mu;
     std::vector<std::thread> th;
@@ -522,6 +530,17 @@ struct Workers {
 } g_workers;
 
 void join_workers_at_exit() { g_workers.join_all(); }
+
+// Loads comgr and runs hiprtc's lazy initialisation on the calling thread (one
+// program created and destroyed, nothing compiled), so that their exit-time
+// destructors are registered before join_workers_at_exit.
+void prime_rtc_runtime() {
+    dlopen("libamd_comgr.so.3", RTLD_NOW | RTLD_GLOBAL);  // kept loaded; hiprtc's own dlopen finds it
+    hiprtcProgram prog;
+    if (hiprtcCreateProgram(&prog, "extern \"C\" __global__ void ngz_prime() {}\n", "ngz_prime.hip", 0, nullptr,
+                            nullptr) == HIPRTC_SUCCESS)
+        hiprtcDestroyProgram(&prog);
+}
 
 Entry *entry_for(int device, const std::string &sig) {
     std::lock_guard<std::mutex> lk(g_mu);
@@ -608,7 +627,10 @@ int ngz_rtc_kernel_async(int device, const DevPlan &P, void **fn, void **entry) 
     if (e->state.compare_exchange_strong(st, 1)) {
         std::string src = generate(P);  // the plan's field table is the caller's: read it now
         static std::once_flag once;
-        std::call_once(once, [] { std::atexit(join_workers_at_exit); });
+        std::call_once(once, [] {
+            prime_rtc_runtime();
+            std::atexit(join_workers_at_exit);
+        });
         std::lock_guard<std::mutex> lk(g_workers.mu);
         g_workers.th.emplace_back(build, e, device, std::move(src), sig);
         return 0;

@@ -14,10 +14,13 @@ processed-count exchange that feeds netgauze.flow.decoder.templates.usage
   * one all_gather of that table over RCCL (backend "nccl", xGMI between the
     GPUs of a node); ~2 KB per rank, latency-bound;
   * the table size is agreed without an extra collective: row 0 of every
-    protocol block carries the rank's template count, and the next step reads
-    the previous gather's counts (long complete by then) - if any rank had more
-    templates than the table holds, every rank sees it in the same gathered
-    data and grows the table the same way.  A step whose table was too small
+    protocol block carries the rank's template count, staged through pinned
+    memory (an async, stream-ordered H2D copy); after the gather those counts
+    come back with an async D2H copy into a pinned ring slot, and the next step
+    reads them behind an event that completed before its decode returned (no
+    .item(), no stream synchronisation) - if any rank had more templates than
+    the table holds, every rank sees it in the same gathered data and grows
+    the table the same way.  A step whose table was too small
     resets nothing: its counts are carried into the next exchange, which has
     room for them (totals() reports whether a step fitted).
 
@@ -40,7 +43,12 @@ class CountExchange:
     """All-gather of every rank's per-template processed counts (both protocols).
 
     codec: a netgauze_amd.flow.FlowInfoCodec, or any object with
-    template_counts(proto, reset) (the CPU tests use the oracle's counts)."""
+    template_counts(proto, reset) (the CPU tests use the oracle's counts).
+    stream: the HIP stream the decode runs on and the collective is issued on
+    (NCCL backend); None = torch's current stream of this rank's device, so the
+    count-table copies are stream-ordered before the all_gather that reads them."""
+
+    RING = 4  # pinned header / size-readback slots (each reused RING steps later)
 
     def __init__(self, codec, group=None, cap=DEFAULT_CAP, stream=None):
         import torch.distributed as dist
@@ -48,11 +56,22 @@ class CountExchange:
         self.codec = codec
         self.group = group
         self.cap = cap
-        self.stream = stream
         self.world = dist.get_world_size(group)
         self.on_device = dist.get_backend(group) == "nccl"
         self.device = torch.device("cuda", torch.cuda.current_device()) if self.on_device else torch.device("cpu")
+        if self.on_device and stream is None:
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+        self.stream = stream
         self.gathered = None
+        self._step = 0
+        if self.on_device:
+            # pinned staging: row-0 headers going up, gathered template counts coming back;
+            # an event per slot orders reuse without waiting on the queue
+            self._hdr = [torch.zeros((len(PROTOS), 2), dtype=torch.int64).pin_memory() for _ in range(self.RING)]
+            self._need = [torch.zeros((self.world, len(PROTOS)), dtype=torch.int64).pin_memory()
+                          for _ in range(self.RING)]
+            self._ev = [None] * self.RING
+            self._tstream = torch.cuda.ExternalStream(self.stream, device=self.device) if self.stream else None
         self._alloc()
 
     def _alloc(self):
@@ -60,7 +79,7 @@ class CountExchange:
         self.local = torch.zeros((len(PROTOS), self.cap + 1, 2), dtype=torch.int64, device=self.device)
         self.out = torch.empty((self.world,) + tuple(self.local.shape), dtype=torch.int64, device=self.device)
 
-    def _fill(self, reset):
+    def _fill(self, reset, slot):
         """Local table of this step; returns the template count per protocol."""
         ns = []
         for p, proto in enumerate(PROTOS):
@@ -78,26 +97,58 @@ class CountExchange:
                 if reset and n <= self.cap:
                     self.codec.template_counts(proto, reset=True)
             ns.append(n)
-        hdr = torch.tensor([[n, 0] for n in ns], dtype=torch.int64)
-        self.local[:, 0].copy_(hdr.to(self.device, non_blocking=True) if self.on_device else hdr)
+        if self.on_device:
+            hdr = self._hdr[slot]
+            hdr[:, 0] = torch.tensor(ns, dtype=torch.int64)
+            self.local[:, 0].copy_(hdr, non_blocking=True)  # pinned -> stream-ordered async H2D
+        else:
+            self.local[:, 0] = torch.tensor([[n, 0] for n in ns], dtype=torch.int64)
         return ns
 
+    def _grow(self, need):
+        if need > self.cap:
+            self.cap = need
+            self._alloc()
+
     def step(self, reset=True):
-        """Exchange this step's counts (collective: every rank calls it)."""
-        if self.gathered is not None:
-            # the previous gather is complete (its step's decode has returned since):
-            # grow the table if any rank had more templates than it holds
-            need = int(self.gathered[:, :, 0, 0].max().item())
-            if need > self.cap:
-                self.cap = need
-                self._alloc()
-        self._fill(reset)
-        self.dist.all_gather_into_tensor(self.out.view(-1), self.local.view(-1), group=self.group)
-        self.gathered = self.out
+        """Exchange this step's counts (collective: every rank calls it).  No host
+        synchronisation: the table size is read from a pinned copy of an earlier
+        gather, complete by the time its slot comes round again."""
+        if not self.on_device:
+            if self.gathered is not None:
+                self._grow(int(self.gathered[:, :, 0, 0].max()))
+            self._fill(reset, 0)
+            self.dist.all_gather_into_tensor(self.out.view(-1), self.local.view(-1), group=self.group)
+            self.gathered = self.out
+            return
+        slot = self._step % self.RING
+        ctx = torch.cuda.stream(self._tstream) if self._tstream is not None else _null()
+        with ctx:
+            if self._ev[slot] is not None:
+                # this slot's header copy and size readback were queued RING steps ago
+                self._ev[slot].synchronize()
+            prev = (self._step - 1) % self.RING
+            if self._step > 0:
+                # the previous gather's sizes: queued before this step's decode, which has
+                # returned since, so the event is complete and this is no wait.  Grow the table
+                # if any rank had more templates than it holds; every rank reads the same
+                # gathered sizes, so every rank grows alike
+                self._ev[prev].synchronize()
+                self._grow(int(self._need[prev].max()))
+            self._fill(reset, slot)
+            self.dist.all_gather_into_tensor(self.out.view(-1), self.local.view(-1), group=self.group)
+            self.gathered = self.out
+            self._need[slot].copy_(self.out[:, :, 0, 0], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            self._ev[slot] = ev
+        self._step += 1
 
     def totals(self):
         """{(proto, template id): node-wide count} of the last exchange, and
         whether every rank's templates fitted the table."""
+        if self.on_device and self._step:
+            self._ev[(self._step - 1) % self.RING].synchronize()  # the last gather is complete
         g = self.gathered.cpu()
         fitted = int(g[:, :, 0, 0].max()) <= self.cap
         total = {}
@@ -107,6 +158,14 @@ class CountExchange:
                 for tid, c in g[r, p, 1:1 + n].tolist():
                     total[(proto, tid)] = total.get((proto, tid), 0) + c
         return total, fitted
+
+
+class _null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
 
 
 def gather_template_counts(counts, proto=10, group=None, device="cpu"):

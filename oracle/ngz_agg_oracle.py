@@ -20,15 +20,19 @@ It restates, over the packets of ngz_oracle.FlowInfoCodec:
     TCPHeaderFlags (FIN most significant, iana/src/tcp.rs:41-70) and of sub-registry enums
     (by discriminant: registered value, then Unassigned(x) after every registered variant);
     Ord::min keeps the left argument on equality, Ord::max takes the right one
-  - AggFlowInfo::into_flowinfo_with_extra_fields (aggregator.rs:203-277), sets in ascending
-    order
-Pinned by the reference's own unit tests (aggregator/tests.rs: test_reduce_add_operations
-:244-337, test_explode_ipfix_repeating_ie_fields :755-827, test_explode_ipfix_missing_fields
-:830-893, test_explode_simple_netflowv9_packet :946-1017), restated as vectors in tests/kats_agg.py.
+  - AggFlowInfo::into_flowinfo_with_extra_fields (aggregator.rs:203-277) with the actor's extra
+    fields windowStart, windowEnd, originalExporterIPv4Address / IPv6Address (actor.rs:206-240),
+    sets in ascending order
+One FlowAggregatorOracle is one shard: FlowCacheKey carries the peer IP (aggregator.rs:119-124)
+and the window aggregator keeps its windows and event time per peer IP (aggregation.rs:96-108,
+TimeSeriesData<IpAddr>::get_key, aggregator.rs:109-117).
+Pinned by the reference's own unit tests (aggregator/tests.rs :72-1377 and the window tests of
+analytics/src/aggregation.rs :579-789), restated as vectors in tests/kats_agg.py.
 
 Values are canonical Python values: ints for integer / ipv4 / tcpControlBits / bool / date-time
 seconds, bytes for byte-like fields, str for strings.
 """
+import ipaddress
 import struct
 
 import ngz_oracle as O
@@ -125,8 +129,12 @@ def map_fields(fields):
     return out
 
 
+DEFAULT_PEER = "192.0.2.1"  # the exporter of pushes that name none (netgauze_amd.aggregate)
+
+
 class FlowAggregatorOracle:
-    """One peer's WindowAggregator<IpAddr, UnifiedConfig, FlowAggregator> (aggregation.rs:96-186).
+    """One shard's WindowAggregator<IpAddr, UnifiedConfig, FlowAggregator> (aggregation.rs:96-186):
+    windows and event time per peer IP.
 
     fields: [(pen, ie_id, index, op)] in transform order; keys and aggregated fields keep
     their relative order (config.rs:252-335)."""
@@ -135,11 +143,11 @@ class FlowAggregatorOracle:
         self.keys = [(pen, ie, idx) for pen, ie, idx, op in fields if op == OP_KEY]
         self.vals = [((pen, ie, idx), op) for pen, ie, idx, op in fields if op != OP_KEY]
         self.window_s, self.lateness_s = window_s, lateness_s
-        self.current_time = None
-        self.groups = {}   # (window_start, flow_type, key tuple) -> record dict
+        self.current_time = {}   # peer IP -> event time
+        self.groups = {}   # (peer IP, window_start, flow_type, key tuple) -> record dict
         self.late = 0
         self.closed = []   # groups of the windows the cutoff closed, not yet taken by emit()
-        self._cutoff = None
+        self._cutoff = {}
 
     def explode(self, pkt, peer_port, collection_ms):
         """aggregator.rs:286-354: one item per data record (non-scope fields)."""
@@ -157,32 +165,37 @@ class FlowAggregatorOracle:
                                            min_export=ts, max_export=ts, min_coll=collection_ms,
                                            max_coll=collection_ms, max_sysup=sysup, vals=vals, count=1)
 
-    def push_packet(self, pkt, peer_port, collection_ms):
+    def push_packet(self, pkt, peer_port, collection_ms, peer_ip=DEFAULT_PEER):
         for flow_type, ts, key, rec in self.explode(pkt, peer_port, collection_ms):
-            # WindowAggregator::process_item (aggregation.rs:135-150), times in seconds (lateness in s)
-            if self.current_time is None:
-                self.current_time = ts
-            if ts < self.current_time - self.lateness_s:
-                self.late += 1
-                continue
-            self.current_time = max(self.current_time, ts)
-            g = (ts - ts % 60, flow_type, key)
-            cur = self.groups.get(g)
-            if cur is None:
-                self.groups[g] = rec
-            else:
-                self.reduce(cur, rec)
-            self._close_windows()
+            self.process_item(peer_ip, flow_type, ts, key, rec)
 
-    def _close_windows(self):
-        """aggregation.rs:154-160: windows starting at or before
-        get_window_start(current_time - lateness) - window_duration leave the active set."""
-        t = self.current_time - self.lateness_s
+    def process_item(self, peer_ip, flow_type, ts, key, rec):
+        """WindowAggregator::process_item (aggregation.rs:124-172), times in seconds (lateness
+        in s): the item's key is its peer IP (aggregator.rs:109-117)."""
+        ct = self.current_time.setdefault(peer_ip, ts)
+        if ts < ct - self.lateness_s:
+            self.late += 1
+            return False
+        self.current_time[peer_ip] = ct = max(ct, ts)
+        g = (peer_ip, ts - ts % 60, flow_type, key)
+        cur = self.groups.get(g)
+        if cur is None:
+            self.groups[g] = rec
+        else:
+            self.reduce(cur, rec)
+        self._close_windows(peer_ip)
+        return True
+
+    def _close_windows(self, peer_ip):
+        """aggregation.rs:154-160: the peer's windows starting at or before
+        get_window_start(current_time - lateness) - window_duration leave its active set."""
+        t = self.current_time[peer_ip] - self.lateness_s
         cutoff = t - t % 60 - self.window_s
-        if self._cutoff is not None and cutoff <= self._cutoff:
+        last = self._cutoff.get(peer_ip)
+        if last is not None and cutoff <= last:
             return
-        self._cutoff = cutoff
-        for g in [g for g in self.groups if g[0] <= cutoff]:
+        self._cutoff[peer_ip] = cutoff
+        for g in [g for g in self.groups if g[0] == peer_ip and g[1] <= cutoff]:
             self.closed.append(self._out(g, self.groups.pop(g)))
 
     def reduce(self, lhs, rhs):
@@ -205,8 +218,8 @@ class FlowAggregatorOracle:
 
     @staticmethod
     def _out(g, r):
-        win, ft, key = g
-        return dict(window_start=win, flow_type=ft, key=key,
+        peer, win, ft, key = g
+        return dict(peer=peer, window_start=win, flow_type=ft, key=key,
                     vals=tuple(None if v is None else v[1] for v in r["vals"]),
                     record_count=r["count"], min_export=r["min_export"], max_export=r["max_export"],
                     max_sysup=r["max_sysup"], min_coll=r["min_coll"], max_coll=r["max_coll"],
@@ -221,13 +234,19 @@ class FlowAggregatorOracle:
         """WindowAggregator::flush: every active group, then forget the event time."""
         out = [self._out(g, r) for g, r in self.groups.items()]
         self.groups = {}
-        self.current_time = None
-        self._cutoff = None
+        self.current_time = {}
+        self._cutoff = {}
         return out
 
     def flowinfo_json(self, group, shard_id=0, seq=0, export_time_ms=0):
         """AggFlowInfo::into_flowinfo_with_extra_fields (aggregator.rs:203-277) of one output
-        group, serde JSON text; the peer port / domain / template sets in ascending order."""
+        group with the actor's extra fields (actor.rs:222-240): windowStart = the window start,
+        windowEnd = start + window duration, the peer IP as originalExporterIPv4Address /
+        IPv6Address; serde JSON text; the peer port / domain / template sets in ascending order."""
+        return O.dumps(self.flowinfo(group, shard_id, seq, export_time_ms))
+
+    def flowinfo(self, group, shard_id=0, seq=0, export_time_ms=0):
+        """The FlowInfo of flowinfo_json as serde's JSON value (dicts and lists)."""
         reg = O.REGISTRY
         fields = []
         for (p, i, _x), v in zip(self.keys, group["key"]):
@@ -243,6 +262,12 @@ class FlowAggregatorOracle:
                    O.Field(reg.lookup(0, 264), O.DateTime(group["min_export"], 0)),
                    O.Field(reg.lookup(0, 260), O.DateTime(group["max_export"], 0)),
                    O.Field(reg.lookup(0, 258), O.DateTime(ms // 1000, (ms % 1000) * 1_000_000))]
+        ws, we = group["window_start"], group["window_start"] * 1000 + int(round(self.window_s * 1000))
+        fields += [O.Field(reg.lookup(3746, 1), O.DateTime(ws, 0)),
+                   O.Field(reg.lookup(3746, 2), O.DateTime(we // 1000, (we % 1000) * 1_000_000))]
+        ip = ipaddress.ip_address(group["peer"])
+        fields.append(O.Field(reg.lookup(0, 403), ("v4", int(ip))) if ip.version == 4
+                      else O.Field(reg.lookup(0, 404), ("v6", int(ip))))
         fields += [O.Field(reg.lookup(3746, 4), p) for p in sorted(group["ports"])]
         fields += [O.Field(reg.lookup(0, 405), d) for d in sorted(group["domains"])]
         fields += [O.Field(reg.lookup(3746, 3), t) for t in sorted(t for _ft, t in group["templates"])]
@@ -256,7 +281,7 @@ class FlowAggregatorOracle:
         else:
             pkt = {"NetFlowV9": {"version": 9, "sys_up_time": group["max_sysup"], "unix_time": et,
                                  "sequence_number": seq, "source_id": shard_id, "sets": sets}}
-        return O.dumps(pkt)
+        return pkt
 
 
 def to_field_value(ie, v):
@@ -279,11 +304,13 @@ def to_field_value(ie, v):
     return v
 
 
-def aggregate_datagrams(fields, datagrams, peer_port=4739, collection_ms=0, window_s=60, lateness_s=10):
+def aggregate_datagrams(fields, datagrams, peer_port=4739, collection_ms=0, window_s=60, lateness_s=10,
+                        peer_ip=DEFAULT_PEER, agg=None, codec=None):
     """Decode `datagrams` in order with one codec (FlowInfoCodec::decode per datagram) and
-    aggregate every decoded packet; failed datagrams yield nothing."""
-    codec = O.FlowInfoCodec()
-    agg = FlowAggregatorOracle(fields, window_s, lateness_s)
+    aggregate every decoded packet as sent by (peer_ip, peer_port); failed datagrams yield
+    nothing.  agg / codec: continue an aggregator (a shard) / a peer's codec."""
+    codec = codec if codec is not None else O.FlowInfoCodec()
+    agg = agg if agg is not None else FlowAggregatorOracle(fields, window_s, lateness_s)
     for d in datagrams:
         buf = bytearray(d)
         try:
@@ -291,5 +318,5 @@ def aggregate_datagrams(fields, datagrams, peer_port=4739, collection_ms=0, wind
         except O.ParseFail:
             continue
         if pkt is not None:
-            agg.push_packet(pkt, peer_port, collection_ms)
+            agg.push_packet(pkt, peer_port, collection_ms, peer_ip)
     return agg

@@ -40,7 +40,7 @@ def test_agg_config_validation_without_device():
     def create(fields, window=60000, lateness=10000):
         arr = (A * max(len(fields), 1))(*[A(p, i, x, o) for p, i, x, o in fields])
         h = ctypes.c_void_p()
-        return lib.ngz_agg_create(0, arr, len(fields), window, lateness, 1024, ctypes.byref(h))
+        return lib.ngz_agg_create(0, arr, len(fields), window, lateness, 1024, 0, ctypes.byref(h))
     ok = [(0, 8, 0, _lib.NGZ_AGG_KEY), (0, 1, 0, _lib.NGZ_AGG_ADD)]
     assert create(ok, window=0) == -1
     assert create(ok, window=1000, lateness=2000) == -1

@@ -61,7 +61,7 @@ def _exact(v):
 def norm(groups):
     out = {}
     for g in groups:
-        k = (g["window_start"], g["flow_type"], tuple(_exact(x) for x in g["key"]))
+        k = (g["peer"], g["window_start"], g["flow_type"], tuple(_exact(x) for x in g["key"]))
         assert k not in out, k
         out[k] = (tuple(_exact(v) for v in g["vals"]), g["record_count"], g["min_export"], g["max_export"],
                   g["max_sysup"],
@@ -574,3 +574,130 @@ def test_owner_path_equals_atomic_5tuple(dev, monkeypatch):
     assert len(rows["own"]) > n // 2
     assert np.array_equal(rows["own"], rows["atomic"])
     codec.close()
+
+
+def run_device_scenario(sc):
+    """A kats_agg scenario through the device: one codec per peer address (a peer's
+    FlowInfoCodec), one aggregator for the shard."""
+    from netgauze_amd.aggregate import FlowAggregator
+    from netgauze_amd.flow import FlowInfoCodec
+    agg = FlowAggregator(sc["fields"], window_s=sc["window_s"], lateness_s=sc["lateness_s"], capacity=1024)
+    codecs, emits, late = {}, [], 0
+    for ip, port, coll, dgrams in sc["pushes"]:
+        codec = codecs.setdefault((ip, port), FlowInfoCodec())
+        late += agg.push(codec.decode_datagrams(dgrams), port, coll, peer_ip=ip)
+        hdr, raw = agg.emit_raw()
+        emits.append((agg.render(hdr, raw), raw))
+    hdr, raw = agg.flush_raw()
+    return agg, emits, (agg.render(hdr, raw), raw), late
+
+
+def _sorted(groups):
+    return sorted(groups, key=lambda g: repr((g["peer"], g["window_start"], g["flow_type"], g["key"])))
+
+
+@pytest.mark.parametrize("sc", K.SCENARIOS + K.WINDOW_SCENARIOS, ids=lambda s: s["name"])
+def test_reference_scenarios(dev, sc):
+    """aggregator/tests.rs (:72-1377) and the analytics window tests (aggregation.rs:498-788) as
+    wire-level scenarios on the device: the expected groups of every push's closed windows and of
+    the flush, the late records, and each group's FlowInfo text equal to the oracle's."""
+    import test_oracle_agg as T
+    agg, emits, (flushed, raw), late = run_device_scenario(sc)
+    o_agg, o_emits, o_flushed = T.run_oracle_scenario(sc)
+    assert late == sc["late"] == o_agg.late
+    assert _sorted(flushed) == _sorted(sc["flush"]) == _sorted(o_flushed)
+    if sc["emits"] is not None:
+        for (got, _raw), exp in zip(emits, sc["emits"]):
+            assert _sorted(got) == _sorted(exp)
+    # the FlowInfo of every flushed group: the oracle's text, windowStart/windowEnd/exporter IP included
+    lines = agg.flowinfo_json(raw, shard_id=2, seq0=7, export_time_ms=1_751_450_400_000)
+    for i, (g, line) in enumerate(zip(flushed, lines)):
+        assert line == o_agg.flowinfo_json(g, shard_id=2, seq=7 + i, export_time_ms=1_751_450_400_000)
+
+
+@pytest.mark.parametrize("flow_type", [10, 9])
+def test_into_flowinfo_with_extra_fields_kat(dev, flow_type):
+    """test_ipfix / test_netflowv9_into_flowinfo_with_extra_fields (tests.rs:339-586) on the device:
+    the record's fields sorted (HashSet order is unspecified) equal the test's expected fields plus
+    the exporter IP the actor appends (actor.rs:222-225); sequence number 42, shard 5 as the
+    observation domain / source id, NetFlow v9 sys-up time 5000."""
+    import json
+    fields, pushes = K.flowinfo_scenario(flow_type)
+    sc = dict(fields=fields, pushes=pushes, window_s=60, lateness_s=10)
+    agg, _emits, (flushed, raw), _late = run_device_scenario(sc)
+    assert len(flushed) == 1
+    (line,) = agg.flowinfo_json(raw, shard_id=5, seq0=42, export_time_ms=K.T_JUL2_10 * 1000)
+    body = json.loads(line)["IPFIX" if flow_type == 10 else "NetFlowV9"]
+    assert body["sequence_number"] == 42
+    assert body["observation_domain_id" if flow_type == 10 else "source_id"] == 5
+    if flow_type == 9:
+        assert body["sys_up_time"] == 5000
+    (st,) = body["sets"]
+    (rec,) = st["Data"]["records"]
+    assert st["Data"]["id"] == 65535 and rec["scope_fields"] == []
+    key = lambda f: json.dumps(f, sort_keys=True)  # noqa: E731
+    assert sorted(rec["fields"], key=key) == sorted(K.FLOWINFO_EXPECTED_FIELDS, key=key)
+
+
+def test_thousand_peers_one_aggregator(dev):
+    """One aggregator serves a shard's 1 000 exporter peers (IPv4 and IPv6): groups are keyed by
+    peer IP, and each peer's event time closes only its own windows (aggregation.rs:96-172).
+    Peers export T20 messages at their own clock offsets; after every round of pushes the
+    emitted windows equal the oracle's, and so does the final flush."""
+    from netgauze_amd import synth
+    from netgauze_amd.aggregate import FlowAggregator
+    from netgauze_amd.flow import FlowInfoCodec
+    import ngz_oracle as O
+    fields = [(0, 4, 0, OK), (0, 61, 0, OK)] + T20_AGG
+    n_peers, rounds, per_msg = 1000, 3, 20
+    rec = synth.t20_records(n_peers * rounds * per_msg, first=0)
+    buf, offs, lens = synth.ipfix_data_stream(rec, 64, rec_per_msg=per_msg)
+    b = bytes(buf.numpy())
+    msgs = [bytearray(b[o:o + ln]) for o, ln in zip(offs.tolist(), lens.tolist())]
+    peers = ["10.%d.%d.1" % (i // 250, i % 250) if i % 3 else "2001:db8::%x" % (i + 1) for i in range(n_peers)]
+    agg = FlowAggregator(fields, capacity=1 << 16, lateness_s=10)
+    o = A.FlowAggregatorOracle(fields, 60, 10)
+    codecs, ocodecs = {}, {}
+    tm = synth.template_message()
+    emitted = 0
+    for r in range(rounds):
+        for i, ip in enumerate(peers):
+            m = msgs[r * n_peers + i]
+            # peer i's clock: offset 7*i s; rounds 50 s apart, so every peer closes windows at its own pace
+            m[4:8] = struct.pack(">I", 1_700_000_000 + 7 * i + 50 * r)
+            dg = ([tm] if r == 0 else []) + [bytes(m)]
+            codec = codecs.setdefault(ip, FlowInfoCodec())
+            agg.push(codec.decode_datagrams(dg), 4739 + i % 5, 1_000 * r, peer_ip=ip)
+            oc = ocodecs.setdefault(ip, O.FlowInfoCodec())
+            A.aggregate_datagrams(fields, dg, 4739 + i % 5, 1_000 * r, peer_ip=ip, agg=o, codec=oc)
+        got, ref = agg.emit(), o.emit()
+        same_groups(got, ref)
+        emitted += len(got)
+    assert emitted > 0 and len({g["peer"] for g in ref}) > 1
+    same_groups(agg.flush(), o.flush())
+
+
+def test_tombstones_do_not_fill_the_table(dev):
+    """windows emitted push after push leave tombstones; pushes keep succeeding while
+    the live groups stay within the capacity (the table is rebuilt before a push when tombstones
+    and the push's new groups would crowd it)."""
+    from netgauze_amd.aggregate import FlowAggregator
+    from netgauze_amd.flow import FlowInfoCodec
+    import ngz_oracle as O
+    fields = [(0, 8, 0, OK), (0, 12, 0, OK), (0, 1, 0, ADD)]
+    agg = FlowAggregator(fields, capacity=2000, lateness_s=0)
+    o = A.FlowAggregatorOracle(fields, 60, 0)
+    codec, oc = FlowInfoCodec(), O.FlowInfoCodec()
+    tpl = [(8, 4), (12, 4), (1, 8)]
+    out = 0
+    for step in range(24):
+        recs = [struct.pack(">IIQ", step * 1000 + j, j, j + 1) for j in range(900)]
+        d = [ipfix_msg(([tset(256, tpl)] if step == 0 else []) + [dset(256, recs[i:i + 300])],
+                       1_700_000_000 + 60 * step) for i in range(0, 900, 300)]
+        agg.push(codec.decode_datagrams(d))
+        A.aggregate_datagrams(fields, d, agg=o, codec=oc)
+        got = agg.emit()
+        same_groups(got, o.emit())
+        out += len(got)
+    assert out == 23 * 900
+    same_groups(agg.flush(), o.flush())

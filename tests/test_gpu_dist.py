@@ -51,9 +51,9 @@ def _worker(rank, world, port, n, q):
         from netgauze_amd.flow import FlowInfoCodec
         templates, data = _stream(n)
         first, last = ndist.shard_range(len(data), rank, world)
-        # compiles on the decode thread: no background compile is still running when the rank
-        # exits (a rank once hung at exit on some boxes with one in flight)
-        codec = FlowInfoCodec(0, specialize=True)
+        # library default: template kernels compiled in the background; a rank may exit with a
+        # compile in flight (ngz_rtc.cpp: the exit join runs before hiprtc's / comgr's teardown)
+        codec = FlowInfoCodec(0)
         codec.decode_datagrams(templates)
         batch = codec.decode_datagrams(data[first:last])
         ok = int((batch.dgram_headers()["status"] == 0).sum())
@@ -104,3 +104,86 @@ def test_two_ranks_decode_shards_and_exchange_counts():
         assert r[6] == {t: 0 for t in oc.ipfix_templates}   # reset after the exchange
         assert r[7] == {t: 0 for t in oc.netflow_templates}
     assert {k[0] for k in exp} == {9, 10}
+
+
+def _nccl_worker(port, n_steps, q):
+    """World-size-1 RCCL ("nccl") group: CountExchange(codec) with its default arguments (stream =
+    torch's current stream), the device count table (ngz_template_counts_device) and the RCCL
+    all_gather.  17 IPFIX templates + 1 NetFlow v9 template outgrow the 16-row default table:
+    the first exchange does not fit (its counts carry over), the next grows the table."""
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        from netgauze_amd import dist as ndist
+        from netgauze_amd import synth
+        from netgauze_amd.flow import FlowInfoCodec
+        codec = FlowInfoCodec(0, specialize=True)
+        ex = ndist.CountExchange(codec)
+        assert ex.on_device and ex.stream == torch.cuda.current_stream().cuda_stream
+        dg = synth.cfg4_datagrams(2000, seed=synth.SEED_CFG4 + 9)
+        buf, offs, lens, _ = synth.mixed_stream(4000, templates=synth.CFG5_TEMPLATES, seed=synth.SEED_CFG5 + 9)
+        b = bytes(buf.numpy())
+        mixed = [b[o:o + ln] for o, ln in zip(offs.tolist(), lens.tolist())]
+        codec.decode_datagrams(dg[:2] + [synth.templates_message(synth.CFG5_TEMPLATES)])
+        steps = []
+        for s in range(n_steps):
+            data = dg[2:] if s % 2 == 0 else mixed
+            codec.decode_datagrams(data)
+            ex.step(reset=True)
+            total, fitted = ex.totals()
+            steps.append((s, fitted, ex.cap, total))
+        q.put(("ok", steps))
+    except Exception as e:
+        q.put(("error", repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_count_exchange_rccl_defaults_and_growth():
+    """the NCCL (RCCL) path of CountExchange with default arguments, against the
+    oracle's processed counts, across a table growth."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import parity
+    from netgauze_amd import synth
+    dg = synth.cfg4_datagrams(2000, seed=synth.SEED_CFG4 + 9)
+    buf, offs, lens, _ = synth.mixed_stream(4000, templates=synth.CFG5_TEMPLATES, seed=synth.SEED_CFG5 + 9)
+    b = bytes(buf.numpy())
+    mixed = [b[o:o + ln] for o, ln in zip(offs.tolist(), lens.tolist())]
+    templates = dg[:2] + [synth.templates_message(synth.CFG5_TEMPLATES)]
+
+    def oracle_counts(data):
+        _, oc = parity.oracle_datagrams(templates + data)
+        c = {(10, t): v.processed_count for t, v in oc.ipfix_templates.items()}
+        c.update({(9, t): v.processed_count for t, v in oc.netflow_templates.items()})
+        return c
+
+    c_cfg4, c_mixed = oracle_counts(dg[2:]), oracle_counts(mixed)
+    keys = set(c_cfg4) | set(c_mixed)
+    assert len([k for k in keys if k[0] == 10]) > 16  # the 16-row default table must grow
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_worker, args=(_free_port(), 3, q))
+    p.start()
+    status, steps = q.get(timeout=240)
+    p.join(timeout=120)
+    assert status == "ok", steps
+    assert p.exitcode == 0
+    # step 0 (config-4 stream): 17 IPFIX templates > 16 rows -> not fitted, nothing reset
+    s0, fit0, cap0, _ = steps[0]
+    assert not fit0 and cap0 == 16
+    # step 1 (config-5 stream): the table grew; the carried config-4 counts go out with this step's
+    s1, fit1, cap1, tot1 = steps[1]
+    assert fit1 and cap1 >= 17
+    exp1 = {k: c_cfg4.get(k, 0) + c_mixed.get(k, 0) for k in keys}
+    assert tot1 == exp1, (tot1, exp1)
+    # step 2 (config-4 again): reset after step 1, so exactly this step's counts
+    s2, fit2, _, tot2 = steps[2]
+    assert fit2 and tot2 == {k: c_cfg4.get(k, 0) for k in keys}

@@ -89,3 +89,37 @@ def test_compile_is_off_the_decode_path():
     o2, _ = parity.oracle_datagrams(dataA, oc)
     assert parity.check_batch(b2, o2)["records"] == 20 * 30
     assert int((b2.dgram_headers()["status"] == L.NGZ_DG_OK).sum()) == 20
+
+
+_EXIT_CHILD = r"""
+import os, struct, sys
+sys.path.insert(0, os.environ["NGZ_ROOT"])
+sys.path.insert(0, os.path.join(os.environ["NGZ_ROOT"], "tests"))
+import test_gpu_rtc as T
+from netgauze_amd import _lib as L
+from netgauze_amd.flow import FlowInfoCodec
+c = FlowInfoCodec(0)  # library default: per-template kernels compiled in the background
+dg = []
+for k in range(4):    # four fresh layouts: four compiles in flight
+    tm, rl = T._fresh_layout(900 + k)
+    dg += [tm] + T._data(900 + k, rl, 2, 20, k)
+b = c.decode_datagrams(dg)
+assert b.n_records == 4 * 2 * 20, b.n_records
+ready = [b.slot_kernel(s.index) for s in b.slots]
+print("EXITING", ready, flush=True)
+sys.exit(0)       # while the background compiles run
+"""
+
+
+def test_exit_with_background_compiles_in_flight():
+    """A process that exits right after a decode started background compiles exits cleanly
+    (r2: a rank hung at exit with one in flight; root cause in ngz_rtc.cpp prime_rtc_runtime)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, NGZ_ROOT=root)
+    p = subprocess.run([sys.executable, "-c", _EXIT_CHILD], env=env, capture_output=True, text=True, timeout=90)
+    assert p.returncode == 0, (p.returncode, p.stdout[-2000:], p.stderr[-2000:])
+    assert "EXITING" in p.stdout

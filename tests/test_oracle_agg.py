@@ -5,6 +5,8 @@ import os
 import struct
 import sys
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -104,3 +106,70 @@ def test_float_and_enum_orders():
     tcp = O.REGISTRY.lookup(0, 6)
     assert A.reduce_value(tcp, A.OP_MAX, 0x01, 0x80) == 0x01  # FIN (bit 0) outranks CWR (bit 7)
     assert A.reduce_value(tcp, A.OP_MIN, 0x02, 0x01) == 0x02  # {SYN} < {FIN}
+
+
+def run_oracle_scenario(sc):
+    """Pushes of a kats_agg scenario through the oracle (one codec per peer address, one shard)."""
+    import ngz_oracle as O
+    agg = A.FlowAggregatorOracle(sc["fields"], sc["window_s"], sc["lateness_s"])
+    codecs, emits = {}, []
+    for ip, port, coll, dgrams in sc["pushes"]:
+        codec = codecs.setdefault((ip, port), O.FlowInfoCodec())
+        A.aggregate_datagrams(sc["fields"], dgrams, port, coll, peer_ip=ip, agg=agg, codec=codec)
+        emits.append(agg.emit())
+    return agg, emits, agg.flush()
+
+
+def _sorted(groups):
+    return sorted(groups, key=lambda g: repr((g["peer"], g["window_start"], g["flow_type"], g["key"])))
+
+
+@pytest.mark.parametrize("sc", K.SCENARIOS + K.WINDOW_SCENARIOS, ids=lambda s: s["name"])
+def test_reference_scenarios(sc):
+    """aggregator/tests.rs and analytics aggregation.rs tests, as wire-level scenarios: the
+    expected cache entries / windows, the late items, and the windows each push closes."""
+    agg, emits, flushed = run_oracle_scenario(sc)
+    assert agg.late == sc["late"]
+    assert _sorted(flushed) == _sorted(sc["flush"])
+    if sc["emits"] is not None:
+        assert len(emits) == len(sc["emits"])
+        for got, exp in zip(emits, sc["emits"]):
+            assert _sorted(got) == _sorted(exp)
+
+
+def test_reduce_full_reference_vector():
+    """test_reduce_add_operations (tests.rs:243-337) in full: sets, time bounds, sys-up time,
+    count and the aggregated values of FlowCacheRecord::reduce."""
+    import ngz_oracle as O
+    o = A.FlowAggregatorOracle(K.REDUCE_FIELDS)
+    ies = [O.REGISTRY.lookup(0, ie) for _p, ie, _i, _op in K.REDUCE_FIELDS]
+    lhs = dict(K.REDUCE_FULL_R1, vals=[None if v is None else (ie, v) for ie, v in zip(ies, K.REDUCE_R1)])
+    rhs = dict(K.REDUCE_FULL_R2, vals=[None if v is None else (ie, v) for ie, v in zip(ies, K.REDUCE_R2)])
+    lhs = {k: (set(v) if isinstance(v, set) else v) for k, v in lhs.items()}
+    o.reduce(lhs, rhs)
+    for k, v in K.REDUCE_FULL_EXPECTED.items():
+        assert lhs[k] == v, k
+    assert tuple(None if v is None else v[1] for v in lhs["vals"]) == K.REDUCE_EXPECTED
+
+
+@pytest.mark.parametrize("flow_type", [10, 9])
+def test_into_flowinfo_with_extra_fields(flow_type):
+    """test_ipfix / test_netflowv9_into_flowinfo_with_extra_fields (tests.rs:339-586): the fields of
+    the one record, compared sorted (the test sorts: HashSet order is unspecified), plus the
+    exporter IP the actor appends; header sequence number / observation domain (shard) /
+    sys-up time."""
+    import json
+    fields, pushes = K.flowinfo_scenario(flow_type)
+    sc = dict(fields=fields, pushes=pushes, window_s=60, lateness_s=10)
+    _agg, _emits, (g,) = run_oracle_scenario(sc)
+    pkt = json.loads(_agg.flowinfo_json(g, shard_id=5, seq=42, export_time_ms=K.T_JUL2_10 * 1000))
+    body = pkt["IPFIX" if flow_type == 10 else "NetFlowV9"]
+    assert body["sequence_number"] == 42
+    assert body["observation_domain_id" if flow_type == 10 else "source_id"] == 5
+    if flow_type == 9:
+        assert body["sys_up_time"] == 5000
+    (st,) = body["sets"]
+    (rec,) = st["Data"]["records"]
+    assert st["Data"]["id"] == 65535 and rec["scope_fields"] == []
+    key = lambda f: json.dumps(f, sort_keys=True)  # noqa: E731
+    assert sorted(rec["fields"], key=key) == sorted(K.FLOWINFO_EXPECTED_FIELDS, key=key)

@@ -9,8 +9,8 @@
   * per-launch HBM traffic of the decode kernel from the separate --pmc passes
     (FETCH_SIZE doubled on gfx950 per MI355X_MICROARCH.md §HBM; both KiB).
 
-Writes <dir>/traffic.json stamped with the product source hash
-(netgauze_amd/buildinfo.py) and, when GIT_SHA is set, the commit.
+Writes <dir>/traffic.json stamped with the product source hash and the decode
+sources' hash (netgauze_amd/buildinfo.py) and, when GIT_SHA is set, the commit.
 usage: summarize_profile.py <dir> [decode-kernel-substring ...]
 """
 import csv
@@ -86,7 +86,8 @@ if "FETCH_SIZE" in out and "WRITE_SIZE" in out:
                "workload": bench["config"]["workload"] if bench else None,
                "alg_bytes_per_launch": alg, "traffic_over_alg": (fetch + write) / alg if alg else None,
                "timed_kernel_ms_trace": timed, "bench_kernel_ms": bench["roofline"]["kernel_ms"] if bench else None,
-               "source_hash": buildinfo.source_hash(), "git_sha": os.environ.get("GIT_SHA"),
+               "source_hash": buildinfo.source_hash(), "decode_source_hash": buildinfo.decode_source_hash(),
+               "git_sha": os.environ.get("GIT_SHA"),
                "kernel": "decode (every decode dispatch of one step)",
                "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes; FETCH_SIZE x2 (gfx950 "
                          "wide-read correction, MI355X_MICROARCH.md HBM)"},
