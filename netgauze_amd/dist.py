@@ -80,8 +80,11 @@ class CountExchange:
         self.out = torch.empty((self.world,) + tuple(self.local.shape), dtype=torch.int64, device=self.device)
 
     def _fill(self, reset, slot):
-        """Local table of this step; returns the template count per protocol."""
+        """Local table of this step; returns the template count per protocol.  The counts
+        are reset only when every protocol's templates fit the table: a step that does not
+        fit resets nothing, and all of its counts go out again with the next exchange."""
         ns = []
+        reset = reset and all(len(self.codec.template_counts(proto, reset=False)) <= self.cap for proto in PROTOS)
         for p, proto in enumerate(PROTOS):
             if self.on_device:
                 row1 = self.local[p, 1:]
@@ -94,7 +97,7 @@ class CountExchange:
                 if counts:
                     kept = counts[:self.cap]
                     self.local[p, 1:1 + len(kept)] = torch.tensor(kept, dtype=torch.int64)
-                if reset and n <= self.cap:
+                if reset:
                     self.codec.template_counts(proto, reset=True)
             ns.append(n)
         if self.on_device:

@@ -236,12 +236,15 @@ def _u64s(n, seed, salt):
     return splitmix64(torch.arange(n, dtype=torch.int64) * 16 + salt, seed).numpy().view("uint64")
 
 
-def vlen_records(n, fields=V900, seed=SEED_CFG4, max_len=40):
+def vlen_records(n, fields=V900, seed=SEED_CFG4, max_len=40, spans=False):
     """n IPFIX records of a template with variable-length fields (numpy, host).
     Variable-length values are printable ASCII of 0..max_len bytes (valid
     UTF-8), written with the 1-byte length prefix, every 97th record's first
     variable field with the 255 + 3-byte escape.  dateTimeMilliseconds stays in
-    chrono's range.  Returns (flat uint8 bytes, record lengths int64)."""
+    chrono's range.  Returns (flat uint8 bytes, record lengths int64), and with
+    spans=True also every field's value span per record: [(start in flat
+    int64[n], length int64[n])] in template order (the generator's ground
+    truth for full-size checks)."""
     import numpy as np
     lens = []
     parts = []
@@ -262,9 +265,11 @@ def vlen_records(n, fields=V900, seed=SEED_CFG4, max_len=40):
     starts[1:] = np.cumsum(rec_len)
     out = np.zeros(int(starts[-1]), dtype=np.uint8)
     cur = starts[:-1].copy()
+    span = []
     for kind, a, b, k in parts:
         if kind == "f":
             ln, ie = a, b
+            span.append((cur.copy(), np.full(n, ln, dtype=np.int64)))
             if ie in (152, 153) and ln == 8:
                 v = 1_700_000_000_000 + (np.arange(n, dtype=np.int64) * 7919) % 1_000_000_000
             else:
@@ -281,6 +286,7 @@ def vlen_records(n, fields=V900, seed=SEED_CFG4, max_len=40):
             out[cur[e] + 2] = (L[e] >> 8).astype(np.uint8)
             out[cur[e] + 3] = (L[e] & 0xFF).astype(np.uint8)
             cur += np.where(esc, 4, 1)
+            span.append((cur.copy(), L.copy()))
             # printable bytes 'a'..'z' for every value byte
             total = int(L.sum())
             if total:
@@ -288,10 +294,10 @@ def vlen_records(n, fields=V900, seed=SEED_CFG4, max_len=40):
                 within = np.arange(total) - np.repeat(np.cumsum(L) - L, L)
                 out[rep + within] = (97 + (rep + within) % 26).astype(np.uint8)
             cur += L
-    return out, rec_len
+    return (out, rec_len, span) if spans else (out, rec_len)
 
 
-def _pack_ipfix(flat, rec_len, tid, max_msg=65000, export_time0=1_700_000_000, domain=1):
+def _pack_ipfix(flat, rec_len, tid, max_msg=65000, export_time0=1_700_000_000, domain=1, firsts=None):
     import numpy as np
     starts = np.zeros(len(rec_len) + 1, dtype=np.int64)
     starts[1:] = np.cumsum(rec_len)
@@ -302,6 +308,8 @@ def _pack_ipfix(flat, rec_len, tid, max_msg=65000, export_time0=1_700_000_000, d
         j = int(np.searchsorted(starts, starts[i] + max_msg - 20, side="right")) - 1
         j = max(j, i + 1)
         body = flat[starts[i]:starts[j]].tobytes()
+        if firsts is not None:
+            firsts.append(i)
         msgs.append(struct.pack(">HHIIIHH", 10, 20 + len(body), export_time0 + len(msgs), i, domain, tid,
                                 4 + len(body)) + body)
         i = j
@@ -328,26 +336,36 @@ def _pack_nfv9(recs, rec_len, tid, per_msg=10, unix0=1_700_000_000, src=1):
     return msgs
 
 
-def cfg4_datagrams(n, seed=SEED_CFG4, ipfix_msg_bytes=1400):
+def cfg4_datagrams(n, seed=SEED_CFG4, ipfix_msg_bytes=1400, layout=False):
     """Config 4: n records, half NetFlow v9 (template 313, 130 B, 10 records
     per packet as Cisco exporters send), half IPFIX with variable-length and
     enterprise IEs (template 900) in MTU-sized messages (~1400 B, ~15
     records), packets interleaved.  The two template packets come first.
-    Returns a list of datagrams (bytes)."""
+    Returns a list of datagrams (bytes); layout=True also returns the IPFIX
+    records' generator layout: dict(flat, rec_len, spans (vlen_records),
+    v_first: first record of each template-900 message, v_pos: index of each
+    such message in the returned list)."""
     import numpy as np
     n_nf = n // 2
     n_v = n - n_nf
     _, rl = field_offsets(NF313)
     nf = template_records(NF313, n_nf, seed, "cpu").numpy()
     nf_msgs = _pack_nfv9(nf, rl, NF313_ID)
-    flat, lens = vlen_records(n_v, V900, seed + 1)
-    v_msgs = _pack_ipfix(flat, lens, V900_ID, max_msg=ipfix_msg_bytes)
+    flat, lens, spans = vlen_records(n_v, V900, seed + 1, spans=True)
+    v_first = []
+    v_msgs = _pack_ipfix(flat, lens, V900_ID, max_msg=ipfix_msg_bytes, firsts=v_first)
     out = [nfv9_template_message(), _ipfix_template_v900()]
     # interleave proportionally: packet i of a stream of m packets at position i/m
     keys = [(i / len(nf_msgs), 0, i) for i in range(len(nf_msgs))] + [(i / len(v_msgs), 1, i) for i in range(len(v_msgs))]
     keys.sort()
     out += [nf_msgs[i] if s == 0 else v_msgs[i] for _, s, i in keys]
-    return out
+    if not layout:
+        return out
+    v_pos = [0] * len(v_msgs)
+    for p, (_, s, i) in enumerate(keys):
+        if s == 1:
+            v_pos[i] = 2 + p
+    return out, dict(flat=flat, rec_len=lens, spans=spans, v_first=v_first, v_pos=v_pos)
 
 
 def _ipfix_template_v900():

@@ -248,6 +248,106 @@ def test_cfg4_full_size_batch_over_2gib(dev):
         assert batch.json(d) == exp, d
 
 
+def test_cfg4_vlen_columns_full_size(dev):
+    """Config 4 at 1.6e7 records: every column of the IPFIX variable-length / enterprise template
+    900 (8e6 records) checked on the GPU against the generator's ground truth.  Each
+    variable-length column entry {u64 batch offset, u32 length, 0} must equal the value's span
+    in the batch as the generator wrote it (u8 length prefix, 255 + 3-byte escape every 97th
+    record; generator.rs:1775-1793), and every fixed field -- those after variable-length
+    fields included -- must equal its wire bytes re-laid at the column width."""
+    from netgauze_amd import synth
+    n = 16_000_000
+    seed = synth.SEED_CFG4 + 99
+    dg, lay = synth.cfg4_datagrams(n, seed=seed, layout=True)
+    codec = new_codec()
+    codec.decode_datagrams(dg[:2])
+    data = dg[2:]
+    buf, offs, lens = synth.host_batch(data, device=dev)
+    batch = codec.decode_batch(buf, offs, lens)
+    assert (batch.dgram_headers()["status"] == 0).all()
+    slot = [s for s in batch.slots if s.template_id == synth.V900_ID][0]
+    nv = n - n // 2
+    assert slot.n_records == nv and len(slot.fields) == len(synth.V900)
+    # batch offset of every record: its message's batch offset + 20 (message + set header)
+    # + its offset inside the message's records
+    rec_len = lay["rec_len"]
+    starts = np.zeros(nv + 1, dtype=np.int64)
+    starts[1:] = np.cumsum(rec_len)
+    first = np.asarray(lay["v_first"], dtype=np.int64)
+    per = np.diff(np.append(first, nv))
+    msg_off = offs.cpu().numpy()[np.asarray(lay["v_pos"], dtype=np.int64) - 2].astype(np.int64)
+    rec_batch = np.repeat(msg_off + 20 - starts[first], per) + starts[:-1]
+    flat = torch.from_numpy(lay["flat"]).to(dev)
+    checked = {"vlen": 0, "fixed": 0}
+    for f, fi in enumerate(slot.fields):
+        start, ln = lay["spans"][f]
+        got = column_on_device(slot, f, nv)
+        if fi.kind == L.K_VLEN:
+            exp_off = torch.from_numpy(rec_batch + (start - starts[:-1])).to(dev)
+            g = got.contiguous().view(torch.int64).view(nv, 2)
+            assert torch.equal(g[:, 0], exp_off), f
+            assert torch.equal(g[:, 1] & 0xFFFFFFFF, torch.from_numpy(ln).to(dev)), f
+            assert torch.equal(g[:, 1] >> 32, torch.zeros_like(g[:, 1])), f
+            checked["vlen"] += 1
+            continue
+        w = int(ln[0])
+        idx = torch.from_numpy(start).to(dev)[:, None] + torch.arange(w, device=dev)[None, :]
+        raw = flat[idx]  # [nv, wire length] big-endian wire bytes
+        if fi.kind == L.K_BYTES:
+            exp = raw
+        else:
+            assert fi.kind in (L.K_UINT, L.K_DTMS), (f, fi.kind)
+            exp = torch.zeros(nv, fi.width, dtype=torch.uint8, device=dev)
+            exp[:, :w] = torch.flip(raw, dims=[1])
+        assert torch.equal(got, exp), f
+        checked["fixed"] += 1
+    assert checked == {"vlen": 5, "fixed": 9}, checked
+
+
+def test_cfg3_mixed_templates_1e8(dev):
+    """Config 3 at its full size, 10^8 records over 8 templates (1.25e7 each): every column of
+    every template compared on the GPU with the wire bytes re-laid."""
+    from netgauze_amd import synth
+    codec = new_codec()
+    codec.decode_datagrams([synth.templates_message(synth.CFG3_TEMPLATES)])
+    b, o, ln, recs = synth.mixed_stream(100_000_000, device=dev)
+    torch.cuda.synchronize()
+    batch = codec.decode_batch(b, o, ln)
+    del b
+    assert batch.n_records == 100_000_000
+    assert (batch.dgram_headers()["status"] == 0).all()
+    by_tid = {s.template_id: s for s in batch.slots if s.n_records}
+    assert set(by_tid) == set(recs)
+    for tid in list(recs):
+        check_slot_full(by_tid[tid], recs.pop(tid))
+
+
+def test_cfg5_shard_full_size(dev):
+    """One config-5 shard at its full size: 1.25e8 records over the 16 templates (rank 0 of
+    10^9 over 8 GPUs, the stream bench.py --workload cfg5 decodes), every column of every
+    template compared on the GPU with the wire bytes re-laid, and the per-template
+    processed counts (one per data set) equal to the messages of each template."""
+    from netgauze_amd import synth
+    n = 125_000_000
+    codec = new_codec()
+    codec.decode_datagrams([synth.templates_message(synth.CFG5_TEMPLATES)])
+    b, o, ln, recs = synth.mixed_stream(n, templates=synth.CFG5_TEMPLATES, seed=synth.SEED_CFG5, device=dev)
+    torch.cuda.synchronize()
+    batch = codec.decode_batch(b, o, ln)
+    del b
+    assert batch.n_records == n
+    assert (batch.dgram_headers()["status"] == 0).all()
+    by_tid = {s.template_id: s for s in batch.slots if s.n_records}
+    assert set(by_tid) == set(recs) and len(recs) == 16
+    msgs = {}
+    for tid, fields in synth.CFG5_TEMPLATES:
+        per = (65535 - 20) // synth.field_offsets(fields)[1]
+        msgs[tid] = -(-recs[tid].shape[0] // per)
+    for tid in list(recs):
+        check_slot_full(by_tid[tid], recs.pop(tid))
+    assert codec.template_counts(10) == msgs
+
+
 def test_cfg3_mixed_templates_oracle(dev):
     """Config 3 shape (8 templates, 40-153 B records, interleaved messages)
     against the oracle, every field."""
