@@ -308,6 +308,13 @@ int64_t ngz_columns_to_host(ngz_ctx *ctx, void *dst, uint64_t cap);
  * parse or is not device-decodable, NGZ_E_DEVICE if compilation failed. */
 int ngz_template_kernel(const uint8_t *tmpl, size_t len, int compile, char *buf, size_t cap);
 
+/* Introspection (no device needed): the multi-template decode kernel of 2-16 IPFIX
+ * template records laid back to back (a template set's body, ipfix.rs:384-413) that
+ * are all LDS-staged with one workgroup shape -- the one launch ngz_decode_batch uses
+ * for such templates of one batch.  As ngz_template_kernel; NGZ_E_INVALID when the
+ * records do not form such a group. */
+int ngz_group_kernel(const uint8_t *tmpls, size_t len, int compile, char *buf, size_t cap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -20,7 +20,7 @@ ABI_FUNCTIONS = [
     "ngz_ctx_create", "ngz_ctx_destroy", "ngz_last_error", "ngz_decode_batch",
     "ngz_decode_batch_host", "ngz_slot_fields", "ngz_dgram_error_json",
     "ngz_templates_json", "ngz_template_counts", "ngz_last_timing", "ngz_ctx_set_option",
-    "ngz_template_kernel", "ngz_columns_to_host", "ngz_dgram_json", "ngz_batch_json",
+    "ngz_template_kernel", "ngz_group_kernel", "ngz_columns_to_host", "ngz_dgram_json", "ngz_batch_json",
     "ngz_dgram_error", "ngz_template_counts_device", "ngz_slot_kernel",
 ]
 NGZ_ABI_VERSION = 2
@@ -191,6 +191,8 @@ def load():
     lib.ngz_columns_to_host.restype = ctypes.c_int64
     lib.ngz_template_kernel.argtypes = [P, ctypes.c_size_t, I, ctypes.c_char_p, ctypes.c_size_t]
     lib.ngz_template_kernel.restype = I
+    lib.ngz_group_kernel.argtypes = [P, ctypes.c_size_t, I, ctypes.c_char_p, ctypes.c_size_t]
+    lib.ngz_group_kernel.restype = I
     lib.ngz_ctx_set_option.argtypes = [P, I, ctypes.c_int64]
     lib.ngz_ctx_set_option.restype = I
     lib.ngz_dgram_json.argtypes = [P, U32, ctypes.c_char_p, ctypes.c_size_t]

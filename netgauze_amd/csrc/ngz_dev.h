@@ -215,18 +215,24 @@ struct ColGlb {
     }
 };
 
-#ifdef NGZ_LDS_WAVES
-// LDS-staged per-template kernels (generated with NGZ_LDS_WAVES / NGZ_LDS_ROWB
-// defined): the decode writes a workgroup window of LDS_ROWS rows into LDS,
-// column-major (column f at LDS_ROWS*col_off, row r at + r*width), and the
-// generated store step writes each column's run to HBM with 16-byte stores.
-constexpr uint32_t LDS_ROWS = NGZ_REG_WINDOW * NGZ_LDS_WAVES;
-__shared__ __attribute__((aligned(16))) uint8_t ngz_lds[LDS_ROWS * NGZ_LDS_ROWB];
+#if defined(NGZ_LDS_WAVES) || defined(NGZ_LDS_BYTES)
+// LDS-staged generated kernels: the decode writes a workgroup window of ROWS
+// rows into LDS, column-major (column f at ROWS*col_off, row r at + r*width),
+// and the generated store step writes each column's run to HBM with 16-byte
+// stores.  A per-template kernel is generated with NGZ_LDS_WAVES / NGZ_LDS_ROWB
+// (ColSt = its LDS column); a multi-template kernel with NGZ_LDS_BYTES (the
+// largest window image of its templates), each template body naming its own
+// ColLds<ROWS>.
+#ifndef NGZ_LDS_BYTES
+#define NGZ_LDS_BYTES (NGZ_REG_WINDOW * NGZ_LDS_WAVES * NGZ_LDS_ROWB)
+#endif
+__shared__ __attribute__((aligned(16))) uint8_t ngz_lds[NGZ_LDS_BYTES];
 
-struct ColSt {
+template <uint32_t ROWS>
+struct ColLds {
     uint32_t base;  // LDS byte offset of this pass's first row in the column
-    __device__ __forceinline__ ColSt(const Pass &P, uint32_t col_off, uint32_t width)
-        : base(LDS_ROWS * col_off + P.wrow * width) {}
+    __device__ __forceinline__ ColLds(const Pass &P, uint32_t col_off, uint32_t width)
+        : base(ROWS * col_off + P.wrow * width) {}
     __device__ __forceinline__ void b8(uint32_t off, uint32_t v) const { ngz_lds[base + off] = (uint8_t)v; }
     __device__ __forceinline__ void b16(uint32_t off, uint32_t v) const {
         *(uint16_t *)&ngz_lds[base + off] = (uint16_t)v;
@@ -258,6 +264,10 @@ __device__ __forceinline__ void lds_flush(uint8_t *dst, uint32_t at, uint32_t ld
         __builtin_amdgcn_raw_buffer_store_b128(x, r, at + 16 * lane, 0, 0);
     }
 }
+#endif
+#ifdef NGZ_LDS_WAVES
+constexpr uint32_t LDS_ROWS = NGZ_REG_WINDOW * NGZ_LDS_WAVES;
+typedef ColLds<LDS_ROWS> ColSt;
 #else
 typedef ColGlb ColSt;
 #endif
@@ -304,7 +314,7 @@ __device__ __forceinline__ void dec_num(const uint32_t (&R)[WIN_DW], const Pass 
 // Numeric field of C consecutive rows per lane (run_chunks<C, true>): the C
 // values are packed into one C*width-byte store per lane when all C rows
 // belong to the chunk (a wave writes 64*C*width contiguous bytes).
-template <int C>
+template <int C, class Col = ColSt>
 __device__ __forceinline__ void dec_num_c(const uint32_t (&R)[C][WIN_DW], const Pass (&P)[C], uint32_t o, uint32_t off,
                                           uint32_t f, uint32_t len, uint32_t width, uint32_t kind, uint32_t col_off) {
     uint64_t v[C];
@@ -314,7 +324,7 @@ __device__ __forceinline__ void dec_num_c(const uint32_t (&R)[C][WIN_DW], const 
         v[k] = num_value(R[k], P[k], o, off, f, len, kind);
         full = full && P[k].valid;
     }
-    const ColSt cs(P[0], col_off, width);
+    const Col cs(P[0], col_off, width);
     if (full) {
         const uint32_t at = P[0].lrow * width;  // lrow of record 0 = C*lane
         if (width == 1) {
@@ -444,14 +454,14 @@ __device__ __forceinline__ void dec_raw(const uint32_t (&R)[WIN_DW], const Pass 
 // the C records' bytes are concatenated in registers and written as
 // C*width/4 dwords (C*width contiguous bytes per lane), instead of per-record
 // byte stores.  Other cases go record by record through dec_raw.
-template <int C>
+template <int C, class Col = ColSt>
 __device__ __forceinline__ void dec_raw_c(const uint32_t (&R)[C][WIN_DW], const Pass (&P)[C], uint32_t o,
                                           uint32_t width, uint32_t col_off) {
     bool full = true;
 #pragma unroll
     for (int k = 0; k < C; ++k) full = full && P[k].valid;
     if (full && C == 4 && width <= 16) {
-        const ColSt cs(P[0], col_off, width);
+        const Col cs(P[0], col_off, width);
         const uint32_t at = P[0].lrow * width;
         // dword m of the lane's 4*width bytes: byte i comes from record (4m+i)/width,
         // field byte (4m+i)%width -- constants once width is
@@ -467,7 +477,7 @@ __device__ __forceinline__ void dec_raw_c(const uint32_t (&R)[C][WIN_DW], const 
         return;
     }
 #pragma unroll
-    for (int k = 0; k < C; ++k) dec_raw(R[k], P[k], o, 0, width, width, col_off, 0);
+    for (int k = 0; k < C; ++k) dec_raw<Col>(R[k], P[k], o, 0, width, width, col_off, 0);
 }
 
 // Walk chunks [c_begin, c_end) of the batch's chunk array, one wave per chunk
@@ -928,7 +938,7 @@ __device__ __forceinline__ void run_windows_staged(const BatchDev &B, uint32_t s
 }
 #endif  // NGZ_VSTAGE
 
-#ifdef NGZ_LDS_WAVES
+#if defined(NGZ_LDS_WAVES) || defined(NGZ_LDS_BYTES)
 // Row source of a chunk-mode window: the window's chunk descriptors, one per
 // lane (e0/e1 as fetched by the wave, cnt valid); a row's record is in the
 // chunk whose row range holds it.
@@ -971,12 +981,12 @@ struct ChunkGatherSrc {
     }
 };
 
-// LDS-staged decode of one slot: workgroup window W = rows [W*LDS_ROWS,
-// (W+1)*LDS_ROWS); wave q decodes its NGZ_REG_WINDOW sub-window s into LDS,
-// then the workgroup writes the window's column runs (store(W, blk, cap),
-// generated per template).  The capacity is a multiple of LDS_ROWS
-// (k_layout), so a window's runs never leave the slot's block; rows past the
-// slot's total carry stale bytes nobody reads.
+// LDS-staged decode of one slot: workgroup window W = rows [W*ROWS,
+// (W+1)*ROWS) with ROWS = NGZ_REG_WINDOW*LW; wave q decodes its NGZ_REG_WINDOW
+// sub-window s into LDS, then the workgroup writes the window's column runs
+// (store(W, blk, cap), generated per template).  The capacity is a multiple of
+// the window (k_layout), so a window's runs never leave the slot's block; rows
+// past the slot's total carry stale bytes nobody reads.
 //
 // Chunk mode: the chunks of sub-window s are [wt[s], wt[s+1]) (k_emit).  A
 // wave holds the window-table entries of its next 64 sub-windows in two
@@ -992,7 +1002,8 @@ struct ChunkGatherSrc {
 // Every XCD then works on one contiguous stretch of the input and of every
 // column: its L2 and its address translations cover an eighth of what they
 // would with windows dealt across all XCDs (those runs were up to 15 %
-// slower, depending on where the allocations landed).
+// slower, depending on where the allocations landed).  A multi-template kernel
+// deals each template's windows this way in turn.
 struct WinSeq {
     uint32_t first, step, end;
     __device__ __forceinline__ uint32_t at(uint32_t i) const { return first + i * step; }
@@ -1008,14 +1019,14 @@ __device__ __forceinline__ WinSeq win_seq(uint32_t nwin) {
     return WinSeq{start + l, G / X, end};
 }
 
-template <int RPL, bool CONSEC, class Shape, class PassFn, class StoreFn>
+template <int RPL, bool CONSEC, uint32_t LW, class Shape, class PassFn, class StoreFn>
 __device__ __forceinline__ void run_lds(const BatchDev &B, uint32_t slot, Shape &&shape, PassFn &&pass,
-                                        StoreFn &&store) {
+                                        StoreFn &&store, const WinSeq ws) {
+    constexpr uint32_t ROWS = NGZ_REG_WINDOW * LW;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t q = sgpr(threadIdx.x >> 6);
     const SlotRT rt = sload(&B.slots[slot]);
     const uint32_t total = rt.total;
-    const uint32_t nwin = (total + LDS_ROWS - 1) / LDS_ROWS;
     const uint32_t nsub = (total + NGZ_REG_WINDOW - 1) / NGZ_REG_WINDOW;
     const RecShape shp = shape(slot);
     uint8_t *blk = B.arena + rt.block;
@@ -1023,13 +1034,12 @@ __device__ __forceinline__ void run_lds(const BatchDev &B, uint32_t slot, Shape 
     const uint32_t *wt = (const uint32_t *)(B.arena + rt.wtab);
     Pass P[RPL];
     row_preset<RPL>(B, rt, P);
-    const WinSeq ws = win_seq(nwin);
     if (rt.mode == NGZ_MODE_ROW) {
         const uint64_t *rs = (const uint64_t *)(B.arena + rt.rows);
         const uint32_t *rd = (const uint32_t *)(B.arena + rt.rows + 8ull * rt.cap);
         for (uint32_t W = ws.first; W < ws.end; W += ws.step) {
-            const uint32_t s = W * NGZ_LDS_WAVES + q;
-            if (s < nsub) row_window<RPL, CONSEC>(B, RowTableSrc{rs, rd}, total, s, W * LDS_ROWS, P, pass);
+            const uint32_t s = W * LW + q;
+            if (s < nsub) row_window<RPL, CONSEC>(B, RowTableSrc{rs, rd}, total, s, W * ROWS, P, pass);
             __syncthreads();
             store(W, blk, rt.cap);
             __syncthreads();
@@ -1039,7 +1049,7 @@ __device__ __forceinline__ void run_lds(const BatchDev &B, uint32_t slot, Shape 
     // window-table entries [cb, ce) of this wave's sub-windows i0 .. i0+63 (lane i)
     auto wt_fetch = [&](uint32_t i0, uint32_t &ta, uint32_t &tb) {
         const uint32_t Wl = ws.at(i0 + lane);
-        const uint32_t sl = Wl * NGZ_LDS_WAVES + q;
+        const uint32_t sl = Wl * LW + q;
         const bool in = Wl < ws.end;
         ta = in && sl < nsub ? wt[sl] : c_end;
         tb = in && sl + 1 < nsub ? wt[sl + 1] : c_end;
@@ -1059,7 +1069,7 @@ __device__ __forceinline__ void run_lds(const BatchDev &B, uint32_t slot, Shape 
     desc_fetch(lane_u32(ta, 0), lane_u32(tb, 0), n0, n1);
     uint32_t i = 0;
     for (uint32_t W = ws.first; W < ws.end; W += ws.step, ++i) {
-        const uint32_t s = W * NGZ_LDS_WAVES + q;
+        const uint32_t s = W * LW + q;
         const uint32_t cb = lane_u32(ta, i & 63), ce = lane_u32(tb, i & 63);
         const uint4 e0 = n0, e1 = n1;
         // prefetch: the next sub-window's descriptors (and table entries every 64)
@@ -1067,7 +1077,7 @@ __device__ __forceinline__ void run_lds(const BatchDev &B, uint32_t slot, Shape 
         desc_fetch(lane_u32(ta, (i + 1) & 63), lane_u32(tb, (i + 1) & 63), n0, n1);
         if (s < nsub) {
             if (ce - cb <= 64) {
-                row_window<RPL, CONSEC>(B, ChunkGatherSrc{e0, e1, ce - cb, shp.rl}, total, s, W * LDS_ROWS, P, pass);
+                row_window<RPL, CONSEC>(B, ChunkGatherSrc{e0, e1, ce - cb, shp.rl}, total, s, W * ROWS, P, pass);
             } else {
                 for (uint32_t c0 = cb; c0 < ce; c0 += 64) {
                     uint4 f0, f1;
@@ -1076,7 +1086,7 @@ __device__ __forceinline__ void run_lds(const BatchDev &B, uint32_t slot, Shape 
                     for (uint32_t j = 0; j < cnt; ++j) {
                         const Chunk cur = chunk_at_lane(f0, f1, j);
                         if (cur.n == 0) continue;  // padding chunk
-                        chunk_passes<RPL, CONSEC>(B, cur, shp.rl, blk, rt.cap, lane, W * LDS_ROWS, pass);
+                        chunk_passes<RPL, CONSEC>(B, cur, shp.rl, blk, rt.cap, lane, W * ROWS, pass);
                     }
                 }
             }

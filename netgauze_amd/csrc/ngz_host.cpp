@@ -20,6 +20,7 @@
 #include <tuple>
 #include <string>
 #include <unordered_map>
+#include <set>
 #include <vector>
 
 #include "ngz/flow_decode.h"
@@ -38,8 +39,14 @@ extern "C" int ngz_launch_decode_generic(const BatchDev *B, uint32_t grid, hipSt
 void *ngz_rtc_kernel(int device, const DevPlan &P);
 int ngz_rtc_kernel_async(int device, const DevPlan &P, void **fn, void **entry);
 int ngz_rtc_poll(void *entry, void **fn);
+void *ngz_rtc_group(int device, const DevPlan *const *plans, uint32_t n);
+int ngz_rtc_group_async(int device, const DevPlan *const *plans, uint32_t n, void **fn, void **entry);
+int ngz_rtc_launch_group(void *fn, const BatchDev *B, const uint32_t *slots, uint32_t n, uint32_t grid, uint32_t block,
+                         hipStream_t st);
+std::string ngz_rtc_group_source(const DevPlan *const *plans, uint32_t n);
 std::string ngz_rtc_source(const DevPlan &P);
 int ngz_rtc_compile_only(const DevPlan &P, std::string *log_out);
+int ngz_rtc_compile_source(const std::string &src, std::string *log_out);
 int ngz_rtc_launch(void *fn, const BatchDev *B, uint32_t slot, uint32_t grid, uint32_t block, hipStream_t st);
 extern "C" int ngz_launch_counts(const BatchDev *B, uint64_t set_cap, hipStream_t st);
 extern "C" int ngz_launch_export(const BatchDev *B, BatchSummary *h_summary, SlotRT *h_slots,
@@ -1033,6 +1040,49 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
         }
         launched[s] = 1;
     }
+    // Several LDS-staged specialised templates of one workgroup shape: one
+    // multi-template launch deals all their windows over the grid (one ramp and
+    // one tail for the batch instead of one per template).  Its kernel compiles
+    // like a template's (in the background unless NGZ_OPT_RTC_SYNC); until it is
+    // ready the templates launch one by one.
+    if (ctx->group_launch && ctx->specialize && todo.size() >= 2) {
+        std::map<uint32_t, std::vector<uint32_t>> by_lw;
+        for (const auto &t : todo) {
+            const Version &v = ctx->versions[ctx->slot_version[t.first]];
+            if (v.rtc_state == 1 && v.plan.lds_waves && !v.plan.has_vlen) by_lw[v.plan.lds_waves].push_back(t.first);
+        }
+        for (auto &kv : by_lw) {
+            std::vector<uint32_t> &sl = kv.second;
+            if (sl.size() < 2) continue;
+            if (sl.size() > NGZ_RTC_GROUP_MAX) sl.resize(NGZ_RTC_GROUP_MAX);
+            std::vector<int32_t> key;
+            std::vector<const DevPlan *> pp;
+            for (uint32_t s : sl) {
+                key.push_back(ctx->slot_version[s]);
+                pp.push_back(&ctx->versions[ctx->slot_version[s]].plan);
+            }
+            ngz_ctx::GroupKernel &gk = ctx->group_kernels[key];
+            if (gk.state == 0) {
+                if (ctx->rtc_sync) {
+                    gk.fn = ngz_rtc_group(ctx->device, pp.data(), (uint32_t)pp.size());
+                    gk.state = gk.fn ? 1 : 2;
+                } else {
+                    const int r = ngz_rtc_group_async(ctx->device, pp.data(), (uint32_t)pp.size(), &gk.fn, &gk.entry);
+                    gk.state = r == 1 ? 1 : r < 0 ? 2 : 3;
+                }
+            } else if (gk.state == 3) {
+                const int r = ngz_rtc_poll(gk.entry, &gk.fn);
+                if (r) gk.state = r > 0 ? 1 : 2;
+            }
+            if (gk.state != 1) continue;
+            const uint32_t g = (uint32_t)ctx->n_cus * ctx->lds_blocks_per_cu;
+            if (ngz_rtc_launch_group(gk.fn, &B, sl.data(), (uint32_t)sl.size(), g, 64 * kv.first, st))
+                return fail(ctx, NGZ_E_DEVICE, "multi-template decode launch");
+            std::set<uint32_t> done(sl.begin(), sl.end());
+            todo.erase(std::remove_if(todo.begin(), todo.end(), [&](const auto &t) { return done.count(t.first) != 0; }),
+                       todo.end());
+        }
+    }
     // several active templates: their kernels run side by side on the context's
     // auxiliary streams (fork/join with events), so one kernel's tail overlaps
     // the next one's start instead of draining the GPU between templates
@@ -1231,6 +1281,7 @@ int ngz_ctx_create(int device, ngz_ctx **out) {
     *ctx->h_done = 0;
     if (const char *e = getenv("NGZ_BLOCKS_PER_CU")) ctx->blocks_per_cu = std::max(1, std::min(32, atoi(e)));
     if (const char *e = getenv("NGZ_LDS_BLOCKS_PER_CU")) ctx->lds_blocks_per_cu = std::max(1, std::min(512, atoi(e)));
+    if (const char *e = getenv("NGZ_GROUP")) ctx->group_launch = atoi(e) != 0;
     *out = ctx;
     return NGZ_OK;
 }
@@ -1785,6 +1836,50 @@ extern "C" int ngz_template_kernel(const uint8_t *tmpl, size_t len, int compile,
     if (compile) {
         std::string log;
         if (ngz_rtc_compile_only(v.plan, &log)) {
+            out += "\n// hiprtc log:\n" + log;
+            rc = NGZ_E_DEVICE;
+        }
+    }
+    if (buf && cap) {
+        const size_t n = std::min(cap - 1, out.size());
+        memcpy(buf, out.data(), n);
+        buf[n] = 0;
+    }
+    return rc;
+}
+
+extern "C" int ngz_group_kernel(const uint8_t *tmpls, size_t len, int compile, char *buf, size_t cap) {
+    if (!tmpls || len < 4 || len > 65535) return NGZ_E_INVALID;
+    Cur c{tmpls, 0, (uint32_t)len};
+    std::vector<Version> vs;
+    while (c.pos + 4 <= len) {
+        Version v;
+        v.proto = 10;
+        v.tid = rd16(tmpls + c.pos);
+        const uint32_t count = rd16(tmpls + c.pos + 2);
+        v.n_scope = 0;
+        c.pos += 4;
+        for (uint32_t i = 0; i < count; ++i) {
+            Spec s;
+            std::string err;
+            if (!parse_field_spec(c, s, err)) return NGZ_E_INVALID;
+            v.specs.push_back(s);
+        }
+        vs.push_back(std::move(v));
+    }
+    if (vs.size() < 2 || vs.size() > NGZ_RTC_GROUP_MAX) return NGZ_E_INVALID;
+    std::vector<const DevPlan *> pp;
+    for (Version &v : vs) {
+        build_plan(v);
+        if (!rtc_eligible(v.plan) || !v.plan.lds_waves || v.plan.has_vlen || v.plan.lds_waves != vs[0].plan.lds_waves)
+            return NGZ_E_INVALID;
+    }
+    for (Version &v : vs) pp.push_back(&v.plan);
+    std::string out = ngz_rtc_group_source(pp.data(), (uint32_t)pp.size());
+    int rc = NGZ_OK;
+    if (compile) {
+        std::string log;
+        if (ngz_rtc_compile_source(out, &log)) {
             out += "\n// hiprtc log:\n" + log;
             rc = NGZ_E_DEVICE;
         }

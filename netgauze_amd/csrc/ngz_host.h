@@ -9,6 +9,7 @@
 #include <cstdint>
 #include <memory>
 #include <string>
+#include <map>
 #include <vector>
 
 #include "ngz/flow_aggregate.h"
@@ -263,6 +264,16 @@ struct ngz_ctx {
     std::vector<uint8_t> slot_spec;             // last batch: slot decoded by its specialised kernel
     uint32_t blocks_per_cu = 4;                 // decode grid: 4 x 256 threads per CU
     uint32_t lds_blocks_per_cu = 8;             // LDS-staged decode grid (2 resident per CU at 64 KB)
+    // multi-template decode launches (ngz_rtc.cpp generate_group): one kernel for the
+    // LDS-staged specialised templates of a batch that share a workgroup shape, per set of
+    // template versions; NGZ_GROUP=1 turns it on (default: one launch per template)
+    struct GroupKernel {
+        int state = 0;  // 0 not looked up, 1 ready, 2 unavailable, 3 compiling
+        void *fn = nullptr;
+        void *entry = nullptr;
+    };
+    std::map<std::vector<int32_t>, GroupKernel> group_kernels;
+    bool group_launch = false;
     // device summary / processed_count increments alternate between two
     // parities: a batch's k_export zeroes the other parity for the next one
     int parity = 0;
@@ -292,7 +303,6 @@ struct ngz_ctx {
     std::vector<ngzh::TemplateSetJson> tmpl_sets;  // template sets of the last batch, (dgram, set_pos) order
     uint64_t batch_serial = 0;                      // bumped by every ngz_decode_batch
     std::shared_ptr<ngzh::JsonView> json_view;      // ngz_dgram_json cache of the last batch
-    // ngz_template_counts_device: pinned staging of the count table and the event of its last copy
     // ngz_template_counts_device staging: a ring of pinned tables, each reused only after
     // the copy that last read it has completed (its event), so no call waits on the copy
     // it or the previous call just queued

@@ -8,6 +8,7 @@
 #define NGZ_LANE_FIELDS 128   // field descriptors the generic kernel keeps in VGPRs (two per lane); the
                               // rest of a wider template's table is read with scalar loads
 #define NGZ_RTC_MAX_FIELDS 512  // widest template that gets a generated kernel (wider: generic kernel)
+#define NGZ_RTC_GROUP_MAX 16    // templates one multi-template decode launch takes (ngz_rtc.cpp generate_group)
 #define NGZ_WALK_MAX 15       // variable-length fields a walk program holds (more: the exact field walk)
 #define NGZ_MAX_SLOTS 1024    // template versions live in one batch
 #define NGZ_NO_SLOT 0xFFFFu

@@ -69,8 +69,17 @@ std::string signature(const DevPlan &P) {
 
 std::string generate_vlen(const DevPlan &P);
 
-std::string generate(const DevPlan &P) {
-    if (P.has_vlen) return generate_vlen(P);
+// The parts of a fixed template's generated decode: the pass body (register
+// windows, extraction, column stores through ColT / ColGlb) and, when staged
+// in LDS, the store step; rows per lane and layout; LDS waves and row bytes.
+struct FixedParts {
+    int rpl = 4;
+    bool consec = true;
+    uint32_t lw = 0, rowb = 0, rec_len = 0;
+    std::string pass, store;
+};
+
+FixedParts fixed_parts(const DevPlan &P) {
     std::vector<Item> items;
     for (uint32_t f = 0; f < P.n_fields; ++f) {
         const DevField &d = P.f[f];
@@ -186,11 +195,11 @@ std::string generate(const DevPlan &P) {
         const uint32_t co = (lw0 && !dir) ? lds_col[it.f] : it.col_off;
         switch (it.type) {
         case 0:
-            snprintf(b, sizeof b, "        dec_num%s(%s, %s, %uu, %uu, %uu, %uu, %uu, %uu, %uu);\n", dir ? "<ColGlb>" : "",
+            snprintf(b, sizeof b, "        dec_num<%s>(%s, %s, %uu, %uu, %uu, %uu, %uu, %uu, %uu);\n", dir ? "ColGlb" : "ColT",
                      R.c_str(), P.c_str(), it.off - wb, it.off, it.f, it.len, it.width, it.kind, co);
             break;
         case 1:
-            snprintf(b, sizeof b, "        dec_raw%s(%s, %s, %uu, %uu, %uu, %uu, %uu, %uu);\n", dir ? "<ColGlb>" : "",
+            snprintf(b, sizeof b, "        dec_raw<%s>(%s, %s, %uu, %uu, %uu, %uu, %uu, %uu);\n", dir ? "ColGlb" : "ColT",
                      R.c_str(), P.c_str(), it.off + it.j - wb, it.j, it.piece, it.width, co, it.pad_to);
             break;
         case 2:
@@ -227,12 +236,12 @@ std::string generate(const DevPlan &P) {
                 if (direct[it.f]) {
                     for (int k = 0; k < rpl; ++k) emit_item(it, wb, k);
                 } else if (it.type == 0) {
-                    snprintf(b, sizeof b, "        dec_num_c<%d>(R, P, %uu, %uu, %uu, %uu, %uu, %uu, %uu);\n", rpl,
+                    snprintf(b, sizeof b, "        dec_num_c<%d, ColT>(R, P, %uu, %uu, %uu, %uu, %uu, %uu, %uu);\n", rpl,
                              it.off - wb, it.off, it.f, it.len, it.width, it.kind, co);
                     body += b;
                 } else if (it.type == 1 && it.j == 0 && it.piece == it.len && it.len == it.width && it.width <= 16) {
                     // whole short raw field: packed C-row store
-                    snprintf(b, sizeof b, "        dec_raw_c<%d>(R, P, %uu, %uu, %uu);\n", rpl, it.off - wb, it.width, co);
+                    snprintf(b, sizeof b, "        dec_raw_c<%d, ColT>(R, P, %uu, %uu, %uu);\n", rpl, it.off - wb, it.width, co);
                     body += b;
                 } else {
                     for (int k = 0; k < rpl; ++k) emit_item(it, wb, k);
@@ -244,26 +253,14 @@ std::string generate(const DevPlan &P) {
         }
         i = e;
     }
-    const std::string RPL = std::to_string(rpl);
+    FixedParts out;
+    out.rpl = rpl;
+    out.consec = consec;
+    out.lw = P.lds_waves;
+    out.rowb = staged_rowb;
+    out.rec_len = P.rec_len;
+    out.pass = body;
     const uint32_t lw = P.lds_waves;
-    std::string src;
-    src += "// generated by ngz_rtc.cpp for plan " + signature(P) + "\n";
-    if (lw) {
-        src += "#define NGZ_LDS_WAVES " + std::to_string(lw) + "\n";
-        src += "#define NGZ_LDS_ROWB " + std::to_string(staged_rowb) + "\n";
-    }
-    src += "#include \"ngz_dev.h\"\nusing namespace ngzdev;\n";
-    src += "extern \"C\" __global__ void __launch_bounds__(" + std::to_string(lw ? 64 * lw : 256) +
-           ") ngz_tpl(BatchDev B, uint32_t slot) {\n";
-    src += "    if (sload(&B.summary->overflow)) return;\n";
-    src += "    const SlotRT rt = sload(&B.slots[slot]);\n";
-    src += "    const uint32_t c0 = rt.chunk0, nc = rt.nchunks;\n";
-    const std::string L = RPL + ", " + (consec ? "true" : "false");
-    src += "    auto shape = [](uint32_t) { return RecShape{" + std::to_string(P.rec_len) + "u, 0u, false}; };\n";
-    src += "    auto pass = [&](const Pass (&P)[" + RPL + "]) {\n";
-    src += "        uint32_t R[" + RPL + "][WIN_DW];\n";
-    src += body;
-    src += "    };\n";
     if (lw) {
         // Store step of the LDS-staged kernel: each column's run of the window
         // (LDS_ROWS*width bytes) cut into 1 KB units (64 lanes x 16 B), dealt
@@ -290,20 +287,107 @@ std::string generate(const DevPlan &P) {
         }
         // NGZ_RTC_EXP=1: no store step (timing experiments only; output invalid)
         if (getenv("NGZ_RTC_EXP") && (atoi(getenv("NGZ_RTC_EXP")) & 1)) per_wave.assign(lw, "");
-        src += "    auto store = [&](uint32_t W, uint8_t *blk, uint32_t cap) {\n";
-        src += "        const uint32_t q = sgpr(threadIdx.x >> 6);\n";
+        std::string st;
+        st += "    auto store = [&](uint32_t W, uint8_t *blk, uint32_t cap) {\n";
+        st += "        const uint32_t q = sgpr(threadIdx.x >> 6);\n";
         for (uint32_t q = 0; q < lw; ++q) {
-            src += q ? "        else if (q == " + std::to_string(q) + ") {\n" : "        if (q == 0) {\n";
-            src += per_wave[q];
-            src += "        }\n";
+            st += q ? "        else if (q == " + std::to_string(q) + ") {\n" : "        if (q == 0) {\n";
+            st += per_wave[q];
+            st += "        }\n";
         }
-        src += "    };\n";
+        st += "    };\n";
+        out.store = st;
+    }
+    return out;
+}
+
+// The lambdas of one fixed template's decode: shape, pass and (LDS-staged) store.
+std::string fixed_lambdas(const FixedParts &F) {
+    const std::string RPL = std::to_string(F.rpl);
+    std::string src;
+    src += "    auto shape = [](uint32_t) { return RecShape{" + std::to_string(F.rec_len) + "u, 0u, false}; };\n";
+    src += "    auto pass = [&](const Pass (&P)[" + RPL + "]) {\n";
+    src += "        uint32_t R[" + RPL + "][WIN_DW];\n";
+    src += F.pass;
+    src += "    };\n";
+    src += F.store;
+    return src;
+}
+
+std::string generate(const DevPlan &P) {
+    if (P.has_vlen) return generate_vlen(P);
+    const FixedParts F = fixed_parts(P);
+    const std::string L = std::to_string(F.rpl) + ", " + (F.consec ? "true" : "false");
+    const uint32_t lw = F.lw;
+    std::string src;
+    src += "// generated by ngz_rtc.cpp for plan " + signature(P) + "\n";
+    if (lw) {
+        src += "#define NGZ_LDS_WAVES " + std::to_string(lw) + "\n";
+        src += "#define NGZ_LDS_ROWB " + std::to_string(F.rowb) + "\n";
+    }
+    src += "#include \"ngz_dev.h\"\nusing namespace ngzdev;\n";
+    src += "extern \"C\" __global__ void __launch_bounds__(" + std::to_string(lw ? 64 * lw : 256) +
+           ") ngz_tpl(BatchDev B, uint32_t slot) {\n";
+    src += "    if (sload(&B.summary->overflow)) return;\n";
+    src += "    const SlotRT rt = sload(&B.slots[slot]);\n";
+    src += "    const uint32_t c0 = rt.chunk0, nc = rt.nchunks;\n";
+    src += "    using ColT = ColSt;\n";
+    src += fixed_lambdas(F);
+    if (lw) {
+        const std::string rows = std::to_string(NGZ_REG_WINDOW * lw);
         src += "    (void)c0; (void)nc;\n";
-        src += "    run_lds<" + L + ">(B, slot, shape, pass, store);\n}\n";
+        src += "    run_lds<" + L + ", " + std::to_string(lw) + ">(B, slot, shape, pass, store, win_seq((rt.total + " + rows +
+               " - 1) / " + rows + "));\n}\n";
         return src;
     }
     src += "    if (rt.mode == NGZ_MODE_ROW) run_windows<" + L + ">(B, slot, shape, pass);\n";
     src += "    else run_chunks<" + L + ">(B, c0, c0 + nc, [](uint32_t) { return true; }, shape, pass);\n}\n";
+    return src;
+}
+
+// One launch for several LDS-staged fixed templates of the same workgroup shape
+// (lds_waves): ngz_tplm(B, slots) runs each template's windows in turn, dealt
+// XCD-aware over the whole grid (win_seq), each decoded by its own specialised
+// body (every field a constant, as in ngz_tpl).
+// Against one launch per template, the batch has one ramp and one tail instead
+// of one per template (config 3: 8 launches of 1.25e7 records each ran 10-15 %
+// below the per-byte rate of one 1e8-record launch).
+std::string generate_group(const DevPlan *const *plans, uint32_t n) {
+    std::string src;
+    src += "// generated by ngz_rtc.cpp: multi-template kernel of " + std::to_string(n) + " plans\n";
+    uint32_t lds = 0, lw = plans[0]->lds_waves;
+    std::vector<FixedParts> parts;
+    for (uint32_t k = 0; k < n; ++k) {
+        parts.push_back(fixed_parts(*plans[k]));
+        lds = std::max<uint32_t>(lds, NGZ_REG_WINDOW * parts.back().lw * parts.back().rowb);
+    }
+    src += "#define NGZ_LDS_BYTES " + std::to_string(std::max<uint32_t>(lds, 16)) + "\n";
+    src += "#include \"ngz_dev.h\"\nusing namespace ngzdev;\n";
+    for (uint32_t k = 0; k < n; ++k) {
+        const FixedParts &F = parts[k];
+        const std::string L = std::to_string(F.rpl) + ", " + (F.consec ? "true" : "false");
+        src += "namespace t" + std::to_string(k) + " {  // " + signature(*plans[k]) + "\n";
+        src += "__device__ __forceinline__ void run(const BatchDev &B, uint32_t slot, const WinSeq ws) {\n";
+        src += "    using ColT = ColLds<" + std::to_string(NGZ_REG_WINDOW * F.lw) + ">;\n";
+        src += fixed_lambdas(F);
+        src += "    run_lds<" + L + ", " + std::to_string(F.lw) + ">(B, slot, shape, pass, store, ws);\n}\n}\n";
+    }
+    src += "struct NgzSlots { uint32_t s[" + std::to_string(NGZ_RTC_GROUP_MAX) + "]; };\n";
+    src += "extern \"C\" __global__ void __launch_bounds__(" + std::to_string(64 * lw) +
+           ") ngz_tplm(BatchDev B, NgzSlots S) {\n";
+    src += "    if (sload(&B.summary->overflow)) return;\n";
+    // every template's windows dealt over the whole grid as its own kernel would (win_seq: an
+    // eighth per XCD), one template after the other: each XCD takes an eighth of every template,
+    // so per-window costs that differ by template (40- to 153-byte records) stay balanced across
+    // the XCDs, and a workgroup goes on to the next template's windows without a kernel boundary
+    const std::string rows = std::to_string(NGZ_REG_WINDOW * lw);
+    src += "    uint32_t nw;\n";
+    for (uint32_t k = 0; k < n; ++k) {
+        const std::string K = std::to_string(k);
+        src += "    nw = (sload(&B.slots[S.s[" + K + "]]).total + " + rows + " - 1) / " + rows + ";\n";
+        src += "    if (nw) t" + K + "::run(B, S.s[" + K + "], win_seq(nw));\n";
+    }
+    src += "}\n";
     return src;
 }
 
@@ -580,7 +664,7 @@ bool compile(const std::string &src, std::vector<char> &code, std::string &log) 
 
 
 // Compile + load one entry (the caller won the 0 -> 1 transition).
-void build(Entry *e, int device, const std::string &src, const std::string &sig) {
+void build(Entry *e, int device, const std::string &src, const std::string &sig, const char *kname) {
     std::vector<char> code;
     std::string log;
     if (getenv("NGZ_RTC_DUMP")) fprintf(stderr, "[ngz rtc] source:\n%s\n", src.c_str());
@@ -590,7 +674,7 @@ void build(Entry *e, int device, const std::string &src, const std::string &sig)
         return;
     }
     if (hipSetDevice(device) != hipSuccess || hipModuleLoadData(&e->mod, code.data()) != hipSuccess ||
-        hipModuleGetFunction(&e->fn, e->mod, "ngz_tpl") != hipSuccess) {
+        hipModuleGetFunction(&e->fn, e->mod, kname) != hipSuccess) {
         fprintf(stderr, "[ngz rtc] module load failed for %s\n", sig.c_str());
         e->fn = nullptr;
         e->state.store(3, std::memory_order_release);
@@ -599,17 +683,15 @@ void build(Entry *e, int device, const std::string &src, const std::string &sig)
     e->state.store(2, std::memory_order_release);
 }
 
-}  // namespace
-
-// Specialised kernel for a plan on `device`, compiled on first use and cached,
-// waiting for it if needed; nullptr when compilation failed (the caller falls
-// back to the generic kernel).
-void *ngz_rtc_kernel(int device, const DevPlan &P) {
-    const std::string sig = signature(P);
+// A cache entry's kernel, compiled from gen() (kernel `kname`) on first use:
+// synchronously (waiting for another thread's compile of it if needed), or in
+// the background (ngz_rtc_poll).
+template <class Gen>
+void *kernel_sync(int device, const std::string &sig, Gen &&gen, const char *kname) {
     Entry *e = entry_for(device, sig);
     int st = 0;
     if (e->state.compare_exchange_strong(st, 1)) {
-        build(e, device, generate(P), sig);
+        build(e, device, gen(), sig, kname);
     } else {
         while ((st = e->state.load(std::memory_order_acquire)) == 1)  // another thread compiles it
             std::this_thread::sleep_for(std::chrono::milliseconds(1));
@@ -617,22 +699,20 @@ void *ngz_rtc_kernel(int device, const DevPlan &P) {
     return e->state.load(std::memory_order_acquire) == 2 ? (void *)e->fn : nullptr;
 }
 
-// Asynchronous form: returns 1 (ready, *fn set), 0 (compiling in the
-// background; poll *entry with ngz_rtc_poll) or -1 (failed).
-int ngz_rtc_kernel_async(int device, const DevPlan &P, void **fn, void **entry) {
-    const std::string sig = signature(P);
+template <class Gen>
+int kernel_async(int device, const std::string &sig, Gen &&gen, const char *kname, void **fn, void **entry) {
     Entry *e = entry_for(device, sig);
     *entry = e;
     int st = 0;
     if (e->state.compare_exchange_strong(st, 1)) {
-        std::string src = generate(P);  // the plan's field table is the caller's: read it now
+        std::string src = gen();  // the plans' field tables are the caller's: read them now
         static std::once_flag once;
         std::call_once(once, [] {
             prime_rtc_runtime();
             std::atexit(join_workers_at_exit);
         });
         std::lock_guard<std::mutex> lk(g_workers.mu);
-        g_workers.th.emplace_back(build, e, device, std::move(src), sig);
+        g_workers.th.emplace_back(build, e, device, std::move(src), sig, kname);
         return 0;
     }
     if (st == 2) {
@@ -640,6 +720,38 @@ int ngz_rtc_kernel_async(int device, const DevPlan &P, void **fn, void **entry) 
         return 1;
     }
     return st == 3 ? -1 : 0;
+}
+
+std::string group_signature(const DevPlan *const *plans, uint32_t n) {
+    std::string s = "G";
+    for (uint32_t k = 0; k < n; ++k) s += "|" + signature(*plans[k]);
+    return s;
+}
+
+}  // namespace
+
+// Specialised kernel for a plan on `device`, compiled on first use and cached,
+// waiting for it if needed; nullptr when compilation failed (the caller falls
+// back to the generic kernel).
+void *ngz_rtc_kernel(int device, const DevPlan &P) {
+    return kernel_sync(device, signature(P), [&] { return generate(P); }, "ngz_tpl");
+}
+
+// Asynchronous form: returns 1 (ready, *fn set), 0 (compiling in the
+// background; poll *entry with ngz_rtc_poll) or -1 (failed).
+int ngz_rtc_kernel_async(int device, const DevPlan &P, void **fn, void **entry) {
+    return kernel_async(device, signature(P), [&] { return generate(P); }, "ngz_tpl", fn, entry);
+}
+
+// The multi-template kernel of n (2..NGZ_RTC_GROUP_MAX) LDS-staged fixed
+// plans of one lds_waves (generate_group), in both forms.
+void *ngz_rtc_group(int device, const DevPlan *const *plans, uint32_t n) {
+    return kernel_sync(device, group_signature(plans, n), [&] { return generate_group(plans, n); }, "ngz_tplm");
+}
+
+int ngz_rtc_group_async(int device, const DevPlan *const *plans, uint32_t n, void **fn, void **entry) {
+    return kernel_async(device, group_signature(plans, n), [&] { return generate_group(plans, n); }, "ngz_tplm", fn,
+                        entry);
 }
 
 int ngz_rtc_poll(void *entry, void **fn) {
@@ -661,6 +773,31 @@ int ngz_rtc_launch(void *fn, const BatchDev *B, uint32_t slot, uint32_t grid, ui
     uint32_t s = slot;
     void *args[] = {&b, &s};
     return hipModuleLaunchKernel((hipFunction_t)fn, grid, 1, 1, block, 1, 1, 0, st, args, nullptr) == hipSuccess ? 0 : -1;
+}
+
+// Launch a multi-template kernel over the slots (the templates' order of the group).
+int ngz_rtc_launch_group(void *fn, const BatchDev *B, const uint32_t *slots, uint32_t n, uint32_t grid, uint32_t block,
+                         hipStream_t st) {
+    if (n > NGZ_RTC_GROUP_MAX) return -1;
+    BatchDev b = *B;
+    struct {
+        uint32_t s[NGZ_RTC_GROUP_MAX];
+    } S{};
+    for (uint32_t k = 0; k < n; ++k) S.s[k] = slots[k];
+    void *args[] = {&b, &S};
+    return hipModuleLaunchKernel((hipFunction_t)fn, grid, 1, 1, block, 1, 1, 0, st, args, nullptr) == hipSuccess ? 0 : -1;
+}
+
+// The generated multi-template source (introspection / tests).
+std::string ngz_rtc_group_source(const DevPlan *const *plans, uint32_t n) { return generate_group(plans, n); }
+
+// Compile a generated source without loading it (no device needed): 0 ok, -1 failed.
+int ngz_rtc_compile_source(const std::string &src, std::string *log_out) {
+    std::vector<char> code;
+    std::string log;
+    const bool ok = compile(src, code, log);
+    if (log_out) *log_out = log;
+    return ok ? 0 : -1;
 }
 
 // Generate and compile without loading (no device needed): 0 ok, -1 failed.

@@ -148,3 +148,33 @@ def test_template_kernels_compile_for_gfx950(tid):
     assert rc == 0, src[-2000:]
     assert "ngz_tpl" in src
     assert ("run_lds" in src) == ("NGZ_LDS_WAVES" in src)
+
+
+@pytest.mark.parametrize("workload", ["cfg3", "cfg5"])
+def test_group_kernels_compile_for_gfx950(workload):
+    """The multi-template decode kernel (one launch for the LDS-staged templates of a batch that
+    share a workgroup shape, ngz_rtc.cpp generate_group) of every such group of config 3 / 5 is
+    generated and compiled for gfx950 by hiprtc; each template keeps its own constant-offset
+    body."""
+    import re
+    import struct
+    from netgauze_amd import _lib, synth
+    tpls = synth.CFG3_TEMPLATES if workload == "cfg3" else synth.CFG5_TEMPLATES
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    buf = ctypes.create_string_buffer(4 << 20)
+    groups = {}
+    for tid, fields in tpls:
+        rec = struct.pack(">HH", tid, len(fields)) + b"".join(struct.pack(">HH", i, ln) for i, ln in fields)
+        assert lib.ngz_template_kernel(rec, len(rec), 0, buf, len(buf)) == 0
+        lw = int(re.search(r"NGZ_LDS_WAVES (\d+)", buf.value.decode()).group(1))
+        groups.setdefault(lw, []).append(rec)
+    assert sum(len(g) for g in groups.values()) == len(tpls)
+    for lw, recs in groups.items():
+        body = b"".join(recs)
+        rc = lib.ngz_group_kernel(body, len(body), 1, buf, len(buf))
+        src = buf.value.decode()
+        assert rc == 0, src[-2000:]
+        assert "ngz_tplm" in src and src.count("::run(B, S.s[") == len(recs)
+        assert "__launch_bounds__(%d)" % (64 * lw) in src
+    one = struct.pack(">HH", 256, len(synth.T20)) + b"".join(struct.pack(">HH", i, ln) for i, ln in synth.T20)
+    assert lib.ngz_group_kernel(one, len(one), 0, buf, len(buf)) == -1  # a group has at least two templates

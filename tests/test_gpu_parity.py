@@ -348,9 +348,12 @@ def test_cfg5_shard_full_size(dev):
     assert codec.template_counts(10) == msgs
 
 
-def test_cfg3_mixed_templates_oracle(dev):
+@pytest.mark.parametrize("group", ["0", "1"])
+def test_cfg3_mixed_templates_oracle(dev, group, monkeypatch):
     """Config 3 shape (8 templates, 40-153 B records, interleaved messages)
-    against the oracle, every field."""
+    against the oracle, every field; one launch per template or one
+    multi-template launch per workgroup shape (NGZ_GROUP)."""
+    monkeypatch.setenv("NGZ_GROUP", group)
     from netgauze_amd import synth
     b, o, ln, _ = synth.mixed_stream(24_000)
     bb = bytes(b.numpy())
@@ -360,10 +363,13 @@ def test_cfg3_mixed_templates_oracle(dev):
     assert codec.template_counts(10) == {t: oc.ipfix_templates[t].processed_count for t, _ in synth.CFG3_TEMPLATES}
 
 
-def test_cfg5_sixteen_templates_sharded(dev):
+@pytest.mark.parametrize("group", ["0", "1"])
+def test_cfg5_sixteen_templates_sharded(dev, group, monkeypatch):
     """Config 5 shape (16 templates: config 3 + width permutations) against
     the oracle, decoded as two shards on two contexts (ranks) as bench.py
-    --gpus N does; the shards' processed counts add up to the oracle's."""
+    --gpus N does; the shards' processed counts add up to the oracle's.  One
+    launch per template or per workgroup shape (NGZ_GROUP)."""
+    monkeypatch.setenv("NGZ_GROUP", group)
     from netgauze_amd import dist, synth
     b, o, ln, _ = synth.mixed_stream(32_000, templates=synth.CFG5_TEMPLATES, seed=synth.SEED_CFG5)
     bb = bytes(b.numpy())
@@ -386,9 +392,12 @@ def test_cfg5_sixteen_templates_sharded(dev):
     assert total == {t: oc.ipfix_templates[t].processed_count for t, _ in synth.CFG5_TEMPLATES}
 
 
-def test_cfg3_mixed_templates_1e7(dev):
+@pytest.mark.parametrize("group", ["0", "1"])
+def test_cfg3_mixed_templates_1e7(dev, group, monkeypatch):
     """Config 3 at 10^7 records (1.25e6 per template): every column of every
-    template compared on the GPU with the wire bytes re-laid."""
+    template compared on the GPU with the wire bytes re-laid, one launch per
+    template or per workgroup shape (NGZ_GROUP)."""
+    monkeypatch.setenv("NGZ_GROUP", group)
     from netgauze_amd import synth
     codec = new_codec()
     codec.decode_datagrams([synth.templates_message(synth.CFG3_TEMPLATES)])
