@@ -333,7 +333,7 @@ def main_agg(args):
         "config": {"workload": "aggregate %d T20 records, %d key fields + %d aggregated fields, 2 minute windows"
                    % (n, len(keys), len(vals)), "groups": groups, "table_capacity": cap, "late_records": late,
                    "first_push_ms": first_push_ms},
-        "push_kernels_ms": avg, "push_records_per_s": n / (avg * 1e-3),
+        "push_kernels_ms": avg, "push_records_per_s": n / (avg * 1e-3), "path": agg.last_path(),
         "roofline": {"bound": "hbm (atomic-throughput limited)", "achieved": alg / (avg * 1e-3) / 1e9,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": alg / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS,
                      "traffic": None, "alg_bytes_per_launch": alg, "alg_bytes_per_record": per_rec}}), flush=True)

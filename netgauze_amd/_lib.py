@@ -40,7 +40,7 @@ INGEST_FUNCTIONS = [
 AGG_FUNCTIONS = [
     "ngz_agg_create", "ngz_agg_destroy", "ngz_agg_last_error", "ngz_agg_push", "ngz_agg_layout",
     "ngz_agg_groups", "ngz_agg_flush", "ngz_agg_closed", "ngz_agg_emit", "ngz_agg_reset", "ngz_agg_sets",
-    "ngz_agg_key_info", "ngz_agg_value_info", "ngz_agg_flowinfo_json", "ngz_agg_last_timing", "ngz_agg_peer",
+    "ngz_agg_key_info", "ngz_agg_value_info", "ngz_agg_flowinfo_json", "ngz_agg_last_timing", "ngz_agg_peer", "ngz_agg_last_path",
 ]
 NGZ_AGG_KEY, NGZ_AGG_ADD, NGZ_AGG_MIN, NGZ_AGG_MAX, NGZ_AGG_OR = range(5)
 NGZ_AGG_E_OVERFLOW, NGZ_AGG_E_COLLISION, NGZ_AGG_E_POISONED = -10, -11, -12
@@ -241,6 +241,8 @@ def load():
     lib.ngz_agg_flowinfo_json.restype = ctypes.c_int64
     lib.ngz_agg_peer.argtypes = [P, U32, ctypes.POINTER(Peer)]
     lib.ngz_agg_peer.restype = I
+    lib.ngz_agg_last_path.argtypes = [P]
+    lib.ngz_agg_last_path.restype = ctypes.c_char_p
     # ingest (flow_ingest.h)
     lib.ngz_pcap_open.argtypes = [ctypes.c_char_p, ctypes.POINTER(P)]
     lib.ngz_pcap_open.restype = I

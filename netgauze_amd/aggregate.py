@@ -78,7 +78,7 @@ def _datetime_ms(ms):
 class FlowAggregator:
     DEFAULT_PEER = "192.0.2.1"  # TEST-NET-1: the exporter of pushes that name none
 
-    def __init__(self, transform, window_s=60, lateness_s=10, capacity=1 << 20, device=0, kinds=None, max_peers=0):
+    def __init__(self, transform, window_s=60, lateness_s=10, capacity=1 << 20, device=0, kinds=None, max_peers=256):
         self.fields = unify(transform) if isinstance(transform, dict) else list(transform)
         self.key_fields = [f for f in self.fields if f[3] == _lib.NGZ_AGG_KEY]
         self.val_fields = [f for f in self.fields if f[3] != _lib.NGZ_AGG_KEY]
@@ -131,6 +131,10 @@ class FlowAggregator:
             lib().ngz_agg_peer(self._h, i, ctypes.byref(p))
             out.append(p.ip())
         return out
+
+    def last_path(self):
+        """"lowcard" or "general": the reduction path of the last push."""
+        return lib().ngz_agg_last_path(self._h).decode()
 
     def push_ms(self):
         t = ctypes.c_float()

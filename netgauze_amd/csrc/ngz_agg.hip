@@ -1374,6 +1374,285 @@ __global__ __launch_bounds__(256) void k_agg_part_reduce(const AggParams P, cons
     }
 }
 
+// ---------------------------------------------------------------------------
+// Low-cardinality pushes (packed keys, few distinct key tuples): no per-record
+// context, slot claim or atomic per record.  k_agg_lc_scan walks the sets (one
+// wave per set, 64 records per step) and lists the push's distinct exact tags
+// (window, flow type, peer, keys) in a small table, each wave offering a tag
+// once; the wave that enters a tag claims its group in the HBM table (the same
+// probe as k_agg_claim).  k_agg_lc_reduce then reads every record's key and
+// value columns once, coalesced, and reduces them in registers: each lane
+// keeps one accumulator per (distinct key tuple, aggregated field) of the
+// current (window, flow type) -- a record updates the accumulators of its key
+// tuple through predicated selects, no atomics -- and the per-set header fields
+// (export time bounds, sys-up time, template and domain sets) are uniform per
+// set.  A wave flushes its accumulators (wave reductions, then the row update of
+// k_agg_apply's leader path) when its sets move to another window and at its
+// end: a few flushes per wave instead of 10^8 LDS atomics.
+// ---------------------------------------------------------------------------
+constexpr uint32_t LC_SLOTS = 256;    // small table of the push's distinct tags (open addressing)
+constexpr uint32_t LC_MAX_TAGS = 64;  // more distinct tags: the general path
+constexpr int LC_NK = 8;              // distinct key tuples a lane accumulates (more: the general path)
+constexpr int LC_MAXV = 8;            // aggregated fields (more: the general path)
+
+struct LcTable {
+    unsigned long long tag[LC_SLOTS];  // 0 = empty
+    uint32_t slot[LC_SLOTS];           // the tag's group in the HBM table
+    uint32_t count;                    // distinct tags entered
+    uint32_t overflow;                 // more than LC_MAX_TAGS
+};
+
+struct LcKeys {  // the push's distinct key tuples (packed key bits of the tag)
+    unsigned long long kp[LC_NK];
+    unsigned long long kmask;  // key bits of a tag
+    uint32_t nk;
+    uint32_t key_bits;
+};
+
+__device__ __forceinline__ uint32_t lc_home(uint64_t tag) { return (uint32_t)(slot_of(tag) & (LC_SLOTS - 1)); }
+
+// XCD-aware set order: workgroup b works through the (b % 8)-th eighth of the sets
+struct SetSeq {
+    uint32_t first, step, end;
+};
+__device__ __forceinline__ SetSeq set_seq(uint32_t n_sets) {
+    const uint32_t wpb = blockDim.x >> 6, q = threadIdx.x >> 6;
+    const uint32_t G = gridDim.x, X = (G % 8 == 0 && G >= 8) ? 8u : 1u;
+    const uint32_t x = blockIdx.x % X, l = blockIdx.x / X;
+    const uint32_t per = (n_sets + X - 1) / X, start = x * per;
+    return SetSeq{start + l * wpb + q, (G / X) * wpb, min(n_sets, start + per)};
+}
+
+// A set's records aggregated by this push: its plan, or null (no records, late or failed
+// datagram, slot not aggregated); *late: the set's records are late
+__device__ __forceinline__ const AggSlotPlan *lc_set(const ngz_set_info &si, const uint16_t *__restrict__ dginfo,
+                                                     const AggSlotPlan *__restrict__ plans, uint32_t n_dgrams,
+                                                     uint32_t n_slots, bool *late, uint16_t *info,
+                                                     unsigned int *__restrict__ err) {
+    *late = false;
+    if (!si.n) return nullptr;
+    if (si.dgram >= n_dgrams || si.slot >= n_slots) {
+        if ((threadIdx.x & 63) == 0) atomicOr(err, 16u);
+        return nullptr;
+    }
+    *info = dginfo[si.dgram];
+    if (*info & DG_LATE) { *late = true; return nullptr; }
+    if (!(*info & DG_USE) || !plans[si.slot].usable) return nullptr;
+    return &plans[si.slot];
+}
+
+__global__ __launch_bounds__(256) void k_agg_lc_scan(const ngz_set_info *__restrict__ sets, uint32_t n_sets,
+                                                     const ngz_dgram_hdr *__restrict__ hdr,
+                                                     const uint16_t *__restrict__ dginfo,
+                                                     const AggSlotPlan *__restrict__ plans, uint32_t n_dgrams,
+                                                     uint32_t n_slots, const AggParams P,
+                                                     unsigned long long *__restrict__ tags, uint8_t *__restrict__ rows,
+                                                     uint32_t *__restrict__ claims,
+                                                     unsigned long long *__restrict__ n_claims,
+                                                     unsigned long long *__restrict__ late_count,
+                                                     LcTable *__restrict__ lt, unsigned int *__restrict__ err) {
+    const uint32_t lane = threadIdx.x & 63;
+    uint64_t seen = 0;  // lane i: the i-th tag this wave entered or found entered
+    uint32_t n_seen = 0;
+    const SetSeq ss = set_seq(n_sets);
+    for (uint32_t s = ss.first; s < ss.end; s += ss.step) {
+        if (*(volatile uint32_t *)&lt->overflow) return;
+        const ngz_set_info si = sets[s];
+        bool late;
+        uint16_t info = 0;
+        const AggSlotPlan *spp = lc_set(si, dginfo, plans, n_dgrams, n_slots, &late, &info, err);
+        if (late && lane == 0) atomicAdd(late_count, (unsigned long long)si.n);
+        if (!spp) continue;
+        const AggSlotPlan &sp = *spp;
+        const uint32_t ts = hdr[si.dgram].time, win = ts - ts % 60;
+        for (uint32_t c = 0; c < si.n; c += 64) {
+            const bool valid = c + lane < si.n;
+            const uint64_t row = (uint64_t)si.rec0 + c + lane;
+            uint32_t kp = 0;
+            KeyVal kv;
+            const uint64_t tag = valid ? key_tag(sp, P, row, win, kp, kv) : 0ull;
+            uint64_t todo = __ballot(valid);
+            while (todo) {
+                const int l0 = __ffsll((unsigned long long)todo) - 1;
+                const uint64_t t = readlane64(tag, l0);
+                todo &= ~__ballot(valid && tag == t);
+                if (__ballot(lane < n_seen && seen == t)) continue;  // offered by this wave already
+                if (lane == (uint32_t)l0) {
+                    uint32_t i = lc_home(t);
+                    for (uint32_t probes = 0;; ++probes, i = (i + 1) & (LC_SLOTS - 1)) {
+                        if (probes == LC_SLOTS) { atomicOr(&lt->overflow, 1u); break; }
+                        unsigned long long cur = lt->tag[i];
+                        if (cur == 0) {
+                            cur = atomicCAS(&lt->tag[i], 0ull, (unsigned long long)t);
+                            if (cur == 0) {  // entered here: claim / find the group
+                                if (atomicAdd(&lt->count, 1u) >= LC_MAX_TAGS) atomicOr(&lt->overflow, 1u);
+                                bool tent = false, claimed = false;
+                                const uint32_t g = probe<false>(sp, P, row, win, kp, kv, t, tags, rows, err, &tent,
+                                                                &claimed);
+                                lt->slot[i] = g;
+                                if (claimed) claims[atomicAdd(n_claims, 1ull)] = g;
+                                break;
+                            }
+                        }
+                        if (cur == t) break;
+                    }
+                }
+                if (n_seen < 64) {
+                    if (lane == n_seen) seen = t;
+                    ++n_seen;
+                }
+            }
+        }
+    }
+}
+
+// One wave per workgroup; its accumulators live in LDS, lane-private: cell (k, v) of lane l
+// at acc[(k * nv + v) * 64 + l] (a lane only touches its own cells, no conflicts between lanes,
+// no atomics), so a record costs one LDS read-modify-write per aggregated field of its key
+// tuple instead of a predicated update of every tuple's accumulators in registers.
+__global__ __launch_bounds__(64) void k_agg_lc_reduce(const ngz_set_info *__restrict__ sets, uint32_t n_sets,
+                                                      const ngz_dgram_hdr *__restrict__ hdr,
+                                                      const uint16_t *__restrict__ dginfo,
+                                                      const AggSlotPlan *__restrict__ plans, uint32_t n_dgrams,
+                                                      uint32_t n_slots, const AggParams P, const LcKeys K,
+                                                      uint8_t *__restrict__ rows, const LcTable *__restrict__ lt,
+                                                      unsigned int *__restrict__ err) {
+    extern __shared__ unsigned long long lc_lds[];
+    const uint32_t nk = K.nk, nv = P.n_vals;
+    unsigned long long *acc = lc_lds;                          // [nk][nv][64]
+    uint32_t *cnt = (uint32_t *)(acc + (size_t)nk * nv * 64);  // [nk][64]
+    // per key tuple, uniform per set (lane k updates entry k once per set): export time bounds,
+    // sys-up time, fields present, template and domain sets
+    __shared__ uint32_t h_tmin[LC_NK], h_tmax[LC_NK], h_smax[LC_NK], h_vp[LC_NK];
+    __shared__ unsigned long long h_tpl[LC_NK], h_d0[LC_NK], h_d1[LC_NK];
+    const uint32_t lane = threadIdx.x;
+    auto reset = [&]() {
+        for (uint32_t k = 0; k < nk; ++k) {
+            cnt[k * 64 + lane] = 0;
+            for (uint32_t v = 0; v < nv; ++v) acc[(k * nv + v) * 64 + lane] = P.val_op[v] == NGZ_AGG_MIN ? ~0ull : 0ull;
+        }
+        if (lane < LC_NK) {
+            h_tmin[lane] = 0xFFFFFFFFu;
+            h_tmax[lane] = h_smax[lane] = h_vp[lane] = 0;
+            h_tpl[lane] = h_d0[lane] = h_d1[lane] = 0;
+        }
+        __syncthreads();
+    };
+    // the accumulators of window context ctx into their groups' rows
+    auto flush = [&](uint64_t ctx) {
+#pragma unroll
+        for (int k = 0; k < LC_NK; ++k) {  // unrolled: K.kp[k] stays a kernel argument register
+            if (k >= (int)nk) break;
+            const uint64_t total = wave_reduce<R_ADD>((uint64_t)cnt[k * 64 + lane]);
+            if (!total) continue;
+            const uint64_t tag = (ctx << K.key_bits) | K.kp[k] | (1ull << 63);  // key_tag's exact tag
+            uint32_t i = lc_home(tag), g = NONE;
+            for (uint32_t probes = 0; probes < LC_SLOTS; ++probes, i = (i + 1) & (LC_SLOTS - 1)) {
+                const unsigned long long t = lt->tag[i];
+                if (t == tag) { g = lt->slot[i]; break; }
+                if (t == 0) break;
+            }
+            if (g == NONE) {
+                if (lane == 0) atomicOr(err, 4u);  // a tag the scan did not enter (cannot happen)
+                continue;
+            }
+            uint8_t *R = rows + (uint64_t)g * P.row_bytes;
+            const uint32_t vpk = h_vp[k];
+            if (lane == 0) {
+                atomicAdd((unsigned long long *)(R + 16), (unsigned long long)total);
+                atomicMin((unsigned int *)(R + 24), h_tmin[k]);
+                atomicMax((unsigned int *)(R + 28), h_tmax[k]);
+                if (h_smax[k]) atomicMax((unsigned int *)(R + 32), h_smax[k]);
+                atomicOr((unsigned long long *)(R + 56), h_tpl[k]);
+                if (h_d0[k]) atomicOr((unsigned long long *)(R + 72), h_d0[k]);
+                if (h_d1[k]) atomicOr((unsigned long long *)(R + 80), h_d1[k]);
+                apply_push_constants(R, P);
+                if (vpk) atomicOr((unsigned int *)(R + 12), vpk);
+            }
+            for (uint32_t v = 0; v < nv; ++v) {
+                if (!((vpk >> v) & 1)) continue;
+                const uint8_t op = P.val_op[v];
+                const uint64_t a = acc[(k * nv + v) * 64 + lane];
+                uint64_t r;
+                switch (op) {
+                case NGZ_AGG_ADD: r = wave_reduce<R_ADD>(a); break;
+                case NGZ_AGG_MIN: r = wave_reduce<R_MIN>(a); break;
+                case NGZ_AGG_MAX: r = wave_reduce<R_MAX>(a); break;
+                default: r = wave_reduce<R_OR>(a); break;
+                }
+                if (lane == 0) apply_value_hot(R + P.val_off[v], op, r);
+            }
+        }
+    };
+    reset();
+    uint64_t cur = ~0ull;  // current window context (window / 60, flow type, peer); none yet
+    const SetSeq ss = set_seq(n_sets);
+    for (uint32_t s = ss.first; s < ss.end; s += ss.step) {
+        const ngz_set_info si = sets[s];
+        bool late;
+        uint16_t info = 0;
+        const AggSlotPlan *spp = lc_set(si, dginfo, plans, n_dgrams, n_slots, &late, &info, err);
+        if (!spp) continue;
+        const AggSlotPlan &sp = *spp;
+        const ngz_dgram_hdr &h = hdr[si.dgram];
+        const uint32_t ts = h.time, win = ts - ts % 60;
+        const uint64_t ctx = ((((uint64_t)(win / 60) << 1) | (sp.proto == 9)) << P.peer_bits) | P.peer;
+        if (ctx != cur) {
+            if (cur != ~0ull) flush(cur);
+            reset();
+            cur = ctx;
+        }
+        uint32_t hv = 0;  // aggregated fields the set's template has (Some)
+        for (uint32_t v = 0; v < nv; ++v)
+            if (sp.val_col[v]) hv |= 1u << v;
+        uint32_t mset = 0;  // key tuples present in the set
+        for (uint32_t c = 0; c < si.n; c += 64) {
+            const bool valid = c + lane < si.n;
+            const uint64_t row = (uint64_t)si.rec0 + c + lane;
+            uint32_t kp = 0;
+            KeyVal kv;
+            const uint64_t key = valid ? (key_tag(sp, P, row, win, kp, kv) & K.kmask) : ~0ull;
+            uint32_t kidx = LC_NK;
+#pragma unroll
+            for (int k = 0; k < LC_NK; ++k)
+                if (k < (int)nk && key == K.kp[k]) kidx = (uint32_t)k;
+            const bool in = valid && kidx < nk;
+#pragma unroll
+            for (int k = 0; k < LC_NK; ++k)
+                if (k < (int)nk && __ballot(in && kidx == (uint32_t)k)) mset |= 1u << k;
+            if (in) {
+                cnt[kidx * 64 + lane] += 1;
+#pragma unroll
+                for (int v = 0; v < LC_MAXV; ++v) {
+                    if (v >= (int)nv) break;
+                    if (!((hv >> v) & 1)) continue;
+                    const uint64_t x = value_operand(sp, P, v, row);
+                    unsigned long long *cell = &acc[(kidx * nv + v) * 64 + lane];
+                    const uint64_t a = *cell;
+                    switch (P.val_op[v]) {
+                    case NGZ_AGG_ADD: *cell = a + x; break;
+                    case NGZ_AGG_MIN: *cell = x < a ? x : a; break;
+                    case NGZ_AGG_MAX: *cell = x > a ? x : a; break;
+                    default: *cell = a | x; break;
+                    }
+                }
+            }
+        }
+        if (lane < nk && ((mset >> lane) & 1)) {
+            const uint32_t k = lane, db = (info >> 2) & 0x7F;
+            h_tmin[k] = min(h_tmin[k], ts);
+            h_tmax[k] = max(h_tmax[k], ts);
+            h_smax[k] = max(h_smax[k], h.version == 9 ? h.sys_up_time : 0u);
+            h_tpl[k] |= sp.tpl_bit;
+            if (db < 64) h_d0[k] |= 1ull << db;
+            else h_d1[k] |= 1ull << (db & 63);
+            h_vp[k] |= hv;
+        }
+        __syncthreads();
+    }
+    if (cur != ~0ull) flush(cur);
+}
+
 __global__ void k_agg_init(uint8_t *__restrict__ rows, uint64_t n_groups, uint32_t row_bytes,
                            const uint32_t *__restrict__ ident, uint32_t ident_words) {
     // every row <- the identity row (min fields at their maximum)
@@ -1512,6 +1791,8 @@ struct ngz_agg {
     size_t rec_cap = 0;
     uint8_t *part_buf = nullptr;  // partitioned reduction: counts, offsets, scan scratch, payloads
     size_t part_cap = 0;
+    LcTable *lc = nullptr;        // low-cardinality path: the push's distinct tags
+    const char *last_path = "";   // the reduction path of the last push ("lowcard" / "general")
 };
 
 namespace {
@@ -1999,6 +2280,7 @@ void ngz_agg_destroy(ngz_agg *a) {
     hipFree(a->scratch);
     hipFree(a->rec_buf);
     hipFree(a->part_buf);
+    hipFree(a->lc);
     if (a->ev0) hipEventDestroy(a->ev0);
     if (a->ev1) hipEventDestroy(a->ev1);
     if (a->stream) hipStreamDestroy(a->stream);
@@ -2282,9 +2564,6 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, const ngz_p
     uint4 *rinfo = (uint4 *)a->rec_buf;
     uint32_t *rec_g = (uint32_t *)(a->rec_buf + 4 * R4), *claims = (uint32_t *)(a->rec_buf + 5 * R4),
              *list_a = (uint32_t *)(a->rec_buf + 6 * R4), *list_b = (uint32_t *)(a->rec_buf + 7 * R4);
-    hipLaunchKernelGGL(k_agg_recinfo, dim3(grid_for(64ull * NS, 256, 4096)), dim3(256), 0, st, sets, rstart, NS, hdr,
-                       dginfo, a->plans, D, S, rinfo, a->err);
-    AGG_HIP(a, hipGetLastError());
     const RecCtx C{rinfo, (uint64_t)n_rec, a->plans};
     const uint32_t blocks = (uint32_t)((n_rec + 255) / 256);
     static const uint32_t grid_cap = getenv("NGZ_AGG_GRID") ? (uint32_t)std::max(1, atoi(getenv("NGZ_AGG_GRID"))) : 4096u;
@@ -2298,6 +2577,72 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, const ngz_p
         if (hipStreamSynchronize(st) != hipSuccess) a->poisoned = true;
         return fail(a, rc, why);
     };
+    // Low-cardinality path (packed keys, no byte-wise / ordered values): k_agg_lc_scan lists
+    // the push's distinct tags and claims their groups; with at most LC_NK distinct key
+    // tuples k_agg_lc_reduce reduces every record in registers.  Otherwise the general
+    // path below takes over from the claims made so far (NGZ_AGG_LC: 0 never, 1 at any
+    // size; default from 2^16 records).
+    static const int lc_env = getenv("NGZ_AGG_LC") ? atoi(getenv("NGZ_AGG_LC")) : -1;
+    const int lc_now = getenv("NGZ_AGG_LC") ? atoi(getenv("NGZ_AGG_LC")) : lc_env;  // read per push (tests)
+    if (n_rec && P.packed && P.lds_ok && P.n_vals <= (uint32_t)LC_MAXV && !ordered && lc_now != 0 &&
+        (lc_now == 1 || n_rec >= (1u << 16))) {
+        if (!a->lc && hipMalloc(&a->lc, sizeof(LcTable)) != hipSuccess) {
+            a->lc = nullptr;
+            restore();
+            upload_domains(a);
+            return fail(a, NGZ_E_NOMEM, "low-cardinality table");
+        }
+        AGG_HIP(a, hipMemsetAsync(a->lc, 0, sizeof(LcTable), st));
+        const uint32_t waves = std::max<uint32_t>(1, std::min<uint32_t>(NS, 256u * 64u));
+        const uint32_t sg = std::max<uint32_t>(8, ((waves + 3) / 4 + 7) & ~7u);
+        hipLaunchKernelGGL(k_agg_lc_scan, dim3(sg), dim3(256), 0, st, sets, NS, hdr, dginfo, a->plans, D, S, P, a->tags,
+                           a->rows, claims, a->n_claims, a->late, a->lc, a->err);
+        AGG_HIP(a, hipGetLastError());
+        LcTable lt;
+        AGG_HIP(a, hipMemcpyAsync(&lt, a->lc, sizeof lt, hipMemcpyDeviceToHost, st));
+        AGG_HIP(a, hipMemcpyAsync(&n_claims, a->n_claims, 8, hipMemcpyDeviceToHost, st));
+        AGG_HIP(a, hipMemcpyAsync(&errv, a->err, 4, hipMemcpyDeviceToHost, st));
+        AGG_HIP(a, hipStreamSynchronize(st));
+        if (errv & 16) { a->poisoned = true; return rollback(NGZ_E_DEVICE, "set table entry out of range"); }
+        if (errv & 2) return rollback(NGZ_AGG_E_OVERFLOW, "group table full");
+        LcKeys K{};
+        uint32_t kb = 0;
+        for (uint32_t k = 0; k < P.n_keys; ++k) kb += 1 + 8 * P.key_pw[k];
+        K.key_bits = kb;
+        K.kmask = (1ull << kb) - 1;
+        bool fast = !lt.overflow;
+        std::vector<unsigned long long> kps;
+        for (uint32_t i = 0; fast && i < LC_SLOTS; ++i) {
+            if (!lt.tag[i]) continue;
+            const unsigned long long kp = lt.tag[i] & K.kmask;
+            if (std::find(kps.begin(), kps.end(), kp) == kps.end()) kps.push_back(kp);
+            fast = kps.size() <= (size_t)LC_NK;
+        }
+        if (fast) {
+            if (a->live + n_claims > a->limit) return rollback(NGZ_AGG_E_OVERFLOW, "more groups than the aggregator's capacity");
+            std::sort(kps.begin(), kps.end());
+            K.nk = (uint32_t)kps.size();
+            for (uint32_t k = 0; k < K.nk; ++k) K.kp[k] = kps[k];
+            // one wave per workgroup; its LDS accumulators bound the residency (160 KB per CU):
+            // a grid of that many workgroups, a multiple of the 8 XCDs
+            const size_t lds = (size_t)K.nk * P.n_vals * 64 * 8 + (size_t)K.nk * 64 * 4;
+            const uint32_t per_cu = (uint32_t)std::max<size_t>(1, std::min<size_t>(16, (160u * 1024 - 1024) / (lds + 512)));
+            const uint32_t rg = std::max<uint32_t>(8, std::min<uint32_t>(256 * per_cu, (NS + 7) & ~7u));
+            hipLaunchKernelGGL(k_agg_lc_reduce, dim3(rg), dim3(64), lds, st, sets, NS, hdr, dginfo, a->plans, D, S, P, K,
+                               a->rows, a->lc, a->err);
+            AGG_HIP(a, hipGetLastError());
+            a->last_path = "lowcard";
+            goto done;
+        }
+        // too many distinct tags / key tuples: the general path (its claims continue the list,
+        // its claim pass counts the late records again)
+        AGG_HIP(a, hipMemsetAsync(a->late, 0, 8, st));
+    }
+    a->last_path = "general";
+    {
+    hipLaunchKernelGGL(k_agg_recinfo, dim3(grid_for(64ull * NS, 256, 4096)), dim3(256), 0, st, sets, rstart, NS, hdr,
+                       dginfo, a->plans, D, S, rinfo, a->err);
+    AGG_HIP(a, hipGetLastError());
     // claim / check keep no state across tiles: one record per thread, all of them in flight
     const uint32_t fg = std::max<uint32_t>(1, std::min<uint32_t>(blocks, 1u << 20));
     if (n_rec) {
@@ -2422,6 +2767,8 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, const ngz_p
         }
     }
     AGG_HIP(a, hipGetLastError());
+    }
+done:
     AGG_HIP(a, hipEventRecord(a->ev1, st));
     uint32_t last_pm = 0;
     unsigned long long late = 0;
@@ -2534,6 +2881,8 @@ int ngz_agg_peer(ngz_agg *a, uint32_t index, ngz_peer *out) {
     if (out) *out = a->out_peers[index];
     return (int)a->out_peers.size();
 }
+
+const char *ngz_agg_last_path(ngz_agg *a) { return a ? a->last_path : ""; }
 
 int ngz_agg_last_timing(ngz_agg *a, float *push_ms) {
     if (!a) return NGZ_E_INVALID;

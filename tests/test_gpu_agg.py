@@ -655,7 +655,7 @@ def test_thousand_peers_one_aggregator(dev):
     b = bytes(buf.numpy())
     msgs = [bytearray(b[o:o + ln]) for o, ln in zip(offs.tolist(), lens.tolist())]
     peers = ["10.%d.%d.1" % (i // 250, i % 250) if i % 3 else "2001:db8::%x" % (i + 1) for i in range(n_peers)]
-    agg = FlowAggregator(fields, capacity=1 << 16, lateness_s=10)
+    agg = FlowAggregator(fields, capacity=1 << 16, lateness_s=10, max_peers=1024)
     o = A.FlowAggregatorOracle(fields, 60, 10)
     codecs, ocodecs = {}, {}
     tm = synth.template_message()
@@ -701,3 +701,98 @@ def test_tombstones_do_not_fill_the_table(dev):
         out += len(got)
     assert out == 23 * 900
     same_groups(agg.flush(), o.flush())
+
+
+@pytest.mark.parametrize("keys", [
+    [(0, 4, 0, OK), (0, 61, 0, OK)],  # protocol + direction: 6 key tuples
+    [(0, 4, 0, OK)],                  # protocol: 3
+    [(0, 61, 0, OK), (0, 60, 0, OK)],  # direction + ipVersion: 2
+])
+def test_lowcard_path_equals_oracle(dev, keys, monkeypatch):
+    """The low-cardinality path (k_agg_lc_scan + k_agg_lc_reduce: per-lane LDS accumulators,
+    no per-record atomics) on T20 streams whose export times go back and forth (late
+    messages dropped, windows closed push by push), equal to the oracle; the path is checked
+    to be the one taken."""
+    monkeypatch.setenv("NGZ_AGG_LC", "1")
+    from netgauze_amd.aggregate import FlowAggregator
+    from netgauze_amd.flow import FlowInfoCodec
+    import ngz_oracle as O
+    times = [1_700_000_010, 1_700_000_030, 1_700_000_015, 1_700_000_045, 1_700_000_020, 1_700_000_050,
+             1_700_000_061, 1_700_000_049]
+    d = t20_datagrams(6000, 100, times)
+    fields = keys + T20_AGG
+    codec, oc = FlowInfoCodec(), O.FlowInfoCodec()
+    agg = FlowAggregator(fields, lateness_s=10)
+    o = A.FlowAggregatorOracle(fields, 60, 10)
+    late = 0
+    for part in (d[:25], d[25:40], d[40:]):
+        late += agg.push(codec.decode_datagrams(part), 4739, 1_700_000_000_000)
+        assert agg.last_path() == "lowcard"
+        A.aggregate_datagrams(fields, part, 4739, 1_700_000_000_000, agg=o, codec=oc)
+        same_groups(agg.emit(), o.emit())
+    assert late == o.late and late > 0
+    same_groups(agg.flush(), o.flush())
+
+
+def test_lowcard_falls_back_on_many_key_tuples(dev, monkeypatch):
+    """A packed key with more than 8 distinct tuples in a push (protocol + source port) leaves
+    the low-cardinality path after its scan: the general path continues from the groups the
+    scan claimed, and every reference capture still equals the oracle."""
+    monkeypatch.setenv("NGZ_AGG_LC", "1")
+    from netgauze_amd.aggregate import FlowAggregator
+    from netgauze_amd.flow import FlowInfoCodec
+    paths = set()
+    for name in [c[0] for c in golden_io.cases()]:
+        for key, dgrams in peers_of(name).items():
+            codec = FlowInfoCodec()
+            agg = FlowAggregator(GOLDEN_AGG_PACKED, lateness_s=60)
+            h = len(dgrams) // 2
+            emitted = []
+            for part in (dgrams[:h], dgrams[h:]):
+                agg.push(codec.decode_datagrams(part), key[1], 1_700_000_000_000)
+                paths.add(agg.last_path())
+                emitted += agg.emit()
+            got = emitted + agg.flush()
+            o = A.aggregate_datagrams(GOLDEN_AGG_PACKED, dgrams, key[1], 1_700_000_000_000, lateness_s=60)
+            same_groups(got, o.emit() + o.flush())
+    assert paths == {"lowcard", "general"}, paths
+
+
+def test_lowcard_equals_general_at_full_size(dev, monkeypatch):
+    """Full size: 10^8 T20 records by protocol + flow direction (12 groups over two windows),
+    two pushes: the low-cardinality path and the general one give byte-identical rows (owner
+    word and push marker aside)."""
+    import numpy as np
+    from netgauze_amd import synth
+    from netgauze_amd.aggregate import FlowAggregator
+    from netgauze_amd.flow import FlowInfoCodec
+    n = 100_000_000
+    codec = FlowInfoCodec(0, rtc_sync=True)
+    codec.decode_datagrams([synth.template_message()])
+    rec = synth.t20_records(n, device=dev)
+    buf, offs, lens = synth.ipfix_data_stream(rec, 64)
+    del rec
+    m = torch.arange(offs.numel(), device=dev, dtype=torch.int64)
+    t = 1_700_000_010 + (m * 60) // offs.numel()  # two minute windows
+    for b in range(4):
+        buf[offs + 4 + b] = ((t >> (8 * (3 - b))) & 0xFF).to(torch.uint8)
+    del m, t
+    batch = codec.decode_batch(buf, offs, lens)
+    assert batch.n_records == n
+    fields = [(0, 4, 0, OK), (0, 61, 0, OK)] + T20_AGG
+    rows = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("NGZ_AGG_LC", mode)
+        agg = FlowAggregator(fields, capacity=1 << 10, lateness_s=60)
+        for _ in range(2):
+            assert agg.push(batch, 4739, 0) == 0
+            assert agg.last_path() == ("lowcard" if mode == "1" else "general")
+        _, raw = agg.flush_raw()
+        agg.close()
+        raw = np.array(raw)
+        raw[:, 88:92] = 0  # owner word
+        raw[:, 36:40] = 0  # push marker
+        rows[mode] = sorted(bytes(r) for r in raw)
+    assert len(rows["1"]) == 12
+    assert rows["0"] == rows["1"]
+    codec.close()
