@@ -221,7 +221,8 @@ int64_t ngz_agg_flowinfo_json(ngz_agg *a, const void *rows, uint64_t n, uint32_t
 int ngz_agg_last_timing(ngz_agg *a, float *push_ms);
 
 /* The reduction path the last push took: "lowcard" (packed keys with at most 8 distinct
- * key tuples: per-set register / LDS reduction, no per-record atomics) or "general". */
+ * key tuples: per-set LDS reduction, no per-record atomics), "general", or "none" (no
+ * record to reduce). */
 const char *ngz_agg_last_path(ngz_agg *a);
 
 #ifdef __cplusplus

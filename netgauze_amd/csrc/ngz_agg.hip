@@ -2311,6 +2311,7 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, const ngz_p
                  int64_t collection_time_ms, uint64_t *late_records, void *hip_stream) {
     if (!a || !ctx || !out || !peer || (peer->family != 4 && peer->family != 6)) return NGZ_E_INVALID;
     if (late_records) *late_records = 0;
+    a->last_path = "none";  // no record to reduce (set below otherwise)
     if (a->poisoned) return fail(a, NGZ_AGG_E_POISONED, "aggregator failed earlier: ngz_agg_reset it");
     AGG_HIP(a, hipSetDevice(a->device));
     if (hip_stream) AGG_HIP(a, hipStreamSynchronize((hipStream_t)hip_stream));
