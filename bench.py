@@ -133,6 +133,7 @@ def main():
                     help="device flow aggregation of decoded T20 columns instead (include/ngz/flow_aggregate.h): "
                          "key protocol+flowDirection (6 groups/window), protocol+dport (~2e5) or the 5-tuple "
                          "(~1 group per record); 7 aggregated fields")
+    ap.add_argument("--agg-max-peers", type=int, default=256, help="--agg: the aggregator's max_peers")
     args = ap.parse_args()
     if args.agg:
         return main_agg(args)
@@ -304,7 +305,7 @@ def main_agg(args):
     cap = {"proto_dir": 1 << 10, "dport": 1 << 20, "5tuple": n}[args.agg]
     # lateness = the window: the same batch pushed again is not late (its export times are
     # within 60 s of the event time), so every step aggregates every record
-    agg = FlowAggregator(keys + vals, capacity=cap, lateness_s=60)
+    agg = FlowAggregator(keys + vals, capacity=cap, lateness_s=60, max_peers=args.agg_max_peers)
     batch = codec.decode_batch(buf, offs, lens)
     assert batch.n_records == n
     # the first push creates every group (slot claims, key writes); the timed steps then

@@ -1466,6 +1466,7 @@ __global__ __launch_bounds__(256) void k_agg_lc_scan(const ngz_set_info *__restr
         const AggSlotPlan &sp = *spp;
         const uint32_t ts = hdr[si.dgram].time, win = ts - ts % 60;
         for (uint32_t c = 0; c < si.n; c += 64) {
+            if (*(volatile uint32_t *)&lt->overflow) return;  // the general path takes the push
             const bool valid = c + lane < si.n;
             const uint64_t row = (uint64_t)si.rec0 + c + lane;
             uint32_t kp = 0;
@@ -1473,19 +1474,24 @@ __global__ __launch_bounds__(256) void k_agg_lc_scan(const ngz_set_info *__restr
             const uint64_t tag = valid ? key_tag(sp, P, row, win, kp, kv) : 0ull;
             uint64_t todo = __ballot(valid);
             while (todo) {
+                if (*(volatile uint32_t *)&lt->overflow) return;
                 const int l0 = __ffsll((unsigned long long)todo) - 1;
                 const uint64_t t = readlane64(tag, l0);
                 todo &= ~__ballot(valid && tag == t);
                 if (__ballot(lane < n_seen && seen == t)) continue;  // offered by this wave already
-                if (lane == (uint32_t)l0) {
+                if (lane == (uint32_t)l0 && !*(volatile uint32_t *)&lt->overflow) {
                     uint32_t i = lc_home(t);
                     for (uint32_t probes = 0;; ++probes, i = (i + 1) & (LC_SLOTS - 1)) {
-                        if (probes == LC_SLOTS) { atomicOr(&lt->overflow, 1u); break; }
+                        // the table holds at most LC_MAX_TAGS of its LC_SLOTS: short probe chains
+                        if (probes == LC_SLOTS / 2) { atomicOr(&lt->overflow, 1u); break; }
                         unsigned long long cur = lt->tag[i];
                         if (cur == 0) {
                             cur = atomicCAS(&lt->tag[i], 0ull, (unsigned long long)t);
                             if (cur == 0) {  // entered here: claim / find the group
-                                if (atomicAdd(&lt->count, 1u) >= LC_MAX_TAGS) atomicOr(&lt->overflow, 1u);
+                                if (atomicAdd(&lt->count, 1u) >= LC_MAX_TAGS) {
+                                    atomicOr(&lt->overflow, 1u);
+                                    break;  // the general path claims it
+                                }
                                 bool tent = false, claimed = false;
                                 const uint32_t g = probe<false>(sp, P, row, win, kp, kv, t, tags, rows, err, &tent,
                                                                 &claimed);
@@ -1620,20 +1626,25 @@ __global__ __launch_bounds__(64) void k_agg_lc_reduce(const ngz_set_info *__rest
 #pragma unroll
             for (int k = 0; k < LC_NK; ++k)
                 if (k < (int)nk && __ballot(in && kidx == (uint32_t)k)) mset |= 1u << k;
+            // every value load is issued before the first LDS access: the column pointers are
+            // generic, so a load after an LDS store would wait for it
+            uint64_t x[LC_MAXV];
+#pragma unroll
+            for (int v = 0; v < LC_MAXV; ++v)
+                x[v] = (in && v < (int)nv && ((hv >> v) & 1)) ? value_operand(sp, P, v, row) : 0ull;
             if (in) {
                 cnt[kidx * 64 + lane] += 1;
 #pragma unroll
                 for (int v = 0; v < LC_MAXV; ++v) {
                     if (v >= (int)nv) break;
                     if (!((hv >> v) & 1)) continue;
-                    const uint64_t x = value_operand(sp, P, v, row);
                     unsigned long long *cell = &acc[(kidx * nv + v) * 64 + lane];
                     const uint64_t a = *cell;
                     switch (P.val_op[v]) {
-                    case NGZ_AGG_ADD: *cell = a + x; break;
-                    case NGZ_AGG_MIN: *cell = x < a ? x : a; break;
-                    case NGZ_AGG_MAX: *cell = x > a ? x : a; break;
-                    default: *cell = a | x; break;
+                    case NGZ_AGG_ADD: *cell = a + x[v]; break;
+                    case NGZ_AGG_MIN: *cell = x[v] < a ? x[v] : a; break;
+                    case NGZ_AGG_MAX: *cell = x[v] > a ? x[v] : a; break;
+                    default: *cell = a | x[v]; break;
                     }
                 }
             }
