@@ -1512,6 +1512,56 @@ __global__ __launch_bounds__(256) void k_agg_lc_scan(const ngz_set_info *__restr
     }
 }
 
+constexpr int LC_CH = 16;  // chunks of 64 records whose column loads k_agg_lc_reduce issues together
+
+// Column cells of rows r0 + 64 c (c < LC_CH, rows past nb of the block: 0) of a w-byte column,
+// little-endian in a u64; col null (the field is None): 0.  One branch on the width, then all
+// the loads, so they are in flight together.
+template <class T>
+__device__ __forceinline__ void lc_load_t(const uint8_t *col, uint64_t r0, uint32_t nb, uint64_t (&x)[LC_CH]) {
+    const uint32_t lane = threadIdx.x & 63;
+    const T *p = (const T *)col;
+#pragma unroll
+    for (int c = 0; c < LC_CH; ++c) x[c] = (64u * c + lane < nb) ? (uint64_t)p[r0 + 64ull * c] : 0ull;
+}
+__device__ __forceinline__ void lc_col_load(const uint8_t *col, uint32_t w, uint64_t r0, uint32_t nb,
+                                            uint64_t (&x)[LC_CH]) {
+    if (!col) {
+#pragma unroll
+        for (int c = 0; c < LC_CH; ++c) x[c] = 0;
+    } else if (w == 8) {
+        lc_load_t<uint64_t>(col, r0, nb, x);
+    } else if (w == 4) {
+        lc_load_t<uint32_t>(col, r0, nb, x);
+    } else if (w == 2) {
+        lc_load_t<uint16_t>(col, r0, nb, x);
+    } else {
+        lc_load_t<uint8_t>(col, r0, nb, x);
+    }
+}
+
+// value_operand of a cell already loaded (raw: the w column bytes, little-endian)
+__device__ __forceinline__ uint64_t lc_operand(const AggParams &P, uint32_t v, uint64_t raw, uint32_t w) {
+    const uint8_t vc = P.val_vc[v];
+    uint64_t x = raw;
+    if (vc == VC_DTFRAC) {
+        x = (raw << 32) | (raw >> 32);  // {u32 secs, u32 nanos} -> (secs, nanos) ordered
+    } else if (vc == VC_SINT && w < 8) {
+        const uint32_t sh = 64 - 8 * w;
+        x = (uint64_t)(((int64_t)(raw << sh)) >> sh);
+    }
+    if (vc == VC_SINT && (P.val_op[v] == NGZ_AGG_MIN || P.val_op[v] == NGZ_AGG_MAX)) x ^= 1ull << 63;
+    if (vc == VC_RANK) {
+        if (P.val_tcp[v]) x = bitrev8((uint32_t)x & 0xFF);
+        else {
+            const uint32_t *known = P.rank_known[v];
+            const bool reg = x < 65536 && known && ((known[x >> 5] >> (x & 31)) & 1);
+            if (!reg) x |= 1ull << 32;
+        }
+    }
+    return x;
+}
+
 // One wave per workgroup; its accumulators live in LDS, lane-private: cell (k, v) of lane l
 // at acc[(k * nv + v) * 64 + l] (a lane only touches its own cells, no conflicts between lanes,
 // no atomics), so a record costs one LDS read-modify-write per aggregated field of its key
@@ -1611,44 +1661,57 @@ __global__ __launch_bounds__(64) void k_agg_lc_reduce(const ngz_set_info *__rest
         uint32_t hv = 0;  // aggregated fields the set's template has (Some)
         for (uint32_t v = 0; v < nv; ++v)
             if (sp.val_col[v]) hv |= 1u << v;
-        uint32_t mset = 0;  // key tuples present in the set
-        for (uint32_t c = 0; c < si.n; c += 64) {
-            const bool valid = c + lane < si.n;
-            const uint64_t row = (uint64_t)si.rec0 + c + lane;
-            uint32_t kp = 0;
-            KeyVal kv;
-            const uint64_t key = valid ? (key_tag(sp, P, row, win, kp, kv) & K.kmask) : ~0ull;
-            uint32_t kidx = LC_NK;
+        // blocks of LC_CH chunks of 64 records: per key field and per aggregated field, the
+        // block's column loads are issued together (one width branch per field and block),
+        // then the records go into their key tuple's accumulators
+        uint32_t pres = 0;  // key tuples this lane saw in the set
+        for (uint32_t b0 = 0; b0 < si.n; b0 += 64 * LC_CH) {
+            const uint32_t nb = min(si.n - b0, 64u * LC_CH);
+            const uint64_t r0 = (uint64_t)si.rec0 + b0 + lane;
+            uint64_t key[LC_CH];
 #pragma unroll
-            for (int k = 0; k < LC_NK; ++k)
-                if (k < (int)nk && key == K.kp[k]) kidx = (uint32_t)k;
-            const bool in = valid && kidx < nk;
+            for (int c = 0; c < LC_CH; ++c) key[c] = 0;
+            for (uint32_t k = 0; k < P.n_keys; ++k) {  // key_tag's packing of the key fields
+                const uint8_t *col = sp.key_col[k];
+                const uint32_t sh = 8 * P.key_pw[k];
+                uint64_t kv[LC_CH];
+                lc_col_load(col, sp.key_w[k], r0, nb, kv);
 #pragma unroll
-            for (int k = 0; k < LC_NK; ++k)
-                if (k < (int)nk && __ballot(in && kidx == (uint32_t)k)) mset |= 1u << k;
-            // every value load is issued before the first LDS access: the column pointers are
-            // generic, so a load after an LDS store would wait for it
-            uint64_t x[LC_MAXV];
+                for (int c = 0; c < LC_CH; ++c) key[c] = ((((key[c] << 1) | (col != nullptr)) << sh)) | kv[c];
+            }
+            uint32_t kid[LC_CH];
 #pragma unroll
-            for (int v = 0; v < LC_MAXV; ++v)
-                x[v] = (in && v < (int)nv && ((hv >> v) & 1)) ? value_operand(sp, P, v, row) : 0ull;
-            if (in) {
-                cnt[kidx * 64 + lane] += 1;
+            for (int c = 0; c < LC_CH; ++c) {
+                kid[c] = LC_NK;
+                const bool valid = 64u * c + lane < nb;
 #pragma unroll
-                for (int v = 0; v < LC_MAXV; ++v) {
-                    if (v >= (int)nv) break;
-                    if (!((hv >> v) & 1)) continue;
-                    unsigned long long *cell = &acc[(kidx * nv + v) * 64 + lane];
+                for (int k = 0; k < LC_NK; ++k)
+                    if (valid && k < (int)nk && key[c] == K.kp[k]) kid[c] = (uint32_t)k;
+                if (kid[c] < nk) {
+                    pres |= 1u << kid[c];
+                    cnt[kid[c] * 64 + lane] += 1;
+                }
+            }
+            for (uint32_t v = 0; v < nv; ++v) {
+                if (!((hv >> v) & 1)) continue;
+                uint64_t x[LC_CH];
+                lc_col_load(sp.val_col[v], sp.val_w[v], r0, nb, x);
+                const uint8_t op = P.val_op[v];
+#pragma unroll
+                for (int c = 0; c < LC_CH; ++c) {
+                    if (kid[c] >= nk) continue;
+                    const uint64_t xv = lc_operand(P, v, x[c], sp.val_w[v]);
+                    unsigned long long *cell = &acc[(kid[c] * nv + v) * 64 + lane];
                     const uint64_t a = *cell;
-                    switch (P.val_op[v]) {
-                    case NGZ_AGG_ADD: *cell = a + x[v]; break;
-                    case NGZ_AGG_MIN: *cell = x[v] < a ? x[v] : a; break;
-                    case NGZ_AGG_MAX: *cell = x[v] > a ? x[v] : a; break;
-                    default: *cell = a | x[v]; break;
-                    }
+                    *cell = op == NGZ_AGG_ADD ? a + xv : op == NGZ_AGG_MIN ? (xv < a ? xv : a)
+                          : op == NGZ_AGG_MAX ? (xv > a ? xv : a) : (a | xv);
                 }
             }
         }
+        // key tuples present in the set: OR over the wave
+        uint32_t mset = pres;
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) mset |= (uint32_t)__shfl_xor((int)mset, m);
         if (lane < nk && ((mset >> lane) & 1)) {
             const uint32_t k = lane, db = (info >> 2) & 0x7F;
             h_tmin[k] = min(h_tmin[k], ts);
