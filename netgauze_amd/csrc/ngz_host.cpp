@@ -923,14 +923,34 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
         if (ctx->d_dsum.ensure(N)) return fail(ctx, NGZ_E_NOMEM, "device alloc (datagram summaries)");
         B.dsum = ctx->d_dsum.p;
     }
+    B.recoff = nullptr;
+    B.recoff_div = 0;
     bool any_vlen = false;
+    uint32_t min_vlen_rec = 0xFFFFFFFFu;
     for (uint32_t s = 0; s < S; ++s) {
         const DevPlan &P = ctx->versions[ctx->slot_version[s]].plan;
-        any_vlen = any_vlen || (P.has_vlen && P.rpl);
+        if (P.has_vlen && P.rpl) {
+            any_vlen = true;
+            min_vlen_rec = std::min<uint32_t>(min_vlen_rec, P.rec_len);
+        }
     }
-    if (any_vlen && getenv("NGZ_RECMAP") == nullptr) {  // NGZ_RECMAP set: walk twice (A/B)
-        if (ctx->d_recmap.ensure(in->bytes_size / 32 + 8)) return fail(ctx, NGZ_E_NOMEM, "device alloc (record map)");
-        B.recmap = ctx->d_recmap.p;
+    // Records of variable-length sets found by k_frame's walk reach k_emit as a list of
+    // record offsets per datagram (2 bytes per record, written in order by the walking
+    // thread; no per-batch zeroing).  Every such record spans at least min_record_length
+    // bytes (ipfix.rs:193-214), so datagram d's list fits from entry offsets[d] / that + d.
+    // Templates whose records may be shorter than 8 bytes use the record-start bitmap (one
+    // bit per batch byte, zeroed per batch).  NGZ_RECMAP: 0 walk twice, 1 bitmap, 2 lists.
+    static const int recmap_env = getenv("NGZ_RECMAP") ? atoi(getenv("NGZ_RECMAP")) : -1;
+    if (any_vlen && recmap_env != 0) {
+        if (recmap_env != 1 && min_vlen_rec >= 8) {
+            if (ctx->d_recoff.ensure(in->bytes_size / min_vlen_rec + N + 8))
+                return fail(ctx, NGZ_E_NOMEM, "device alloc (record offsets)");
+            B.recoff = ctx->d_recoff.p;
+            B.recoff_div = min_vlen_rec;
+        } else {
+            if (ctx->d_recmap.ensure(in->bytes_size / 32 + 8)) return fail(ctx, NGZ_E_NOMEM, "device alloc (record map)");
+            B.recmap = ctx->d_recmap.p;
+        }
     }
     B.summary = d_sum;
 
@@ -1294,7 +1314,7 @@ void ngz_ctx_destroy(ngz_ctx *ctx) {
     ctx->d_tl_slot.release(); ctx->d_hf_flag.release(); ctx->d_hf_hdr.release(); ctx->d_hf_first.release(); ctx->d_hf_sets.release();
     ctx->d_hdr.release(); ctx->d_counts.release(); ctx->d_scan.release(); ctx->d_scan_tmp.release();
     ctx->d_slots.release(); ctx->d_chunks.release(); ctx->d_sets.release(); ctx->d_arena.release();
-    ctx->d_proc.release(); ctx->d_summary.release(); ctx->d_recmap.release(); ctx->d_dsum.release(); ctx->d_in_bytes.release(); ctx->d_in_off.release();
+    ctx->d_proc.release(); ctx->d_summary.release(); ctx->d_recmap.release(); ctx->d_recoff.release(); ctx->d_dsum.release(); ctx->d_in_bytes.release(); ctx->d_in_off.release();
     ctx->d_in_len.release();
     for (auto &e : ctx->ev) hipEventDestroy(e);
     for (uint32_t i = 0; i < ctx->n_aux; ++i) {

@@ -240,6 +240,7 @@ struct ngz_ctx {
     ngzh::DevBuf<unsigned long long> d_proc;
     ngzh::DevBuf<BatchSummary> d_summary;
     ngzh::DevBuf<uint32_t> d_recmap;            // record-start bitmap of variable-length sets
+    ngzh::DevBuf<uint16_t> d_recoff;            // per-datagram record-offset lists of variable-length sets
     ngzh::DevBuf<unsigned long long> d_dsum;    // per datagram: its one data set (k_frame -> k_emit)
     // host staging for ngz_decode_batch_host
     ngzh::DevBuf<uint8_t> d_in_bytes;

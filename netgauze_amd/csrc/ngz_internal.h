@@ -295,6 +295,11 @@ struct BatchDev {        // device pointers of one batch
     uint32_t cap_pad_windows;  // extra workgroup windows of capacity per slot (column placement tuning)
     uint32_t reserved_b;
     uint32_t *recmap;          // variable-length slots: 1 bit per batch byte, set at every complete record
+                               // (used when recoff is null)
+    uint16_t *recoff;          // variable-length slots: per datagram, the offsets of its complete records
+                               // in datagram order then 0xFFFF, from entry offsets[d] / recoff_div + d
+    uint32_t recoff_div;       // the smallest min_record_length of the batch's variable-length templates
+    uint32_t reserved_c;
     unsigned long long *dsum;  // per datagram: its one data set (k_frame -> k_emit), 0 = walk it again
                                // start by k_frame's walk, read by k_emit instead of walking again (or null)
 };

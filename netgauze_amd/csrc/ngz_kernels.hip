@@ -252,6 +252,8 @@ struct CountVis {
     const DevPlan *plans;
     uint32_t *recmap;
     uint64_t dg_off;
+    uint16_t *ro = nullptr;  // this datagram's record-offset list (BatchDev::recoff), or null
+    uint32_t ro_n = 0;
     uint64_t sum = 0;  // the first data set: set_pos | slot << 16 | n << 32 | (end - set_pos, or 1) << 48
     uint64_t dg_end = 0;  // batch offset past the datagram
     // record-start marks of the word being filled (record starts only ever move forward)
@@ -267,6 +269,10 @@ struct CountVis {
     __device__ uint32_t vlen(const uint8_t *p, uint32_t pos, uint32_t end, uint32_t, const DevPlan &pl, uint64_t *err) {
         if (!sets) sum = (uint64_t)(end - (pos - 4)) << 48;
         return ngz_vlen_walk(p, pos, end, pl, err, [this](uint32_t, uint32_t at) {
+            if (ro) {  // the record's offset in the datagram, appended to the datagram's list
+                ro[ro_n++] = (uint16_t)at;
+                return;
+            }
             if (!recmap) return;
             const uint64_t b = dg_off + at;
             if ((b >> 5) != mw) {
@@ -293,9 +299,11 @@ __global__ void __launch_bounds__(kFrameBlock) k_frame(BatchDev B, const uint32_
     if (d == 0) B.counts[(uint64_t)(2 * B.n_slots + 1) * B.n] = 0;  // the scan's trailing element
     CountVis vis{B.counts, B.n, B.n_slots, d, 0, B.plans, B.recmap, B.offsets[d]};
     vis.dg_end = vis.dg_off + B.lengths[d];
+    if (B.recoff) vis.ro = B.recoff + vis.dg_off / B.recoff_div + d;
     WalkOut o;
     walk_datagram(B, hf_flag, hf_first, d, o, vis);
     vis.mark_flush();
+    if (vis.ro) vis.ro[vis.ro_n] = 0xFFFFu;  // end of the list
     // a walk that ended OK visited every set (template sets end it with HOST)
     if (o.status != NGZ_FR_HOST && o.status != NGZ_FR_OK && !(hf_flag && hf_flag[d]) && has_template_sets(B, d))
         o.status = NGZ_FR_HOST;
@@ -398,6 +406,7 @@ struct EmitVis {
     bool ok;
     const uint32_t (*tab)[4];  // staged slots: {slot, first row, LDS row, rows}
     uint32_t ntab;
+    const uint16_t *ro;        // the datagram's record-offset list (k_frame), at its next set's first record
     uint64_t *lrs;             // LDS row tables
     uint32_t *lrd;
     // row mode: every record's batch offset and datagram, rows rec0.. of this set
@@ -415,6 +424,24 @@ struct EmitVis {
                 rs = lrs + tab[k][2] + (rec0 - tab[k][1]);
                 rd = lrd + tab[k][2] + (rec0 - tab[k][1]);
             }
+        if (ro) {
+            // k_frame's walk listed every complete record's offset: the set's are the next
+            // entries below its end (the list ends with 0xFFFF)
+            uint32_t k = 0;
+            uint64_t prev = 0;
+            for (uint32_t at = *ro; at < end; at = *++ro) {
+                const uint64_t b = dg_off + at;
+                if (k) rs[k - 1] = ngz_row_entry(prev, b - prev);
+                prev = b;
+                rd[k] = d;
+                ++k;
+            }
+            if (k) rs[k - 1] = ngz_row_entry(prev, dg_off + end - prev);  // the last record: up to the set's end
+            const uint64_t ek = ((const ngz_dgram_hdr *)B->hdr)[d].err_key;
+            const uint32_t stop = (uint32_t)(ek >> 48);
+            if (ek != NGZ_NO_ERR && stop >= pos && stop <= end) *err = ek;
+            return k;
+        }
         if (B->recmap) {
             // k_frame's walk marked every complete record start: read the marks
             // instead of walking the records again (independent loads, no
@@ -569,6 +596,7 @@ __global__ void __launch_bounds__(256) k_emit(BatchDev B, const uint32_t *hf_fla
         vis.ntab = ntab;
         vis.lrs = st_rs;
         vis.lrd = st_rd;
+        vis.ro = B.recoff ? B.recoff + vis.dg_off / B.recoff_div + d : nullptr;
         const unsigned long long sm = B.dsum ? B.dsum[d] : 0ull;
         if (sm) {
             // k_frame's summary of the datagram's one data set (same calls as walk_datagram)
