@@ -112,6 +112,24 @@ def committed_traffic(records, workload):
     return best
 
 
+def committed_agg_traffic(key, workload):
+    """Per-push HBM bytes of one aggregation key from a committed profile
+    (profiles/**/agg_KEY/traffic.json, tools/summarize_agg_profile.py) of THIS
+    tree's aggregation sources (buildinfo.agg_source_hash), or None."""
+    import glob
+    from netgauze_amd import buildinfo
+    want = buildinfo.agg_source_hash()
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "**", "agg_%s" % key, "traffic.json"), recursive=True)):
+        try:
+            t = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if t.get("workload") == workload and t.get("agg_source_hash") == want:
+            best = (t["traffic_bytes"], os.path.relpath(f, ROOT))
+    return best
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -326,18 +344,21 @@ def main_agg(args):
     elapsed = time.perf_counter() - t0
     avg = sum(push_ms) / len(push_ms)
     alg = per_rec * n
+    workload = "aggregate %d T20 records, %d key fields + %d aggregated fields, 2 minute windows" % (
+        n, len(keys), len(vals))
+    traffic = committed_agg_traffic(args.agg, workload)
     print(json.dumps({
         "metric": "flow records aggregated/sec (device-resident decoded columns), T20, key %s" % args.agg,
         "value": n * args.steps / elapsed, "unit": "records/s", "n_gpus": 1, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "u64", "data": "synthetic T20 (seed 0x4E475A4500000002)",
-        "config": {"workload": "aggregate %d T20 records, %d key fields + %d aggregated fields, 2 minute windows"
-                   % (n, len(keys), len(vals)), "groups": groups, "table_capacity": cap, "late_records": late,
-                   "first_push_ms": first_push_ms},
+        "config": {"workload": workload, "records": n, "groups": groups, "table_capacity": cap,
+                   "late_records": late, "first_push_ms": first_push_ms},
         "push_kernels_ms": avg, "push_records_per_s": n / (avg * 1e-3), "path": agg.last_path(),
         "roofline": {"bound": "hbm (atomic-throughput limited)", "achieved": alg / (avg * 1e-3) / 1e9,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": alg / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                     "traffic": None, "alg_bytes_per_launch": alg, "alg_bytes_per_record": per_rec}}), flush=True)
+                     "traffic": traffic[0] if traffic else None, "traffic_src": traffic[1] if traffic else None,
+                     "alg_bytes_per_launch": alg, "alg_bytes_per_record": per_rec}}), flush=True)
 
 
 def main_e2e(args):

@@ -9,7 +9,8 @@ source_hash() covers every library source.  decode_source_hash() covers the
 sources the decode step is built from (the kernels and host pipeline of
 ngz_decode_batch, the run-time kernel generator and its device headers, the IE
 table and the decode ABI): a change to aggregation, JSON or capture code does
-not change a decode kernel's HBM traffic, and does not void its profile."""
+not change a decode kernel's HBM traffic, and does not void its profile.
+agg_source_hash() covers the aggregation kernels' sources the same way."""
 import glob
 import hashlib
 import os
@@ -32,9 +33,18 @@ def _digest(patterns):
     return h.hexdigest()[:16]
 
 
+_AGG = ("netgauze_amd/csrc/ngz_agg.hip", "netgauze_amd/csrc/ngz_host.h", "netgauze_amd/csrc/ngz_internal.h",
+        "include/ngz/flow_aggregate.h", "include/ngz/flow_decode.h", "netgauze_amd/csrc/ie_table.inc")
+
+
 def source_hash():
     return _digest(_PATTERNS)
 
 
 def decode_source_hash():
     return _digest(_DECODE)
+
+
+def agg_source_hash():
+    """The aggregation kernels' sources (ngz_agg.hip and the headers it includes)."""
+    return _digest(_AGG)
