@@ -1474,12 +1474,11 @@ __global__ __launch_bounds__(256) void k_agg_lc_scan(const ngz_set_info *__restr
             const uint64_t tag = valid ? key_tag(sp, P, row, win, kp, kv) : 0ull;
             uint64_t todo = __ballot(valid);
             while (todo) {
-                if (*(volatile uint32_t *)&lt->overflow) return;
                 const int l0 = __ffsll((unsigned long long)todo) - 1;
                 const uint64_t t = readlane64(tag, l0);
                 todo &= ~__ballot(valid && tag == t);
                 if (__ballot(lane < n_seen && seen == t)) continue;  // offered by this wave already
-                if (lane == (uint32_t)l0 && !*(volatile uint32_t *)&lt->overflow) {
+                if (lane == (uint32_t)l0) {
                     uint32_t i = lc_home(t);
                     for (uint32_t probes = 0;; ++probes, i = (i + 1) & (LC_SLOTS - 1)) {
                         // the table holds at most LC_MAX_TAGS of its LC_SLOTS: short probe chains
@@ -1867,6 +1866,7 @@ struct ngz_agg {
     size_t part_cap = 0;
     LcTable *lc = nullptr;        // low-cardinality path: the push's distinct tags
     const char *last_path = "";   // the reduction path of the last push ("lowcard" / "general")
+    uint32_t lc_skip = 0;         // pushes left before the low-cardinality scan is tried again
 };
 
 namespace {
@@ -2659,8 +2659,10 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, const ngz_p
     // size; default from 2^16 records).
     static const int lc_env = getenv("NGZ_AGG_LC") ? atoi(getenv("NGZ_AGG_LC")) : -1;
     const int lc_now = getenv("NGZ_AGG_LC") ? atoi(getenv("NGZ_AGG_LC")) : lc_env;  // read per push (tests)
-    if (n_rec && P.packed && P.lds_ok && P.n_vals <= (uint32_t)LC_MAXV && !ordered && lc_now != 0 &&
-        (lc_now == 1 || n_rec >= (1u << 16))) {
+    // a push whose scan found too many distinct tags sends the next 15 pushes of the
+    // aggregator straight to the general path (high-cardinality keys pay for one scan in 16)
+    const bool lc_try = lc_now == 1 || (lc_now != 0 && n_rec >= (1u << 16) && (a->lc_skip == 0 || --a->lc_skip == 0));
+    if (n_rec && P.packed && P.lds_ok && P.n_vals <= (uint32_t)LC_MAXV && !ordered && lc_try) {
         if (!a->lc && hipMalloc(&a->lc, sizeof(LcTable)) != hipSuccess) {
             a->lc = nullptr;
             restore();
@@ -2712,6 +2714,7 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, const ngz_p
         // too many distinct tags / key tuples: the general path (its claims continue the list,
         // its claim pass counts the late records again)
         AGG_HIP(a, hipMemsetAsync(a->late, 0, 8, st));
+        a->lc_skip = 15;
     }
     a->last_path = "general";
     {
