@@ -164,6 +164,14 @@ const char *ngz_last_error(ngz_ctx *ctx);
                                    definition waits for its compile (deterministic kernel choice) */
 int ngz_ctx_set_option(ngz_ctx *ctx, int opt, int64_t value);
 
+/* Wait for every background template compile of the process (NGZ_OPT_RTC_SYNC 0) to finish
+ * and load.  Call it before the host starts tearing the process down (the Python binding
+ * registers it with atexit; a Rust host calls it before returning from main): a compile
+ * still inside hiprtc/comgr when the C exit handlers run can outlive the compiler's own
+ * static objects, which exit destroys in an order the library cannot control.  Returns
+ * the number of compiles waited for. */
+int ngz_rtc_drain(void);
+
 /* --- decode ------------------------------------------------------------- */
 /* Decode every datagram of `in` in order against the context's template
  * state.  Synchronous: on return the device arrays in *out are complete and

@@ -21,7 +21,7 @@ ABI_FUNCTIONS = [
     "ngz_decode_batch_host", "ngz_slot_fields", "ngz_dgram_error_json",
     "ngz_templates_json", "ngz_template_counts", "ngz_last_timing", "ngz_ctx_set_option",
     "ngz_template_kernel", "ngz_group_kernel", "ngz_columns_to_host", "ngz_dgram_json", "ngz_batch_json",
-    "ngz_dgram_error", "ngz_template_counts_device", "ngz_slot_kernel",
+    "ngz_dgram_error", "ngz_template_counts_device", "ngz_slot_kernel", "ngz_rtc_drain",
 ]
 NGZ_ABI_VERSION = 2
 # ngz_error.kind / .layer (flow_decode.h)
@@ -161,6 +161,9 @@ SET_INFO_DTYPE = np.dtype([("dgram", "<u4"), ("set_pos", "<u2"), ("slot", "<u2")
 assert DGRAM_HDR_DTYPE.itemsize == 32 and SET_INFO_DTYPE.itemsize == 16
 
 
+_DRAIN_REGISTERED = False
+
+
 def load():
     if not os.path.exists(LIB_PATH):
         raise RuntimeError("netgauze_amd: %s is missing — run __graft_entry__.build() (hipcc, gfx950); "
@@ -205,6 +208,15 @@ def load():
     lib.ngz_dgram_error.restype = I
     lib.ngz_template_counts_device.argtypes = [P, I, P, U32, I, P]
     lib.ngz_template_counts_device.restype = I
+    lib.ngz_rtc_drain.argtypes = []
+    lib.ngz_rtc_drain.restype = I
+    global _DRAIN_REGISTERED
+    if not _DRAIN_REGISTERED:
+        # background template compiles finish before the interpreter tears down and the C
+        # exit handlers run (flow_decode.h ngz_rtc_drain; the r2/r3 exit hang of a dist rank)
+        import atexit
+        atexit.register(lib.ngz_rtc_drain)
+        _DRAIN_REGISTERED = True
     # aggregation (flow_aggregate.h)
     lib.ngz_agg_create.argtypes = [I, ctypes.POINTER(AggField), U32, U64, U64, U64, U32, ctypes.POINTER(P)]
     lib.ngz_agg_create.restype = I

@@ -598,17 +598,30 @@ std::map<std::pair<int, std::string>, std::unique_ptr<Entry>> g_cache;
 // is registered once hiprtc and comgr are loaded and initialised
 // (prime_rtc_runtime): every destructor they register comes before it and
 // runs after the join.
+//
+// That ordering is not enough on its own: comgr / LLVM also construct
+// function-local statics during a compile, on the worker, and those register
+// their destructors after the handler, so exit runs them first.  A dist rank
+// that exited with compiles in flight still hung in r3.  The complete rule is
+// that no compile is in flight when the exit handlers start: ngz_rtc_drain joins
+// every worker, and the hosts call it before tearing down (netgauze_amd._lib
+// registers it with Python's atexit, which runs before any C exit handler).
 struct Workers {
     std::mutex mu;
     std::vector<std::thread> th;
-    void join_all() {
+    int join_all() {
         std::vector<std::thread> v;
         {
             std::lock_guard<std::mutex> lk(mu);
             v.swap(th);
         }
+        int n = 0;
         for (auto &t : v)
-            if (t.joinable()) t.join();
+            if (t.joinable()) {
+                t.join();
+                ++n;
+            }
+        return n;
     }
     ~Workers() { join_all(); }
 } g_workers;
@@ -712,7 +725,10 @@ int kernel_async(int device, const std::string &sig, Gen &&gen, const char *knam
             std::atexit(join_workers_at_exit);
         });
         std::lock_guard<std::mutex> lk(g_workers.mu);
-        g_workers.th.emplace_back(build, e, device, std::move(src), sig, kname);
+        g_workers.th.emplace_back([=, src = std::move(src)]() {
+            pthread_setname_np(pthread_self(), "ngz-rtc");  // visible in /proc/<pid>/task/*/comm
+            build(e, device, src, sig, kname);
+        });
         return 0;
     }
     if (st == 2) {
@@ -752,6 +768,13 @@ void *ngz_rtc_group(int device, const DevPlan *const *plans, uint32_t n) {
 int ngz_rtc_group_async(int device, const DevPlan *const *plans, uint32_t n, void **fn, void **entry) {
     return kernel_async(device, group_signature(plans, n), [&] { return generate_group(plans, n); }, "ngz_tplm", fn,
                         entry);
+}
+
+extern "C" int ngz_rtc_drain(void) {
+    // workers started while this runs (another host thread decoding) are joined too
+    int n = 0;
+    for (int k; (k = g_workers.join_all()) > 0;) n += k;
+    return n;
 }
 
 int ngz_rtc_poll(void *entry, void **fn) {

@@ -39,6 +39,38 @@ def _stream(n):
     return dg[:2] + [synth.template_message()], data
 
 
+def _threads(pid):
+    """Threads of a process that did not exit: name, state, kernel wait channel, syscall."""
+    out = []
+    base = "/proc/%d/task" % pid
+    try:
+        tids = sorted(os.listdir(base))
+    except OSError:
+        return ["(gone)"]
+    for t in tids:
+        info = [t]
+        for f in ("comm", "wchan", "syscall"):
+            try:
+                info.append(open(os.path.join(base, t, f)).read().strip()[:80])
+            except OSError:
+                info.append("?")
+        out.append(" | ".join(info))
+    return out
+
+
+def _join_all(procs, timeout=120):
+    """Join the ranks; a rank still running after the timeout is described and killed, so a
+    hang fails the test with its threads instead of holding the test runner at exit."""
+    hung = {}
+    for p in procs:
+        p.join(timeout=timeout)
+        if p.exitcode is None:
+            hung[p.pid] = _threads(p.pid)
+            p.kill()
+            p.join(timeout=10)
+    return hung
+
+
 def _worker(rank, world, port, n, q):
     sys.path.insert(0, ROOT)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -91,8 +123,8 @@ def test_two_ranks_decode_shards_and_exchange_counts():
     for p in procs:
         p.start()
     res = sorted((q.get(timeout=240) for _ in range(world)), key=lambda r: r[0])
-    for p in procs:
-        p.join(timeout=120)
+    hung = _join_all(procs)
+    assert not hung, hung
     assert all(r[1] != "error" for r in res), res
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     assert sum(r[3] for r in res) == len(data)              # every message in exactly one shard
@@ -173,7 +205,8 @@ def test_count_exchange_rccl_defaults_and_growth():
     p = ctx.Process(target=_nccl_worker, args=(_free_port(), 3, q))
     p.start()
     status, steps = q.get(timeout=240)
-    p.join(timeout=120)
+    hung = _join_all([p])
+    assert not hung, hung
     assert status == "ok", steps
     assert p.exitcode == 0
     # step 0 (config-4 stream): 17 IPFIX templates > 16 rows -> not fitted, nothing reset
