@@ -1375,53 +1375,45 @@ __global__ __launch_bounds__(256) void k_agg_part_reduce(const AggParams P, cons
 }
 
 // ---------------------------------------------------------------------------
-// Low-cardinality pushes (packed keys, few distinct key tuples): no per-record
-// context, slot claim or atomic per record.  k_agg_lc_scan walks the sets (one
-// wave per set, 64 records per step) and lists the push's distinct exact tags
-// (window, flow type, peer, keys) in a small table, each wave offering a tag
-// once; the wave that enters a tag claims its group in the HBM table (the same
-// probe as k_agg_claim).  k_agg_lc_reduce then reads every record's key and
-// value columns once, coalesced, and reduces them in registers: each lane
-// keeps one accumulator per (distinct key tuple, aggregated field) of the
-// current (window, flow type) -- a record updates the accumulators of its key
-// tuple through predicated selects, no atomics -- and the per-set header fields
-// (export time bounds, sys-up time, template and domain sets) are uniform per
-// set.  A wave flushes its accumulators (wave reductions, then the row update of
-// k_agg_apply's leader path) when its sets move to another window and at its
-// end: a few flushes per wave instead of 10^8 LDS atomics.
+// Low-cardinality pushes (packed keys, few distinct key tuples): one pass over
+// the key and value columns, no per-record context, slot claim or HBM atomic.
+//
+// k_agg_lc_part: one wave per workgroup walks its sets (XCD-aware), 256 records
+// per pass (4 rows per lane, rows 64 apart: every column load of the wave is one
+// contiguous run) with every key and value column of the pass loaded together
+// and the next pass of the set prefetched.  The wave finds its key tuples as it
+// goes (a wave-uniform list of at most LC_NK per window context) and reduces each
+// record into lane-private LDS cells, cell (tuple, field, lane): one LDS atomic
+// per record and aggregated field, no conflicts between lanes.  Per-set header
+// fields (export time bounds, sys-up time, template and domain sets) are uniform
+// per set and kept per tuple in lane `tuple`'s registers.  When its sets move to
+// another window context, and at its end, the wave reduces its cells and
+// appends one partial entry per tuple to a small list.
+//
+// k_agg_lc_merge (one workgroup): the partial entries, a few per wave, combined
+// per exact tag in LDS; then each distinct tag finds or claims its group in the
+// HBM table and is applied to the row.  A push that needs more than the
+// capacity, or meets a full table, releases its claims and changes nothing.
+//
+// A wave that meets more than LC_NK key tuples in one window context (or an
+// entry list that would overflow) raises the overflow flag: every wave stops,
+// the merge does nothing, and the push takes the general path from the start.
 // ---------------------------------------------------------------------------
-constexpr uint32_t LC_SLOTS = 256;    // small table of the push's distinct tags (open addressing)
-constexpr uint32_t LC_MAX_TAGS = 64;  // more distinct tags: the general path
-constexpr int LC_NK = 8;              // distinct key tuples a lane accumulates (more: the general path)
+constexpr uint32_t LC_SLOTS = 256;    // merge: open-addressing table of the push's distinct tags
+constexpr uint32_t LC_MAX_TAGS = 64;  // more distinct tags in one push: the general path
+constexpr int LC_NK = 8;              // key tuples a wave accumulates per window context (more: general path)
 constexpr int LC_MAXV = 8;            // aggregated fields (more: the general path)
+constexpr int LC_RPL = 16;            // rows per lane and block (1024 rows: a whole MTU-to-64 KB set)
 
-struct LcTable {
-    unsigned long long tag[LC_SLOTS];  // 0 = empty
-    uint32_t slot[LC_SLOTS];           // the tag's group in the HBM table
-    uint32_t count;                    // distinct tags entered
-    uint32_t overflow;                 // more than LC_MAX_TAGS
+struct LcEntry {  // one wave's partial group (128 B)
+    unsigned long long tag;  // exact packed tag (window / 60, flow type, peer, keys)
+    unsigned long long cnt;
+    uint32_t tmin, tmax, smax, vp;
+    unsigned long long tpl, d0, d1;
+    unsigned long long acc[LC_MAXV];
+    unsigned long long pad;
 };
-
-struct LcKeys {  // the push's distinct key tuples (packed key bits of the tag)
-    unsigned long long kp[LC_NK];
-    unsigned long long kmask;  // key bits of a tag
-    uint32_t nk;
-    uint32_t key_bits;
-};
-
-__device__ __forceinline__ uint32_t lc_home(uint64_t tag) { return (uint32_t)(slot_of(tag) & (LC_SLOTS - 1)); }
-
-// XCD-aware set order: workgroup b works through the (b % 8)-th eighth of the sets
-struct SetSeq {
-    uint32_t first, step, end;
-};
-__device__ __forceinline__ SetSeq set_seq(uint32_t n_sets) {
-    const uint32_t wpb = blockDim.x >> 6, q = threadIdx.x >> 6;
-    const uint32_t G = gridDim.x, X = (G % 8 == 0 && G >= 8) ? 8u : 1u;
-    const uint32_t x = blockIdx.x % X, l = blockIdx.x / X;
-    const uint32_t per = (n_sets + X - 1) / X, start = x * per;
-    return SetSeq{start + l * wpb + q, (G / X) * wpb, min(n_sets, start + per)};
-}
+static_assert(sizeof(LcEntry) == 128, "LcEntry");
 
 // A set's records aggregated by this push: its plan, or null (no records, late or failed
 // datagram, slot not aggregated); *late: the set's records are late
@@ -1441,101 +1433,33 @@ __device__ __forceinline__ const AggSlotPlan *lc_set(const ngz_set_info &si, con
     return &plans[si.slot];
 }
 
-__global__ __launch_bounds__(256) void k_agg_lc_scan(const ngz_set_info *__restrict__ sets, uint32_t n_sets,
-                                                     const ngz_dgram_hdr *__restrict__ hdr,
-                                                     const uint16_t *__restrict__ dginfo,
-                                                     const AggSlotPlan *__restrict__ plans, uint32_t n_dgrams,
-                                                     uint32_t n_slots, const AggParams P,
-                                                     unsigned long long *__restrict__ tags, uint8_t *__restrict__ rows,
-                                                     uint32_t *__restrict__ claims,
-                                                     unsigned long long *__restrict__ n_claims,
-                                                     unsigned long long *__restrict__ late_count,
-                                                     LcTable *__restrict__ lt, unsigned int *__restrict__ err) {
-    const uint32_t lane = threadIdx.x & 63;
-    uint64_t seen = 0;  // lane i: the i-th tag this wave entered or found entered
-    uint32_t n_seen = 0;
-    const SetSeq ss = set_seq(n_sets);
-    for (uint32_t s = ss.first; s < ss.end; s += ss.step) {
-        if (*(volatile uint32_t *)&lt->overflow) return;
-        const ngz_set_info si = sets[s];
-        bool late;
-        uint16_t info = 0;
-        const AggSlotPlan *spp = lc_set(si, dginfo, plans, n_dgrams, n_slots, &late, &info, err);
-        if (late && lane == 0) atomicAdd(late_count, (unsigned long long)si.n);
-        if (!spp) continue;
-        const AggSlotPlan &sp = *spp;
-        const uint32_t ts = hdr[si.dgram].time, win = ts - ts % 60;
-        for (uint32_t c = 0; c < si.n; c += 64) {
-            if (*(volatile uint32_t *)&lt->overflow) return;  // the general path takes the push
-            const bool valid = c + lane < si.n;
-            const uint64_t row = (uint64_t)si.rec0 + c + lane;
-            uint32_t kp = 0;
-            KeyVal kv;
-            const uint64_t tag = valid ? key_tag(sp, P, row, win, kp, kv) : 0ull;
-            uint64_t todo = __ballot(valid);
-            while (todo) {
-                const int l0 = __ffsll((unsigned long long)todo) - 1;
-                const uint64_t t = readlane64(tag, l0);
-                todo &= ~__ballot(valid && tag == t);
-                if (__ballot(lane < n_seen && seen == t)) continue;  // offered by this wave already
-                if (lane == (uint32_t)l0) {
-                    uint32_t i = lc_home(t);
-                    for (uint32_t probes = 0;; ++probes, i = (i + 1) & (LC_SLOTS - 1)) {
-                        // the table holds at most LC_MAX_TAGS of its LC_SLOTS: short probe chains
-                        if (probes == LC_SLOTS / 2) { atomicOr(&lt->overflow, 1u); break; }
-                        unsigned long long cur = lt->tag[i];
-                        if (cur == 0) {
-                            cur = atomicCAS(&lt->tag[i], 0ull, (unsigned long long)t);
-                            if (cur == 0) {  // entered here: claim / find the group
-                                if (atomicAdd(&lt->count, 1u) >= LC_MAX_TAGS) {
-                                    atomicOr(&lt->overflow, 1u);
-                                    break;  // the general path claims it
-                                }
-                                bool tent = false, claimed = false;
-                                const uint32_t g = probe<false>(sp, P, row, win, kp, kv, t, tags, rows, err, &tent,
-                                                                &claimed);
-                                lt->slot[i] = g;
-                                if (claimed) claims[atomicAdd(n_claims, 1ull)] = g;
-                                break;
-                            }
-                        }
-                        if (cur == t) break;
-                    }
-                }
-                if (n_seen < 64) {
-                    if (lane == n_seen) seen = t;
-                    ++n_seen;
-                }
-            }
-        }
-    }
-}
-
-constexpr int LC_CH = 16;  // chunks of 64 records whose column loads k_agg_lc_reduce issues together
-
-// Column cells of rows r0 + 64 c (c < LC_CH, rows past nb of the block: 0) of a w-byte column,
-// little-endian in a u64; col null (the field is None): 0.  One branch on the width, then all
-// the loads, so they are in flight together.
+// Cells of rows r0 + 64 j (j < LC_RPL; rows at or past `end`: 0) of a w-byte column,
+// little-endian in a u64; col null (the field is None): 0.  One branch on the width,
+// then every load, so they are in flight together.
 template <class T>
-__device__ __forceinline__ void lc_load_t(const uint8_t *col, uint64_t r0, uint32_t nb, uint64_t (&x)[LC_CH]) {
-    const uint32_t lane = threadIdx.x & 63;
-    const T *p = (const T *)col;
+__device__ __forceinline__ void lc_load_t(const uint8_t *col, uint64_t r0, uint64_t end, uint64_t (&x)[LC_RPL]) {
+    // the column pointers come from the plan table in memory: generic to the compiler, so the
+    // loads would be flat ones (counted against LDS operations too); they are global memory
+    typedef const __attribute__((address_space(1))) T *gptr;
+    const gptr p = (gptr)col;
+    // rows past the set read its last row (every load unconditional, straight-line; the
+    // caller gives those rows no key tuple)
 #pragma unroll
-    for (int c = 0; c < LC_CH; ++c) x[c] = (64u * c + lane < nb) ? (uint64_t)p[r0 + 64ull * c] : 0ull;
+    for (int j = 0; j < LC_RPL; ++j) x[j] = (uint64_t)p[min(r0 + 64u * j, end - 1)];
 }
-__device__ __forceinline__ void lc_col_load(const uint8_t *col, uint32_t w, uint64_t r0, uint32_t nb,
-                                            uint64_t (&x)[LC_CH]) {
+__device__ __forceinline__ void lc_col_load(const uint8_t *col, uint32_t w, uint64_t r0, uint64_t end,
+                                            uint64_t (&x)[LC_RPL]) {
     if (!col) {
 #pragma unroll
-        for (int c = 0; c < LC_CH; ++c) x[c] = 0;
+        for (int j = 0; j < LC_RPL; ++j) x[j] = 0;
     } else if (w == 8) {
-        lc_load_t<uint64_t>(col, r0, nb, x);
+        lc_load_t<uint64_t>(col, r0, end, x);
     } else if (w == 4) {
-        lc_load_t<uint32_t>(col, r0, nb, x);
+        lc_load_t<uint32_t>(col, r0, end, x);
     } else if (w == 2) {
-        lc_load_t<uint16_t>(col, r0, nb, x);
+        lc_load_t<uint16_t>(col, r0, end, x);
     } else {
-        lc_load_t<uint8_t>(col, r0, nb, x);
+        lc_load_t<uint8_t>(col, r0, end, x);
     }
 }
 
@@ -1561,169 +1485,375 @@ __device__ __forceinline__ uint64_t lc_operand(const AggParams &P, uint32_t v, u
     return x;
 }
 
-// One wave per workgroup; its accumulators live in LDS, lane-private: cell (k, v) of lane l
-// at acc[(k * nv + v) * 64 + l] (a lane only touches its own cells, no conflicts between lanes,
-// no atomics), so a record costs one LDS read-modify-write per aggregated field of its key
-// tuple instead of a predicated update of every tuple's accumulators in registers.
-__global__ __launch_bounds__(64) void k_agg_lc_reduce(const ngz_set_info *__restrict__ sets, uint32_t n_sets,
-                                                      const ngz_dgram_hdr *__restrict__ hdr,
-                                                      const uint16_t *__restrict__ dginfo,
-                                                      const AggSlotPlan *__restrict__ plans, uint32_t n_dgrams,
-                                                      uint32_t n_slots, const AggParams P, const LcKeys K,
-                                                      uint8_t *__restrict__ rows, const LcTable *__restrict__ lt,
-                                                      unsigned int *__restrict__ err) {
-    extern __shared__ unsigned long long lc_lds[];
-    const uint32_t nk = K.nk, nv = P.n_vals;
-    unsigned long long *acc = lc_lds;                          // [nk][nv][64]
-    uint32_t *cnt = (uint32_t *)(acc + (size_t)nk * nv * 64);  // [nk][64]
-    // per key tuple, uniform per set (lane k updates entry k once per set): export time bounds,
-    // sys-up time, fields present, template and domain sets
-    __shared__ uint32_t h_tmin[LC_NK], h_tmax[LC_NK], h_smax[LC_NK], h_vp[LC_NK];
-    __shared__ unsigned long long h_tpl[LC_NK], h_d0[LC_NK], h_d1[LC_NK];
-    const uint32_t lane = threadIdx.x;
-    auto reset = [&]() {
-        for (uint32_t k = 0; k < nk; ++k) {
-            cnt[k * 64 + lane] = 0;
-            for (uint32_t v = 0; v < nv; ++v) acc[(k * nv + v) * 64 + lane] = P.val_op[v] == NGZ_AGG_MIN ? ~0ull : 0ull;
-        }
-        if (lane < LC_NK) {
-            h_tmin[lane] = 0xFFFFFFFFu;
-            h_tmax[lane] = h_smax[lane] = h_vp[lane] = 0;
-            h_tpl[lane] = h_d0[lane] = h_d1[lane] = 0;
-        }
-        __syncthreads();
-    };
-    // the accumulators of window context ctx into their groups' rows
-    auto flush = [&](uint64_t ctx) {
+__device__ __forceinline__ uint64_t lc_identity(uint8_t op) { return op == NGZ_AGG_MIN ? ~0ull : 0ull; }
+
+__global__ __launch_bounds__(64) void k_agg_lc_part(const ngz_set_info *__restrict__ sets, uint32_t n_sets,
+                                                    const ngz_dgram_hdr *__restrict__ hdr,
+                                                    const uint16_t *__restrict__ dginfo,
+                                                    const AggSlotPlan *__restrict__ plans, uint32_t n_dgrams,
+                                                    uint32_t n_slots, const AggParams P, uint32_t key_bits,
+                                                    LcEntry *__restrict__ out, unsigned int *__restrict__ n_out,
+                                                    uint32_t cap, unsigned long long *__restrict__ late_count,
+                                                    unsigned int *__restrict__ flag, unsigned int *__restrict__ err) {
+    extern __shared__ unsigned long long lc_cells[];  // [tuple][field][lane]
+    const uint32_t nv = P.n_vals, lane = threadIdx.x;
+    uint64_t kl[LC_NK];  // the wave's key tuples of the current window context (wave-uniform)
+    uint32_t nkw = 0;
+    uint32_t cnt[LC_NK];
+    // lane k: header fields of tuple k
+    uint32_t h_tmin = 0xFFFFFFFFu, h_tmax = 0, h_smax = 0, h_vp = 0;
+    uint64_t h_tpl = 0, h_d0 = 0, h_d1 = 0;
 #pragma unroll
-        for (int k = 0; k < LC_NK; ++k) {  // unrolled: K.kp[k] stays a kernel argument register
-            if (k >= (int)nk) break;
-            const uint64_t total = wave_reduce<R_ADD>((uint64_t)cnt[k * 64 + lane]);
-            if (!total) continue;
-            const uint64_t tag = (ctx << K.key_bits) | K.kp[k] | (1ull << 63);  // key_tag's exact tag
-            uint32_t i = lc_home(tag), g = NONE;
-            for (uint32_t probes = 0; probes < LC_SLOTS; ++probes, i = (i + 1) & (LC_SLOTS - 1)) {
-                const unsigned long long t = lt->tag[i];
-                if (t == tag) { g = lt->slot[i]; break; }
-                if (t == 0) break;
-            }
-            if (g == NONE) {
-                if (lane == 0) atomicOr(err, 4u);  // a tag the scan did not enter (cannot happen)
-                continue;
-            }
-            uint8_t *R = rows + (uint64_t)g * P.row_bytes;
-            const uint32_t vpk = h_vp[k];
-            if (lane == 0) {
-                atomicAdd((unsigned long long *)(R + 16), (unsigned long long)total);
-                atomicMin((unsigned int *)(R + 24), h_tmin[k]);
-                atomicMax((unsigned int *)(R + 28), h_tmax[k]);
-                if (h_smax[k]) atomicMax((unsigned int *)(R + 32), h_smax[k]);
-                atomicOr((unsigned long long *)(R + 56), h_tpl[k]);
-                if (h_d0[k]) atomicOr((unsigned long long *)(R + 72), h_d0[k]);
-                if (h_d1[k]) atomicOr((unsigned long long *)(R + 80), h_d1[k]);
-                apply_push_constants(R, P);
-                if (vpk) atomicOr((unsigned int *)(R + 12), vpk);
+    for (int k = 0; k < LC_NK; ++k) {
+        kl[k] = 0;
+        cnt[k] = 0;
+    }
+    auto reset = [&]() {
+        for (uint32_t c = 0; c < (uint32_t)LC_NK * nv; ++c) lc_cells[c * 64 + lane] = lc_identity(P.val_op[c % nv]);
+#pragma unroll
+        for (int k = 0; k < LC_NK; ++k) cnt[k] = 0;
+        nkw = 0;
+        h_tmin = 0xFFFFFFFFu;
+        h_tmax = h_smax = h_vp = 0;
+        h_tpl = h_d0 = h_d1 = 0;
+    };
+    // the cells of window context ctx -> one entry per key tuple; false: the list is full
+    auto flush = [&](uint64_t ctx) -> bool {
+        if (!nkw) return true;
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(n_out, nkw);
+        base = (uint32_t)__shfl((int)base, 0);
+        if (base + nkw > cap) {
+            if (lane == 0) atomicOr(flag, 1u);
+            return false;
+        }
+#pragma unroll
+        for (int k = 0; k < LC_NK; ++k) {
+            if (k >= (int)nkw) break;
+            const uint64_t total = wave_reduce<R_ADD>((uint64_t)cnt[k]);
+            LcEntry *e = out + base + k;
+            if (lane == (uint32_t)k) {  // the tuple's header lives in lane k
+                e->tag = (ctx << key_bits) | kl[k] | (1ull << 63);  // key_tag's exact tag
+                e->cnt = total;
+                e->tmin = h_tmin;
+                e->tmax = h_tmax;
+                e->smax = h_smax;
+                e->vp = h_vp;
+                e->tpl = h_tpl;
+                e->d0 = h_d0;
+                e->d1 = h_d1;
             }
             for (uint32_t v = 0; v < nv; ++v) {
-                if (!((vpk >> v) & 1)) continue;
-                const uint8_t op = P.val_op[v];
-                const uint64_t a = acc[(k * nv + v) * 64 + lane];
+                const uint64_t a = lc_cells[(k * nv + v) * 64 + lane];
                 uint64_t r;
-                switch (op) {
+                switch (P.val_op[v]) {
                 case NGZ_AGG_ADD: r = wave_reduce<R_ADD>(a); break;
                 case NGZ_AGG_MIN: r = wave_reduce<R_MIN>(a); break;
                 case NGZ_AGG_MAX: r = wave_reduce<R_MAX>(a); break;
                 default: r = wave_reduce<R_OR>(a); break;
                 }
-                if (lane == 0) apply_value_hot(R + P.val_off[v], op, r);
+                if (lane == 0) e->acc[v] = r;
             }
         }
+        return true;
     };
     reset();
     uint64_t cur = ~0ull;  // current window context (window / 60, flow type, peer); none yet
-    const SetSeq ss = set_seq(n_sets);
-    for (uint32_t s = ss.first; s < ss.end; s += ss.step) {
-        const ngz_set_info si = sets[s];
+    // one wave per workgroup: the set sequence, the set and its plan are wave-uniform (scalar
+    // loads, no EXEC masking around them)
+    const uint32_t G = gridDim.x, X = (G % 8 == 0 && G >= 8) ? 8u : 1u;
+    const uint32_t per = (n_sets + X - 1) / X, s_end = min(n_sets, (blockIdx.x % X) * per + per);
+    for (uint32_t s = (blockIdx.x % X) * per + blockIdx.x / X; s < s_end; s += G / X) {
+        if (*(volatile unsigned int *)flag) return;  // some wave overflowed: the general path takes the push
+        ngz_set_info si = sets[s];
+        si.dgram = __builtin_amdgcn_readfirstlane(si.dgram);
+        si.slot = (uint16_t)__builtin_amdgcn_readfirstlane(si.slot);
+        si.rec0 = __builtin_amdgcn_readfirstlane(si.rec0);
+        si.n = __builtin_amdgcn_readfirstlane(si.n);
         bool late;
         uint16_t info = 0;
         const AggSlotPlan *spp = lc_set(si, dginfo, plans, n_dgrams, n_slots, &late, &info, err);
+        info = (uint16_t)__builtin_amdgcn_readfirstlane(info);
+        if (late && lane == 0) atomicAdd(late_count, (unsigned long long)si.n);
         if (!spp) continue;
-        const AggSlotPlan &sp = *spp;
+        // the plan through the constant address space: its fields are wave-uniform and read
+        // with scalar loads, also at a runtime field index (a generic pointer made them vector
+        // loads, each a memory round trip before the field's column loads could issue)
+        typedef const __attribute__((address_space(4))) AggSlotPlan *cplan;
+        const auto &sp = *(cplan)spp;
         const ngz_dgram_hdr &h = hdr[si.dgram];
-        const uint32_t ts = h.time, win = ts - ts % 60;
+        const uint32_t ts = __builtin_amdgcn_readfirstlane(h.time), win = ts - ts % 60;
         const uint64_t ctx = ((((uint64_t)(win / 60) << 1) | (sp.proto == 9)) << P.peer_bits) | P.peer;
         if (ctx != cur) {
-            if (cur != ~0ull) flush(cur);
+            if (cur != ~0ull && !flush(cur)) return;
             reset();
             cur = ctx;
         }
         uint32_t hv = 0;  // aggregated fields the set's template has (Some)
         for (uint32_t v = 0; v < nv; ++v)
             if (sp.val_col[v]) hv |= 1u << v;
-        // blocks of LC_CH chunks of 64 records: per key field and per aggregated field, the
-        // block's column loads are issued together (one width branch per field and block),
-        // then the records go into their key tuple's accumulators
+        const uint64_t end = (uint64_t)si.rec0 + si.n;
         uint32_t pres = 0;  // key tuples this lane saw in the set
-        for (uint32_t b0 = 0; b0 < si.n; b0 += 64 * LC_CH) {
-            const uint32_t nb = min(si.n - b0, 64u * LC_CH);
+        // blocks of 1024 rows, LC_RPL per lane 64 apart: the block's key tuples first (every
+        // key column's loads in flight together), then field by field (a runtime loop, one
+        // copy of the code): the field's LC_RPL loads together, then its LDS updates
+        for (uint32_t b0 = 0; b0 < si.n; b0 += 64 * LC_RPL) {
             const uint64_t r0 = (uint64_t)si.rec0 + b0 + lane;
-            uint64_t key[LC_CH];
+            uint64_t key[LC_RPL];
 #pragma unroll
-            for (int c = 0; c < LC_CH; ++c) key[c] = 0;
+            for (int j = 0; j < LC_RPL; ++j) key[j] = 0;
             for (uint32_t k = 0; k < P.n_keys; ++k) {  // key_tag's packing of the key fields
                 const uint8_t *col = sp.key_col[k];
                 const uint32_t sh = 8 * P.key_pw[k];
-                uint64_t kv[LC_CH];
-                lc_col_load(col, sp.key_w[k], r0, nb, kv);
+                uint64_t kv[LC_RPL];
+                lc_col_load(col, sp.key_w[k], r0, end, kv);
 #pragma unroll
-                for (int c = 0; c < LC_CH; ++c) key[c] = ((((key[c] << 1) | (col != nullptr)) << sh)) | kv[c];
+                for (int j = 0; j < LC_RPL; ++j) key[j] = (((key[j] << 1) | (col != nullptr)) << sh) | kv[j];
             }
-            uint32_t kid[LC_CH];
+            // each row's tuple in the wave's list, extended by any tuple it has not met yet
+            uint32_t kid[LC_RPL];
 #pragma unroll
-            for (int c = 0; c < LC_CH; ++c) {
-                kid[c] = LC_NK;
-                const bool valid = 64u * c + lane < nb;
+            for (int j = 0; j < LC_RPL; ++j) {
+                kid[j] = LC_NK;
 #pragma unroll
                 for (int k = 0; k < LC_NK; ++k)
-                    if (valid && k < (int)nk && key[c] == K.kp[k]) kid[c] = (uint32_t)k;
-                if (kid[c] < nk) {
-                    pres |= 1u << kid[c];
-                    cnt[kid[c] * 64 + lane] += 1;
+                    if (k < (int)nkw && key[j] == kl[k]) kid[j] = (uint32_t)k;
+            }
+            for (int j = 0; j < LC_RPL; ++j) {  // not unrolled: new tuples are rare
+                const bool valid = r0 + 64u * j < end;
+                uint64_t todo = __ballot(valid && kid[j] == LC_NK);
+                while (todo) {
+                    const int l0 = __ffsll((unsigned long long)todo) - 1;
+                    const uint64_t t = readlane64(key[j], l0);
+                    if (nkw == (uint32_t)LC_NK) {
+                        if (lane == 0) atomicOr(flag, 1u);
+                        return;
+                    }
+#pragma unroll
+                    for (int k = 0; k < LC_NK; ++k)
+                        if (k == (int)nkw) kl[k] = t;
+#pragma unroll
+                    for (int i = 0; i < LC_RPL; ++i)
+                        if (r0 + 64u * i < end && key[i] == t) kid[i] = nkw;
+                    ++nkw;
+                    todo &= ~__ballot(valid && key[j] == t);
                 }
             }
+            // counts, present tuples; rows past the set keep kid LC_NK
+#pragma unroll
+            for (int j = 0; j < LC_RPL; ++j) {
+                if (r0 + 64u * j >= end) kid[j] = LC_NK;
+                pres |= kid[j] < (uint32_t)LC_NK ? 1u << kid[j] : 0u;
+#pragma unroll
+                for (int k = 0; k < LC_NK; ++k) cnt[k] += kid[j] == (uint32_t)k;
+            }
+            // lane-private cell offsets of the rows' tuples (field 0); rows without one: none
+            uint32_t cell[LC_RPL];
+#pragma unroll
+            for (int j = 0; j < LC_RPL; ++j) cell[j] = kid[j] * nv * 64 + lane;
             for (uint32_t v = 0; v < nv; ++v) {
                 if (!((hv >> v) & 1)) continue;
-                uint64_t x[LC_CH];
-                lc_col_load(sp.val_col[v], sp.val_w[v], r0, nb, x);
-                const uint8_t op = P.val_op[v];
+                uint64_t x[LC_RPL];
+                const uint32_t w = sp.val_w[v];
+                lc_col_load(sp.val_col[v], w, r0, end, x);
+                const uint8_t vc = P.val_vc[v], op = P.val_op[v];
+                if (!(vc == VC_UINT || (vc == VC_SINT && w == 8 && op != NGZ_AGG_MIN && op != NGZ_AGG_MAX))) {
 #pragma unroll
-                for (int c = 0; c < LC_CH; ++c) {
-                    if (kid[c] >= nk) continue;
-                    const uint64_t xv = lc_operand(P, v, x[c], sp.val_w[v]);
-                    unsigned long long *cell = &acc[(kid[c] * nv + v) * 64 + lane];
-                    const uint64_t a = *cell;
-                    *cell = op == NGZ_AGG_ADD ? a + xv : op == NGZ_AGG_MIN ? (xv < a ? xv : a)
-                          : op == NGZ_AGG_MAX ? (xv > a ? xv : a) : (a | xv);
+                    for (int j = 0; j < LC_RPL; ++j) x[j] = lc_operand(P, v, x[j], w);
+                }
+                unsigned long long *cv = lc_cells + v * 64;
+                switch (op) {
+                case NGZ_AGG_ADD:
+#pragma unroll
+                    for (int j = 0; j < LC_RPL; ++j)
+                        if (kid[j] < (uint32_t)LC_NK) atomicAdd(cv + cell[j], (unsigned long long)x[j]);
+                    break;
+                case NGZ_AGG_MIN:
+#pragma unroll
+                    for (int j = 0; j < LC_RPL; ++j)
+                        if (kid[j] < (uint32_t)LC_NK) atomicMin(cv + cell[j], (unsigned long long)x[j]);
+                    break;
+                case NGZ_AGG_MAX:
+#pragma unroll
+                    for (int j = 0; j < LC_RPL; ++j)
+                        if (kid[j] < (uint32_t)LC_NK) atomicMax(cv + cell[j], (unsigned long long)x[j]);
+                    break;
+                default:
+#pragma unroll
+                    for (int j = 0; j < LC_RPL; ++j)
+                        if (kid[j] < (uint32_t)LC_NK) atomicOr(cv + cell[j], (unsigned long long)x[j]);
+                    break;
                 }
             }
         }
-        // key tuples present in the set: OR over the wave
+        // key tuples present in the set: OR over the wave; lane k updates tuple k's header
         uint32_t mset = pres;
 #pragma unroll
         for (int m = 32; m >= 1; m >>= 1) mset |= (uint32_t)__shfl_xor((int)mset, m);
-        if (lane < nk && ((mset >> lane) & 1)) {
-            const uint32_t k = lane, db = (info >> 2) & 0x7F;
-            h_tmin[k] = min(h_tmin[k], ts);
-            h_tmax[k] = max(h_tmax[k], ts);
-            h_smax[k] = max(h_smax[k], h.version == 9 ? h.sys_up_time : 0u);
-            h_tpl[k] |= sp.tpl_bit;
-            if (db < 64) h_d0[k] |= 1ull << db;
-            else h_d1[k] |= 1ull << (db & 63);
-            h_vp[k] |= hv;
+        if (lane < nkw && ((mset >> lane) & 1)) {
+            const uint32_t db = (info >> 2) & 0x7F;
+            h_tmin = min(h_tmin, ts);
+            h_tmax = max(h_tmax, ts);
+            h_smax = max(h_smax, h.version == 9 ? h.sys_up_time : 0u);
+            h_tpl |= sp.tpl_bit;
+            if (db < 64) h_d0 |= 1ull << db;
+            else h_d1 |= 1ull << (db & 63);
+            h_vp |= hv;
         }
-        __syncthreads();
     }
     if (cur != ~0ull) flush(cur);
+}
+
+// The key bytes of a packed tag into a claimed row (key_write's layout for packed keys)
+__device__ __forceinline__ void lc_key_write(uint8_t *R, const AggParams &P, uint64_t tag) {
+    uint64_t x = tag & ~(1ull << 63);
+    uint32_t kp = 0;
+    for (int k = (int)P.n_keys - 1; k >= 0; --k) {
+        const uint32_t bits = 8 * P.key_pw[k];
+        const uint64_t v = bits >= 64 ? x : (x & ((1ull << bits) - 1));
+        x = bits >= 64 ? 0 : x >> bits;
+        const bool present = x & 1;
+        x >>= 1;
+        if (present) kp |= 1u << k;
+        uint32_t *dst = (uint32_t *)(R + P.key_off[k]);
+        for (uint32_t j = 0; j < P.key_slot[k] / 4; ++j) dst[j] = present && j < 2 ? (uint32_t)(v >> (32 * j)) : 0u;
+    }
+    const uint32_t peer = (uint32_t)(x & ((1ull << P.peer_bits) - 1));
+    x >>= P.peer_bits;
+    const uint32_t proto = (x & 1) ? 9u : 10u;
+    *(uint32_t *)(R + 0) = (uint32_t)(x >> 1) * 60u;
+    *(uint32_t *)(R + 4) = proto | (peer << 16);
+    *(uint32_t *)(R + 8) = kp;
+}
+
+// One workgroup: the partial entries combined per tag, each tag's group found or claimed,
+// then applied.  err bits: 2 table full, 32 capacity (both: nothing claimed, nothing applied)
+constexpr int LCM_THREADS = 1024;
+__global__ __launch_bounds__(LCM_THREADS) void k_agg_lc_merge(const LcEntry *__restrict__ in,
+                                                              const unsigned int *__restrict__ n_in_p, uint32_t cap,
+                                                              const AggParams P, unsigned long long *__restrict__ tags,
+                                                              uint8_t *__restrict__ rows, uint64_t room,
+                                                              uint32_t *__restrict__ claims,
+                                                              unsigned long long *__restrict__ n_claims,
+                                                              unsigned int *__restrict__ flag,
+                                                              unsigned int *__restrict__ err) {
+    __shared__ unsigned long long t_tag[LC_SLOTS];
+    __shared__ uint32_t t_idx[LC_SLOTS];
+    __shared__ unsigned long long m_tag[LC_MAX_TAGS], m_cnt[LC_MAX_TAGS], m_tpl[LC_MAX_TAGS], m_d0[LC_MAX_TAGS],
+        m_d1[LC_MAX_TAGS], m_acc[LC_MAX_TAGS][LC_MAXV];
+    __shared__ uint32_t m_tmin[LC_MAX_TAGS], m_tmax[LC_MAX_TAGS], m_smax[LC_MAX_TAGS], m_vp[LC_MAX_TAGS],
+        m_g[LC_MAX_TAGS], m_claimed[LC_MAX_TAGS];
+    __shared__ uint32_t n_tags, s_full, s_new;
+    if (*(volatile unsigned int *)flag) return;
+    const uint32_t tid = threadIdx.x, nv = P.n_vals;
+    const uint32_t n_in = min(*n_in_p, cap);
+    for (uint32_t i = tid; i < LC_SLOTS; i += LCM_THREADS) {
+        t_tag[i] = 0;
+        t_idx[i] = NONE;
+    }
+    if (tid == 0) n_tags = s_full = s_new = 0;
+    __syncthreads();
+    auto find = [&](uint64_t tag, bool insert) -> uint32_t {
+        uint32_t i = (uint32_t)(slot_of(tag) & (LC_SLOTS - 1));
+        for (uint32_t probes = 0; probes < LC_SLOTS; ++probes, i = (i + 1) & (LC_SLOTS - 1)) {
+            unsigned long long c = t_tag[i];
+            if (c == 0 && insert) c = atomicCAS(&t_tag[i], 0ull, (unsigned long long)tag);
+            if (c == 0) return insert ? i : NONE;
+            if (c == tag) return i;
+        }
+        return NONE;
+    };
+    // 1. distinct tags
+    for (uint32_t i = tid; i < n_in; i += LCM_THREADS) find(in[i].tag, true);
+    __syncthreads();
+    for (uint32_t i = tid; i < LC_SLOTS; i += LCM_THREADS) {
+        if (!t_tag[i]) continue;
+        const uint32_t m = atomicAdd(&n_tags, 1u);
+        if (m >= LC_MAX_TAGS) continue;
+        t_idx[i] = m;
+        m_tag[m] = t_tag[i];
+        m_cnt[m] = m_tpl[m] = m_d0[m] = m_d1[m] = 0;
+        m_tmin[m] = 0xFFFFFFFFu;
+        m_tmax[m] = m_smax[m] = m_vp[m] = 0;
+        for (uint32_t v = 0; v < nv; ++v) m_acc[m][v] = lc_identity(P.val_op[v]);
+    }
+    __syncthreads();
+    if (n_tags > LC_MAX_TAGS) {  // too many groups for this path: the general path takes the push
+        if (tid == 0) atomicOr(flag, 1u);
+        return;
+    }
+    // 2. entries combined per tag
+    for (uint32_t i = tid; i < n_in; i += LCM_THREADS) {
+        const LcEntry &e = in[i];
+        const uint32_t m = t_idx[find(e.tag, false)];
+        atomicAdd(&m_cnt[m], e.cnt);
+        atomicMin(&m_tmin[m], e.tmin);
+        atomicMax(&m_tmax[m], e.tmax);
+        atomicMax(&m_smax[m], e.smax);
+        atomicOr(&m_vp[m], e.vp);
+        atomicOr(&m_tpl[m], e.tpl);
+        atomicOr(&m_d0[m], e.d0);
+        atomicOr(&m_d1[m], e.d1);
+        for (uint32_t v = 0; v < nv; ++v) {
+            switch (P.val_op[v]) {
+            case NGZ_AGG_ADD: atomicAdd(&m_acc[m][v], e.acc[v]); break;
+            case NGZ_AGG_MIN: atomicMin(&m_acc[m][v], e.acc[v]); break;
+            case NGZ_AGG_MAX: atomicMax(&m_acc[m][v], e.acc[v]); break;
+            default: atomicOr(&m_acc[m][v], e.acc[v]); break;
+            }
+        }
+    }
+    __syncthreads();
+    // 3. each tag's group: found, or claimed (this workgroup is the push's only claimer)
+    if (tid < n_tags) {
+        const uint64_t h = m_tag[tid];
+        uint64_t g = slot_of(h) & P.mask;
+        uint32_t found = NONE, claimed = 0;
+        for (uint64_t probes = 0; probes <= P.mask; ++probes, g = (g + 1) & P.mask) {
+            unsigned long long c = tags[g];
+            if (c == TAG_EMPTY) {
+                c = atomicCAS(&tags[g], TAG_EMPTY, (unsigned long long)h);
+                if (c == TAG_EMPTY) {
+                    lc_key_write(rows + g * P.row_bytes, P, h);
+                    found = (uint32_t)g;
+                    claimed = 1;
+                    break;
+                }
+            }
+            if (c == h) {
+                found = (uint32_t)g;
+                break;
+            }
+        }
+        m_g[tid] = found;
+        m_claimed[tid] = claimed;
+        if (found == NONE) atomicOr(&s_full, 1u);
+        if (claimed) atomicAdd(&s_new, 1u);
+    }
+    __syncthreads();
+    if (s_full || s_new > room) {  // nothing changes: release this push's claims
+        if (tid < n_tags && m_claimed[tid]) tags[m_g[tid]] = TAG_EMPTY;
+        if (tid == 0) atomicOr(err, s_full ? 2u : 32u);
+        return;
+    }
+    // 4. the rows
+    if (tid < n_tags) {
+        const uint32_t g = m_g[tid];
+        if (m_claimed[tid]) claims[atomicAdd(n_claims, 1ull)] = g;
+        uint8_t *R = rows + (uint64_t)g * P.row_bytes;
+        atomicAdd((unsigned long long *)(R + 16), m_cnt[tid]);
+        atomicMin((unsigned int *)(R + 24), m_tmin[tid]);
+        atomicMax((unsigned int *)(R + 28), m_tmax[tid]);
+        if (m_smax[tid]) atomicMax((unsigned int *)(R + 32), m_smax[tid]);
+        atomicOr((unsigned long long *)(R + 56), m_tpl[tid]);
+        if (m_d0[tid]) atomicOr((unsigned long long *)(R + 72), m_d0[tid]);
+        if (m_d1[tid]) atomicOr((unsigned long long *)(R + 80), m_d1[tid]);
+        apply_push_constants(R, P);
+        const uint32_t vp = m_vp[tid];
+        if (vp) atomicOr((unsigned int *)(R + 12), vp);
+        for (uint32_t v = 0; v < nv; ++v)
+            if ((vp >> v) & 1) apply_value_hot(R + P.val_off[v], P.val_op[v], m_acc[tid][v]);
+    }
 }
 
 __global__ void k_agg_init(uint8_t *__restrict__ rows, uint64_t n_groups, uint32_t row_bytes,
@@ -1864,7 +1994,9 @@ struct ngz_agg {
     size_t rec_cap = 0;
     uint8_t *part_buf = nullptr;  // partitioned reduction: counts, offsets, scan scratch, payloads
     size_t part_cap = 0;
-    LcTable *lc = nullptr;        // low-cardinality path: the push's distinct tags
+    LcEntry *lc = nullptr;        // low-cardinality path: the waves' partial groups
+    uint32_t lc_cap = 0;          // ... entries allocated
+    unsigned int *lc_cnt = nullptr;  // [0] entries written, [1] overflow flag
     const char *last_path = "";   // the reduction path of the last push ("lowcard" / "general")
     uint32_t lc_skip = 0;         // pushes left before the low-cardinality scan is tried again
 };
@@ -2355,6 +2487,7 @@ void ngz_agg_destroy(ngz_agg *a) {
     hipFree(a->rec_buf);
     hipFree(a->part_buf);
     hipFree(a->lc);
+    hipFree(a->lc_cnt);
     if (a->ev0) hipEventDestroy(a->ev0);
     if (a->ev1) hipEventDestroy(a->ev1);
     if (a->stream) hipStreamDestroy(a->stream);
@@ -2652,67 +2785,62 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, const ngz_p
         if (hipStreamSynchronize(st) != hipSuccess) a->poisoned = true;
         return fail(a, rc, why);
     };
-    // Low-cardinality path (packed keys, no byte-wise / ordered values): k_agg_lc_scan lists
-    // the push's distinct tags and claims their groups; with at most LC_NK distinct key
-    // tuples k_agg_lc_reduce reduces every record in registers.  Otherwise the general
-    // path below takes over from the claims made so far (NGZ_AGG_LC: 0 never, 1 at any
-    // size; default from 2^16 records).
+    // Low-cardinality path (packed keys, no byte-wise / ordered values): k_agg_lc_part reduces
+    // every record in one pass into per-wave partial groups, k_agg_lc_merge combines them
+    // per tag, claims and applies.  A wave with more than LC_NK key tuples in one window
+    // context, or more than LC_MAX_TAGS tags in the push, sends the push to the general
+    // path below, with nothing claimed or applied (NGZ_AGG_LC: 0 never, 1 at any size;
+    // default from 2^16 records).
     static const int lc_env = getenv("NGZ_AGG_LC") ? atoi(getenv("NGZ_AGG_LC")) : -1;
     const int lc_now = getenv("NGZ_AGG_LC") ? atoi(getenv("NGZ_AGG_LC")) : lc_env;  // read per push (tests)
-    // a push whose scan found too many distinct tags sends the next 15 pushes of the
-    // aggregator straight to the general path (high-cardinality keys pay for one scan in 16)
+    // a push that found too many key tuples sends the next 15 pushes of the aggregator
+    // straight to the general path (high-cardinality keys pay for one try in 16)
     const bool lc_try = lc_now == 1 || (lc_now != 0 && n_rec >= (1u << 16) && (a->lc_skip == 0 || --a->lc_skip == 0));
     if (n_rec && P.packed && P.lds_ok && P.n_vals <= (uint32_t)LC_MAXV && !ordered && lc_try) {
-        if (!a->lc && hipMalloc(&a->lc, sizeof(LcTable)) != hipSuccess) {
+        // one-wave workgroups; the lane-private LDS cells of LC_NK tuples bound the residency
+        // (160 KB per CU): a grid of that many workgroups, a multiple of the 8 XCDs
+        const size_t lds = (size_t)LC_NK * P.n_vals * 64 * 8;
+        const uint32_t per_cu = (uint32_t)std::max<size_t>(1, std::min<size_t>(16, (160u * 1024 - 1024) / (lds + 256)));
+        const uint32_t rg = std::max<uint32_t>(8, std::min<uint32_t>(256 * per_cu, (NS + 7) & ~7u));
+        const uint32_t cap = rg * LC_NK * 4;  // 4 window contexts per wave; more: the general path
+        if (cap > a->lc_cap || !a->lc_cnt) {
+            hipFree(a->lc);
             a->lc = nullptr;
-            restore();
-            upload_domains(a);
-            return fail(a, NGZ_E_NOMEM, "low-cardinality table");
+            a->lc_cap = 0;
+            if (!a->lc_cnt && hipMalloc(&a->lc_cnt, 8) != hipSuccess) a->lc_cnt = nullptr;
+            if (!a->lc_cnt || hipMalloc(&a->lc, sizeof(LcEntry) * (size_t)cap) != hipSuccess) {
+                a->lc = nullptr;
+                restore();
+                upload_domains(a);
+                return fail(a, NGZ_E_NOMEM, "low-cardinality buffers");
+            }
+            a->lc_cap = cap;
         }
-        AGG_HIP(a, hipMemsetAsync(a->lc, 0, sizeof(LcTable), st));
-        const uint32_t waves = std::max<uint32_t>(1, std::min<uint32_t>(NS, 256u * 64u));
-        const uint32_t sg = std::max<uint32_t>(8, ((waves + 3) / 4 + 7) & ~7u);
-        hipLaunchKernelGGL(k_agg_lc_scan, dim3(sg), dim3(256), 0, st, sets, NS, hdr, dginfo, a->plans, D, S, P, a->tags,
-                           a->rows, claims, a->n_claims, a->late, a->lc, a->err);
+        uint32_t kb = 0;
+        for (uint32_t k = 0; k < P.n_keys; ++k) kb += 1 + 8 * P.key_pw[k];
+        AGG_HIP(a, hipMemsetAsync(a->lc_cnt, 0, 8, st));
+        hipLaunchKernelGGL(k_agg_lc_part, dim3(rg), dim3(64), lds, st, sets, NS, hdr, dginfo, a->plans, D, S, P, kb,
+                           a->lc, a->lc_cnt, cap, a->late, a->lc_cnt + 1, a->err);
         AGG_HIP(a, hipGetLastError());
-        LcTable lt;
-        AGG_HIP(a, hipMemcpyAsync(&lt, a->lc, sizeof lt, hipMemcpyDeviceToHost, st));
+        const uint64_t room = a->limit - std::min(a->live, a->limit);
+        hipLaunchKernelGGL(k_agg_lc_merge, dim3(1), dim3(LCM_THREADS), 0, st, a->lc, a->lc_cnt, cap, P, a->tags,
+                           a->rows, room, claims, a->n_claims, a->lc_cnt + 1, a->err);
+        AGG_HIP(a, hipGetLastError());
+        unsigned int lcc[2] = {0, 0};
+        AGG_HIP(a, hipMemcpyAsync(lcc, a->lc_cnt, 8, hipMemcpyDeviceToHost, st));
         AGG_HIP(a, hipMemcpyAsync(&n_claims, a->n_claims, 8, hipMemcpyDeviceToHost, st));
         AGG_HIP(a, hipMemcpyAsync(&errv, a->err, 4, hipMemcpyDeviceToHost, st));
         AGG_HIP(a, hipStreamSynchronize(st));
         if (errv & 16) { a->poisoned = true; return rollback(NGZ_E_DEVICE, "set table entry out of range"); }
-        if (errv & 2) return rollback(NGZ_AGG_E_OVERFLOW, "group table full");
-        LcKeys K{};
-        uint32_t kb = 0;
-        for (uint32_t k = 0; k < P.n_keys; ++k) kb += 1 + 8 * P.key_pw[k];
-        K.key_bits = kb;
-        K.kmask = (1ull << kb) - 1;
-        bool fast = !lt.overflow;
-        std::vector<unsigned long long> kps;
-        for (uint32_t i = 0; fast && i < LC_SLOTS; ++i) {
-            if (!lt.tag[i]) continue;
-            const unsigned long long kp = lt.tag[i] & K.kmask;
-            if (std::find(kps.begin(), kps.end(), kp) == kps.end()) kps.push_back(kp);
-            fast = kps.size() <= (size_t)LC_NK;
-        }
-        if (fast) {
-            if (a->live + n_claims > a->limit) return rollback(NGZ_AGG_E_OVERFLOW, "more groups than the aggregator's capacity");
-            std::sort(kps.begin(), kps.end());
-            K.nk = (uint32_t)kps.size();
-            for (uint32_t k = 0; k < K.nk; ++k) K.kp[k] = kps[k];
-            // one wave per workgroup; its LDS accumulators bound the residency (160 KB per CU):
-            // a grid of that many workgroups, a multiple of the 8 XCDs
-            const size_t lds = (size_t)K.nk * P.n_vals * 64 * 8 + (size_t)K.nk * 64 * 4;
-            const uint32_t per_cu = (uint32_t)std::max<size_t>(1, std::min<size_t>(16, (160u * 1024 - 1024) / (lds + 512)));
-            const uint32_t rg = std::max<uint32_t>(8, std::min<uint32_t>(256 * per_cu, (NS + 7) & ~7u));
-            hipLaunchKernelGGL(k_agg_lc_reduce, dim3(rg), dim3(64), lds, st, sets, NS, hdr, dginfo, a->plans, D, S, P, K,
-                               a->rows, a->lc, a->err);
-            AGG_HIP(a, hipGetLastError());
+        if (!lcc[1]) {
+            // the merge released its claims when the push did not fit: nothing to undo
+            if (errv & 2) return rollback(NGZ_AGG_E_OVERFLOW, "group table full");
+            if (errv & 32) return rollback(NGZ_AGG_E_OVERFLOW, "more groups than the aggregator's capacity");
             a->last_path = "lowcard";
             goto done;
         }
-        // too many distinct tags / key tuples: the general path (its claims continue the list,
-        // its claim pass counts the late records again)
+        // too many key tuples / distinct tags: the general path from the start (nothing was
+        // claimed or applied; its claim pass counts the late records again)
         AGG_HIP(a, hipMemsetAsync(a->late, 0, 8, st));
         a->lc_skip = 15;
     }
