@@ -91,8 +91,8 @@ enum : uint8_t {
 struct AggSlotPlan {            // per batch slot, built on the host every push
     const uint8_t *key_col[NGZ_AGG_MAX_KEYS];   // null: the record has no such field (None)
     const uint8_t *val_col[NGZ_AGG_MAX_VALUES];
-    uint16_t key_w[NGZ_AGG_MAX_KEYS];
-    uint16_t val_w[NGZ_AGG_MAX_VALUES];
+    uint32_t key_w[NGZ_AGG_MAX_KEYS];           // 32-bit: a kernel reading the plan with scalar loads
+    uint32_t val_w[NGZ_AGG_MAX_VALUES];         // gets them without a vector load (SMEM is dword-wide)
     uint64_t tpl_bit;
     uint32_t proto;
     uint32_t usable;                            // 0: slot not aggregated (no records / not device-decoded)
@@ -1403,7 +1403,8 @@ constexpr uint32_t LC_SLOTS = 256;    // merge: open-addressing table of the pus
 constexpr uint32_t LC_MAX_TAGS = 64;  // more distinct tags in one push: the general path
 constexpr int LC_NK = 8;              // key tuples a wave accumulates per window context (more: general path)
 constexpr int LC_MAXV = 8;            // aggregated fields (more: the general path)
-constexpr int LC_RPL = 16;            // rows per lane and block (1024 rows: a whole MTU-to-64 KB set)
+constexpr int LC_CELLS = 32;          // lane-private cells per (tuple, field): lanes l and l + 32 share
+                                      // one (they reach the LDS in different cycles, no conflict)
 
 struct LcEntry {  // one wave's partial group (128 B)
     unsigned long long tag;  // exact packed tag (window / 60, flow type, peer, keys)
@@ -1415,53 +1416,59 @@ struct LcEntry {  // one wave's partial group (128 B)
 };
 static_assert(sizeof(LcEntry) == 128, "LcEntry");
 
-// A set's records aggregated by this push: its plan, or null (no records, late or failed
-// datagram, slot not aggregated); *late: the set's records are late
-__device__ __forceinline__ const AggSlotPlan *lc_set(const ngz_set_info &si, const uint16_t *__restrict__ dginfo,
-                                                     const AggSlotPlan *__restrict__ plans, uint32_t n_dgrams,
-                                                     uint32_t n_slots, bool *late, uint16_t *info,
-                                                     unsigned int *__restrict__ err) {
-    *late = false;
-    if (!si.n) return nullptr;
-    if (si.dgram >= n_dgrams || si.slot >= n_slots) {
-        if ((threadIdx.x & 63) == 0) atomicOr(err, 16u);
-        return nullptr;
-    }
-    *info = dginfo[si.dgram];
-    if (*info & DG_LATE) { *late = true; return nullptr; }
-    if (!(*info & DG_USE) || !plans[si.slot].usable) return nullptr;
-    return &plans[si.slot];
+// The buffer resource of a column's rows from A to the set's end (rounded up to 16 rows:
+// range checks are per dword, so the set's last rows are never in a partly covered dword;
+// in bounds, capacities being whole 256-row windows).  Reads past it return 0, so lanes past
+// the set's end need no clamp, and an absent field (col null) is a resource of 0 bytes.
+// Every input provably wave-uniform: a resource the compiler takes for a divergent one gets
+// a waterfall loop around each load.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t lc_rsrc(const uint8_t *col, uint32_t w, uint64_t A, uint64_t end) {
+    const int bytes = __builtin_amdgcn_readfirstlane(
+        col ? (int)min<uint64_t>((((end + 15) & ~15ull) - A) * w, 0x7FFFFFF0ull) : 0);
+    const uint64_t base = (uint64_t)(col ? col + A * w : nullptr);
+    const uint64_t ub = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(base >> 32)) << 32) |
+                        (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)base);
+    return __builtin_amdgcn_make_buffer_rsrc((void *)ub, (short)0, bytes, 0x00020000);
 }
 
-// Cells of rows r0 + 64 j (j < LC_RPL; rows at or past `end`: 0) of a w-byte column,
-// little-endian in a u64; col null (the field is None): 0.  One branch on the width,
-// then every load, so they are in flight together.
-template <class T>
-__device__ __forceinline__ void lc_load_t(const uint8_t *col, uint64_t r0, uint64_t end, uint64_t (&x)[LC_RPL]) {
-    // the column pointers come from the plan table in memory: generic to the compiler, so the
-    // loads would be flat ones (counted against LDS operations too); they are global memory
-    typedef const __attribute__((address_space(1))) T *gptr;
-    const gptr p = (gptr)col;
-    // rows past the set read its last row (every load unconditional, straight-line; the
-    // caller gives those rows no key tuple)
+constexpr int LC_G = 4;  // groups of 4 consecutive rows per lane and block: 1024 rows per block
+
+// The lane's rows of a W-byte column: group q holds rows A + 256 q + 4 lane + (0..3), 4W bytes
+// (4W-aligned), one 4-, 8- or 16-byte load (two for W = 8) per group, all in flight together.
+// Each width has its own instantiation, and the caller consumes the words inside it: loads
+// whose results merged across a branch on the width made the compiler wait on each at once.
+template <int W>
+struct LcCol {
+    static constexpr int NW = W;  // dwords per group
+    uint32_t d[LC_G][NW];
+    __device__ __forceinline__ void load(const __amdgpu_buffer_rsrc_t r, uint32_t lane) {
+        typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+        typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 #pragma unroll
-    for (int j = 0; j < LC_RPL; ++j) x[j] = (uint64_t)p[min(r0 + 64u * j, end - 1)];
-}
-__device__ __forceinline__ void lc_col_load(const uint8_t *col, uint32_t w, uint64_t r0, uint64_t end,
-                                            uint64_t (&x)[LC_RPL]) {
-    if (!col) {
+        for (int q = 0; q < LC_G; ++q) {
+            const uint32_t o = (256u * q + 4u * lane) * W;
+            if constexpr (W == 1) {
+                d[q][0] = __builtin_amdgcn_raw_buffer_load_b32(r, o, 0, 0);
+            } else if constexpr (W == 2) {
+                const v2u t = __builtin_amdgcn_raw_buffer_load_b64(r, o, 0, 0);
+                d[q][0] = t.x, d[q][1] = t.y;
+            } else {
 #pragma unroll
-        for (int j = 0; j < LC_RPL; ++j) x[j] = 0;
-    } else if (w == 8) {
-        lc_load_t<uint64_t>(col, r0, end, x);
-    } else if (w == 4) {
-        lc_load_t<uint32_t>(col, r0, end, x);
-    } else if (w == 2) {
-        lc_load_t<uint16_t>(col, r0, end, x);
-    } else {
-        lc_load_t<uint8_t>(col, r0, end, x);
+                for (int h = 0; h < W / 4; ++h) {
+                    const v4u t = __builtin_amdgcn_raw_buffer_load_b128(r, o + 16 * h, 0, 0);
+                    d[q][4 * h] = t.x, d[q][4 * h + 1] = t.y, d[q][4 * h + 2] = t.z, d[q][4 * h + 3] = t.w;
+                }
+            }
+        }
     }
-}
+    // row i (0-3) of group q, little-endian
+    __device__ __forceinline__ uint64_t cell(int q, int i) const {
+        if constexpr (W == 8) return d[q][2 * i] | ((uint64_t)d[q][2 * i + 1] << 32);
+        else if constexpr (W == 4) return d[q][i];
+        else if constexpr (W == 2) return (d[q][i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+        else return (d[q][0] >> (8 * i)) & 0xFFu;
+    }
+};
 
 // value_operand of a cell already loaded (raw: the w column bytes, little-endian)
 __device__ __forceinline__ uint64_t lc_operand(const AggParams &P, uint32_t v, uint64_t raw, uint32_t w) {
@@ -1487,31 +1494,144 @@ __device__ __forceinline__ uint64_t lc_operand(const AggParams &P, uint32_t v, u
 
 __device__ __forceinline__ uint64_t lc_identity(uint8_t op) { return op == NGZ_AGG_MIN ? ~0ull : 0ull; }
 
-__global__ __launch_bounds__(64) void k_agg_lc_part(const ngz_set_info *__restrict__ sets, uint32_t n_sets,
-                                                    const ngz_dgram_hdr *__restrict__ hdr,
-                                                    const uint16_t *__restrict__ dginfo,
-                                                    const AggSlotPlan *__restrict__ plans, uint32_t n_dgrams,
-                                                    uint32_t n_slots, const AggParams P, uint32_t key_bits,
-                                                    LcEntry *__restrict__ out, unsigned int *__restrict__ n_out,
-                                                    uint32_t cap, unsigned long long *__restrict__ late_count,
-                                                    unsigned int *__restrict__ flag, unsigned int *__restrict__ err) {
-    extern __shared__ unsigned long long lc_cells[];  // [tuple][field][lane]
-    const uint32_t nv = P.n_vals, lane = threadIdx.x;
+constexpr int LC_MAXK = 4;  // key fields (packed keys: at most 35 bits of them)
+
+// One set as k_agg_lc_part needs it, resolved ahead (no dependent chain set -> datagram
+// -> plan per set in the reduce loop): 32 B, one scalar load
+struct LcSet {
+    uint32_t rec0, n, ts, sysup;
+    uint32_t slot;  // NONE: no records aggregated (empty, late, failed datagram, slot not aggregated)
+    uint32_t info;  // bits 0-6: observation domain entry
+    uint32_t pad[2];
+};
+static_assert(sizeof(LcSet) == 32, "LcSet");
+
+// a descriptor through the constant address space (scalar loads; the set index is uniform)
+__device__ __forceinline__ LcSet lc_desc(const LcSet *p) {
+    typedef const __attribute__((address_space(4))) LcSet *cset;
+    const cset q = (cset)p;
+    LcSet d;
+    d.rec0 = q->rec0;
+    d.n = q->n;
+    d.ts = q->ts;
+    d.sysup = q->sysup;
+    d.slot = q->slot;
+    d.info = q->info;
+    d.pad[0] = d.pad[1] = 0;
+    return d;
+}
+
+__global__ __launch_bounds__(256) void k_agg_lc_sets(const ngz_set_info *__restrict__ sets, uint32_t n_sets,
+                                                     const ngz_dgram_hdr *__restrict__ hdr,
+                                                     const uint16_t *__restrict__ dginfo,
+                                                     const AggSlotPlan *__restrict__ plans, uint32_t n_dgrams,
+                                                     uint32_t n_slots, LcSet *__restrict__ out,
+                                                     unsigned long long *__restrict__ late_count,
+                                                     unsigned int *__restrict__ err) {
+    for (uint32_t s0 = blockIdx.x * blockDim.x; s0 < n_sets; s0 += gridDim.x * blockDim.x) {
+    const uint32_t s = s0 + threadIdx.x;
+    uint64_t late_n = 0;
+    if (s < n_sets) {
+        const ngz_set_info si = sets[s];
+        LcSet d{si.rec0, si.n, 0, 0, NONE, 0, {0, 0}};
+        if (si.n) {
+            if (si.dgram >= n_dgrams || si.slot >= n_slots) {
+                atomicOr(err, 16u);
+            } else {
+                const uint16_t info = dginfo[si.dgram];
+                if (info & DG_LATE) {
+                    late_n = si.n;
+                } else if ((info & DG_USE) && plans[si.slot].usable) {
+                    const ngz_dgram_hdr &h = hdr[si.dgram];
+                    d.ts = h.time;
+                    d.sysup = h.version == 9 ? h.sys_up_time : 0u;
+                    d.slot = si.slot;
+                    d.info = (info >> 2) & 0x7F;
+                }
+            }
+        }
+        out[s] = d;
+    }
+    late_n = wave_reduce<R_ADD>(late_n);  // one counter atomic per wave
+    if ((threadIdx.x & 63) == 0 && late_n) atomicAdd(late_count, (unsigned long long)late_n);
+    }
+}
+
+// One aggregated field of a block, W-byte column: the block's loads, then one LDS atomic per
+// row into the row's tuple cell (rows outside the set have the spare tuple LC_NK)
+template <int W>
+__device__ __forceinline__ void lc_reduce_field(const __amdgpu_buffer_rsrc_t r, const AggParams &P, uint32_t v,
+                                                uint32_t lane, const uint32_t (&cell)[LC_G * 4],
+                                                unsigned long long *__restrict__ cv) {
+    LcCol<W> c;
+    c.load(r, lane);
+    const uint8_t op = P.val_op[v], vc = P.val_vc[v];
+    const bool plain = vc == VC_UINT || (vc == VC_SINT && W == 8 && op != NGZ_AGG_MIN && op != NGZ_AGG_MAX);
+    uint64_t x[LC_G * 4];
+#pragma unroll
+    for (int q = 0; q < LC_G; ++q)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) x[4 * q + i] = c.cell(q, i);
+    if (!plain) {
+#pragma unroll
+        for (int j = 0; j < LC_G * 4; ++j) x[j] = lc_operand(P, v, x[j], W);
+    }
+    switch (op) {
+    case NGZ_AGG_ADD:
+#pragma unroll
+        for (int j = 0; j < LC_G * 4; ++j) atomicAdd(cv + cell[j], (unsigned long long)x[j]);
+        break;
+    case NGZ_AGG_MIN:
+#pragma unroll
+        for (int j = 0; j < LC_G * 4; ++j) atomicMin(cv + cell[j], (unsigned long long)x[j]);
+        break;
+    case NGZ_AGG_MAX:
+#pragma unroll
+        for (int j = 0; j < LC_G * 4; ++j) atomicMax(cv + cell[j], (unsigned long long)x[j]);
+        break;
+    default:
+#pragma unroll
+        for (int j = 0; j < LC_G * 4; ++j) atomicOr(cv + cell[j], (unsigned long long)x[j]);
+        break;
+    }
+}
+
+// One key field of a block into the packed keys: key = ((key << 1) | present) << 8W | value
+template <int W>
+__device__ __forceinline__ void lc_key_field(const __amdgpu_buffer_rsrc_t r, uint32_t lane, uint64_t has,
+                                             uint64_t (&key)[LC_G * 4]) {
+    LcCol<W> c;
+    c.load(r, lane);
+#pragma unroll
+    for (int q = 0; q < LC_G; ++q)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) key[4 * q + i] = (((key[4 * q + i] << 1) | has) << (8 * W)) | c.cell(q, i);
+}
+
+// LDS per wave: value cells [tuple 0..LC_NK][field][LC_CELLS] (u64; tuple LC_NK takes the
+// rows outside the set and is never read), then counts [tuple][LC_CELLS] (u32)
+__host__ __device__ constexpr size_t lc_lds_bytes(uint32_t nv) {
+    return (size_t)(LC_NK + 1) * nv * LC_CELLS * 8 + (size_t)(LC_NK + 1) * LC_CELLS * 4;
+}
+
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_agg_lc_part(
+    const LcSet *__restrict__ descs, uint32_t n_sets, const AggSlotPlan *__restrict__ plans, const AggParams P,
+    uint32_t key_bits, LcEntry *__restrict__ out, unsigned int *__restrict__ n_out, uint32_t cap,
+    unsigned int *__restrict__ flag, uint32_t dbg) {
+    extern __shared__ unsigned long long lc_cells[];
+    const uint32_t nv = P.n_vals, lane = threadIdx.x, cl = lane & (LC_CELLS - 1);
+    unsigned int *lc_cnt = (unsigned int *)(lc_cells + (size_t)(LC_NK + 1) * nv * LC_CELLS);
     uint64_t kl[LC_NK];  // the wave's key tuples of the current window context (wave-uniform)
     uint32_t nkw = 0;
-    uint32_t cnt[LC_NK];
     // lane k: header fields of tuple k
     uint32_t h_tmin = 0xFFFFFFFFu, h_tmax = 0, h_smax = 0, h_vp = 0;
     uint64_t h_tpl = 0, h_d0 = 0, h_d1 = 0;
 #pragma unroll
-    for (int k = 0; k < LC_NK; ++k) {
-        kl[k] = 0;
-        cnt[k] = 0;
-    }
+    for (int k = 0; k < LC_NK; ++k) kl[k] = 0;
     auto reset = [&]() {
-        for (uint32_t c = 0; c < (uint32_t)LC_NK * nv; ++c) lc_cells[c * 64 + lane] = lc_identity(P.val_op[c % nv]);
-#pragma unroll
-        for (int k = 0; k < LC_NK; ++k) cnt[k] = 0;
+        for (uint32_t c = 0; c < (uint32_t)(LC_NK + 1) * nv; ++c)
+            lc_cells[c * LC_CELLS + cl] = lc_identity(P.val_op[c % nv]);
+        for (uint32_t k = 0; k <= (uint32_t)LC_NK; ++k) lc_cnt[k * LC_CELLS + cl] = 0;
         nkw = 0;
         h_tmin = 0xFFFFFFFFu;
         h_tmax = h_smax = h_vp = 0;
@@ -1530,7 +1650,7 @@ __global__ __launch_bounds__(64) void k_agg_lc_part(const ngz_set_info *__restri
 #pragma unroll
         for (int k = 0; k < LC_NK; ++k) {
             if (k >= (int)nkw) break;
-            const uint64_t total = wave_reduce<R_ADD>((uint64_t)cnt[k]);
+            const uint64_t total = wave_reduce<R_ADD>(lane < LC_CELLS ? (uint64_t)lc_cnt[k * LC_CELLS + cl] : 0ull);
             LcEntry *e = out + base + k;
             if (lane == (uint32_t)k) {  // the tuple's header lives in lane k
                 e->tag = (ctx << key_bits) | kl[k] | (1ull << 63);  // key_tag's exact tag
@@ -1544,9 +1664,10 @@ __global__ __launch_bounds__(64) void k_agg_lc_part(const ngz_set_info *__restri
                 e->d1 = h_d1;
             }
             for (uint32_t v = 0; v < nv; ++v) {
-                const uint64_t a = lc_cells[(k * nv + v) * 64 + lane];
+                const uint8_t op = P.val_op[v];
+                const uint64_t a = lane < LC_CELLS ? lc_cells[(k * nv + v) * LC_CELLS + cl] : lc_identity(op);
                 uint64_t r;
-                switch (P.val_op[v]) {
+                switch (op) {
                 case NGZ_AGG_ADD: r = wave_reduce<R_ADD>(a); break;
                 case NGZ_AGG_MIN: r = wave_reduce<R_MIN>(a); break;
                 case NGZ_AGG_MAX: r = wave_reduce<R_MAX>(a); break;
@@ -1560,29 +1681,24 @@ __global__ __launch_bounds__(64) void k_agg_lc_part(const ngz_set_info *__restri
     reset();
     uint64_t cur = ~0ull;  // current window context (window / 60, flow type, peer); none yet
     // one wave per workgroup: the set sequence, the set and its plan are wave-uniform (scalar
-    // loads, no EXEC masking around them)
+    // loads, no EXEC masking around them); XCD-aware: workgroup b walks the (b % 8)-th eighth
     const uint32_t G = gridDim.x, X = (G % 8 == 0 && G >= 8) ? 8u : 1u;
     const uint32_t per = (n_sets + X - 1) / X, s_end = min(n_sets, (blockIdx.x % X) * per + per);
-    for (uint32_t s = (blockIdx.x % X) * per + blockIdx.x / X; s < s_end; s += G / X) {
-        if (*(volatile unsigned int *)flag) return;  // some wave overflowed: the general path takes the push
-        ngz_set_info si = sets[s];
-        si.dgram = __builtin_amdgcn_readfirstlane(si.dgram);
-        si.slot = (uint16_t)__builtin_amdgcn_readfirstlane(si.slot);
-        si.rec0 = __builtin_amdgcn_readfirstlane(si.rec0);
-        si.n = __builtin_amdgcn_readfirstlane(si.n);
-        bool late;
-        uint16_t info = 0;
-        const AggSlotPlan *spp = lc_set(si, dginfo, plans, n_dgrams, n_slots, &late, &info, err);
-        info = (uint16_t)__builtin_amdgcn_readfirstlane(info);
-        if (late && lane == 0) atomicAdd(late_count, (unsigned long long)si.n);
-        if (!spp) continue;
+    typedef const __attribute__((address_space(4))) AggSlotPlan *cplan;
+    const uint32_t s0 = (blockIdx.x % X) * per + blockIdx.x / X, step = G / X;
+    LcSet dn{};  // the next set's descriptor, loaded one set ahead
+    if (s0 < s_end) dn = lc_desc(descs + s0);
+    uint32_t it = 0;
+    for (uint32_t s = s0; s < s_end; s += step, ++it) {
+        // some wave overflowed: the general path takes the push (checked every 16 sets)
+        if ((it & 15) == 15 && *(volatile unsigned int *)flag) return;
+        const LcSet d = dn;
+        if (s + step < s_end) dn = lc_desc(descs + s + step);
+        if (d.slot == NONE) continue;
         // the plan through the constant address space: its fields are wave-uniform and read
-        // with scalar loads, also at a runtime field index (a generic pointer made them vector
-        // loads, each a memory round trip before the field's column loads could issue)
-        typedef const __attribute__((address_space(4))) AggSlotPlan *cplan;
-        const auto &sp = *(cplan)spp;
-        const ngz_dgram_hdr &h = hdr[si.dgram];
-        const uint32_t ts = __builtin_amdgcn_readfirstlane(h.time), win = ts - ts % 60;
+        // with scalar loads, also at a runtime field index
+        const auto &sp = ((cplan)plans)[d.slot];
+        const uint32_t ts = d.ts, win = ts - ts % 60;
         const uint64_t ctx = ((((uint64_t)(win / 60) << 1) | (sp.proto == 9)) << P.peer_bits) | P.peer;
         if (ctx != cur) {
             if (cur != ~0ull && !flush(cur)) return;
@@ -1592,37 +1708,52 @@ __global__ __launch_bounds__(64) void k_agg_lc_part(const ngz_set_info *__restri
         uint32_t hv = 0;  // aggregated fields the set's template has (Some)
         for (uint32_t v = 0; v < nv; ++v)
             if (sp.val_col[v]) hv |= 1u << v;
-        const uint64_t end = (uint64_t)si.rec0 + si.n;
+        const uint64_t end = (uint64_t)d.rec0 + d.n;
         uint32_t pres = 0;  // key tuples this lane saw in the set
-        // blocks of 1024 rows, LC_RPL per lane 64 apart: the block's key tuples first (every
-        // key column's loads in flight together), then field by field (a runtime loop, one
-        // copy of the code): the field's LC_RPL loads together, then its LDS updates
-        for (uint32_t b0 = 0; b0 < si.n; b0 += 64 * LC_RPL) {
-            const uint64_t r0 = (uint64_t)si.rec0 + b0 + lane;
-            uint64_t key[LC_RPL];
+        // blocks of 1024 rows from the set's first row rounded down to 4: lane l takes rows
+        // A + 256 q + 4 l + i, so every column load is 4W-aligned and one wave instruction
+        // covers 256 W contiguous bytes
+        for (uint64_t A = d.rec0 & ~3ull; A < end; A += 256 * LC_G) {
+            const uint32_t lo = (uint32_t)(d.rec0 > A ? d.rec0 - A : 0), hi = (uint32_t)min<uint64_t>(end - A, 256 * LC_G);
+            uint64_t key[LC_G * 4];
 #pragma unroll
-            for (int j = 0; j < LC_RPL; ++j) key[j] = 0;
+            for (int j = 0; j < LC_G * 4; ++j) key[j] = 0;
             for (uint32_t k = 0; k < P.n_keys; ++k) {  // key_tag's packing of the key fields
                 const uint8_t *col = sp.key_col[k];
-                const uint32_t sh = 8 * P.key_pw[k];
-                uint64_t kv[LC_RPL];
-                lc_col_load(col, sp.key_w[k], r0, end, kv);
-#pragma unroll
-                for (int j = 0; j < LC_RPL; ++j) key[j] = (((key[j] << 1) | (col != nullptr)) << sh) | kv[j];
+                const __amdgpu_buffer_rsrc_t r = lc_rsrc(col, P.key_pw[k], A, end);
+                const uint64_t has = col != nullptr;
+                switch (P.key_pw[k]) {
+                case 1: lc_key_field<1>(r, lane, has, key); break;
+                case 2: lc_key_field<2>(r, lane, has, key); break;
+                default: lc_key_field<4>(r, lane, has, key); break;
+                }
             }
-            // each row's tuple in the wave's list, extended by any tuple it has not met yet
-            uint32_t kid[LC_RPL];
+            // each row's tuple in the wave's list, extended by any tuple it has not met yet;
+            // rows outside the set: the spare tuple LC_NK
+            uint32_t kid[LC_G * 4], vm = 0;
 #pragma unroll
-            for (int j = 0; j < LC_RPL; ++j) {
+            for (int j = 0; j < LC_G * 4; ++j) {
+                const uint32_t rel = 256u * (j >> 2) + 4u * lane + (j & 3);
+                if (rel - lo < hi - lo) vm |= 1u << j;  // lo <= rel < hi
                 kid[j] = LC_NK;
-#pragma unroll
-                for (int k = 0; k < LC_NK; ++k)
-                    if (k < (int)nkw && key[j] == kl[k]) kid[j] = (uint32_t)k;
             }
-            for (int j = 0; j < LC_RPL; ++j) {  // not unrolled: new tuples are rare
-                const bool valid = r0 + 64u * j < end;
+            // the wave's tuples one at a time (a uniform exit after the last one met)
+#pragma unroll
+            for (int k = 0; k < LC_NK; ++k) {
+                if (k >= (int)nkw) break;
+#pragma unroll
+                for (int j = 0; j < LC_G * 4; ++j) kid[j] = key[j] == kl[k] ? (uint32_t)k : kid[j];
+            }
+            uint32_t unmatched = 0;
+#pragma unroll
+            for (int j = 0; j < LC_G * 4; ++j) unmatched |= kid[j] == LC_NK ? 1u << j : 0u;
+            // rows whose tuple the wave has not met yet: rare, one ballot tells
+            if (__ballot((unmatched & vm) != 0))
+#pragma unroll
+            for (int j = 0; j < LC_G * 4; ++j) {
+                const bool valid = (vm >> j) & 1;
                 uint64_t todo = __ballot(valid && kid[j] == LC_NK);
-                while (todo) {
+                while (todo) {  // rare: a tuple new to this wave and window context
                     const int l0 = __ffsll((unsigned long long)todo) - 1;
                     const uint64_t t = readlane64(key[j], l0);
                     if (nkw == (uint32_t)LC_NK) {
@@ -1633,68 +1764,44 @@ __global__ __launch_bounds__(64) void k_agg_lc_part(const ngz_set_info *__restri
                     for (int k = 0; k < LC_NK; ++k)
                         if (k == (int)nkw) kl[k] = t;
 #pragma unroll
-                    for (int i = 0; i < LC_RPL; ++i)
-                        if (r0 + 64u * i < end && key[i] == t) kid[i] = nkw;
+                    for (int i = 0; i < LC_G * 4; ++i)
+                        if (((vm >> i) & 1) && key[i] == t) kid[i] = nkw;
                     ++nkw;
                     todo &= ~__ballot(valid && key[j] == t);
                 }
             }
-            // counts, present tuples; rows past the set keep kid LC_NK
+            uint32_t cell[LC_G * 4];
 #pragma unroll
-            for (int j = 0; j < LC_RPL; ++j) {
-                if (r0 + 64u * j >= end) kid[j] = LC_NK;
-                pres |= kid[j] < (uint32_t)LC_NK ? 1u << kid[j] : 0u;
-#pragma unroll
-                for (int k = 0; k < LC_NK; ++k) cnt[k] += kid[j] == (uint32_t)k;
+            for (int j = 0; j < LC_G * 4; ++j) {
+                if (!((vm >> j) & 1)) kid[j] = LC_NK;
+                pres |= (1u << kid[j]);
+                atomicAdd(&lc_cnt[kid[j] * LC_CELLS + cl], 1u);
+                cell[j] = kid[j] * nv * LC_CELLS + cl;
             }
-            // lane-private cell offsets of the rows' tuples (field 0); rows without one: none
-            uint32_t cell[LC_RPL];
-#pragma unroll
-            for (int j = 0; j < LC_RPL; ++j) cell[j] = kid[j] * nv * 64 + lane;
+            // field by field: the field's loads for the block in flight together, then its
+            // LDS updates (the width's own instantiation; a runtime loop over the fields)
             for (uint32_t v = 0; v < nv; ++v) {
-                if (!((hv >> v) & 1)) continue;
-                uint64_t x[LC_RPL];
+                if (!((hv >> v) & 1) || (dbg & 1)) continue;
                 const uint32_t w = sp.val_w[v];
-                lc_col_load(sp.val_col[v], w, r0, end, x);
-                const uint8_t vc = P.val_vc[v], op = P.val_op[v];
-                if (!(vc == VC_UINT || (vc == VC_SINT && w == 8 && op != NGZ_AGG_MIN && op != NGZ_AGG_MAX))) {
-#pragma unroll
-                    for (int j = 0; j < LC_RPL; ++j) x[j] = lc_operand(P, v, x[j], w);
-                }
-                unsigned long long *cv = lc_cells + v * 64;
-                switch (op) {
-                case NGZ_AGG_ADD:
-#pragma unroll
-                    for (int j = 0; j < LC_RPL; ++j)
-                        if (kid[j] < (uint32_t)LC_NK) atomicAdd(cv + cell[j], (unsigned long long)x[j]);
-                    break;
-                case NGZ_AGG_MIN:
-#pragma unroll
-                    for (int j = 0; j < LC_RPL; ++j)
-                        if (kid[j] < (uint32_t)LC_NK) atomicMin(cv + cell[j], (unsigned long long)x[j]);
-                    break;
-                case NGZ_AGG_MAX:
-#pragma unroll
-                    for (int j = 0; j < LC_RPL; ++j)
-                        if (kid[j] < (uint32_t)LC_NK) atomicMax(cv + cell[j], (unsigned long long)x[j]);
-                    break;
-                default:
-#pragma unroll
-                    for (int j = 0; j < LC_RPL; ++j)
-                        if (kid[j] < (uint32_t)LC_NK) atomicOr(cv + cell[j], (unsigned long long)x[j]);
-                    break;
+                const __amdgpu_buffer_rsrc_t r = lc_rsrc((dbg & 2) ? nullptr : sp.val_col[v], w, A, end);
+                unsigned long long *cv = lc_cells + v * LC_CELLS;
+                switch (w) {
+                case 8: lc_reduce_field<8>(r, P, v, lane, cell, cv); break;
+                case 4: lc_reduce_field<4>(r, P, v, lane, cell, cv); break;
+                case 2: lc_reduce_field<2>(r, P, v, lane, cell, cv); break;
+                default: lc_reduce_field<1>(r, P, v, lane, cell, cv); break;
                 }
             }
         }
         // key tuples present in the set: OR over the wave; lane k updates tuple k's header
-        uint32_t mset = pres;
+        uint32_t mset = pres & ((1u << LC_NK) - 1);
 #pragma unroll
         for (int m = 32; m >= 1; m >>= 1) mset |= (uint32_t)__shfl_xor((int)mset, m);
         if (lane < nkw && ((mset >> lane) & 1)) {
-            const uint32_t db = (info >> 2) & 0x7F;
+            const uint32_t db = d.info;
             h_tmin = min(h_tmin, ts);
             h_tmax = max(h_tmax, ts);
-            h_smax = max(h_smax, h.version == 9 ? h.sys_up_time : 0u);
+            h_smax = max(h_smax, d.sysup);
             h_tpl |= sp.tpl_bit;
             if (db < 64) h_d0 |= 1ull << db;
             else h_d1 |= 1ull << (db & 63);
@@ -1726,87 +1833,142 @@ __device__ __forceinline__ void lc_key_write(uint8_t *R, const AggParams &P, uin
     *(uint32_t *)(R + 8) = kp;
 }
 
-// One workgroup: the partial entries combined per tag, each tag's group found or claimed,
-// then applied.  err bits: 2 table full, 32 capacity (both: nothing claimed, nothing applied)
-constexpr int LCM_THREADS = 1024;
-__global__ __launch_bounds__(LCM_THREADS) void k_agg_lc_merge(const LcEntry *__restrict__ in,
-                                                              const unsigned int *__restrict__ n_in_p, uint32_t cap,
-                                                              const AggParams P, unsigned long long *__restrict__ tags,
-                                                              uint8_t *__restrict__ rows, uint64_t room,
-                                                              uint32_t *__restrict__ claims,
-                                                              unsigned long long *__restrict__ n_claims,
-                                                              unsigned int *__restrict__ flag,
-                                                              unsigned int *__restrict__ err) {
-    __shared__ unsigned long long t_tag[LC_SLOTS];
-    __shared__ uint32_t t_idx[LC_SLOTS];
-    __shared__ unsigned long long m_tag[LC_MAX_TAGS], m_cnt[LC_MAX_TAGS], m_tpl[LC_MAX_TAGS], m_d0[LC_MAX_TAGS],
+// The partial entries, a few per wave, combined per exact tag: LCM_BLOCKS workgroups each
+// combine a slice in LDS and write one entry per tag they met; the workgroup that finishes last
+// combines those, then each distinct tag finds or claims its group and is applied to the row.
+// err bits: 2 table full, 32 capacity (both: nothing claimed, nothing applied)
+constexpr int LCM_THREADS = 256;
+constexpr int LCM_BLOCKS = 64;
+
+struct LcMergeLds {
+    unsigned long long t_tag[LC_SLOTS];
+    uint32_t t_idx[LC_SLOTS];
+    unsigned long long m_tag[LC_MAX_TAGS], m_cnt[LC_MAX_TAGS], m_tpl[LC_MAX_TAGS], m_d0[LC_MAX_TAGS],
         m_d1[LC_MAX_TAGS], m_acc[LC_MAX_TAGS][LC_MAXV];
-    __shared__ uint32_t m_tmin[LC_MAX_TAGS], m_tmax[LC_MAX_TAGS], m_smax[LC_MAX_TAGS], m_vp[LC_MAX_TAGS],
-        m_g[LC_MAX_TAGS], m_claimed[LC_MAX_TAGS];
-    __shared__ uint32_t n_tags, s_full, s_new;
-    if (*(volatile unsigned int *)flag) return;
+    uint32_t m_tmin[LC_MAX_TAGS], m_tmax[LC_MAX_TAGS], m_smax[LC_MAX_TAGS], m_vp[LC_MAX_TAGS], m_g[LC_MAX_TAGS],
+        m_claimed[LC_MAX_TAGS];
+    uint32_t n_tags, s_full, s_new, s_last;
+};
+
+// entries i = first, first + stride, ... < n of `in` combined into L; false: more than
+// LC_MAX_TAGS distinct tags
+__device__ bool lc_combine(LcMergeLds &L, const LcEntry *__restrict__ in, uint32_t first, uint32_t stride, uint32_t n,
+                           const AggParams &P) {
     const uint32_t tid = threadIdx.x, nv = P.n_vals;
-    const uint32_t n_in = min(*n_in_p, cap);
-    for (uint32_t i = tid; i < LC_SLOTS; i += LCM_THREADS) {
-        t_tag[i] = 0;
-        t_idx[i] = NONE;
+    for (uint32_t i = tid; i < LC_SLOTS; i += blockDim.x) {
+        L.t_tag[i] = 0;
+        L.t_idx[i] = NONE;
     }
-    if (tid == 0) n_tags = s_full = s_new = 0;
+    if (tid == 0) L.n_tags = 0;
     __syncthreads();
     auto find = [&](uint64_t tag, bool insert) -> uint32_t {
         uint32_t i = (uint32_t)(slot_of(tag) & (LC_SLOTS - 1));
         for (uint32_t probes = 0; probes < LC_SLOTS; ++probes, i = (i + 1) & (LC_SLOTS - 1)) {
-            unsigned long long c = t_tag[i];
-            if (c == 0 && insert) c = atomicCAS(&t_tag[i], 0ull, (unsigned long long)tag);
+            unsigned long long c = L.t_tag[i];
+            if (c == 0 && insert) c = atomicCAS(&L.t_tag[i], 0ull, (unsigned long long)tag);
             if (c == 0) return insert ? i : NONE;
             if (c == tag) return i;
         }
         return NONE;
     };
-    // 1. distinct tags
-    for (uint32_t i = tid; i < n_in; i += LCM_THREADS) find(in[i].tag, true);
+    for (uint32_t i = first + tid * stride; i < n; i += blockDim.x * stride)
+        if (in[i].tag) find(in[i].tag, true);  // tag 0: an unused slice entry
     __syncthreads();
-    for (uint32_t i = tid; i < LC_SLOTS; i += LCM_THREADS) {
-        if (!t_tag[i]) continue;
-        const uint32_t m = atomicAdd(&n_tags, 1u);
+    for (uint32_t i = tid; i < LC_SLOTS; i += blockDim.x) {
+        if (!L.t_tag[i]) continue;
+        const uint32_t m = atomicAdd(&L.n_tags, 1u);
         if (m >= LC_MAX_TAGS) continue;
-        t_idx[i] = m;
-        m_tag[m] = t_tag[i];
-        m_cnt[m] = m_tpl[m] = m_d0[m] = m_d1[m] = 0;
-        m_tmin[m] = 0xFFFFFFFFu;
-        m_tmax[m] = m_smax[m] = m_vp[m] = 0;
-        for (uint32_t v = 0; v < nv; ++v) m_acc[m][v] = lc_identity(P.val_op[v]);
+        L.t_idx[i] = m;
+        L.m_tag[m] = L.t_tag[i];
+        L.m_cnt[m] = L.m_tpl[m] = L.m_d0[m] = L.m_d1[m] = 0;
+        L.m_tmin[m] = 0xFFFFFFFFu;
+        L.m_tmax[m] = L.m_smax[m] = L.m_vp[m] = 0;
+        for (uint32_t v = 0; v < nv; ++v) L.m_acc[m][v] = lc_identity(P.val_op[v]);
     }
     __syncthreads();
-    if (n_tags > LC_MAX_TAGS) {  // too many groups for this path: the general path takes the push
-        if (tid == 0) atomicOr(flag, 1u);
-        return;
-    }
-    // 2. entries combined per tag
-    for (uint32_t i = tid; i < n_in; i += LCM_THREADS) {
+    if (L.n_tags > LC_MAX_TAGS) return false;
+    for (uint32_t i = first + tid * stride; i < n; i += blockDim.x * stride) {
         const LcEntry &e = in[i];
-        const uint32_t m = t_idx[find(e.tag, false)];
-        atomicAdd(&m_cnt[m], e.cnt);
-        atomicMin(&m_tmin[m], e.tmin);
-        atomicMax(&m_tmax[m], e.tmax);
-        atomicMax(&m_smax[m], e.smax);
-        atomicOr(&m_vp[m], e.vp);
-        atomicOr(&m_tpl[m], e.tpl);
-        atomicOr(&m_d0[m], e.d0);
-        atomicOr(&m_d1[m], e.d1);
+        if (!e.tag) continue;
+        const uint32_t m = L.t_idx[find(e.tag, false)];
+        atomicAdd(&L.m_cnt[m], e.cnt);
+        atomicMin(&L.m_tmin[m], e.tmin);
+        atomicMax(&L.m_tmax[m], e.tmax);
+        atomicMax(&L.m_smax[m], e.smax);
+        atomicOr(&L.m_vp[m], e.vp);
+        atomicOr(&L.m_tpl[m], e.tpl);
+        atomicOr(&L.m_d0[m], e.d0);
+        atomicOr(&L.m_d1[m], e.d1);
         for (uint32_t v = 0; v < nv; ++v) {
             switch (P.val_op[v]) {
-            case NGZ_AGG_ADD: atomicAdd(&m_acc[m][v], e.acc[v]); break;
-            case NGZ_AGG_MIN: atomicMin(&m_acc[m][v], e.acc[v]); break;
-            case NGZ_AGG_MAX: atomicMax(&m_acc[m][v], e.acc[v]); break;
-            default: atomicOr(&m_acc[m][v], e.acc[v]); break;
+            case NGZ_AGG_ADD: atomicAdd(&L.m_acc[m][v], e.acc[v]); break;
+            case NGZ_AGG_MIN: atomicMin(&L.m_acc[m][v], e.acc[v]); break;
+            case NGZ_AGG_MAX: atomicMax(&L.m_acc[m][v], e.acc[v]); break;
+            default: atomicOr(&L.m_acc[m][v], e.acc[v]); break;
             }
         }
     }
     __syncthreads();
+    return true;
+}
+
+// part: LCM_BLOCKS * LC_MAX_TAGS entries of scratch; cnt: [0] entries written by
+// k_agg_lc_part, [1] overflow flag, [2] workgroups done (zeroed before the launch)
+__global__ __launch_bounds__(LCM_THREADS) void k_agg_lc_merge(const LcEntry *__restrict__ in, uint32_t cap,
+                                                              LcEntry *__restrict__ part,
+                                                              unsigned int *__restrict__ cnt, const AggParams P,
+                                                              unsigned long long *__restrict__ tags,
+                                                              uint8_t *__restrict__ rows, uint64_t room,
+                                                              uint32_t *__restrict__ claims,
+                                                              unsigned long long *__restrict__ n_claims,
+                                                              unsigned int *__restrict__ err) {
+    __shared__ LcMergeLds L;
+    unsigned int *flag = cnt + 1;
+    if (*(volatile unsigned int *)flag) return;  // uniform per launch: every workgroup returns
+    const uint32_t tid = threadIdx.x, nv = P.n_vals;
+    const uint32_t n_in = min(*(volatile unsigned int *)cnt, cap);
+    // 1. this workgroup's slice (entries b, b + LCM_BLOCKS, ...) -> one entry per tag
+    const bool ok = lc_combine(L, in, blockIdx.x, gridDim.x, n_in, P);
+    LcEntry *mine = part + (size_t)blockIdx.x * LC_MAX_TAGS;
+    const uint32_t nt = ok ? L.n_tags : 0;
+    if (!ok && tid == 0) atomicOr(flag, 1u);
+    for (uint32_t m = tid; m < LC_MAX_TAGS; m += blockDim.x) {
+        LcEntry &e = mine[m];
+        e.tag = m < nt ? L.m_tag[m] : 0ull;  // tag 0: no entry
+        if (m >= nt) continue;
+        e.cnt = L.m_cnt[m];
+        e.tmin = L.m_tmin[m];
+        e.tmax = L.m_tmax[m];
+        e.smax = L.m_smax[m];
+        e.vp = L.m_vp[m];
+        e.tpl = L.m_tpl[m];
+        e.d0 = L.m_d0[m];
+        e.d1 = L.m_d1[m];
+        for (uint32_t v = 0; v < nv; ++v) e.acc[v] = L.m_acc[m][v];
+    }
+    // 2. the last workgroup to finish combines the slices (release: every store of this
+    // workgroup before its arrival; acquire: the last one's loads after every arrival)
+    __syncthreads();
+    if (tid == 0)
+        L.s_last = __hip_atomic_fetch_add(cnt + 2, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    __syncthreads();
+    if (!L.s_last) return;
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);  // every thread of the last workgroup
+    if (*(volatile unsigned int *)flag) return;
+    // slices' tag-0 entries (none) fall in their own LDS slot and are skipped below
+    if (!lc_combine(L, part, 0, 1, gridDim.x * LC_MAX_TAGS, P)) {
+        if (tid == 0) atomicOr(flag, 1u);  // too many groups for this path: the general path
+        return;
+    }
+    if (tid == 0) L.s_full = L.s_new = 0;
+    __syncthreads();
     // 3. each tag's group: found, or claimed (this workgroup is the push's only claimer)
-    if (tid < n_tags) {
-        const uint64_t h = m_tag[tid];
+    const uint32_t n_tags = L.n_tags;
+    for (uint32_t m = tid; m < n_tags; m += blockDim.x) {
+        L.m_g[m] = NONE;
+        L.m_claimed[m] = 0;
+        const uint64_t h = L.m_tag[m];
+        if (!h) continue;
         uint64_t g = slot_of(h) & P.mask;
         uint32_t found = NONE, claimed = 0;
         for (uint64_t probes = 0; probes <= P.mask; ++probes, g = (g + 1) & P.mask) {
@@ -1825,34 +1987,36 @@ __global__ __launch_bounds__(LCM_THREADS) void k_agg_lc_merge(const LcEntry *__r
                 break;
             }
         }
-        m_g[tid] = found;
-        m_claimed[tid] = claimed;
-        if (found == NONE) atomicOr(&s_full, 1u);
-        if (claimed) atomicAdd(&s_new, 1u);
+        L.m_g[m] = found;
+        L.m_claimed[m] = claimed;
+        if (found == NONE) atomicOr(&L.s_full, 1u);
+        if (claimed) atomicAdd(&L.s_new, 1u);
     }
     __syncthreads();
-    if (s_full || s_new > room) {  // nothing changes: release this push's claims
-        if (tid < n_tags && m_claimed[tid]) tags[m_g[tid]] = TAG_EMPTY;
-        if (tid == 0) atomicOr(err, s_full ? 2u : 32u);
+    if (L.s_full || L.s_new > room) {  // nothing changes: release this push's claims
+        for (uint32_t m = tid; m < n_tags; m += blockDim.x)
+            if (L.m_claimed[m]) tags[L.m_g[m]] = TAG_EMPTY;
+        if (tid == 0) atomicOr(err, L.s_full ? 2u : 32u);
         return;
     }
     // 4. the rows
-    if (tid < n_tags) {
-        const uint32_t g = m_g[tid];
-        if (m_claimed[tid]) claims[atomicAdd(n_claims, 1ull)] = g;
+    for (uint32_t m = tid; m < n_tags; m += blockDim.x) {
+        if (!L.m_tag[m]) continue;
+        const uint32_t g = L.m_g[m];
+        if (L.m_claimed[m]) claims[atomicAdd(n_claims, 1ull)] = g;
         uint8_t *R = rows + (uint64_t)g * P.row_bytes;
-        atomicAdd((unsigned long long *)(R + 16), m_cnt[tid]);
-        atomicMin((unsigned int *)(R + 24), m_tmin[tid]);
-        atomicMax((unsigned int *)(R + 28), m_tmax[tid]);
-        if (m_smax[tid]) atomicMax((unsigned int *)(R + 32), m_smax[tid]);
-        atomicOr((unsigned long long *)(R + 56), m_tpl[tid]);
-        if (m_d0[tid]) atomicOr((unsigned long long *)(R + 72), m_d0[tid]);
-        if (m_d1[tid]) atomicOr((unsigned long long *)(R + 80), m_d1[tid]);
+        atomicAdd((unsigned long long *)(R + 16), L.m_cnt[m]);
+        atomicMin((unsigned int *)(R + 24), L.m_tmin[m]);
+        atomicMax((unsigned int *)(R + 28), L.m_tmax[m]);
+        if (L.m_smax[m]) atomicMax((unsigned int *)(R + 32), L.m_smax[m]);
+        atomicOr((unsigned long long *)(R + 56), L.m_tpl[m]);
+        if (L.m_d0[m]) atomicOr((unsigned long long *)(R + 72), L.m_d0[m]);
+        if (L.m_d1[m]) atomicOr((unsigned long long *)(R + 80), L.m_d1[m]);
         apply_push_constants(R, P);
-        const uint32_t vp = m_vp[tid];
+        const uint32_t vp = L.m_vp[m];
         if (vp) atomicOr((unsigned int *)(R + 12), vp);
         for (uint32_t v = 0; v < nv; ++v)
-            if ((vp >> v) & 1) apply_value_hot(R + P.val_off[v], P.val_op[v], m_acc[tid][v]);
+            if ((vp >> v) & 1) apply_value_hot(R + P.val_off[v], P.val_op[v], L.m_acc[m][v]);
     }
 }
 
@@ -1996,7 +2160,9 @@ struct ngz_agg {
     size_t part_cap = 0;
     LcEntry *lc = nullptr;        // low-cardinality path: the waves' partial groups
     uint32_t lc_cap = 0;          // ... entries allocated
-    unsigned int *lc_cnt = nullptr;  // [0] entries written, [1] overflow flag
+    unsigned int *lc_cnt = nullptr;  // [0] entries written, [1] overflow flag, [2] merge workgroups done
+    LcSet *lc_sets = nullptr;     // ... the push's set descriptors
+    uint32_t lc_sets_cap = 0;
     const char *last_path = "";   // the reduction path of the last push ("lowcard" / "general")
     uint32_t lc_skip = 0;         // pushes left before the low-cardinality scan is tried again
 };
@@ -2488,6 +2654,7 @@ void ngz_agg_destroy(ngz_agg *a) {
     hipFree(a->part_buf);
     hipFree(a->lc);
     hipFree(a->lc_cnt);
+    hipFree(a->lc_sets);
     if (a->ev0) hipEventDestroy(a->ev0);
     if (a->ev1) hipEventDestroy(a->ev1);
     if (a->stream) hipStreamDestroy(a->stream);
@@ -2796,10 +2963,11 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, const ngz_p
     // a push that found too many key tuples sends the next 15 pushes of the aggregator
     // straight to the general path (high-cardinality keys pay for one try in 16)
     const bool lc_try = lc_now == 1 || (lc_now != 0 && n_rec >= (1u << 16) && (a->lc_skip == 0 || --a->lc_skip == 0));
-    if (n_rec && P.packed && P.lds_ok && P.n_vals <= (uint32_t)LC_MAXV && !ordered && lc_try) {
+    if (n_rec && P.packed && P.lds_ok && P.n_vals <= (uint32_t)LC_MAXV && P.n_keys <= (uint32_t)LC_MAXK &&
+        !ordered && lc_try) {
         // one-wave workgroups; the lane-private LDS cells of LC_NK tuples bound the residency
         // (160 KB per CU): a grid of that many workgroups, a multiple of the 8 XCDs
-        const size_t lds = (size_t)LC_NK * P.n_vals * 64 * 8;
+        const size_t lds = lc_lds_bytes(P.n_vals);
         const uint32_t per_cu = (uint32_t)std::max<size_t>(1, std::min<size_t>(16, (160u * 1024 - 1024) / (lds + 256)));
         const uint32_t rg = std::max<uint32_t>(8, std::min<uint32_t>(256 * per_cu, (NS + 7) & ~7u));
         const uint32_t cap = rg * LC_NK * 4;  // 4 window contexts per wave; more: the general path
@@ -2807,8 +2975,10 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, const ngz_p
             hipFree(a->lc);
             a->lc = nullptr;
             a->lc_cap = 0;
-            if (!a->lc_cnt && hipMalloc(&a->lc_cnt, 8) != hipSuccess) a->lc_cnt = nullptr;
-            if (!a->lc_cnt || hipMalloc(&a->lc, sizeof(LcEntry) * (size_t)cap) != hipSuccess) {
+            if (!a->lc_cnt && hipMalloc(&a->lc_cnt, 16) != hipSuccess) a->lc_cnt = nullptr;
+            // the waves' entries, then the merge workgroups' slices
+            if (!a->lc_cnt ||
+                hipMalloc(&a->lc, sizeof(LcEntry) * ((size_t)cap + LCM_BLOCKS * LC_MAX_TAGS)) != hipSuccess) {
                 a->lc = nullptr;
                 restore();
                 upload_domains(a);
@@ -2816,15 +2986,30 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, const ngz_p
             }
             a->lc_cap = cap;
         }
+        if (NS > a->lc_sets_cap) {
+            hipFree(a->lc_sets);
+            a->lc_sets_cap = 0;
+            if (hipMalloc(&a->lc_sets, sizeof(LcSet) * (size_t)NS) != hipSuccess) {
+                a->lc_sets = nullptr;
+                restore();
+                upload_domains(a);
+                return fail(a, NGZ_E_NOMEM, "low-cardinality set descriptors");
+            }
+            a->lc_sets_cap = NS;
+        }
         uint32_t kb = 0;
         for (uint32_t k = 0; k < P.n_keys; ++k) kb += 1 + 8 * P.key_pw[k];
-        AGG_HIP(a, hipMemsetAsync(a->lc_cnt, 0, 8, st));
-        hipLaunchKernelGGL(k_agg_lc_part, dim3(rg), dim3(64), lds, st, sets, NS, hdr, dginfo, a->plans, D, S, P, kb,
-                           a->lc, a->lc_cnt, cap, a->late, a->lc_cnt + 1, a->err);
+        // measurement only (wrong results): 1 skips the LDS updates, 2 the value loads
+        static const uint32_t lc_dbg = getenv("NGZ_AGG_LC_DBG") ? (uint32_t)atoi(getenv("NGZ_AGG_LC_DBG")) : 0u;
+        AGG_HIP(a, hipMemsetAsync(a->lc_cnt, 0, 16, st));
+        hipLaunchKernelGGL(k_agg_lc_sets, dim3(grid_for(NS)), dim3(256), 0, st, sets, NS, hdr, dginfo, a->plans, D, S,
+                           a->lc_sets, a->late, a->err);
+        hipLaunchKernelGGL(k_agg_lc_part, dim3(rg), dim3(64), lds, st, a->lc_sets, NS, a->plans, P, kb, a->lc,
+                           a->lc_cnt, cap, a->lc_cnt + 1, lc_dbg);
         AGG_HIP(a, hipGetLastError());
         const uint64_t room = a->limit - std::min(a->live, a->limit);
-        hipLaunchKernelGGL(k_agg_lc_merge, dim3(1), dim3(LCM_THREADS), 0, st, a->lc, a->lc_cnt, cap, P, a->tags,
-                           a->rows, room, claims, a->n_claims, a->lc_cnt + 1, a->err);
+        hipLaunchKernelGGL(k_agg_lc_merge, dim3(LCM_BLOCKS), dim3(LCM_THREADS), 0, st, a->lc, cap, a->lc + cap,
+                           a->lc_cnt, P, a->tags, a->rows, room, claims, a->n_claims, a->err);
         AGG_HIP(a, hipGetLastError());
         unsigned int lcc[2] = {0, 0};
         AGG_HIP(a, hipMemcpyAsync(lcc, a->lc_cnt, 8, hipMemcpyDeviceToHost, st));
