@@ -1614,7 +1614,7 @@ __host__ __device__ constexpr size_t lc_lds_bytes(uint32_t nv) {
     return (size_t)(LC_NK + 1) * nv * LC_CELLS * 8 + (size_t)(LC_NK + 1) * LC_CELLS * 4;
 }
 
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_agg_lc_part(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_agg_lc_part(
     const LcSet *__restrict__ descs, uint32_t n_sets, const AggSlotPlan *__restrict__ plans, const AggParams P,
     uint32_t key_bits, LcEntry *__restrict__ out, unsigned int *__restrict__ n_out, uint32_t cap,
     unsigned int *__restrict__ flag, uint32_t dbg) {
@@ -1747,28 +1747,30 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
             uint32_t unmatched = 0;
 #pragma unroll
             for (int j = 0; j < LC_G * 4; ++j) unmatched |= kid[j] == LC_NK ? 1u << j : 0u;
-            // rows whose tuple the wave has not met yet: rare, one ballot tells
-            if (__ballot((unmatched & vm) != 0))
+            // rows whose tuple the wave has not met yet (rare): one tuple at a time, taken from the
+            // first such row of the first such lane, entered into the list, matched everywhere
+            uint32_t um = unmatched & vm;
+            while (__ballot(um != 0)) {
+                const int l0 = __ffsll((unsigned long long)__ballot(um != 0)) - 1;
+                const uint32_t j0 = (uint32_t)__shfl((int)(um ? __builtin_ctz(um) : 0), l0);
+                uint64_t kj = 0;
 #pragma unroll
-            for (int j = 0; j < LC_G * 4; ++j) {
-                const bool valid = (vm >> j) & 1;
-                uint64_t todo = __ballot(valid && kid[j] == LC_NK);
-                while (todo) {  // rare: a tuple new to this wave and window context
-                    const int l0 = __ffsll((unsigned long long)todo) - 1;
-                    const uint64_t t = readlane64(key[j], l0);
-                    if (nkw == (uint32_t)LC_NK) {
-                        if (lane == 0) atomicOr(flag, 1u);
-                        return;
-                    }
-#pragma unroll
-                    for (int k = 0; k < LC_NK; ++k)
-                        if (k == (int)nkw) kl[k] = t;
-#pragma unroll
-                    for (int i = 0; i < LC_G * 4; ++i)
-                        if (((vm >> i) & 1) && key[i] == t) kid[i] = nkw;
-                    ++nkw;
-                    todo &= ~__ballot(valid && key[j] == t);
+                for (int j = 0; j < LC_G * 4; ++j) kj = (uint32_t)j == j0 ? key[j] : kj;
+                const uint64_t t = readlane64(kj, l0);
+                if (nkw == (uint32_t)LC_NK) {
+                    if (lane == 0) atomicOr(flag, 1u);
+                    return;
                 }
+#pragma unroll
+                for (int k = 0; k < LC_NK; ++k)
+                    if (k == (int)nkw) kl[k] = t;
+#pragma unroll
+                for (int i = 0; i < LC_G * 4; ++i)
+                    if (((um >> i) & 1) && key[i] == t) {
+                        kid[i] = nkw;
+                        um &= ~(1u << i);
+                    }
+                ++nkw;
             }
             uint32_t cell[LC_G * 4];
 #pragma unroll
