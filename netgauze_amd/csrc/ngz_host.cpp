@@ -837,7 +837,17 @@ struct HostFramed {
 int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const HostFramed *hf) {
     const uint32_t N = in->n;
     const uint32_t S = (uint32_t)ctx->slot_version.size();
-    const uint64_t n_items = (uint64_t)(2 * S + 1) * N + 1;
+    // count-matrix rows: steady state gives rows only to the slots that had records in the last
+    // batch (config 4's context holds 18 template slots, 2 with data: 37 rows of 4 bytes per
+    // datagram were zeroed, filled and scanned for 5); a set of another slot makes k_frame raise
+    // overflow bit 8 and the batch runs again with a row for every slot
+    const bool few_rows = ctx->pred_valid && ctx->pred_versions == ctx->slot_version && !hf && !ctx->rows_all &&
+                          ctx->pred_active.size() == S;
+    std::vector<uint16_t> rows(S, (uint16_t)NGZ_NO_ROW);
+    uint32_t A = 0;
+    for (uint32_t s = 0; s < S; ++s)
+        if (!few_rows || ctx->pred_active[s]) rows[s] = (uint16_t)A++;
+    const uint64_t n_items = (uint64_t)(2 * A + 1) * N + 1;
     if (n_items > 0x7FFFFFF0ull) return fail(ctx, NGZ_E_LIMIT, "batch too large for the count matrix");
     size_t scan_tmp = 0;
     if (ngz_scan_temp_bytes(n_items, &scan_tmp)) return fail(ctx, NGZ_E_DEVICE, "scan temp size");
@@ -855,11 +865,17 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
     uint64_t arena_cap = (uint64_t)(ratio * (double)in->bytes_size) +
                          (uint64_t)S * (1 + ctx->cap_pad_windows) * (maxwin_row + 256) + 4096;
     arena_cap = std::max<uint64_t>(arena_cap + ctx->arena_shift, ctx->d_arena.cap);
+    const uint16_t *old_rows = ctx->d_slot_row.p;
     if (ctx->d_hdr.ensure(std::max<uint32_t>(N, 1)) || ctx->d_counts.ensure(n_items) || ctx->d_scan.ensure(n_items) ||
         ctx->d_scan_tmp.ensure(scan_tmp + 1) || ctx->d_slots.ensure(std::max<uint32_t>(S, 1)) ||
         ctx->d_chunks.ensure(chunk_cap) || ctx->d_sets.ensure(set_cap) || ctx->d_arena.ensure(arena_cap) ||
-        ctx->d_proc.ensure(2 * NGZ_MAX_SLOTS) || ctx->d_summary.ensure(2))
+        ctx->d_proc.ensure(2 * NGZ_MAX_SLOTS) || ctx->d_summary.ensure(2) ||
+        ctx->d_slot_row.ensure(std::max<uint32_t>(S, 1)))
         return fail(ctx, NGZ_E_NOMEM, "device alloc (batch)");
+    if (rows != ctx->slot_row_host || ctx->d_slot_row.p != old_rows) {  // changed, or a new buffer
+        if (S) HIPCHK(hipMemcpy(ctx->d_slot_row.p, rows.data(), S * 2, hipMemcpyHostToDevice));
+        ctx->slot_row_host = rows;
+    }
     const int par = ctx->parity;
     BatchSummary *d_sum = ctx->d_summary.p + par;
     unsigned long long *d_proc = ctx->d_proc.p + (size_t)par * NGZ_MAX_SLOTS;
@@ -902,6 +918,8 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
     B.lengths = in->lengths;
     B.n = N;
     B.n_slots = S;
+    B.slot_row = ctx->d_slot_row.p;
+    B.n_rows = A;
     B.plans = ctx->d_plans.p;
     B.cur_slot = ctx->d_cur_slot.p;
     B.hdr = ctx->d_hdr.p;
@@ -943,7 +961,7 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
     static const int recmap_env = getenv("NGZ_RECMAP") ? atoi(getenv("NGZ_RECMAP")) : -1;
     if (any_vlen && recmap_env != 0) {
         if (recmap_env != 1 && min_vlen_rec >= 8) {
-            if (ctx->d_recoff.ensure(in->bytes_size / min_vlen_rec + N + 8))
+            if (ctx->d_recoff.ensure(in->bytes_size / min_vlen_rec + 8ull * N + 16))
                 return fail(ctx, NGZ_E_NOMEM, "device alloc (record offsets)");
             B.recoff = ctx->d_recoff.p;
             B.recoff_div = min_vlen_rec;
@@ -1029,6 +1047,7 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
     auto check_summary = [&]() -> int {
         ctx->summary = *ctx->h_summary;
         if (ctx->summary.overflow) {
+            if (ctx->summary.overflow & 8) ctx->rows_all = true;  // a slot without a count row had a set
             if (ctx->summary.overflow & 1) ctx->d_arena.ensure(ctx->summary.arena_used + 4096);
             if (ctx->summary.overflow & 2) ctx->d_chunks.ensure(ctx->summary.n_chunks + 1024);
             if (ctx->summary.overflow & 4) ctx->d_sets.ensure(ctx->summary.n_sets + 1024);
@@ -1159,6 +1178,7 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
         ctx->pred_active[s] = rt.total && !(rt.mode == NGZ_MODE_CHUNK && !rt.nchunks);
     }
     ctx->pred_valid = !hf;
+    ctx->rows_all = false;
     hipEventElapsedTime(&ctx->t_decode, ctx->ev[1], ctx->ev[2]);
     hipEventElapsedTime(&ctx->t_pipeline, ctx->ev[0], ctx->ev[3]);
     return 0;
@@ -1314,7 +1334,7 @@ void ngz_ctx_destroy(ngz_ctx *ctx) {
     ctx->d_tl_slot.release(); ctx->d_hf_flag.release(); ctx->d_hf_hdr.release(); ctx->d_hf_first.release(); ctx->d_hf_sets.release();
     ctx->d_hdr.release(); ctx->d_counts.release(); ctx->d_scan.release(); ctx->d_scan_tmp.release();
     ctx->d_slots.release(); ctx->d_chunks.release(); ctx->d_sets.release(); ctx->d_arena.release();
-    ctx->d_proc.release(); ctx->d_summary.release(); ctx->d_recmap.release(); ctx->d_recoff.release(); ctx->d_dsum.release(); ctx->d_in_bytes.release(); ctx->d_in_off.release();
+    ctx->d_proc.release(); ctx->d_summary.release(); ctx->d_recmap.release(); ctx->d_recoff.release(); ctx->d_dsum.release(); ctx->d_slot_row.release(); ctx->d_in_bytes.release(); ctx->d_in_off.release();
     ctx->d_in_len.release();
     for (auto &e : ctx->ev) hipEventDestroy(e);
     for (uint32_t i = 0; i < ctx->n_aux; ++i) {

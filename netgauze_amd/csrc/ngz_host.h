@@ -301,6 +301,12 @@ struct ngz_ctx {
     bool pred_valid = false;
     std::vector<int32_t> pred_versions;
     std::vector<uint8_t> pred_active;
+    // count-matrix rows (BatchDev::slot_row): the slots of the last batch, or every slot (first
+    // batch after a template change, host-framed batches, and the retry of a batch that met a
+    // slot without a row)
+    bool rows_all = false;
+    std::vector<uint16_t> slot_row_host;  // what d_slot_row holds
+    ngzh::DevBuf<uint16_t> d_slot_row;
     std::vector<ngzh::TemplateSetJson> tmpl_sets;  // template sets of the last batch, (dgram, set_pos) order
     uint64_t batch_serial = 0;                      // bumped by every ngz_decode_batch
     std::shared_ptr<ngzh::JsonView> json_view;      // ngz_dgram_json cache of the last batch

@@ -257,7 +257,7 @@ struct BatchSummary {    // device -> host at the end of a batch
     uint32_t n_chunks;
     uint32_t n_sets;
     uint32_t n_host;        // datagrams needing host framing (template sets)
-    uint32_t overflow;      // 1: arena, 2: chunks, 4: sets
+    uint32_t overflow;      // 1: arena, 2: chunks, 4: sets, 8: a set of a slot without a count row
     uint32_t n_unsupported;
     uint64_t arena_used;
 };
@@ -281,7 +281,7 @@ struct BatchDev {        // device pointers of one batch
     const HostSet *hf_sets;
     const void *hf_hdr;        // [hosts] ngz_dgram_hdr of host-framed datagrams (hf_flag[d]-1 indexes)
     void *hdr;                 // ngz_dgram_hdr[n]
-    uint32_t *counts;          // [(2*n_slots+1)*n + 1]
+    uint32_t *counts;          // [(2*n_rows+1)*n + 1]
     uint32_t *scan;            // same length
     SlotRT *slots;             // [n_slots]
     Chunk *chunks;
@@ -297,9 +297,16 @@ struct BatchDev {        // device pointers of one batch
     uint32_t *recmap;          // variable-length slots: 1 bit per batch byte, set at every complete record
                                // (used when recoff is null)
     uint16_t *recoff;          // variable-length slots: per datagram, the offsets of its complete records
-                               // in datagram order then 0xFFFF, from entry offsets[d] / recoff_div + d
+                               // in datagram order then 0xFFFF, from entry ceil8(offsets[d] / recoff_div + 8 d)
     uint32_t recoff_div;       // the smallest min_record_length of the batch's variable-length templates
     uint32_t reserved_c;
     unsigned long long *dsum;  // per datagram: its one data set (k_frame -> k_emit), 0 = walk it again
                                // start by k_frame's walk, read by k_emit instead of walking again (or null)
+    // count-matrix rows: only the template slots expected to carry records in this batch have
+    // one (the slots that did in the previous batch, or every slot); a set of another slot makes
+    // k_frame raise overflow bit 8 and the batch runs again with every slot
+    const uint16_t *slot_row;  // [n_slots]: the slot's row, or NGZ_NO_ROW
+    uint32_t n_rows;           // rows A: counts / scan are [(2A + 1) n + 1]
+    uint32_t reserved_d;
 };
+#define NGZ_NO_ROW 0xFFFFu

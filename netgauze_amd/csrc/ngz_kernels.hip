@@ -241,19 +241,45 @@ __device__ bool has_template_sets(const BatchDev &B, uint32_t d) {
 
 constexpr uint32_t kFrameBlock = 256;
 
+// Datagram d's record-offset list: 16-byte aligned, at entry ceil8(offsets[d] / div + 8 d).  A
+// datagram of L bytes has at most L / div records (+ the terminator), so the lists of datagrams
+// whose bytes do not overlap do not overlap either, whole 16-byte pieces included
+__device__ __forceinline__ uint16_t *ngz_ro_list(const BatchDev &B, uint64_t dg_off, uint32_t d) {
+    return B.recoff + ((dg_off / B.recoff_div + 8ull * d + 7) & ~7ull);
+}
+
 // Count matrix, slot-major rows of N datagrams (scanned in one pass):
 //   rows [0, S)      records of slot s in datagram d
 //   rows [S, 2S)     decode chunks of slot s in datagram d
 //   row  2S          data sets in datagram d
 struct CountVis {
     uint32_t *counts;
-    uint32_t N, S, d;
+    uint32_t N, A, d;  // A: count-matrix rows (slots with a row)
     uint32_t sets;
     const DevPlan *plans;
     uint32_t *recmap;
     uint64_t dg_off;
     uint16_t *ro = nullptr;  // this datagram's record-offset list (BatchDev::recoff), or null
-    uint32_t ro_n = 0;
+    // the list goes out 8 entries (16 bytes) at a time from two registers: stored entry by entry,
+    // 64 lanes' 2-byte stores to 64 lists were 64 partial-line writes each (0.5 GB of WRITE_SIZE
+    // per config-4 step for 20 MB of offsets)
+    uint64_t q0 = 0, q1 = 0;
+    uint32_t qn = 0;  // entries held
+    __device__ void ro_push(uint32_t at) {
+        const uint64_t e = (uint64_t)(at & 0xFFFFu);
+        if (qn < 4) q0 |= e << (16 * qn);
+        else q1 |= e << (16 * (qn - 4));
+        if (++qn == 8) {
+            *(uint4 *)ro = make_uint4((uint32_t)q0, (uint32_t)(q0 >> 32), (uint32_t)q1, (uint32_t)(q1 >> 32));
+            ro += 8;
+            q0 = q1 = 0;
+            qn = 0;
+        }
+    }
+    __device__ void ro_finish() {  // the 0xFFFF terminator, and the last (partial) 16 bytes
+        ro_push(0xFFFFu);
+        if (qn) *(uint4 *)ro = make_uint4((uint32_t)q0, (uint32_t)(q0 >> 32), (uint32_t)q1, (uint32_t)(q1 >> 32));
+    }
     uint64_t sum = 0;  // the first data set: set_pos | slot << 16 | n << 32 | (end - set_pos, or 1) << 48
     uint64_t dg_end = 0;  // batch offset past the datagram
     // record-start marks of the word being filled (record starts only ever move forward)
@@ -270,7 +296,7 @@ struct CountVis {
         if (!sets) sum = (uint64_t)(end - (pos - 4)) << 48;
         return ngz_vlen_walk(p, pos, end, pl, err, [this](uint32_t, uint32_t at) {
             if (ro) {  // the record's offset in the datagram, appended to the datagram's list
-                ro[ro_n++] = (uint16_t)at;
+                ro_push(at);
                 return;
             }
             if (!recmap) return;
@@ -283,10 +309,17 @@ struct CountVis {
             mbits |= 1u << (b & 31);
         });
     }
+    const uint16_t *row;
+    BatchSummary *summary;
     __device__ void on_set(uint32_t set_pos, uint32_t slot, uint32_t n, uint32_t, uint32_t) {
         if (!sets) sum = (sum ? sum : 1ull << 48) | set_pos | ((uint64_t)slot << 16) | ((uint64_t)(n & 0xFFFF) << 32);
-        counts[(uint64_t)slot * N + d] += n;
-        if (n) counts[(uint64_t)(S + slot) * N + d] += (n + plans[slot].window - 1) / plans[slot].window + 1;
+        const uint32_t r = row[slot];
+        if (r == NGZ_NO_ROW) {
+            atomicOr(&summary->overflow, 8u);  // the batch runs again with a row for every slot
+        } else {
+            counts[(uint64_t)r * N + d] += n;
+            if (n) counts[(uint64_t)(A + r) * N + d] += (n + plans[slot].window - 1) / plans[slot].window + 1;
+        }
         sets += 1;
     }
 };
@@ -295,20 +328,22 @@ __global__ void __launch_bounds__(kFrameBlock) k_frame(BatchDev B, const uint32_
     const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
     if (d >= B.n) return;
     // this datagram's column of the count matrix starts at zero (no memset pass)
-    for (uint32_t r = 0; r < 2 * B.n_slots; ++r) B.counts[(uint64_t)r * B.n + d] = 0;
-    if (d == 0) B.counts[(uint64_t)(2 * B.n_slots + 1) * B.n] = 0;  // the scan's trailing element
-    CountVis vis{B.counts, B.n, B.n_slots, d, 0, B.plans, B.recmap, B.offsets[d]};
+    for (uint32_t r = 0; r < 2 * B.n_rows; ++r) B.counts[(uint64_t)r * B.n + d] = 0;
+    if (d == 0) B.counts[(uint64_t)(2 * B.n_rows + 1) * B.n] = 0;  // the scan's trailing element
+    CountVis vis{B.counts, B.n, B.n_rows, d, 0, B.plans, B.recmap, B.offsets[d]};
+    vis.row = B.slot_row;
+    vis.summary = B.summary;
     vis.dg_end = vis.dg_off + B.lengths[d];
-    if (B.recoff) vis.ro = B.recoff + vis.dg_off / B.recoff_div + d;
+    if (B.recoff) vis.ro = ngz_ro_list(B, vis.dg_off, d);
     WalkOut o;
     walk_datagram(B, hf_flag, hf_first, d, o, vis);
     vis.mark_flush();
-    if (vis.ro) vis.ro[vis.ro_n] = 0xFFFFu;  // end of the list
+    if (vis.ro) vis.ro_finish();  // end of the list
     // a walk that ended OK visited every set (template sets end it with HOST)
     if (o.status != NGZ_FR_HOST && o.status != NGZ_FR_OK && !(hf_flag && hf_flag[d]) && has_template_sets(B, d))
         o.status = NGZ_FR_HOST;
     const uint64_t N = B.n;
-    B.counts[(uint64_t)(2 * B.n_slots) * N + d] = vis.sets;
+    B.counts[(uint64_t)(2 * B.n_rows) * N + d] = vis.sets;
     // one data set, parsed cleanly: k_emit takes it from here instead of walking the datagram again
     if (B.dsum)
         B.dsum[d] = (o.status == NGZ_FR_OK && o.err == NGZ_NO_ERR && vis.sets == 1 && !(hf_flag && hf_flag[d]) &&
@@ -337,12 +372,15 @@ __global__ void __launch_bounds__(kFrameBlock) k_frame(BatchDev B, const uint32_
 __global__ void k_layout(BatchDev B) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     const uint64_t N = B.n;
-    const uint32_t S = B.n_slots;
-    const uint32_t chunk_base = B.scan[(uint64_t)S * N];
+    const uint32_t S = B.n_slots, A = B.n_rows;
+    const uint32_t chunk_base = B.scan[(uint64_t)A * N];
     uint64_t off = 0;
     for (uint32_t s = 0; s < S; ++s) {
-        const uint32_t base = B.scan[(uint64_t)s * N];
-        const uint32_t next = B.scan[(uint64_t)(s + 1) * N];
+        const uint32_t r = B.slot_row[s];
+        const bool has = r != NGZ_NO_ROW;
+        // a slot without a row has no records in this batch (else the batch runs again)
+        const uint32_t base = has ? B.scan[(uint64_t)r * N] : chunk_base;
+        const uint32_t next = has ? B.scan[(uint64_t)(r + 1) * N] : chunk_base;
         const uint32_t total = next - base;
         const uint32_t w = B.plans[s].window ? B.plans[s].window : 64;
         // LDS-staged kernels store whole workgroup windows: capacity in those
@@ -353,9 +391,9 @@ __global__ void k_layout(BatchDev B) {
         rt.cap = cap;
         rt.total = total;
         rt.base = base;
-        rt.chunk0 = B.scan[(uint64_t)(S + s) * N] - chunk_base;
-        rt.nchunks = B.scan[(uint64_t)(S + s + 1) * N] - B.scan[(uint64_t)(S + s) * N];
-        rt.chunk_scan0 = B.scan[(uint64_t)(S + s) * N];
+        rt.chunk_scan0 = has ? B.scan[(uint64_t)(A + r) * N] : B.scan[(uint64_t)(2 * A) * N];
+        rt.chunk0 = rt.chunk_scan0 - chunk_base;
+        rt.nchunks = has ? B.scan[(uint64_t)(A + r + 1) * N] - rt.chunk_scan0 : 0;
         // row mode for variable-length records and for sets so small that
         // set-relative chunks would leave most lanes idle (< 25 % of rows used).
         // A specialised LDS-staged kernel gathers the rows of a window across
@@ -376,13 +414,13 @@ __global__ void k_layout(BatchDev B) {
         off += (col_bytes + row_bytes_extra + 255) & ~255ull;
     }
     const uint32_t rec_total = chunk_base;
-    const uint32_t chunks = B.scan[(uint64_t)(2 * S) * N] - chunk_base;
-    const uint32_t sets = B.scan[(uint64_t)(2 * S + 1) * N] - B.scan[(uint64_t)(2 * S) * N];
+    const uint32_t chunks = B.scan[(uint64_t)(2 * A) * N] - chunk_base;
+    const uint32_t sets = B.scan[(uint64_t)(2 * A + 1) * N] - B.scan[(uint64_t)(2 * A) * N];
     B.summary->n_records_total = rec_total;
     B.summary->n_chunks = chunks;
     B.summary->n_sets = sets;
     B.summary->arena_used = off;
-    uint32_t ov = 0;
+    uint32_t ov = B.summary->overflow & 8u;  // k_frame's: a set of a slot without a row
     if (off > B.arena_cap) ov |= 1;
     if (chunks > B.chunk_cap) ov |= 2;
     if (sets > B.set_cap) ov |= 4;
@@ -416,7 +454,7 @@ struct EmitVis {
     }
     __device__ uint32_t vlen(const uint8_t *p, uint32_t pos, uint32_t end, uint32_t slot, const DevPlan &pl,
                              uint64_t *err) {
-        const uint32_t rec0 = B->scan[(uint64_t)slot * B->n + d] - B->slots[slot].base;
+        const uint32_t rec0 = B->scan[(uint64_t)B->slot_row[slot] * B->n + d] - B->slots[slot].base;
         uint64_t *rs = rowsrc(slot) + rec0;
         uint32_t *rd = rowdg(slot) + rec0;
         for (uint32_t k = 0; k < ntab; ++k)
@@ -494,7 +532,8 @@ struct EmitVis {
     }
     __device__ void on_set(uint32_t set_pos, uint32_t slot, uint32_t n, uint32_t payload_pos, uint32_t rl) {
         const uint64_t N = B->n;
-        uint32_t *cell = &B->scan[(uint64_t)slot * N + d];
+        const uint32_t row = B->slot_row[slot];
+        uint32_t *cell = &B->scan[(uint64_t)row * N + d];
         const uint32_t rec0 = *cell - B->slots[slot].base;
         *cell += n;
         if (!ok) return;
@@ -520,7 +559,7 @@ struct EmitVis {
         const uint32_t reserved = (n + W - 1) / W + 1;
         // this slot's chunk cursor; the scan row's own first cell is another
         // thread's cursor, so the row base comes from SlotRT (k_layout)
-        uint32_t *ccell = &B->scan[(uint64_t)(B->n_slots + slot) * N + d];
+        uint32_t *ccell = &B->scan[(uint64_t)(B->n_rows + row) * N + d];
         const uint32_t chunk_at = *ccell - B->slots[slot].chunk_scan0 + B->slots[slot].chunk0;
         *ccell += reserved;
         uint32_t r = 0, used = 0;
@@ -561,17 +600,17 @@ __global__ void __launch_bounds__(256) k_emit(BatchDev B, const uint32_t *hf_fla
     const uint32_t d0 = blockIdx.x * blockDim.x;
     const uint32_t d = d0 + t;
     const uint64_t N = B.n;
-    const uint32_t S = B.n_slots;
+    const uint32_t S = B.n_slots, A = B.n_rows;
     const uint32_t dl = min(d0 + blockDim.x, B.n) - 1;  // the workgroup's last datagram
     if (t == 0) st_cnt = st_used = 0;
     __syncthreads();
     // the workgroup's row range of every variable-length row-mode slot, read
     // before any thread moves its scan cursors
     for (uint32_t s = t; s < S; s += blockDim.x) {
-        if (!B.plans[s].has_vlen || B.slots[s].mode != NGZ_MODE_ROW) continue;
-        const uint32_t base = B.slots[s].base;
-        const uint32_t r0 = B.scan[(uint64_t)s * N + d0] - base;
-        const uint32_t r1 = B.scan[(uint64_t)s * N + dl] - base + B.counts[(uint64_t)s * N + dl];
+        if (!B.plans[s].has_vlen || B.slots[s].mode != NGZ_MODE_ROW || B.slot_row[s] == NGZ_NO_ROW) continue;
+        const uint32_t base = B.slots[s].base, sr = B.slot_row[s];
+        const uint32_t r0 = B.scan[(uint64_t)sr * N + d0] - base;
+        const uint32_t r1 = B.scan[(uint64_t)sr * N + dl] - base + B.counts[(uint64_t)sr * N + dl];
         const uint32_t n = r1 - r0;
         if (!n) continue;
         const uint32_t off = atomicAdd(&st_used, n);
@@ -590,13 +629,13 @@ __global__ void __launch_bounds__(256) k_emit(BatchDev B, const uint32_t *hf_fla
         vis.B = &B;
         vis.d = d;
         vis.dg_off = B.offsets[d];
-        vis.set_at = B.scan[(uint64_t)(2 * S) * N + d] - B.scan[(uint64_t)(2 * S) * N];
+        vis.set_at = B.scan[(uint64_t)(2 * A) * N + d] - B.scan[(uint64_t)(2 * A) * N];
         vis.ok = true;
         vis.tab = st_tab;
         vis.ntab = ntab;
         vis.lrs = st_rs;
         vis.lrd = st_rd;
-        vis.ro = B.recoff ? B.recoff + vis.dg_off / B.recoff_div + d : nullptr;
+        vis.ro = B.recoff ? ngz_ro_list(B, vis.dg_off, d) : nullptr;
         const unsigned long long sm = B.dsum ? B.dsum[d] : 0ull;
         if (sm) {
             // k_frame's summary of the datagram's one data set (same calls as walk_datagram)
