@@ -45,6 +45,12 @@
 extern "C" {
 #endif
 
+#define NGZ_AGG_ABI_VERSION 2 /* 2: ngz_agg_create takes max_peers, ngz_agg_push a const ngz_peer * (the
+                                 exporter's address; 1 took a uint16 port) */
+
+/* NGZ_AGG_ABI_VERSION the library was built with (checked by hosts like ngz_abi_version). */
+int ngz_agg_abi_version(void);
+
 /* Transform ops (config.rs Op).  KEY selects a key field; the others an aggregated field. */
 #define NGZ_AGG_KEY 0
 #define NGZ_AGG_ADD 1

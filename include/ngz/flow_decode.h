@@ -40,8 +40,9 @@
 extern "C" {
 #endif
 
-#define NGZ_ABI_VERSION 2  /* 2: ngz_slot_info.n_fields is 32-bit (no field cap), ngz_dgram_error,
-                              ngz_template_counts_device */
+#define NGZ_ABI_VERSION 3  /* 2: ngz_slot_info.n_fields is 32-bit (no field cap), ngz_dgram_error,
+                              ngz_template_counts_device; 3: ngz_abi_version, ngz_ctx_destroy joins the
+                              context's background compiles */
 
 /* return codes */
 #define NGZ_OK 0
@@ -143,8 +144,15 @@ typedef struct {
     uint32_t n_template_dgrams;  /* datagrams with (options) template sets */
 } ngz_batch_out;
 
+/* NGZ_ABI_VERSION the library was built with: a host checks it against the header it was
+ * compiled with before any other call. */
+int ngz_abi_version(void);
+
 /* --- context ------------------------------------------------------------ */
 int ngz_ctx_create(int device, ngz_ctx **out);
+/* Synchronous, as the reference codec's drop (codec.rs:68-82): waits for the
+ * context's stream and joins every background template compile the context
+ * started or was waiting on, so a host may return from main right after. */
 void ngz_ctx_destroy(ngz_ctx *ctx);
 const char *ngz_last_error(ngz_ctx *ctx);
 
@@ -165,11 +173,11 @@ const char *ngz_last_error(ngz_ctx *ctx);
 int ngz_ctx_set_option(ngz_ctx *ctx, int opt, int64_t value);
 
 /* Wait for every background template compile of the process (NGZ_OPT_RTC_SYNC 0) to finish
- * and load.  Call it before the host starts tearing the process down (the Python binding
- * registers it with atexit; a Rust host calls it before returning from main): a compile
- * still inside hiprtc/comgr when the C exit handlers run can outlive the compiler's own
- * static objects, which exit destroys in an order the library cannot control.  Returns
- * the number of compiles waited for. */
+ * and load.  A compile still inside hiprtc/comgr when the C exit handlers run can outlive
+ * the compiler's own static objects, which exit destroys in an order the library cannot
+ * control.  ngz_ctx_destroy (and so ngz_collector_destroy / ngz_pcap_to_jsonl) already
+ * joins its context's compiles; this is for hosts that exit with contexts still alive (the
+ * Python binding registers it with atexit).  Returns the number of compiles waited for. */
 int ngz_rtc_drain(void);
 
 /* --- decode ------------------------------------------------------------- */

@@ -21,9 +21,10 @@ ABI_FUNCTIONS = [
     "ngz_decode_batch_host", "ngz_slot_fields", "ngz_dgram_error_json",
     "ngz_templates_json", "ngz_template_counts", "ngz_last_timing", "ngz_ctx_set_option",
     "ngz_template_kernel", "ngz_group_kernel", "ngz_columns_to_host", "ngz_dgram_json", "ngz_batch_json",
-    "ngz_dgram_error", "ngz_template_counts_device", "ngz_slot_kernel", "ngz_rtc_drain",
+    "ngz_dgram_error", "ngz_template_counts_device", "ngz_slot_kernel", "ngz_rtc_drain", "ngz_abi_version",
 ]
-NGZ_ABI_VERSION = 2
+NGZ_ABI_VERSION = 3
+NGZ_AGG_ABI_VERSION = 2
 # ngz_error.kind / .layer (flow_decode.h)
 ERR_KINDS = ["NONE", "UNSUPPORTED_VERSION", "INVALID_LENGTH", "UNEXPECTED_EOF", "INVALID_PADDING_LENGTH",
              "INVALID_SET_ID", "NO_TEMPLATE", "INVALID_PADDING_VALUE", "INVALID_COUNT", "INVALID_TEMPLATE_ID",
@@ -41,6 +42,7 @@ AGG_FUNCTIONS = [
     "ngz_agg_create", "ngz_agg_destroy", "ngz_agg_last_error", "ngz_agg_push", "ngz_agg_layout",
     "ngz_agg_groups", "ngz_agg_flush", "ngz_agg_closed", "ngz_agg_emit", "ngz_agg_reset", "ngz_agg_sets",
     "ngz_agg_key_info", "ngz_agg_value_info", "ngz_agg_flowinfo_json", "ngz_agg_last_timing", "ngz_agg_peer", "ngz_agg_last_path",
+    "ngz_agg_abi_version",
 ]
 NGZ_AGG_KEY, NGZ_AGG_ADD, NGZ_AGG_MIN, NGZ_AGG_MAX, NGZ_AGG_OR = range(5)
 NGZ_AGG_E_OVERFLOW, NGZ_AGG_E_COLLISION, NGZ_AGG_E_POISONED = -10, -11, -12
@@ -170,6 +172,14 @@ def load():
                            "there is no CPU fallback" % LIB_PATH)
     lib = ctypes.CDLL(LIB_PATH)
     P, U32, U64, I = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
+    # the structs and signatures below are those of NGZ_ABI_VERSION / NGZ_AGG_ABI_VERSION: a library
+    # built from other headers is refused before any call that could misread an argument
+    lib.ngz_abi_version.argtypes, lib.ngz_abi_version.restype = [], I
+    lib.ngz_agg_abi_version.argtypes, lib.ngz_agg_abi_version.restype = [], I
+    got = (lib.ngz_abi_version(), lib.ngz_agg_abi_version())
+    if got != (NGZ_ABI_VERSION, NGZ_AGG_ABI_VERSION):
+        raise RuntimeError("netgauze_amd: %s has ABI versions %s, this binding needs %s -- rebuild it"
+                           % (LIB_PATH, got, (NGZ_ABI_VERSION, NGZ_AGG_ABI_VERSION)))
     lib.ngz_ctx_create.argtypes = [I, ctypes.POINTER(P)]
     lib.ngz_ctx_create.restype = I
     lib.ngz_ctx_destroy.argtypes = [P]

@@ -78,7 +78,11 @@ def _datetime_ms(ms):
 class FlowAggregator:
     DEFAULT_PEER = "192.0.2.1"  # TEST-NET-1: the exporter of pushes that name none
 
-    def __init__(self, transform, window_s=60, lateness_s=10, capacity=1 << 20, device=0, kinds=None, max_peers=256):
+    def __init__(self, transform, window_s=60, lateness_s=10, capacity=1 << 20, device=0, kinds=None, max_peers=0):
+        """max_peers: distinct exporter IPs the aggregator takes between flushes (0: the library's
+        NGZ_AGG_MAX_PEERS, 65536).  Entries are kept until flush / reset, as each peer's event time
+        is; a push from a new IP beyond it fails (AggError, NGZ_AGG_E_OVERFLOW).  A smaller bound
+        leaves more bits of the exact 63-bit group tag to the key fields (flow_aggregate.h)."""
         self.fields = unify(transform) if isinstance(transform, dict) else list(transform)
         self.key_fields = [f for f in self.fields if f[3] == _lib.NGZ_AGG_KEY]
         self.val_fields = [f for f in self.fields if f[3] != _lib.NGZ_AGG_KEY]

@@ -1948,8 +1948,10 @@ __global__ __launch_bounds__(LCM_THREADS) void k_agg_lc_merge(const LcEntry *__r
         e.d1 = L.m_d1[m];
         for (uint32_t v = 0; v < nv; ++v) e.acc[v] = L.m_acc[m][v];
     }
-    // 2. the last workgroup to finish combines the slices (release: every store of this
-    // workgroup before its arrival; acquire: the last one's loads after every arrival)
+    // 2. the last workgroup to finish combines the slices.  Release: every thread fences its own
+    // slice stores at agent scope before the barrier (whichever waves wrote slice entries), then
+    // one thread arrives; acquire: the last workgroup's loads after every arrival
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     __syncthreads();
     if (tid == 0)
         L.s_last = __hip_atomic_fetch_add(cnt + 2, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
@@ -2438,6 +2440,8 @@ std::string peer_key(const ngz_peer &p) {
 
 extern "C" {
 
+int ngz_agg_abi_version(void) { return NGZ_AGG_ABI_VERSION; }
+
 int ngz_agg_create(int device, const ngz_agg_field *fields, uint32_t n_fields, uint64_t window_ms,
                    uint64_t lateness_ms, uint64_t capacity, uint32_t max_peers, ngz_agg **out) {
     if (!out || (n_fields && !fields)) return NGZ_E_INVALID;
@@ -2702,7 +2706,10 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, const ngz_p
             pi = it->second;
         } else {
             if (a->peers.size() >= a->max_peers)
-                return fail(a, NGZ_AGG_E_OVERFLOW, "more peer IPs than the aggregator's max_peers");
+                return fail(a, NGZ_AGG_E_OVERFLOW,
+                            ("a new peer IP beyond max_peers (" + std::to_string(a->max_peers) +
+                             " distinct peer IPs since the last flush; entries are kept until ngz_agg_flush / "
+                             "ngz_agg_reset, as each peer's event time is)"));
             pi = (uint32_t)a->peers.size();
             ngz_peer p = *peer;
             if (p.family == 4) memset(p.addr + 4, 0, 12);
@@ -3029,7 +3036,7 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, const ngz_p
         // too many key tuples / distinct tags: the general path from the start (nothing was
         // claimed or applied; its claim pass counts the late records again)
         AGG_HIP(a, hipMemsetAsync(a->late, 0, 8, st));
-        a->lc_skip = 15;
+        a->lc_skip = 16;  // the next 15 pushes take the general path, the 16th tries this one again
     }
     a->last_path = "general";
     {

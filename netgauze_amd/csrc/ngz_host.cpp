@@ -39,6 +39,7 @@ extern "C" int ngz_launch_decode_generic(const BatchDev *B, uint32_t grid, hipSt
 void *ngz_rtc_kernel(int device, const DevPlan &P);
 int ngz_rtc_kernel_async(int device, const DevPlan &P, void **fn, void **entry);
 int ngz_rtc_poll(void *entry, void **fn);
+int ngz_rtc_join(void *const *entries, size_t n);
 void *ngz_rtc_group(int device, const DevPlan *const *plans, uint32_t n);
 int ngz_rtc_group_async(int device, const DevPlan *const *plans, uint32_t n, void **fn, void **entry);
 int ngz_rtc_launch_group(void *fn, const BatchDev *B, const uint32_t *slots, uint32_t n, uint32_t grid, uint32_t block,
@@ -1276,6 +1277,8 @@ int finish_batch(ngz_ctx *ctx, const ngz_batch_in *in, ngz_batch_out *out, hipSt
 // ------------------------------------------------------------------------
 extern "C" {
 
+int ngz_abi_version(void) { return NGZ_ABI_VERSION; }
+
 int ngz_ctx_create(int device, ngz_ctx **out) {
     if (!out) return NGZ_E_INVALID;
     *out = nullptr;
@@ -1328,6 +1331,17 @@ int ngz_ctx_create(int device, ngz_ctx **out) {
 
 void ngz_ctx_destroy(ngz_ctx *ctx) {
     if (!ctx) return;
+    {
+        // Synchronous drop, as the reference codec's (codec.rs:68-82): no kernel compile this context
+        // started or waits on is still running once it returns, so a C / Rust host may return from main
+        // right after (a compile inside hiprtc/comgr during exit can hang it, ngz_rtc.cpp Workers)
+        std::vector<void *> entries;
+        for (const ngzh::Version &v : ctx->versions)
+            if (v.rtc_entry) entries.push_back(v.rtc_entry);
+        for (const auto &kv : ctx->group_kernels)
+            if (kv.second.entry) entries.push_back(kv.second.entry);
+        ngz_rtc_join(entries.data(), entries.size());
+    }
     hipSetDevice(ctx->device);
     hipStreamSynchronize(ctx->stream);
     ctx->d_plans.release(); ctx->d_fields.release(); ctx->d_cur_slot.release(); ctx->d_tl_key.release(); ctx->d_tl_dgram.release();

@@ -603,26 +603,42 @@ std::map<std::pair<int, std::string>, std::unique_ptr<Entry>> g_cache;
 // function-local statics during a compile, on the worker, and those register
 // their destructors after the handler, so exit runs them first.  A dist rank
 // that exited with compiles in flight still hung in r3.  The complete rule is
-// that no compile is in flight when the exit handlers start: ngz_rtc_drain joins
-// every worker, and the hosts call it before tearing down (netgauze_amd._lib
-// registers it with Python's atexit, which runs before any C exit handler).
+// that no compile is in flight when the exit handlers start.  Each compile's
+// thread is kept with its cache entry: ngz_ctx_destroy joins the threads of
+// every entry its context started or waits on (ngz_rtc_join), so a C / Rust
+// host that destroys its contexts (the codec's drop is synchronous,
+// codec.rs:68-82) has nothing in flight when it returns from main;
+// ngz_rtc_drain joins every worker (netgauze_amd._lib registers it with
+// Python's atexit, which runs before any C exit handler).
 struct Workers {
     std::mutex mu;
-    std::vector<std::thread> th;
-    int join_all() {
+    std::vector<std::pair<const void *, std::thread>> th;  // (cache entry, its compile)
+    // join the workers of the given entries (all when entries is null); returns how many
+    int join(const void *const *entries, size_t n) {
         std::vector<std::thread> v;
         {
             std::lock_guard<std::mutex> lk(mu);
-            v.swap(th);
+            for (size_t i = 0; i < th.size();) {
+                bool take = entries == nullptr;
+                for (size_t k = 0; k < n && !take; ++k) take = th[i].first == entries[k];
+                if (take) {
+                    v.push_back(std::move(th[i].second));
+                    th[i] = std::move(th.back());
+                    th.pop_back();
+                } else {
+                    ++i;
+                }
+            }
         }
-        int n = 0;
+        int k = 0;
         for (auto &t : v)
             if (t.joinable()) {
                 t.join();
-                ++n;
+                ++k;
             }
-        return n;
+        return k;
     }
+    int join_all() { return join(nullptr, 0); }
     ~Workers() { join_all(); }
 } g_workers;
 
@@ -725,10 +741,10 @@ int kernel_async(int device, const std::string &sig, Gen &&gen, const char *knam
             std::atexit(join_workers_at_exit);
         });
         std::lock_guard<std::mutex> lk(g_workers.mu);
-        g_workers.th.emplace_back([=, src = std::move(src)]() {
+        g_workers.th.emplace_back(e, std::thread([=, src = std::move(src)]() {
             pthread_setname_np(pthread_self(), "ngz-rtc");  // visible in /proc/<pid>/task/*/comm
             build(e, device, src, sig, kname);
-        });
+        }));
         return 0;
     }
     if (st == 2) {
@@ -776,6 +792,10 @@ extern "C" int ngz_rtc_drain(void) {
     for (int k; (k = g_workers.join_all()) > 0;) n += k;
     return n;
 }
+
+// Join the background compiles of these cache entries (whichever context
+// started them); returns how many were still registered.
+int ngz_rtc_join(void *const *entries, size_t n) { return n ? g_workers.join(entries, n) : 0; }
 
 int ngz_rtc_poll(void *entry, void **fn) {
     Entry *e = (Entry *)entry;

@@ -55,6 +55,10 @@ int main(int argc, char **argv) {
         else { fprintf(stderr, "unexpected argument '%s'\n", a.c_str()); usage(argv[0]); return 2; }
     }
     if (!input || !protocol || ports.empty()) { usage(argv[0]); return 2; }
+    if (ngz_abi_version() != NGZ_ABI_VERSION) {
+        fprintf(stderr, "ngz-pcap-decoder: libngz ABI %d, built against %d\n", ngz_abi_version(), NGZ_ABI_VERSION);
+        return 2;
+    }
     std::string p = protocol;
     for (auto &ch : p) ch = (char)tolower(ch);
     if (p != "flow") {

@@ -16,6 +16,7 @@ import re
 import sys
 
 FILES = [
+    "crates/flow-pkt/src/wire/tests/mod.rs",
     "crates/flow-pkt/src/wire/tests/ipfix.rs",
     "crates/flow-pkt/src/wire/tests/netflow.rs",
     "crates/flow-pkt/benches/serde_benchmark.rs",

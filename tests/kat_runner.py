@@ -75,6 +75,47 @@ NF9_WRAP_HDR = {"version": 9, "sys_up_time": 0, "unix_time": "1970-01-01T00:00:0
                 "source_id": 0}
 
 
+IPFIX_WRAP_HDR = {"version": 10, "export_time": "1970-01-01T00:00:00Z", "sequence_number": 0,
+                  "observation_domain_id": 0}
+IPFIX_WRAPPED = ("ipfixset", "tplrec", "fspec", "datarec")
+# where the lone item starts inside its wrapping message
+_WRAP_AT = {"ipfixset": 16, "tplrec": 20, "fspec": 24, "datarec": 20}
+
+
+def ipfix_wrap(kind, b, tid=None):
+    """A lone IPFIX set / template record / field specifier / data record of
+    template `tid` inside a one-set IPFIX message (zero header fields)."""
+    if kind == "ipfixset":
+        st = b
+    else:
+        body = {"tplrec": b, "fspec": struct.pack(">HH", 256, 1) + b, "datarec": b}[kind]
+        st = struct.pack(">HH", tid if kind == "datarec" else 2, 4 + len(body)) + body
+    return struct.pack(">HHIII", 10, 16 + len(st), 0, 0, 0) + st
+
+
+def _shift_offsets(v, by):
+    if isinstance(v, dict):
+        return {k: (x + by if k == "offset" else _shift_offsets(x, by)) for k, x in v.items()}
+    return v
+
+
+def ipfix_wrapped_expect(kind, ek, ev, tid=None):
+    """The packet value (ek "ok") or IpfixPacketParsingError (ek "err") the
+    wrapping message must give for an item-level expectation: the item nested
+    as the reference's types nest it (Set / TemplateRecord / FieldSpecifier /
+    DataRecord, ipfix.rs:99-108,212-221,419-424), errors wrapped as
+    IpfixPacketParsingError::SetParsingError(SetParsingError::
+    TemplateRecordError(..)) (ipfix.rs:51,124) with offsets made absolute."""
+    if ek == "ok":
+        st = {"ipfixset": ev, "tplrec": {"Template": [ev]},
+              "fspec": {"Template": [{"id": 256, "field_specifiers": [ev]}]},
+              "datarec": {"Data": {"id": tid, "records": [ev]}}}[kind]
+        return dict(IPFIX_WRAP_HDR, sets=[st])
+    if ek == "err" and kind == "tplrec":
+        return {"SetParsingError": {"TemplateRecordError": _shift_offsets(ev, _WRAP_AT[kind])}}
+    return None
+
+
 def step_wire(w):
     return K.wire(w) if isinstance(w, str) else bytes(w)
 
@@ -99,8 +140,21 @@ def oracle_step(kind, wire, tmap):
         if kind == "nf9":
             pkt = O.parse_netflow_packet(cur, tmap)
             return "ok", jsonify(pkt.to_json())["NetFlowV9"], cur.offset()
-        s = O._nf_set(cur, tmap)
-        return "ok", jsonify(O._set_json(s, True)), cur.offset()
+        if kind == "nf9set":
+            s = O._nf_set(cur, tmap)
+            return "ok", jsonify(O._set_json(s, True)), cur.offset()
+        if kind == "ipfixset":
+            return "ok", jsonify(O._set_json(O._ipfix_set(cur, tmap), False)), cur.offset()
+        if kind == "tplrec":
+            return "ok", jsonify(O._ipfix_template_record(cur, tmap)), cur.offset()
+        if kind == "fspec":
+            return "ok", jsonify(O.parse_field_specifier(cur).to_json()), cur.offset()
+        if kind == "datarec":
+            (t,) = tmap.values()
+            scope, fields = O._ipfix_data_record(cur, t)
+            return "ok", jsonify({"scope_fields": [O.field_json(x) for x in scope],
+                                  "fields": [O.field_json(x) for x in fields]}), cur.offset()
+        raise AssertionError(kind)
     except O.ParseFail as e:
         return "err", jsonify(e.err), None
 
@@ -116,5 +170,9 @@ def codec_datagrams(case_map):
     steps = []
     for i, (kind, w, exp) in enumerate(case_map["steps"]):
         b = step_wire(w)
-        steps.append((i, nf9_wrap(b) if kind == "nf9set" else b))
+        if kind == "nf9set":
+            b = nf9_wrap(b)
+        elif kind in IPFIX_WRAPPED:
+            b = ipfix_wrap(kind, b, next(iter(case_map.get("preload", {})), None))
+        steps.append((i, b))
     return pre, steps

@@ -8,6 +8,7 @@ Expected values are restated in the oracle's value model:
 import calendar
 import struct
 
+import kats_packets as K
 import ngz_oracle as O
 
 
@@ -81,4 +82,21 @@ KATS = [
     ("reader_i32_full_width", 434, 4, bytes([0xFF, 0xFF, 0xFF, 0xFE]), -2),
     # reader.rs:360-369 (read_padded left-aligns, zero-pads the tail) through an unsigned256 IE
     ("reader_padded_short", 515, 2, bytes([0xAA, 0xBB]), bytes([0xAA, 0xBB]) + bytes(30)),
+] + [
+    # mod.rs:131-157 test_mac_address_value, :187-214 test_pkg_record_value and :316-344
+    # test_record_value (the same vector in three tests): sourceMacAddress 12:c6:21:12:69:32; length 2 is
+    # InvalidLength at the field start
+    (t + suffix, 56, ln, K.wire("mod.rs:%s:value_wire" % t), exp)
+    for t in ("test_mac_address_value", "test_pkg_record_value", "test_record_value")
+    for suffix, ln, exp in (
+        ("", 6, bytes([0x12, 0xc6, 0x21, 0x12, 0x69, 0x32])),
+        ("_invalid_length", 2, {"InvalidLength": {"offset": 0, "ie_name": "sourceMacAddress", "length": 2}}))
+] + [
+    # mod.rs:159-185 test_ipv4_address_value: sourceIPv4Address 70.1.115.1; length 2 is InvalidLength
+    ("ipv4_address_value", 8, 4, K.wire("mod.rs:test_ipv4_address_value:good_wire"), ("v4", 0x46017301)),
+    ("ipv4_address_invalid_length", 8, 2, K.wire("mod.rs:test_ipv4_address_value:good_wire"),
+     {"InvalidLength": {"offset": 0, "ie_name": "sourceIPv4Address", "length": 2}}),
+    # mod.rs:297-314 test_string_value: interfaceName declared 16 bytes, "lo" + 14 NULs -> "lo"
+    # (a fixed-length string is cut at its first NUL, generator.rs:1635-1672)
+    ("string_fixed_nul_truncated", 82, 16, K.wire("mod.rs:test_string_value:good_wire"), "lo"),
 ]

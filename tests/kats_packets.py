@@ -11,7 +11,11 @@ A case is a list of template maps ("peers"); each map is a sequence of steps
     (kind, wire, expect)
   kind    "ipfix" = IpfixPacket::parse, "nf9" = NetFlowV9Packet::parse,
           "nf9set" = netflow Set::parse of a lone set (wrapped into a v9
-          message for the codec-level device run)
+          message for the codec-level device run); "ipfixset" = IPFIX
+          Set::parse of a lone set, "tplrec" = TemplateRecord::parse,
+          "fspec" = FieldSpecifier::parse, "datarec" = DataRecord::parse with
+          the map's one preloaded template (each wrapped into an IPFIX
+          message, kat_runner.ipfix_wrap)
   wire    fixture key, or raw bytes
   expect  ("ok", packet_json)    parsed completely, equal to the Rust value
           ("ok?", None)          the test only unwraps Ok (values unpinned)
@@ -225,6 +229,7 @@ _APP = [(0x50, "2426945984", "4285581510"), (0x51, "877825990", "1742571168"), (
         (0x59, "1342289478", "3856588635")]  # ipfix.rs:1616-1685
 
 W = "ipfix.rs:"
+M = "mod.rs:"
 N = "netflow.rs:"
 B = "serde_benchmark.rs:<top>:"
 
@@ -449,6 +454,30 @@ CASES = {
         ("ipfix", B + "IPFIX_PKT_DATA_PKT_ONLY", ("ok?", None)),
         ("ipfix", B + "IPFIX_PKT_DATA_PKT_ONLY", ("same", 1)),
     ]}],
+
+    # mod.rs:35-65 test_template_record: TemplateRecord::parse of a lone record (wrapped into a template set
+    # of an IPFIX message for the codec-level device run); template id 0 is InvalidTemplateId at the record
+    # start (ipfix.rs:384-413)
+    "mod_template_record": [{"steps": [
+        ("tplrec", M + "test_template_record:good_wire",
+         ("ok", T(2049, S("sourceIPv6Address", 16), S("destinationIPv6Address", 16)))),
+        ("tplrec", M + "test_template_record:bad_template_id_wire",
+         ("err", {"InvalidTemplateId": {"offset": 0, "template_id": 0}})),
+    ]}],
+    # mod.rs:67-74 test_field: FieldSpecifier::parse (deserializer/mod.rs:53-66), wrapped into a one-field
+    # template record 256
+    "mod_field": [{"steps": [("fspec", M + "test_field:good_ipv4_src_wire", ("ok", S("sourceIPv4Address", 4)))]}],
+    # mod.rs:346-374 test_data_record_value: DataRecord::parse with the DecodingTemplate [sourceMacAddress 6,
+    # destinationMacAddress 6] (inserted as template 256; the record wrapped into a data set of it)
+    "mod_data_record_value": [{"preload": {256: ([], [S("sourceMacAddress", 6), S("destinationMacAddress", 6)])},
+                               "steps": [
+        ("datarec", M + "test_data_record_value:value_wire", ("ok", R([
+            ("sourceMacAddress", [0x12, 0xc6, 0x21, 0x12, 0x69, 0x32]),
+            ("destinationMacAddress", [0x12, 0xc6, 0x21, 0x12, 0x69, 0x32])]))),
+    ]}],
+    # mod.rs:376-420 test_set_template: Set::parse of a lone template set (template 307), wrapped into an
+    # IPFIX message
+    "mod_set_template": [{"steps": [("ipfixset", M + "test_set_template:good_wire", ("ok", TS(T(307, *T307))))]}],
 
     # netflow.rs:30-69
     "nf9_template_record": [{"steps": [

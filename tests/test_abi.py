@@ -26,6 +26,18 @@ def test_header_declares_abi():
     assert declared_functions(HEADERS[2:]) == sorted(_lib.AGG_FUNCTIONS)
 
 
+def test_abi_versions_match_headers():
+    """The library reports the NGZ_ABI_VERSION / NGZ_AGG_ABI_VERSION of the headers it was built
+    from, and the binding refuses any other (a host built against an older flow_aggregate.h would
+    pass a port where ngz_agg_push takes a const ngz_peer *)."""
+    from netgauze_amd import _lib
+    lib = _lib.load()
+    hdr = {m.group(1): int(m.group(2)) for h in HEADERS for m in
+           re.finditer(r"#define (NGZ_(?:AGG_)?ABI_VERSION) (\d+)", open(h).read())}
+    assert hdr == {"NGZ_ABI_VERSION": _lib.NGZ_ABI_VERSION, "NGZ_AGG_ABI_VERSION": _lib.NGZ_AGG_ABI_VERSION}
+    assert (lib.ngz_abi_version(), lib.ngz_agg_abi_version()) == (_lib.NGZ_ABI_VERSION, _lib.NGZ_AGG_ABI_VERSION)
+
+
 def test_agg_config_validation_without_device():
     """AggregationConfig::validate / validate_operation_compatibility are checked before any
     device call (config.rs:107-119, 212-250) with IE::supports_{arithmetic,comparison,bitwise}_ops

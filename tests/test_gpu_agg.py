@@ -76,7 +76,8 @@ def run_device(fields, batches, port=4739, coll=1_700_000_000_000, lateness_s=10
     from netgauze_amd.aggregate import FlowAggregator
     from netgauze_amd.flow import FlowInfoCodec
     codec = FlowInfoCodec()
-    agg = FlowAggregator(fields, lateness_s=lateness_s, capacity=capacity)
+    # one peer: 8 peer bits (max_peers 256) keep keys up to 35 bits in the exact packed tag
+    agg = FlowAggregator(fields, lateness_s=lateness_s, capacity=capacity, max_peers=256)
     late = 0
     emitted = []
     for b in batches:
@@ -524,7 +525,7 @@ def test_partitioned_equals_atomic_at_full_size(dev, monkeypatch):
     rows = {}
     for mode in ("0", "1"):
         monkeypatch.setenv("NGZ_AGG_PART", mode)
-        agg = FlowAggregator(fields, capacity=1 << 20, lateness_s=60)
+        agg = FlowAggregator(fields, capacity=1 << 20, lateness_s=60, max_peers=256)  # packed, as the bench
         for _ in range(2):
             assert agg.push(batch, 4739, 0) == 0
         _, raw = agg.flush_raw()
@@ -709,7 +710,7 @@ def test_tombstones_do_not_fill_the_table(dev):
     [(0, 61, 0, OK), (0, 60, 0, OK)],  # direction + ipVersion: 2
 ])
 def test_lowcard_path_equals_oracle(dev, keys, monkeypatch):
-    """The low-cardinality path (k_agg_lc_scan + k_agg_lc_reduce: per-lane LDS accumulators,
+    """The low-cardinality path (k_agg_lc_part + k_agg_lc_merge: per-lane LDS accumulators,
     no per-record atomics) on T20 streams whose export times go back and forth (late
     messages dropped, windows closed push by push), equal to the oracle; the path is checked
     to be the one taken."""
@@ -734,10 +735,60 @@ def test_lowcard_path_equals_oracle(dev, keys, monkeypatch):
     same_groups(agg.flush(), o.flush())
 
 
+@pytest.mark.parametrize("max_peers", [4, 1024, 0])
+def test_lowcard_path_many_peers(dev, max_peers, monkeypatch):
+    """the low-cardinality path packs the peer entry into the window context
+    (k_agg_lc_part) and unpacks it when it writes the group's key (lc_key_write).  Four exporter
+    peers (IPv4 and IPv6) at their own clock offsets push T20 messages in turn, each push taking
+    the low-cardinality path, with max_peers 4 / 1024 / 65536 (2, 10 and 16 peer bits of the
+    packed tag): every push's emitted windows and the final flush equal the oracle's, groups
+    land on their own peer and close at that peer's own event time."""
+    monkeypatch.setenv("NGZ_AGG_LC", "1")
+    from netgauze_amd import synth
+    from netgauze_amd.aggregate import FlowAggregator
+    from netgauze_amd.flow import FlowInfoCodec
+    import ngz_oracle as O
+    fields = [(0, 4, 0, OK), (0, 61, 0, OK)] + T20_AGG
+    peers = ["10.0.0.1", "2001:db8::7", "192.0.2.200", "10.0.3.9"]
+    rounds, msgs_per_push, per_msg = 4, 3, 100
+    rec = synth.t20_records(len(peers) * rounds * msgs_per_push * per_msg, first=0)
+    buf, offs, lens = synth.ipfix_data_stream(rec, 64, rec_per_msg=per_msg)
+    b = bytes(buf.numpy())
+    msgs = [bytearray(b[o:o + ln]) for o, ln in zip(offs.tolist(), lens.tolist())]
+    agg = FlowAggregator(fields, capacity=1 << 12, lateness_s=10, max_peers=max_peers)
+    o = A.FlowAggregatorOracle(fields, 60, 10)
+    codecs, ocodecs = {}, {}
+    tm = synth.template_message()
+    seen_peers = set()
+    k = 0
+    for r in range(rounds):
+        for i, ip in enumerate(peers):
+            dg = [tm] if r == 0 else []
+            for j in range(msgs_per_push):
+                m = msgs[k]
+                k += 1
+                # peer i's clock: offset 13*i s, rounds 40 s apart, one message 30 s behind (late)
+                m[4:8] = struct.pack(">I", 1_700_000_000 + 13 * i + 40 * r - (30 if j == 1 else 0))
+                dg.append(bytes(m))
+            codec = codecs.setdefault(ip, FlowInfoCodec())
+            agg.push(codec.decode_datagrams(dg), 4739 + i, 1_000 * r, peer_ip=ip)
+            assert agg.last_path() == "lowcard"
+            oc = ocodecs.setdefault(ip, O.FlowInfoCodec())
+            A.aggregate_datagrams(fields, dg, 4739 + i, 1_000 * r, peer_ip=ip, agg=o, codec=oc)
+            got, ref = agg.emit(), o.emit()
+            same_groups(got, ref)
+            seen_peers |= {g["peer"] for g in ref}
+    assert len(seen_peers) > 1
+    fin = o.flush()
+    same_groups(agg.flush(), fin)
+    assert len({g["peer"] for g in fin}) == len(peers)
+
+
 def test_lowcard_falls_back_on_many_key_tuples(dev, monkeypatch):
-    """A packed key with more than 8 distinct tuples in a push (protocol + source port) leaves
-    the low-cardinality path after its scan: the general path continues from the groups the
-    scan claimed, and every reference capture still equals the oracle."""
+    """A packed key with more than 8 distinct tuples in a push (protocol + source port) makes a
+    wave of k_agg_lc_part raise the overflow flag: k_agg_lc_merge does nothing and the push runs
+    the general path from scratch (nothing claimed), and every reference capture still equals
+    the oracle."""
     monkeypatch.setenv("NGZ_AGG_LC", "1")
     from netgauze_amd.aggregate import FlowAggregator
     from netgauze_amd.flow import FlowInfoCodec
@@ -745,7 +796,7 @@ def test_lowcard_falls_back_on_many_key_tuples(dev, monkeypatch):
     for name in [c[0] for c in golden_io.cases()]:
         for key, dgrams in peers_of(name).items():
             codec = FlowInfoCodec()
-            agg = FlowAggregator(GOLDEN_AGG_PACKED, lateness_s=60)
+            agg = FlowAggregator(GOLDEN_AGG_PACKED, lateness_s=60, max_peers=256)  # 8 peer bits: packed tags
             h = len(dgrams) // 2
             emitted = []
             for part in (dgrams[:h], dgrams[h:]):

@@ -123,3 +123,22 @@ def test_exit_with_background_compiles_in_flight():
     p = subprocess.run([sys.executable, "-c", _EXIT_CHILD], env=env, capture_output=True, text=True, timeout=90)
     assert p.returncode == 0, (p.returncode, p.stdout[-2000:], p.stderr[-2000:])
     assert "EXITING" in p.stdout
+
+
+def test_c_host_exits_after_destroy_with_compiles_in_flight():
+    """A plain C host (tests/native/exit_after_compile.c) that starts four background compiles,
+    destroys its context and returns from main -- without ngz_rtc_drain -- exits 0:
+    ngz_ctx_destroy joins the compiles its context started or waits on (synchronous drop,
+    codec.rs:68-82).  The compiles were still running when the batch returned (slot kernel 2)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "netgauze_amd", "bin", "ngz-exit-check")
+    assert os.path.exists(exe), "built by __graft_entry__.build()"
+    env = {k: v for k, v in os.environ.items() if not k.startswith("NGZ_")}
+    p = subprocess.run([exe], env=env, capture_output=True, text=True, timeout=90)
+    assert p.returncode == 0, (p.returncode, p.stdout[-2000:], p.stderr[-2000:])
+    fields = dict(kv.split("=") for kv in p.stdout.split())
+    assert int(fields["records"]) == 4 * 2 * 200
+    assert int(fields["compiling"]) >= 1, p.stdout

@@ -104,3 +104,24 @@ def test_reader_shortened_and_too_wide():
     for op, ln, exp in K.READER_TOO_WIDE:
         r = O.Reader(bytearray(16))
         assert _reader_op(r, op, (ln,)) == exp and r.offset() == 0
+
+
+@pytest.mark.parametrize("name", sorted(n for n, c in K.CASES.items()
+                                        if any(k in kat_runner.IPFIX_WRAPPED for m in c for k, _, _ in m["steps"])))
+def test_wrapped_item_kats_at_packet_level(name):
+    """The item-level KATs (mod.rs TemplateRecord / FieldSpecifier / DataRecord
+    / Set) wrapped into the message the device tests send: the oracle's packet
+    parse of it equals the reference value nested as its types nest it
+    (kat_runner.ipfix_wrapped_expect), errors included with absolute offsets."""
+    for m in K.CASES[name]:
+        tmap = {}
+        kat_runner.preload(tmap, m.get("preload", {}))
+        tid = next(iter(m.get("preload", {})), None)
+        pre, steps = kat_runner.codec_datagrams(m)
+        for (i, dgram), (kind, w, (ek, ev)) in zip(steps, m["steps"]):
+            st, val, consumed = kat_runner.oracle_step("ipfix", dgram, tmap)
+            exp = kat_runner.ipfix_wrapped_expect(kind, ek, ev, tid)
+            assert st == ("ok" if ek == "ok" else "err"), (name, i, val)
+            assert val == exp, (name, i, val, exp)
+            if st == "ok":
+                assert consumed == len(dgram)
