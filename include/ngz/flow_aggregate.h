@@ -45,8 +45,9 @@
 extern "C" {
 #endif
 
-#define NGZ_AGG_ABI_VERSION 2 /* 2: ngz_agg_create takes max_peers, ngz_agg_push a const ngz_peer * (the
-                                 exporter's address; 1 took a uint16 port) */
+#define NGZ_AGG_ABI_VERSION 3 /* 2: ngz_agg_create takes max_peers, ngz_agg_push a const ngz_peer * (the
+                                 exporter's address; 1 took a uint16 port); 3: byte-valued keys and values
+                                 of any length (kkind 3, vclass 8 / 9, ngz_agg_row_bytes) */
 
 /* NGZ_AGG_ABI_VERSION the library was built with (checked by hosts like ngz_abi_version). */
 int ngz_agg_abi_version(void);
@@ -93,9 +94,9 @@ typedef struct {
 /* Validates the config like AggregationConfig::validate + validate_operation_compatibility
  * (window > 0, lateness <= window; the op allowed by IE::supports_{arithmetic,comparison,
  * bitwise}_ops, generator.rs:1176-1272 -- data type, sub-registry and dataTypeSemantics
- * identifier/flags): NGZ_E_INVALID where the reference rejects the config, NGZ_E_LIMIT where
- * it accepts one the device does not run (Min/Max over list types or the nested reason-code
- * sub-registry of forwardingStatus).  Key fields keep their order (key_select), aggregated
+ * identifier/flags): NGZ_E_INVALID where the reference rejects the config.  Every config the
+ * reference accepts runs (NGZ_E_LIMIT only beyond the compiled limits: NGZ_AGG_MAX_KEYS /
+ * NGZ_AGG_MAX_VALUES, capacity, max_peers).  Key fields keep their order (key_select), aggregated
  * fields theirs (agg_select).  capacity: live groups held at most, up to 2^30 (the HBM table
  * has at least twice as many slots).  max_peers: distinct peer IPs the aggregator takes
  * between flushes (0 = NGZ_AGG_MAX_PEERS); a small bound leaves more bits of the exact
@@ -181,13 +182,21 @@ int ngz_agg_sets(ngz_agg *a, uint32_t *templates, uint32_t *n_templates, uint16_
 int ngz_agg_peer(ngz_agg *a, uint32_t index, ngz_peer *out);
 
 /* How a key / value is stored in an output row.
- * Key kkind: 0 the decoded column cell (width bytes), 1 a fixed string up to its first
- * NUL (zero padded to the slot), 2 an octet array: u32 length, then the bytes.
+ * Key kkind: 0 the decoded column cell (width bytes); 3 a byte value of any length (string,
+ * octetArray, list and unknown IEs; fixed or variable-length on the wire): u32 length, u32
+ * reserved, then the first 32 bytes (zero padded) -- the whole value through
+ * ngz_agg_row_bytes.  A string key is its text: a fixed-length cell up to its first NUL
+ * (Field::String, generator.rs:1654-1669), a variable-length one as sent, so the same text
+ * declared at different lengths or variable-length is one key.  (kkinds 1 and 2 are no
+ * longer produced.)
  * Value vclass: 0 unsigned / 1 signed integer (little-endian at the IE width, the
  * Rust type's wrap-around for Add), 2 dateTime micro/nanoseconds (u64 secs<<32 | nanos),
- * 3 bytes (OR), 4 sub-registry / TCP flags value (little-endian at the width), 5 f32,
- * 6 f64, 7 IPv6 address (16 bytes, network order).  kind: the decoded column kind
- * (NGZ_K_*) and width the column width, both as first seen (0 before). */
+ * 3 bytes (OR of a fixed-size type: macAddress, ipv6Address, unsigned256, MPLS label),
+ * 4 sub-registry / TCP flags value (little-endian at the width), 5 f32, 6 f64, 7 IPv6
+ * address (16 bytes, network order), 8 octetArray BoolMapOr, 9 list Min / Max (both in the
+ * kkind 3 form: length, reserved, first 32 bytes; ngz_agg_row_bytes for all of them).
+ * kind: the decoded column kind (NGZ_K_*) and width the column width, both as first seen
+ * (0 before). */
 typedef struct {
     uint8_t kkind;
     uint8_t kind;
@@ -203,6 +212,11 @@ typedef struct {
 } ngz_agg_value_desc;
 int ngz_agg_key_info(ngz_agg *a, uint32_t k, ngz_agg_key_desc *out);
 int ngz_agg_value_info(ngz_agg *a, uint32_t v, ngz_agg_value_desc *out);
+
+/* The whole byte value of key k (is_value 0, kkind 3) or aggregated field v (is_value 1,
+ * vclass 8 / 9) of an output row of the last ngz_agg_flush / ngz_agg_emit call: up to cap
+ * bytes into dst (may be NULL); returns the value's length, or NGZ_E_INVALID. */
+int64_t ngz_agg_row_bytes(ngz_agg *a, const void *row, int is_value, uint32_t index, uint8_t *dst, uint64_t cap);
 
 /* AggFlowInfo::into_flowinfo_with_extra_fields (aggregator.rs:203-277) of output rows,
  * with the extra fields the aggregation actor always passes (actor.rs:222-240), for the

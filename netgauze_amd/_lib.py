@@ -24,7 +24,7 @@ ABI_FUNCTIONS = [
     "ngz_dgram_error", "ngz_template_counts_device", "ngz_slot_kernel", "ngz_rtc_drain", "ngz_abi_version",
 ]
 NGZ_ABI_VERSION = 3
-NGZ_AGG_ABI_VERSION = 2
+NGZ_AGG_ABI_VERSION = 3
 # ngz_error.kind / .layer (flow_decode.h)
 ERR_KINDS = ["NONE", "UNSUPPORTED_VERSION", "INVALID_LENGTH", "UNEXPECTED_EOF", "INVALID_PADDING_LENGTH",
              "INVALID_SET_ID", "NO_TEMPLATE", "INVALID_PADDING_VALUE", "INVALID_COUNT", "INVALID_TEMPLATE_ID",
@@ -42,13 +42,14 @@ AGG_FUNCTIONS = [
     "ngz_agg_create", "ngz_agg_destroy", "ngz_agg_last_error", "ngz_agg_push", "ngz_agg_layout",
     "ngz_agg_groups", "ngz_agg_flush", "ngz_agg_closed", "ngz_agg_emit", "ngz_agg_reset", "ngz_agg_sets",
     "ngz_agg_key_info", "ngz_agg_value_info", "ngz_agg_flowinfo_json", "ngz_agg_last_timing", "ngz_agg_peer", "ngz_agg_last_path",
-    "ngz_agg_abi_version",
+    "ngz_agg_abi_version", "ngz_agg_row_bytes",
 ]
 NGZ_AGG_KEY, NGZ_AGG_ADD, NGZ_AGG_MIN, NGZ_AGG_MAX, NGZ_AGG_OR = range(5)
 NGZ_AGG_E_OVERFLOW, NGZ_AGG_E_COLLISION, NGZ_AGG_E_POISONED = -10, -11, -12
 # ngz_agg_key_desc.kkind / ngz_agg_value_desc.vclass
-AGG_KK_FIXED, AGG_KK_STR, AGG_KK_OCTETS = range(3)
-AGG_VC_UINT, AGG_VC_SINT, AGG_VC_DTFRAC, AGG_VC_BYTES, AGG_VC_RANK, AGG_VC_F32, AGG_VC_F64, AGG_VC_IPV6 = range(8)
+AGG_KK_FIXED, AGG_KK_BYTES = 0, 3
+(AGG_VC_UINT, AGG_VC_SINT, AGG_VC_DTFRAC, AGG_VC_BYTES, AGG_VC_RANK, AGG_VC_F32, AGG_VC_F64, AGG_VC_IPV6,
+ AGG_VC_VBYTES, AGG_VC_VLIST) = range(10)
 NGZ_COLLECT_PCAP_DECODER, NGZ_COLLECT_FLOW_INFO = 0, 1
 NGZ_PROTO_TCP, NGZ_PROTO_UDP = 6, 17
 
@@ -259,6 +260,8 @@ def load():
     lib.ngz_agg_key_info.restype = I
     lib.ngz_agg_value_info.argtypes = [P, U32, ctypes.POINTER(AggValueDesc)]
     lib.ngz_agg_value_info.restype = I
+    lib.ngz_agg_row_bytes.argtypes = [P, P, I, U32, P, U64]
+    lib.ngz_agg_row_bytes.restype = ctypes.c_int64
     lib.ngz_agg_flowinfo_json.argtypes = [P, P, U64, U32, U32, ctypes.c_int64, JSON_LINE_FN, P]
     lib.ngz_agg_flowinfo_json.restype = ctypes.c_int64
     lib.ngz_agg_peer.argtypes = [P, U32, ctypes.POINTER(Peer)]

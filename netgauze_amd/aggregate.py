@@ -233,11 +233,17 @@ class FlowAggregator:
                 if not (int(h["key_present"]) >> k) & 1:
                     key.append(None)
                     continue
+                if kd[k].kkind == _lib.AGG_KK_BYTES:
+                    key.append(self._render_bytes(pen, ie, self._row_bytes(r, 0, k)))
+                    continue
                 key.append(self._render_key(pen, ie, kd[k], bytes(r[ko[k]:ko[k] + kd[k].slot])))
             vals = []
             for v, (pen, ie, _i, op) in enumerate(self.val_fields):
                 if not (int(h["val_present"]) >> v) & 1:
                     vals.append(None)
+                    continue
+                if vd[v].vclass in (_lib.AGG_VC_VBYTES, _lib.AGG_VC_VLIST):
+                    vals.append(self._row_bytes(r, 1, v))
                     continue
                 vals.append(self._render_value(pen, ie, vd[v], bytes(r[vo[v]:vo[v] + 32])))
             dom_bits = int(h["domain_bits"][0]) | (int(h["domain_bits"][1]) << 64)
@@ -251,13 +257,24 @@ class FlowAggregator:
                             ports=bits(h["port_bits"], ports), domains=bits(dom_bits, doms)))
         return out
 
+    def _row_bytes(self, row, is_value, index):
+        """The whole byte value of a BVAL key / value of an output row (ngz_agg_row_bytes)."""
+        row = np.ascontiguousarray(row)
+        n = self._check(lib().ngz_agg_row_bytes(self._h, row.ctypes.data, is_value, index, None, 0))
+        buf = (ctypes.c_uint8 * max(n, 1))()
+        lib().ngz_agg_row_bytes(self._h, row.ctypes.data, is_value, index, buf, n)
+        return bytes(buf[:n])
+
+    def _render_bytes(self, pen, ie, b):
+        kind = self.kinds.get((pen, ie))
+        if kind == "str" or (kind is None and ie_dtype(pen, ie) == "string"):
+            return b.decode("utf-8")
+        return b
+
     def _render_key(self, pen, ie, d, b):
         kind = self.kinds.get((pen, ie))
-        if d.kkind == _lib.AGG_KK_STR or kind == "str":
+        if kind == "str":
             return b.split(b"\0", 1)[0].decode("utf-8")
-        if d.kkind == _lib.AGG_KK_OCTETS:
-            n = int.from_bytes(b[:4], "little")
-            return b[4:4 + n]
         return self._render_cell(pen, ie, d.kind, d.width, b, kind)
 
     def _render_value(self, pen, ie, d, b):

@@ -78,15 +78,29 @@ enum : uint8_t {
     VC_F32 = 5,    // OrderedFloat<f32> (ordered path)
     VC_F64 = 6,    // OrderedFloat<f64> (ordered path)
     VC_IPV6 = 7,   // Ipv6Addr Min / Max (16 bytes, big-endian order; ordered path)
+    VC_VBYTES = 8, // octetArray BoolMapOr, any length: the group keeps its first value's length and ORs
+                   // the others into it, zipped (`lhs.iter_mut().zip(rhs)`, generator.rs:1051-1059);
+                   // BVAL row form (below); ordered path
+    VC_VLIST = 9,  // basicList / subTemplateList / subTemplateMultiList Min / Max: Box<[u8]>'s
+                   // lexicographic Ord; BVAL row form; ordered path
 };
-__host__ __device__ inline bool vc_ordered(uint8_t vc) { return vc == VC_F32 || vc == VC_F64 || vc == VC_IPV6; }
+__host__ __device__ inline bool vc_ordered(uint8_t vc) {
+    return vc == VC_F32 || vc == VC_F64 || vc == VC_IPV6 || vc == VC_VBYTES || vc == VC_VLIST;
+}
 
 // key kinds: canonical key bytes in the row
 enum : uint8_t {
     KK_FIXED = 0,  // the column cell, zero padded
-    KK_STR = 1,    // fixed string: bytes up to the first NUL (Field::String, generator.rs:1654-1669), zero padded
-    KK_OCTETS = 2, // octetArray: u32 length + bytes (Box<[u8]> compares its length too)
+    KK_BYTES = 3,  // a byte value of any length (string / octetArray / list / unknown IEs): BVAL row form.
+                   // A string is its text: a fixed-length cell up to its first NUL (Field::String,
+                   // generator.rs:1654-1669), a variable-length one as sent; octets / lists / unknown
+                   // IEs their bytes (Box<[u8]> compares the length too)
 };
+
+// BVAL row form of a byte value: u32 length n, u32 arena offset of bytes 32.. (when n > 32), the
+// first 32 bytes zero padded.  Values longer than 32 bytes keep their tail in the aggregator's
+// byte arena (bump-allocated per group, compacted when the table is rebuilt, emptied by flush).
+constexpr uint32_t BVAL_BYTES = 40, BVAL_INLINE = 32;
 
 struct AggSlotPlan {            // per batch slot, built on the host every push
     const uint8_t *key_col[NGZ_AGG_MAX_KEYS];   // null: the record has no such field (None)
@@ -96,6 +110,8 @@ struct AggSlotPlan {            // per batch slot, built on the host every push
     uint64_t tpl_bit;
     uint32_t proto;
     uint32_t usable;                            // 0: slot not aggregated (no records / not device-decoded)
+    const uint8_t *bytes;                       // the batch bytes (variable-length cells point into them)
+    uint32_t key_vlen, val_vlen;                // bit k / v: a variable-length column ({u64 offset, u32 length})
 };
 
 struct AggParams {
@@ -124,6 +140,13 @@ struct AggParams {
     uint8_t kw_key[8], kw_idx[8];  // key word j: its key field and its word within the field
     uint64_t unit_op[2];        // owner path: 4-bit op of each 8-byte unit of the row (units 0-15, 16-31)
     uint64_t unit_src[2];       // ... and its operand (U_SRC_*)
+    uint32_t key_str;           // bit k: key k is a string (KK_BYTES text: fixed cells NUL-truncated)
+    uint32_t has_bytes;         // some key / value is in the BVAL form
+    uint8_t *arena;             // byte arena: tails of BVAL values longer than 32 bytes
+    uint64_t arena_cap;
+    unsigned long long *arena_used;  // device bump counter (bytes)
+    const unsigned long long *rank_nested[NGZ_AGG_MAX_VALUES];  // VC_RANK of a nested sub-registry: rank of
+                                                                 // values 0..255, [256]: outer Unassigned
 };
 
 __device__ __forceinline__ uint64_t mix64(uint64_t h, uint64_t v) {
@@ -157,17 +180,96 @@ __device__ __forceinline__ uint32_t cell_word(const uint8_t *p, uint32_t w, uint
     return r;
 }
 
-// canonical key word j of key k (KK_OCTETS: word 0 is the length)
+// canonical key word j of a fixed key cell
 struct KeyWords {
     const uint8_t *p;
     uint32_t w;
-    uint8_t kind;
     bool nul = false;
-    __device__ uint32_t operator()(uint32_t j) {
-        if (kind == KK_OCTETS) return j == 0 ? w : cell_word(p, w, j - 1, false, nul);
-        return cell_word(p, w, j, kind == KK_STR, nul);
-    }
+    __device__ uint32_t operator()(uint32_t j) { return cell_word(p, w, j, false, nul); }
 };
+
+// A byte value of a record: where its bytes are and how many (BVAL keys and values)
+struct Span {
+    const uint8_t *p;
+    uint32_t n;
+};
+
+__device__ __forceinline__ Span cell_span(const uint8_t *col, uint32_t w, bool vlen, bool str, const uint8_t *bytes,
+                                          uint64_t row) {
+    if (vlen) {  // {u64 offset into the batch bytes, u32 length, u32 0} (NGZ_K_VLEN)
+        const uint8_t *c = col + row * 16;
+        return Span{bytes + *(const uint64_t *)c, *(const uint32_t *)(c + 8)};
+    }
+    const uint8_t *q = col + row * w;
+    uint32_t n = w;
+    if (str) {  // a fixed-length string is its text up to the first NUL
+        n = 0;
+        while (n < w && q[n]) ++n;
+    }
+    return Span{q, n};
+}
+
+__device__ __forceinline__ Span key_span(const AggSlotPlan &sp, const AggParams &P, uint32_t k, uint64_t row) {
+    return cell_span(sp.key_col[k], sp.key_w[k], (sp.key_vlen >> k) & 1, (P.key_str >> k) & 1, sp.bytes, row);
+}
+
+__device__ __forceinline__ Span val_span(const AggSlotPlan &sp, uint32_t v, uint64_t row) {
+    return cell_span(sp.val_col[v], sp.val_w[v], (sp.val_vlen >> v) & 1, false, sp.bytes, row);
+}
+
+// word j (little-endian) of bytes [0, n) of p, zero past n
+__device__ __forceinline__ uint32_t span_word(const uint8_t *p, uint32_t n, uint32_t j) {
+    uint32_t r = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < 4; ++b) {
+        const uint32_t i = 4 * j + b;
+        if (i < n) r |= (uint32_t)p[i] << (8 * b);
+    }
+    return r;
+}
+
+// A BVAL value in a row: byte i is inline (i < 32) or in the arena
+struct BRef {
+    const uint8_t *a, *b;  // bytes [0, split) at a, [split, n) at b - split
+    uint32_t split, n;
+    __device__ __forceinline__ uint8_t at(uint32_t i) const { return i < split ? a[i] : b[i - split]; }
+};
+
+__device__ __forceinline__ BRef bval_ref(const uint8_t *slot, const AggParams &P) {
+    const uint32_t n = *(const uint32_t *)slot, off = *(const uint32_t *)(slot + 4);
+    return BRef{slot + 8, P.arena + off, BVAL_INLINE, n};
+}
+
+// Box<[u8]> / [u8] Ord: lexicographic, then by length
+__device__ __forceinline__ int bytes_cmp(const BRef &x, const BRef &y) {
+    const uint32_t m = min(x.n, y.n);
+    for (uint32_t i = 0; i < m; ++i) {
+        const uint8_t a = x.at(i), b = y.at(i);
+        if (a != b) return a < b ? -1 : 1;
+    }
+    return x.n < y.n ? -1 : (x.n > y.n ? 1 : 0);
+}
+
+// Writes a record's byte value in the BVAL form at slot (tail bytes into the arena).  The
+// push sized the arena for every tail it can write (k_agg_tail_need); err bit 64 if not.
+__device__ __forceinline__ void bval_write(uint8_t *slot, const Span s, const AggParams &P,
+                                           unsigned int *__restrict__ err) {
+    uint32_t *d = (uint32_t *)slot;
+    d[0] = s.n;
+    d[1] = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < BVAL_INLINE / 4; ++j) d[2 + j] = span_word(s.p, min(s.n, BVAL_INLINE), j);
+    if (s.n > BVAL_INLINE) {
+        const uint64_t need = s.n - BVAL_INLINE;
+        const uint64_t off = atomicAdd(P.arena_used, (unsigned long long)need);
+        if (off + need > P.arena_cap) {
+            atomicOr(err, 64u);
+            return;
+        }
+        for (uint32_t i = 0; i < need; ++i) P.arena[off + i] = s.p[BVAL_INLINE + i];
+        d[1] = (uint32_t)off;
+    }
+}
 
 // Canonical key words of a record held in registers (hashed keys of at most 8 words): the
 // record's columns are read once, and the slot's key is compared with a few wide loads
@@ -186,9 +288,7 @@ __device__ __forceinline__ void key_words(const AggSlotPlan &sp, const AggParams
         if (!c) continue;
         const uint32_t w = sp.key_w[k];
         if (i == 0) nul = false;
-        const uint8_t *q = c + row * w;
-        if (P.key_kind[k] == KK_OCTETS) kv.w[j] = i == 0 ? w : cell_word(q, w, i - 1, false, nul);
-        else kv.w[j] = cell_word(q, w, i, P.key_kind[k] == KK_STR, nul);
+        kv.w[j] = cell_word(c + row * w, w, i, false, nul);  // KeyVal keys are fixed cells
     }
 }
 
@@ -235,7 +335,13 @@ __device__ __forceinline__ uint64_t key_tag(const AggSlotPlan &sp, const AggPara
             h = mix64(h, c ? 0x100u : 0u);
             if (!c) continue;
             present |= 1u << k;
-            KeyWords kw{c + row * sp.key_w[k], sp.key_w[k], P.key_kind[k]};
+            if (P.key_kind[k] == KK_BYTES) {  // its length and every byte
+                const Span s = key_span(sp, P, k, row);
+                h = mix64(h, s.n);
+                for (uint32_t j = 0; j < (s.n + 3) / 4; ++j) h = mix64(h, span_word(s.p, s.n, j));
+                continue;
+            }
+            KeyWords kw{c + row * sp.key_w[k], sp.key_w[k]};
             for (uint32_t j = 0; j < P.key_slot[k] / 4; ++j) h = mix64(h, kw(j));
         }
     }
@@ -276,15 +382,26 @@ __device__ __forceinline__ bool key_equal(const uint8_t *R, const AggSlotPlan &s
     for (uint32_t k = 0; k < P.n_keys && same; ++k) {
         const uint8_t *c = sp.key_col[k];
         if (!c) continue;
-        KeyWords kw{c + row * sp.key_w[k], sp.key_w[k], P.key_kind[k]};
-        for (uint32_t j = 0; j < P.key_slot[k] / 4 && same; ++j)
-            same = ((const uint32_t *)(R + P.key_off[k]))[j] == kw(j);
+        const uint32_t *rk = (const uint32_t *)(R + P.key_off[k]);
+        if (P.key_kind[k] == KK_BYTES) {
+            const Span s = key_span(sp, P, k, row);
+            same = rk[0] == s.n;
+            for (uint32_t j = 0; j < BVAL_INLINE / 4 && same; ++j)
+                same = rk[2 + j] == span_word(s.p, min(s.n, BVAL_INLINE), j);
+            if (same && s.n > BVAL_INLINE) {
+                const uint8_t *t = P.arena + rk[1];
+                for (uint32_t i = BVAL_INLINE; i < s.n && same; ++i) same = t[i - BVAL_INLINE] == s.p[i];
+            }
+            continue;
+        }
+        KeyWords kw{c + row * sp.key_w[k], sp.key_w[k]};
+        for (uint32_t j = 0; j < P.key_slot[k] / 4 && same; ++j) same = rk[j] == kw(j);
     }
     return same;
 }
 
 __device__ __forceinline__ void key_write(uint8_t *R, const AggSlotPlan &sp, const AggParams &P, uint64_t row,
-                                          uint32_t win, uint32_t kp, const KeyVal &kv) {
+                                          uint32_t win, uint32_t kp, const KeyVal &kv, unsigned int *__restrict__ err) {
     *(uint32_t *)(R + 0) = win;
     *(uint32_t *)(R + 4) = hdr_word(sp, P);
     *(uint32_t *)(R + 8) = kp;
@@ -301,7 +418,11 @@ __device__ __forceinline__ void key_write(uint8_t *R, const AggSlotPlan &sp, con
             for (uint32_t j = 0; j < P.key_slot[k] / 4; ++j) dst[j] = 0;
             continue;
         }
-        KeyWords kw{c + row * sp.key_w[k], sp.key_w[k], P.key_kind[k]};
+        if (P.key_kind[k] == KK_BYTES) {
+            bval_write((uint8_t *)dst, key_span(sp, P, k, row), P, err);
+            continue;
+        }
+        KeyWords kw{c + row * sp.key_w[k], sp.key_w[k]};
         for (uint32_t j = 0; j < P.key_slot[k] / 4; ++j) dst[j] = kw(j);
     }
 }
@@ -333,13 +454,17 @@ __host__ __device__ __forceinline__ uint32_t bitrev8(uint32_t x) {
 // holds.  Ranks: TCPHeaderFlags derives Ord over (FIN, SYN, ..., CWR) in declaration order, so
 // FIN is the most significant (iana/src/tcp.rs:41-70); a sub-registry enum orders by its
 // discriminant: a registered value is its own discriminant, Unassigned(x) comes after every
-// registered variant (generator_sub_registries.rs: `Unassigned(ty)` declared last).
+// registered variant (generator_sub_registries.rs: `Unassigned(ty)` declared last).  A nested
+// sub-registry (forwardingStatus) orders by its outer variant (one per 64-value group, then
+// Unassigned), then by the reason enum's discriminant, then by the value: a host-built table
+// (rank_nested, the value in the low 32 bits).
 __device__ __forceinline__ uint64_t value_operand(const AggSlotPlan &sp, const AggParams &P, uint32_t v, uint64_t row) {
     const uint8_t vc = P.val_vc[v];
     uint64_t x = load_value(sp.val_col[v] + row * sp.val_w[v], sp.val_w[v], vc == VC_RANK ? VC_UINT : vc);
     if (vc == VC_SINT && (P.val_op[v] == NGZ_AGG_MIN || P.val_op[v] == NGZ_AGG_MAX)) x ^= 1ull << 63;
     if (vc == VC_RANK) {
         if (P.val_tcp[v]) x = bitrev8((uint32_t)x & 0xFF);
+        else if (const unsigned long long *nr = P.rank_nested[v]) x = x < 256 ? nr[x] : nr[256] | x;
         else {
             const uint32_t *known = P.rank_known[v];
             const bool reg = x < 65536 && known && ((known[x >> 5] >> (x & 31)) & 1);
@@ -520,7 +645,7 @@ __device__ __forceinline__ uint32_t probe(const AggSlotPlan &sp, const AggParams
         if (cur == TAG_EMPTY) {
             cur = atomicCAS(&tags[g], TAG_EMPTY, (unsigned long long)h);
             if (cur == TAG_EMPTY) {
-                key_write(rows + g * P.row_bytes, sp, P, row, win, kp, kv);
+                key_write(rows + g * P.row_bytes, sp, P, row, win, kp, kv, err);
                 *claimed = true;
                 return (uint32_t)g;
             }
@@ -1180,6 +1305,69 @@ __global__ __launch_bounds__(256) void k_agg_ordered(const RecCtx C, const AggPa
             const uint8_t op = P.val_op[v];
             bool have = (vp >> v) & 1;
             uint8_t *dst = R + P.val_off[v];
+            if (vc == VC_VBYTES) {
+                // octetArray `|=`: the first value keeps its length, later ones OR in their zipped
+                // prefix (generator.rs:1051-1059); the tail of a value longer than 32 bytes is ORed
+                // in place in the arena
+                uint32_t *d = (uint32_t *)dst;
+                uint32_t n0 = have ? d[0] : 0u, inl[BVAL_INLINE / 4];
+#pragma unroll
+                for (uint32_t j = 0; j < BVAL_INLINE / 4; ++j) inl[j] = have ? d[2 + j] : 0u;
+                for (uint64_t j = i; j < n && sg[j] == g; ++j) {
+                    const Rec r = rec_of(C, sr[j], err);
+                    if (!r.valid) continue;
+                    const AggSlotPlan &sp = C.plans[r.slot];
+                    if (!sp.val_col[v]) continue;
+                    const Span s = val_span(sp, v, r.row);
+                    if (!have) {
+                        bval_write(dst, s, P, err);  // the group's first value, tail included
+                        n0 = s.n;
+#pragma unroll
+                        for (uint32_t q = 0; q < BVAL_INLINE / 4; ++q) inl[q] = d[2 + q];
+                        have = true;
+                        continue;
+                    }
+                    const uint32_t m = min(n0, s.n);
+#pragma unroll
+                    for (uint32_t q = 0; q < BVAL_INLINE / 4; ++q) inl[q] |= span_word(s.p, min(m, BVAL_INLINE), q);
+                    if (m > BVAL_INLINE) {
+                        uint8_t *t = P.arena + d[1];
+                        for (uint32_t b = BVAL_INLINE; b < m; ++b) t[b - BVAL_INLINE] |= s.p[b];
+                    }
+                }
+                if (have) {
+#pragma unroll
+                    for (uint32_t q = 0; q < BVAL_INLINE / 4; ++q) d[2 + q] = inl[q];
+                    vp |= 1u << v;
+                }
+                continue;
+            }
+            if (vc == VC_VLIST) {
+                // Box<[u8]> Min / Max: the best value so far is the group's (in the row) or a record's
+                // (in the batch); written once at the end
+                BRef best = have ? bval_ref(dst, P) : BRef{nullptr, nullptr, 0, 0};
+                bool from_rec = false;
+                Span bs{nullptr, 0};
+                for (uint64_t j = i; j < n && sg[j] == g; ++j) {
+                    const Rec r = rec_of(C, sr[j], err);
+                    if (!r.valid) continue;
+                    const AggSlotPlan &sp = C.plans[r.slot];
+                    if (!sp.val_col[v]) continue;
+                    const Span s = val_span(sp, v, r.row);
+                    const BRef x{s.p, nullptr, s.n, s.n};
+                    if (!have || take_new(op, bytes_cmp(best, x))) {
+                        best = x;
+                        bs = s;
+                        from_rec = true;
+                    }
+                    have = true;
+                }
+                if (from_rec) {
+                    bval_write(dst, bs, P, err);
+                    vp |= 1u << v;
+                }
+                continue;
+            }
             double cd = 0;
             float cf = 0;
             uint8_t c6[16];
@@ -1483,6 +1671,7 @@ __device__ __forceinline__ uint64_t lc_operand(const AggParams &P, uint32_t v, u
     if (vc == VC_SINT && (P.val_op[v] == NGZ_AGG_MIN || P.val_op[v] == NGZ_AGG_MAX)) x ^= 1ull << 63;
     if (vc == VC_RANK) {
         if (P.val_tcp[v]) x = bitrev8((uint32_t)x & 0xFF);
+        else if (const unsigned long long *nr = P.rank_nested[v]) x = x < 256 ? nr[x] : nr[256] | x;
         else {
             const uint32_t *known = P.rank_known[v];
             const bool reg = x < 65536 && known && ((known[x >> 5] >> (x & 31)) & 1);
@@ -2107,6 +2296,63 @@ __global__ void k_agg_rehash(const unsigned long long *__restrict__ tags, const 
     }
 }
 
+// ---- byte values (BVAL) longer than 32 bytes: their tails in the byte arena ----
+// Tail bytes a push can write at most: every present BVAL key and value of every valid record
+// beyond its first 32 bytes (a group's claim or its ordered fold writes at most one record's)
+__global__ void k_agg_tail_need(const RecCtx C, const AggParams P, unsigned long long *__restrict__ need) {
+    uint64_t mine = 0;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < C.n_rec; t += (uint64_t)gridDim.x * blockDim.x) {
+        const Rec r = rec_of(C, t, nullptr);
+        if (!r.valid) continue;
+        const AggSlotPlan &sp = C.plans[r.slot];
+        for (uint32_t k = 0; k < P.n_keys; ++k)
+            if (P.key_kind[k] == KK_BYTES && sp.key_col[k]) {
+                const Span s = key_span(sp, P, k, r.row);
+                if (s.n > BVAL_INLINE) mine += s.n - BVAL_INLINE;
+            }
+        for (uint32_t v = 0; v < P.n_vals; ++v)
+            if ((P.val_vc[v] == VC_VBYTES || P.val_vc[v] == VC_VLIST) && sp.val_col[v]) {
+                const Span s = val_span(sp, v, r.row);
+                if (s.n > BVAL_INLINE) mine += s.n - BVAL_INLINE;
+            }
+    }
+    for (int m = 32; m >= 1; m >>= 1) mine += (uint64_t)__shfl_xor((long long)mine, m);
+    if ((threadIdx.x & 63) == 0 && mine) atomicAdd(need, (unsigned long long)mine);
+}
+
+// Moves the tails of one row's BVAL keys / values from arena `from` to `to` (bump cursor),
+// rewriting the row's offsets
+__device__ __forceinline__ void move_tails(uint8_t *R, const AggParams &P, const uint8_t *__restrict__ from,
+                                           uint8_t *__restrict__ to, unsigned long long *__restrict__ cursor) {
+    const uint32_t kp = *(const uint32_t *)(R + 8), vp = *(const uint32_t *)(R + 12);
+    auto one = [&](uint8_t *slot) {
+        uint32_t *d = (uint32_t *)slot;
+        if (d[0] <= BVAL_INLINE) return;
+        const uint64_t n = d[0] - BVAL_INLINE;
+        const uint64_t off = atomicAdd(cursor, (unsigned long long)n);
+        for (uint64_t i = 0; i < n; ++i) to[off + i] = from[d[1] + i];
+        d[1] = (uint32_t)off;
+    };
+    for (uint32_t k = 0; k < P.n_keys; ++k)
+        if (P.key_kind[k] == KK_BYTES && ((kp >> k) & 1)) one(R + P.key_off[k]);
+    for (uint32_t v = 0; v < P.n_vals; ++v)
+        if ((P.val_vc[v] == VC_VBYTES || P.val_vc[v] == VC_VLIST) && ((vp >> v) & 1)) one(R + P.val_off[v]);
+}
+
+// output rows (k_agg_take) -> their tails gathered into one buffer the host copies out
+__global__ void k_agg_out_tails(uint8_t *__restrict__ out_rows, uint64_t n, const AggParams P,
+                                uint8_t *__restrict__ tails, unsigned long long *__restrict__ cursor) {
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n; g += (uint64_t)gridDim.x * blockDim.x)
+        move_tails(out_rows + g * P.row_bytes, P, P.arena, tails, cursor);
+}
+
+// arena compaction: the live rows' tails into a fresh arena (emitted groups' tails dropped)
+__global__ void k_agg_compact(const unsigned long long *__restrict__ tags, uint8_t *__restrict__ rows, uint64_t n_slots,
+                              const AggParams P, uint8_t *__restrict__ to, unsigned long long *__restrict__ cursor) {
+    for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < n_slots; g += (uint64_t)gridDim.x * blockDim.x)
+        if (tag_live(tags[g])) move_tails(rows + g * P.row_bytes, P, P.arena, to, cursor);
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
@@ -2150,6 +2396,13 @@ struct ngz_agg {
     unsigned long long *n_claims = nullptr;
     unsigned int *n_coll = nullptr;
     unsigned long long *used = nullptr;
+    // byte arena of BVAL tails (values longer than 32 bytes): bump-allocated by the kernels
+    // (arena_used[0]); arena_used[1] is the push's tail-byte bound (k_agg_tail_need).  arena_mark:
+    // the bytes in use after the last push (a failed push puts the counter back to it)
+    uint8_t *arena = nullptr;
+    uint64_t arena_cap = 0, arena_mark = 0;
+    unsigned long long *arena_used = nullptr;
+    std::vector<uint8_t> out_tails;  // tails of the rows last returned by flush / emit
     int64_t *cut = nullptr;         // per-peer window cutoffs of ngz_agg_closed / ngz_agg_emit
     uint32_t cut_cap = 0;
     uint32_t *rank_maps = nullptr;  // one 65536-bit map per VC_RANK sub-registry value
@@ -2204,8 +2457,7 @@ int reset_rows(ngz_agg *a, unsigned long long *tags, uint8_t *rows) {
 // Value class of (IE, op), following IE::supports_{arithmetic,comparison,bitwise}_ops
 // (generator.rs:1176-1272) for acceptance and the generated Field ops (generator.rs:580-629,
 // 896-1080) for the arithmetic.  Returns the value class or -1 (rejected by the reference's
-// validate_operation_compatibility, config.rs:212-250) or -2 (accepted there, not on the
-// device: why says which).
+// validate_operation_compatibility, config.rs:212-250).
 int value_class(const ngzh::IeRow *r, uint8_t op, std::string &why) {
     using namespace ngzh;
     const uint8_t dt = r ? r->dtype : DT_octetArray;  // IE::Unknown: octetArray
@@ -2229,19 +2481,10 @@ int value_class(const ngzh::IeRow *r, uint8_t op, std::string &why) {
             why = "field does not support comparison operations";
             return -1;
         }
-        if (dt == DT_basicList || dt == DT_subTemplateList || dt == DT_subTemplateMultiList) {
-            why = "list fields are variable-length (not on the device)";
-            return -2;
-        }
+        if (dt == DT_basicList || dt == DT_subTemplateList || dt == DT_subTemplateMultiList) return VC_VLIST;
         if (flt) return dt == DT_float32 ? VC_F32 : VC_F64;
         if (dt == DT_ipv6Address) return VC_IPV6;
-        if (tcp || subreg) {
-            if (subreg && !tcp && ngzh::subreg_kind(r->pen, r->id) != 1) {
-                why = "Min/Max over a nested reason-code sub-registry is not on the device";
-                return -2;
-            }
-            return VC_RANK;
-        }
+        if (tcp || subreg) return VC_RANK;  // nested sub-registries (forwardingStatus) get a rank table
         if (integer || dt == DT_ipv4Address || dt == DT_dateTimeSeconds) return sgn ? VC_SINT : VC_UINT;
         if (dt == DT_dateTimeMilliseconds) return VC_SINT;
         return VC_DTFRAC;
@@ -2254,13 +2497,17 @@ int value_class(const ngzh::IeRow *r, uint8_t op, std::string &why) {
         }
         // sub-registry enums OR their raw values (generator_sub_registries.rs: BitOrAssign)
         if (integer || dt == DT_boolean || dt == DT_ipv4Address) return VC_UINT;
-        return VC_BYTES;  // octetArray, macAddress, ipv6Address, unsigned256
+        // octetArray as Box<[u8]> (any length, IE::Unknown included); the MPLS label stacks are [u8; 3]
+        if (dt == DT_octetArray && !(r && (r->flags & 1))) return VC_VBYTES;
+        return VC_BYTES;  // macAddress, ipv6Address, unsigned256, MPLS label
     }
     why = "unknown op";
     return -1;
 }
 
-uint32_t value_slot_bytes(int vc) { return vc == VC_BYTES ? 32 : vc == VC_IPV6 ? 16 : 8; }
+uint32_t value_slot_bytes(int vc) {
+    return vc == VC_VBYTES || vc == VC_VLIST ? BVAL_BYTES : vc == VC_BYTES ? 32 : vc == VC_IPV6 ? 16 : 8;
+}
 
 // dictionary entry for value x (reusing a free position), or -1 when all SET_BITS / cap are used
 int dict_put(std::vector<int64_t> &d, int64_t x, uint32_t cap) {
@@ -2326,6 +2573,45 @@ int rehash(ngz_agg *a) {
     a->tags = ntags;
     a->rows = nrows;
     a->tombs = 0;
+    if (a->arena_mark) {
+        // the emitted groups' tails are garbage: move the live ones into a fresh arena
+        uint8_t *to = nullptr;
+        if (hipMalloc(&to, a->arena_cap) != hipSuccess) return NGZ_OK;  // keep the garbage (retried next time)
+        unsigned long long used = 0;
+        AGG_HIP(a, hipMemsetAsync(a->arena_used + 1, 0, 8, a->stream));
+        hipLaunchKernelGGL(k_agg_compact, dim3(grid_for(a->slots)), dim3(256), 0, a->stream, a->tags, a->rows, a->slots,
+                           a->P, to, a->arena_used + 1);
+        AGG_HIP(a, hipMemcpyAsync(&used, a->arena_used + 1, 8, hipMemcpyDeviceToHost, a->stream));
+        AGG_HIP(a, hipMemcpyAsync(a->arena_used, a->arena_used + 1, 8, hipMemcpyDeviceToDevice, a->stream));
+        AGG_HIP(a, hipStreamSynchronize(a->stream));
+        hipFree(a->arena);
+        a->arena = a->P.arena = to;
+        a->arena_mark = used;
+    }
+    return NGZ_OK;
+}
+
+// Byte arena: room for `need` more bytes after the ones in use (grown to at least twice its size,
+// the bytes in use moved over)
+int arena_reserve(ngz_agg *a, uint64_t need) {
+    if (a->arena_mark + need <= a->arena_cap) return NGZ_OK;
+    const uint64_t cap = std::max<uint64_t>({a->arena_mark + need, 2 * a->arena_cap, 1u << 20});
+    uint8_t *p = nullptr;
+    if (hipMalloc(&p, cap) != hipSuccess) return fail(a, NGZ_E_NOMEM, "byte arena");
+    if (a->arena_mark) AGG_HIP(a, hipMemcpyAsync(p, a->arena, a->arena_mark, hipMemcpyDeviceToDevice, a->stream));
+    AGG_HIP(a, hipStreamSynchronize(a->stream));
+    hipFree(a->arena);
+    a->arena = p;
+    a->arena_cap = cap;
+    a->P.arena = p;
+    a->P.arena_cap = cap;
+    return NGZ_OK;
+}
+
+// every group gone (flush / reset): the arena starts over
+int arena_clear(ngz_agg *a) {
+    a->arena_mark = 0;
+    AGG_HIP(a, hipMemsetAsync(a->arena_used, 0, 8, a->stream));
     return NGZ_OK;
 }
 
@@ -2345,7 +2631,8 @@ void finish_rows(ngz_agg *a, uint8_t *dst, int64_t n) {
             const int vc = a->P.val_vc[v];
             uint8_t *p = R + a->P.val_off[v];
             if (!(vp >> v & 1)) { memset(p, 0, value_slot_bytes(vc)); continue; }
-            if (vc == VC_BYTES || vc == VC_IPV6 || vc == VC_F32 || vc == VC_F64) continue;
+            if (vc == VC_BYTES || vc == VC_IPV6 || vc == VC_F32 || vc == VC_F64 || vc == VC_VBYTES || vc == VC_VLIST)
+                continue;
             uint64_t x;
             memcpy(&x, p, 8);
             const uint8_t op = a->P.val_op[v];
@@ -2379,9 +2666,30 @@ int64_t take_rows(ngz_agg *a, void *dst, uint64_t cap, const int64_t *cut, bool 
         AGG_HIP(a, hipMemsetAsync(a->cursor, 0, 8, a->stream));
         hipLaunchKernelGGL(k_agg_take, dim3(grid_for(a->slots)), dim3(256), 0, a->stream, a->tags, a->rows, a->slots, RB,
                            cut, tomb ? 1 : 0, tmp, a->cursor);
-        hipError_t e = hipMemcpyAsync(dst, tmp, (uint64_t)n * RB, hipMemcpyDeviceToHost, a->stream);
+        // byte values longer than 32 bytes: their tails gathered for the host (ngz_agg_row_bytes),
+        // the rows' offsets rewritten to point there
+        uint8_t *tails = nullptr;
+        unsigned long long nt = 0;
+        hipError_t e = hipSuccess;
+        a->out_tails.clear();
+        if (a->arena_mark) {
+            e = hipMalloc(&tails, a->arena_mark);
+            if (e == hipSuccess) e = hipMemsetAsync(a->arena_used + 1, 0, 8, a->stream);
+            if (e == hipSuccess) {
+                hipLaunchKernelGGL(k_agg_out_tails, dim3(grid_for(n)), dim3(256), 0, a->stream, tmp, (uint64_t)n, a->P,
+                                   tails, a->arena_used + 1);
+                e = hipMemcpyAsync(&nt, a->arena_used + 1, 8, hipMemcpyDeviceToHost, a->stream);
+            }
+            if (e == hipSuccess) e = hipStreamSynchronize(a->stream);
+            if (e == hipSuccess && nt) {
+                a->out_tails.resize(nt);
+                e = hipMemcpyAsync(a->out_tails.data(), tails, nt, hipMemcpyDeviceToHost, a->stream);
+            }
+        }
+        if (e == hipSuccess) e = hipMemcpyAsync(dst, tmp, (uint64_t)n * RB, hipMemcpyDeviceToHost, a->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(a->stream);
         hipFree(tmp);
+        hipFree(tails);
         if (e != hipSuccess) { a->poisoned = true; return fail(a, NGZ_E_DEVICE, hipGetErrorString(e)); }
         finish_rows(a, (uint8_t *)dst, (int64_t)n);
     }
@@ -2461,7 +2769,6 @@ int ngz_agg_create(int device, const ngz_agg_field *fields, uint32_t n_fields, u
         std::string why;
         const int vc = value_class(ngzh::ie_find(f.pen, f.ie_id), f.op, why);
         if (vc == -1) { delete a; return NGZ_E_INVALID; }
-        if (vc == -2) { delete a; return NGZ_E_LIMIT; }
         a->vals.push_back(f);
         vcs.push_back(vc);
     }
@@ -2478,8 +2785,8 @@ int ngz_agg_create(int device, const ngz_agg_field *fields, uint32_t n_fields, u
     P.n_vals = (uint32_t)a->vals.size();
     for (uint32_t k = 0; k < P.n_keys; ++k) {
         const ngzh::IeRow *r = ngzh::ie_find(a->keys[k].pen, a->keys[k].ie_id);
-        uint32_t slot = 32;
-        uint8_t kind = KK_OCTETS;
+        uint32_t slot = BVAL_BYTES;
+        uint8_t kind = KK_BYTES;  // IE::Unknown / vendor Unknown: raw bytes
         int fw = 0;  // packed-key eligibility: IEs whose column width is fixed by the Rust type (1/2/4/8 bytes)
         if (r) {
             kind = KK_FIXED;
@@ -2495,13 +2802,12 @@ int ngz_agg_create(int device, const ngz_agg_field *fields, uint32_t n_fields, u
             case ngzh::DT_macAddress: slot = 8; break;
             case ngzh::DT_ipv6Address: slot = 16; break;
             case ngzh::DT_unsigned256: slot = 32; break;
-            case ngzh::DT_string: slot = 32; kind = KK_STR; break;
-            default: slot = 36; kind = KK_OCTETS; break;  // octetArray (and MPLS sections): length + 32 bytes
+            case ngzh::DT_string: slot = BVAL_BYTES; kind = KK_BYTES; P.key_str |= 1u << k; break;
+            default: slot = BVAL_BYTES; kind = KK_BYTES; break;  // octetArray, lists: Box<[u8]>
             }
             if ((r->flags & 1) && r->dtype == ngzh::DT_octetArray) { slot = 4; kind = KK_FIXED; }  // [u8; 3]
-        } else {
-            slot = 36;  // IE::Unknown: raw bytes
         }
+        if (kind == KK_BYTES) P.has_bytes = 1;
         P.key_off[k] = off;
         P.key_slot[k] = slot;
         P.key_kind[k] = kind;
@@ -2518,6 +2824,7 @@ int ngz_agg_create(int device, const ngz_agg_field *fields, uint32_t n_fields, u
         P.val_vc[v] = (uint8_t)vcs[v];
         P.val_tcp[v] = vcs[v] == VC_RANK && r && (r->flags & 2);
         ranks = ranks || (vcs[v] == VC_RANK && !P.val_tcp[v]);
+        if (vcs[v] == VC_VBYTES || vcs[v] == VC_VLIST) P.has_bytes = 1;
         off += value_slot_bytes(vcs[v]);
     }
     // whole 128-byte lines: a row at a random slot then touches ceil(row/128) lines, not one
@@ -2612,14 +2919,24 @@ int ngz_agg_create(int device, const ngz_agg_field *fields, uint32_t n_fields, u
         hipMalloc(&a->newdom, NEWDOM_SLOTS * 8) != hipSuccess || hipMalloc(&a->err, 4) != hipSuccess ||
         hipMalloc(&a->late, 8) != hipSuccess || hipMalloc(&a->cursor, 8) != hipSuccess ||
         hipMalloc(&a->n_claims, 8) != hipSuccess || hipMalloc(&a->n_coll, 4) != hipSuccess ||
-        hipMalloc(&a->used, 32) != hipSuccess)
+        hipMalloc(&a->used, 32) != hipSuccess || hipMalloc(&a->arena_used, 16) != hipSuccess)
         return bail(NGZ_E_NOMEM, "hipMalloc (group table)");
+    hipMemset(a->arena_used, 0, 16);
+    P.arena_used = a->arena_used;
     if (ranks) {
         // sub-registry ranks: which values are registered variants (known bitmap per value)
         if (hipMalloc(&a->rank_maps, (size_t)P.n_vals * 8192) != hipSuccess) return bail(NGZ_E_NOMEM, "hipMalloc (ranks)");
         std::vector<uint32_t> map(2048);
         for (uint32_t v = 0; v < P.n_vals; ++v) {
             if (P.val_vc[v] != VC_RANK || P.val_tcp[v]) continue;
+            uint64_t nested[257];
+            if (ngzh::subreg_nested_ranks(a->vals[v].pen, a->vals[v].ie_id, nested)) {
+                // the 8 KB map slot holds the 257 ranks of a nested sub-registry instead
+                unsigned long long *dst = (unsigned long long *)(a->rank_maps + (size_t)v * 2048);
+                hipMemcpy(dst, nested, sizeof nested, hipMemcpyHostToDevice);
+                P.rank_nested[v] = dst;
+                continue;
+            }
             std::fill(map.begin(), map.end(), 0u);
             for (uint32_t x = 0; x < 65536; ++x)
                 if (ngzh::subreg_known(a->vals[v].pen, a->vals[v].ie_id, x)) map[x >> 5] |= 1u << (x & 31);
@@ -2652,6 +2969,8 @@ void ngz_agg_destroy(ngz_agg *a) {
     hipFree(a->n_claims);
     hipFree(a->n_coll);
     hipFree(a->used);
+    hipFree(a->arena);
+    hipFree(a->arena_used);
     hipFree(a->cut);
     hipFree(a->rank_maps);
     hipFree(a->plans);
@@ -2770,6 +3089,7 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, const ngz_p
         memset(&sp, 0, sizeof sp);
         const ngz_slot_info &si = out->slots[s];
         sp.proto = si.proto;
+        sp.bytes = ctx->last_in.bytes;
         if (!si.n_records || !si.columns) continue;
         const int nf = ngz_slot_fields(ctx, s, nullptr, 0);
         if (nf < 0) { restore(); return fail(a, NGZ_E_INVALID, "ngz_slot_fields"); }
@@ -2794,12 +3114,21 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, const ngz_p
             const int i = find_field(a->keys[k]);
             if (i < 0) continue;
             const ngz_field_info &f = fi[i];
+            if (a->P.key_kind[k] == KK_BYTES) {
+                // any length, fixed or variable-length (a record's text / bytes, BVAL)
+                if (f.kind == NGZ_K_FAIL) { restore(); return fail(a, NGZ_E_LIMIT, "key field of a failing template"); }
+                if (f.kind == NGZ_K_VLEN) sp.key_vlen |= 1u << k;
+                sp.key_col[k] = si.columns + (uint64_t)si.capacity * f.col_off;
+                sp.key_w[k] = f.width;
+                if (a->key_w[k] < 0) a->key_w[k] = f.width;
+                if (a->key_kind_seen[k] < 0) a->key_kind_seen[k] = f.kind;
+                continue;
+            }
             if (f.kind == NGZ_K_VLEN || f.kind == NGZ_K_FAIL) {
                 restore();
-                return fail(a, NGZ_E_LIMIT, "variable-length key field (not on the device)");
+                return fail(a, NGZ_E_LIMIT, "fixed-size key field sent variable-length (its records fail to decode)");
             }
-            const uint32_t room = a->P.key_slot[k] - (a->P.key_kind[k] == KK_OCTETS ? 4 : 0);
-            if (f.width > room) { restore(); return fail(a, NGZ_E_LIMIT, "key field wider than its row slot"); }
+            if (f.width > a->P.key_slot[k]) { restore(); return fail(a, NGZ_E_LIMIT, "key field wider than its row slot"); }
             if (a->P.packed && f.width != a->P.key_pw[k]) {
                 restore();
                 return fail(a, NGZ_E_LIMIT, "key column width differs from the IE's width");
@@ -2814,9 +3143,18 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, const ngz_p
             if (i < 0) continue;
             const ngz_field_info &f = fi[i];
             const int vc = a->P.val_vc[v];
+            if ((vc == VC_VBYTES || vc == VC_VLIST) && f.kind != NGZ_K_FAIL) {
+                // Box<[u8]> values: any length, fixed or variable-length (BVAL)
+                if (f.kind == NGZ_K_VLEN) sp.val_vlen |= 1u << v;
+                if (a->val_w[v] < 0) a->val_w[v] = f.width;
+                if (a->val_kind_seen[v] < 0) a->val_kind_seen[v] = f.kind;
+                sp.val_col[v] = si.columns + (uint64_t)si.capacity * f.col_off;
+                sp.val_w[v] = f.width;
+                continue;
+            }
             if (f.kind == NGZ_K_VLEN || f.kind == NGZ_K_FAIL || (vc == VC_BYTES && f.width > 32)) {
                 restore();
-                return fail(a, NGZ_E_LIMIT, "aggregated field is variable-length or wider than 32 bytes");
+                return fail(a, NGZ_E_LIMIT, "fixed-size aggregated field sent variable-length (its records fail to decode)");
             }
             const bool int_like = vc == VC_UINT || vc == VC_SINT || vc == VC_RANK;
             if ((int_like && f.width != 1 && f.width != 2 && f.width != 4 && f.width != 8) ||
@@ -2956,6 +3294,8 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, const ngz_p
     auto rollback = [&](int rc, const std::string &why) {
         if (n_claims)
             hipLaunchKernelGGL(k_agg_unclaim, dim3(grid_for(n_claims)), dim3(256), 0, st, a->tags, claims, (uint64_t)n_claims);
+        if (P.has_bytes)  // the released claims' key tails: the arena as after the last push
+            hipMemcpyAsync(a->arena_used, &a->arena_mark, 8, hipMemcpyHostToDevice, st);
         restore();
         upload_domains(a);
         if (hipStreamSynchronize(st) != hipSuccess) a->poisoned = true;
@@ -3043,6 +3383,18 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, const ngz_p
     hipLaunchKernelGGL(k_agg_recinfo, dim3(grid_for(64ull * NS, 256, 4096)), dim3(256), 0, st, sets, rstart, NS, hdr,
                        dginfo, a->plans, D, S, rinfo, a->err);
     AGG_HIP(a, hipGetLastError());
+    if (P.has_bytes && n_rec) {
+        // byte values longer than 32 bytes: room in the arena for every tail this push can write
+        // (key claims and ordered folds write at most one record's per group and field)
+        unsigned long long need = 0;
+        AGG_HIP(a, hipMemsetAsync(a->arena_used + 1, 0, 8, st));
+        hipLaunchKernelGGL(k_agg_tail_need, dim3(grid_for(n_rec, 256, 4096)), dim3(256), 0, st, C, P, a->arena_used + 1);
+        AGG_HIP(a, hipMemcpyAsync(&need, a->arena_used + 1, 8, hipMemcpyDeviceToHost, st));
+        AGG_HIP(a, hipStreamSynchronize(st));
+        if (int r = arena_reserve(a, need)) { restore(); upload_domains(a); return r; }
+        P.arena = a->P.arena;
+        P.arena_cap = a->P.arena_cap;
+    }
     // claim / check keep no state across tiles: one record per thread, all of them in flight
     const uint32_t fg = std::max<uint32_t>(1, std::min<uint32_t>(blocks, 1u << 20));
     if (n_rec) {
@@ -3171,10 +3523,21 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, const ngz_p
 done:
     AGG_HIP(a, hipEventRecord(a->ev1, st));
     uint32_t last_pm = 0;
-    unsigned long long late = 0;
+    unsigned long long late = 0, arena_now = a->arena_mark;
     AGG_HIP(a, hipMemcpyAsync(&last_pm, pm + (D - 1), 4, hipMemcpyDeviceToHost, st));
     AGG_HIP(a, hipMemcpyAsync(&late, a->late, 8, hipMemcpyDeviceToHost, st));
+    if (P.has_bytes) {
+        AGG_HIP(a, hipMemcpyAsync(&arena_now, a->arena_used, 8, hipMemcpyDeviceToHost, st));
+        AGG_HIP(a, hipMemcpyAsync(&errv, a->err, 4, hipMemcpyDeviceToHost, st));
+    }
     AGG_HIP(a, hipStreamSynchronize(st));
+    if (P.has_bytes) {
+        a->arena_mark = arena_now;
+        if (errv & 64) {  // cannot happen: the push reserved every tail it writes
+            a->poisoned = true;
+            return fail(a, NGZ_E_DEVICE, "byte arena overrun");
+        }
+    }
     hipEventElapsedTime(&a->t_push, a->ev0, a->ev1);
     a->live += n_claims;
     if (last_pm > a->peer_time[pi]) a->peer_time[pi] = last_pm;
@@ -3201,6 +3564,7 @@ int64_t ngz_agg_flush(ngz_agg *a, void *dst, uint64_t cap) {
     a->live = a->tombs = 0;
     int rc = reset_rows(a, a->tags, a->rows);
     if (rc == NGZ_OK) rc = upload_domains(a);
+    if (rc == NGZ_OK) rc = arena_clear(a);
     if (rc != NGZ_OK) return rc;
     AGG_HIP(a, hipStreamSynchronize(a->stream));
     return n;
@@ -3256,6 +3620,7 @@ int ngz_agg_reset(ngz_agg *a) {
     a->live = a->tombs = 0;
     int rc = reset_rows(a, a->tags, a->rows);
     if (rc == NGZ_OK) rc = upload_domains(a);
+    if (rc == NGZ_OK) rc = arena_clear(a);
     if (rc != NGZ_OK) return rc;
     AGG_HIP(a, hipStreamSynchronize(a->stream));
     return NGZ_OK;
@@ -3297,6 +3662,28 @@ int ngz_agg_value_info(ngz_agg *a, uint32_t v, ngz_agg_value_desc *out) {
     out->width = (uint16_t)std::max(a->val_w[v], 0);
     out->kind = (uint8_t)std::max(a->val_kind_seen[v], 0);
     return NGZ_OK;
+}
+
+int64_t ngz_agg_row_bytes(ngz_agg *a, const void *row, int is_value, uint32_t index, uint8_t *dst, uint64_t cap) {
+    if (!a || !row) return NGZ_E_INVALID;
+    uint32_t off;
+    if (is_value) {
+        if (index >= a->P.n_vals || (a->P.val_vc[index] != VC_VBYTES && a->P.val_vc[index] != VC_VLIST))
+            return NGZ_E_INVALID;
+        off = a->P.val_off[index];
+    } else {
+        if (index >= a->P.n_keys || a->P.key_kind[index] != KK_BYTES) return NGZ_E_INVALID;
+        off = a->P.key_off[index];
+    }
+    const uint8_t *slot = (const uint8_t *)row + off;
+    uint32_t n, toff;
+    memcpy(&n, slot, 4);
+    memcpy(&toff, slot + 4, 4);
+    if (n > BVAL_INLINE && (uint64_t)toff + (n - BVAL_INLINE) > a->out_tails.size()) return NGZ_E_INVALID;
+    if (dst)
+        for (uint64_t i = 0; i < n && i < cap; ++i)
+            dst[i] = i < BVAL_INLINE ? slot[8 + i] : a->out_tails[toff + i - BVAL_INLINE];
+    return (int64_t)n;
 }
 
 int ngz_agg_key_info(ngz_agg *a, uint32_t k, ngz_agg_key_desc *out) {

@@ -56,6 +56,8 @@ const char *vendor_name(uint32_t pen);
 int subreg_kind(uint32_t pen, uint16_t id);
 // is v a registered variant of the IE's sub-registry enum
 bool subreg_known(uint32_t pen, uint16_t id, uint64_t v);
+// ranks of values 0..255 (+ [256] for larger ones) in the Ord of a nested sub-registry's enum (ngz_json.cpp)
+bool subreg_nested_ranks(uint32_t pen, uint16_t id, uint64_t rank[257]);
 
 // ------------------------------------------------------------------------
 // Template model

@@ -478,6 +478,34 @@ int subreg_kind(uint32_t pen, uint16_t id) {
     return r ? (r->nested ? 2 : 1) : 0;
 }
 
+// Rank of the values 0..255 of a nested sub-registry (forwardingStatus) in the derived Ord of its
+// enum (generator_sub_registries.rs:96-140): the outer variant (one per 64-value group, declared in
+// group order, then Unassigned), then the reason enum's discriminant (a registered reason is its
+// value, its Unassigned(x) the last registered value + 1), then the value: rank = outer << 56 |
+// discriminant << 32 | value.  rank[256] is the outer Unassigned's (values from 256 OR into it).
+bool subreg_nested_ranks(uint32_t pen, uint16_t id, uint64_t rank[257]) {
+    const SubReg *r = subreg_find(pen, id);
+    if (!r || !r->nested) return false;
+    for (uint64_t x = 0; x < 256; ++x) {
+        const uint64_t gi = x / 64;
+        if (gi >= r->count) {
+            rank[x] = ((uint64_t)r->count << 56) | x;
+            continue;
+        }
+        const SubGroup &g = kSubGroups[r->first + gi];
+        uint64_t disc = 0;  // an enum with no registered reason: Unassigned is its only variant
+        bool known = false;
+        for (uint32_t i = g.first; i < g.first + g.count; ++i) {
+            if (kSubVals[i].v == x) known = true;
+            disc = kSubVals[i].v + 1;  // implicit discriminant after the last declared one
+        }
+        if (known) disc = x;
+        rank[x] = ((uint64_t)gi << 56) | (disc << 32) | x;
+    }
+    rank[256] = (uint64_t)r->count << 56;
+    return true;
+}
+
 bool subreg_known(uint32_t pen, uint16_t id, uint64_t v) {
     const SubReg *r = subreg_find(pen, id);
     if (!r || r->nested) return false;
@@ -518,6 +546,28 @@ void put_cell(std::string &o, uint32_t pen, uint16_t id, uint8_t kind, uint16_t 
     fd.kind = kind;
     fd.width = width;
     put_field(o, spec_of(pen, id), fd, cell, nullptr);
+}
+
+// a byte value of any length (BVAL keys / values): rendered as the decode path renders a
+// variable-length field of the IE (string text, or the bytes as a list)
+void put_bytes(std::string &o, uint32_t pen, uint16_t id, const std::vector<uint8_t> &b) {
+    const Spec s = spec_of(pen, id);
+    DevField fd{};
+    fd.kind = NGZ_K_VLEN;
+    fd.width = 16;
+    fd.flags = s.dtype == DT_string ? 0x80 : 0;
+    uint8_t cell[16] = {};
+    const uint32_t n = (uint32_t)b.size();
+    memcpy(cell + 8, &n, 4);
+    put_field(o, s, fd, cell, b.data());
+}
+
+// the whole byte value of a row's BVAL key / value
+std::vector<uint8_t> row_bytes(ngz_agg *a, const uint8_t *R, int is_value, uint32_t i) {
+    const int64_t n = ngz_agg_row_bytes(a, R, is_value, i, nullptr, 0);
+    std::vector<uint8_t> b(n > 0 ? (size_t)n : 0);
+    if (n > 0) ngz_agg_row_bytes(a, R, is_value, i, b.data(), b.size());
+    return b;
 }
 
 }  // namespace
@@ -567,12 +617,8 @@ extern "C" int64_t ngz_agg_flowinfo_json(ngz_agg *a, const void *rows, uint64_t 
             if (!(h.key_present >> k & 1)) continue;
             sep();
             const uint8_t *c = R + ko[k];
-            if (kd[k].kkind == 2) {  // octet array: length, bytes
-                uint32_t len;
-                memcpy(&len, c, 4);
-                put_cell(o, keys[k].pen, keys[k].ie_id, NGZ_K_BYTES, (uint16_t)len, c + 4);
-            } else if (kd[k].kkind == 1) {
-                put_cell(o, keys[k].pen, keys[k].ie_id, NGZ_K_STR, kd[k].slot, c);
+            if (kd[k].kkind == 3) {  // a byte value of any length
+                put_bytes(o, keys[k].pen, keys[k].ie_id, row_bytes(a, R, 0, k));
             } else {
                 put_cell(o, keys[k].pen, keys[k].ie_id, kd[k].kind, kd[k].width, c);
             }
@@ -595,6 +641,8 @@ extern "C" int64_t ngz_agg_flowinfo_json(ngz_agg *a, const void *rows, uint64_t 
             case 5: put_cell(o, vals[v].pen, vals[v].ie_id, NGZ_K_UINT, 4, c); break;
             case 6: put_cell(o, vals[v].pen, vals[v].ie_id, NGZ_K_UINT, 8, c); break;
             case 7: put_cell(o, vals[v].pen, vals[v].ie_id, NGZ_K_BYTES, 16, c); break;
+            case 8:
+            case 9: put_bytes(o, vals[v].pen, vals[v].ie_id, row_bytes(a, R, 1, v)); break;
             default: put_cell(o, vals[v].pen, vals[v].ie_id, vd[v].kind, vd[v].width, c); break;
             }
         }

@@ -90,6 +90,17 @@ def _rank(ie, v):
     if ie.subreg is not None and ie.subreg["kind"] == "vnd":
         known = {val for val, _ in ie.subreg["entries"]}
         return v if v in known else (1 << 32) | v  # Unassigned(x) after every registered variant
+    if ie.subreg is not None and ie.subreg["kind"] == "nested":
+        # forwardingStatus (generator_sub_registries.rs:96-140): one outer variant per 64-value
+        # group in declaration order, then Unassigned(x); inside a group the reason enum's
+        # discriminant (a registered reason is its value, its Unassigned(x) the last declared
+        # value + 1 -- Rust's implicit discriminant), then the value
+        groups = ie.subreg["entries"]
+        gi = v // 64
+        if gi >= len(groups):
+            return (len(groups), 0, v)
+        reasons = [rv for rv, _ in groups[gi][2]]
+        return (gi, v if v in reasons else (reasons[-1] + 1 if reasons else 0), v)
     return v
 
 

@@ -43,8 +43,9 @@ def test_agg_config_validation_without_device():
     device call (config.rs:107-119, 212-250) with IE::supports_{arithmetic,comparison,bitwise}_ops
     (generator.rs:1176-1272): the reference's accept / reject table, row by row.  Accepted
     configs go on to the device (no GPU here: NGZ_E_DEVICE / NGZ_E_NOMEM); rejected ones
-    return NGZ_E_INVALID; the two the reference accepts but the device does not run return
-    NGZ_E_LIMIT."""
+    return NGZ_E_INVALID.  Every accepted config runs on the device: Min / Max over lists
+    (Box<[u8]> order) and over forwardingStatus's nested reason codes, octet-array ORs and
+    string / octet / list keys of any length included (no NGZ_E_LIMIT row is left)."""
     from netgauze_amd import _lib
     lib = _lib.load()
     A = _lib.AggField
@@ -87,8 +88,10 @@ def test_agg_config_validation_without_device():
         ((0, 82), MIN, REJECT),     # string
         ((0, 70), MAX, REJECT),     # octetArray
         ((0, 515), MIN, REJECT),    # unsigned256
-        ((0, 291), MIN, LIMIT),     # basicList: accepted, variable-length
-        ((0, 89), MAX, LIMIT),      # forwardingStatus: nested reason-code sub-registry
+        ((0, 291), MIN, ACCEPT),    # basicList: Box<[u8]> lexicographic order
+        ((0, 292), MAX, ACCEPT),    # subTemplateList
+        ((0, 293), MIN, ACCEPT),    # subTemplateMultiList
+        ((0, 89), MAX, ACCEPT),     # forwardingStatus: nested reason-code sub-registry order
         # bitwise
         ((0, 6), OR, ACCEPT),       # tcpControlBits
         ((0, 4), OR, ACCEPT),       # protocolIdentifier: BitOrAssign of the raw values
@@ -96,12 +99,17 @@ def test_agg_config_validation_without_device():
         ((0, 27), OR, ACCEPT),      # ipv6Address
         ((0, 276), OR, ACCEPT),     # boolean
         ((0, 515), OR, ACCEPT),     # unsigned256
-        ((0, 70), OR, ACCEPT),      # octetArray
+        ((0, 70), OR, ACCEPT),      # mplsTopLabelStackSection: [u8; 3]
+        ((0, 210), OR, ACCEPT),     # paddingOctets: octetArray of any length
         ((0, 311), OR, REJECT),     # float64
         ((0, 82), OR, REJECT),      # string
         ((0, 150), OR, REJECT),     # dateTimeSeconds
         ((0, 292), OR, REJECT),     # subTemplateList
     ]
+    # key fields of every kind are accepted: strings, octet arrays, lists, unknown IEs
+    for key in [(0, 82), (0, 236), (0, 210), (0, 291), (2011, 1000), (213, 5)]:
+        assert create([key + (0, _lib.NGZ_AGG_KEY), (0, 1, 0, ADD)]) in (-2, -3, 0), key
+    assert LIMIT not in {v for _, _, v in table}
     for (pen, ie), op, verdict in table:
         rc = create([(pen, ie, 0, op)])
         if verdict == ACCEPT:

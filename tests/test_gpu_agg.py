@@ -237,15 +237,10 @@ GOLDEN_AGG_PACKED = [(0, 4, 0, OK), (0, 7, 0, OK), (0, 1, 0, ADD), (0, 2, 0, ADD
 def test_reference_captures(dev, name, fields):
     """Every reference capture, per exporter peer (IPFIX and NetFlow v9, options data,
     several templates and observation domains), in two batches."""
-    from netgauze_amd.aggregate import AggError
     sel = GOLDEN_AGG if fields == "wide" else GOLDEN_AGG_PACKED
     for key, dgrams in peers_of(name).items():
         h = len(dgrams) // 2
-        try:
-            check(sel, [dgrams[:h], dgrams[h:]], port=key[1], lateness_s=60)
-        except AggError as e:
-            # selected fields that are variable-length in some template are not on the device yet
-            assert "variable-length" in str(e), e
+        check(sel, [dgrams[:h], dgrams[h:]], port=key[1], lateness_s=60)
 
 
 def test_wave_preaggregation_bytes_and_presence(dev):
@@ -675,6 +670,116 @@ def test_thousand_peers_one_aggregator(dev):
         same_groups(got, ref)
         emitted += len(got)
     assert emitted > 0 and len({g["peer"] for g in ref}) > 1
+    same_groups(agg.flush(), o.flush())
+
+
+# ---- byte values of any length (BVAL): string / octet-array / list keys and values, fixed or
+# variable-length on the wire, longer than 32 bytes included (the tail in the byte arena) ----
+HUAWEI_BYTES = [(0, 497, 0, OK), (0, 236, 0, OK), (0, 1, 0, ADD), (0, 2, 0, ADD), (0, 210, 0, OR), (0, 210, 1, OR),
+                (2011, 704, 0, OR), (2011, 232, 0, OR), (0, 90, 0, OR)]
+SRV6_BYTES = [(0, 84, 0, OK), (0, 82, 0, OK), (0, 83, 0, OK), (0, 236, 0, OK), (0, 1, 0, ADD), (0, 90, 0, OR),
+              (0, 2, 0, ADD)]
+
+
+@pytest.mark.parametrize("name,fields", [("106-IPFIXv10-HUAWEI-vrf_name__traffic-00", HUAWEI_BYTES),
+                                         ("srv6__srv6", SRV6_BYTES)])
+def test_byte_keys_and_values_on_captures(dev, name, fields):
+    """the Huawei 106 capture keyed on its variable-length SRv6 segment list
+    (srhSegmentIPv6ListSection) and VRF name, with octet-array ORs over paddingOctets (declared
+    3 and 1 bytes wide in two templates: the group keeps its first value's length), Huawei
+    vendor-unknown fields and the route distinguisher; the srv6 capture keyed on its 90-byte
+    samplerName and 64-byte interface name / description (tails beyond 32 bytes in the arena)
+    and VRF name.  Per peer, two pushes, equal to the oracle (aggregator.rs:123, 286-354)."""
+    long_keys = 0
+    for key, dgrams in peers_of(name).items():
+        h = len(dgrams) // 2
+        groups = check(fields, [dgrams[:h], dgrams[h:]], port=key[1], lateness_s=60)
+        long_keys += sum(1 for g in groups for x in g["key"] if isinstance(x, (bytes, str)) and len(x) > 32)
+    assert long_keys > 0
+
+
+def _vlen(b):
+    return (bytes([len(b)]) if len(b) < 255 else b"\xff" + len(b).to_bytes(3, "big")) + b
+
+
+def byte_value_stream(n_msgs, per_msg, seed=11, t0=1_700_000_000, step=20):
+    """Three templates sending the same fields at different wire forms: VRFname (236) fixed 16 /
+    fixed 48 / variable-length, forwardingStatus (89) 1 / 4 / 1 bytes, basicList (291) and
+    subTemplateList (292) variable-length or fixed, applicationId (95) variable-length / fixed 6."""
+    import random
+    rnd = random.Random(seed)
+    names = [b"red", b"blue", b"", b"a-vrf-name-that-is-longer-than-thirty-two-bytes", b"red\0tail",
+             b"x" * 300, "gr\u00fcn".encode()]
+    fwd = [0, 3, 64, 66, 68, 69, 100, 128, 143, 150, 192, 195, 200, 255]
+    t1 = [(8, 4), (236, 16), (1, 8), (89, 1), (291, 0xFFFF), (95, 0xFFFF)]
+    t2 = [(8, 4), (236, 48), (1, 8), (89, 4), (291, 20), (95, 6)]
+    t3 = [(8, 4), (236, 0xFFFF), (1, 8), (89, 1), (292, 0xFFFF), (95, 0xFFFF)]
+    msgs = [ipfix_msg([tset(600, t1), tset(601, t2), tset(602, t3)], t0)]
+    for m in range(n_msgs):
+        tid = 600 + m % 3
+        recs = []
+        for _ in range(per_msg):
+            nm = rnd.choice(names)
+            blob = bytes(rnd.getrandbits(8) for _ in range(rnd.choice([0, 3, 20, 33, 70])))
+            app = bytes(rnd.getrandbits(8) for _ in range(rnd.choice([2, 6, 40])))
+            r = struct.pack(">I", rnd.choice([1, 2])) if tid != 601 else struct.pack(">I", rnd.choice([1, 2, 3]))
+            if tid == 600:
+                r += nm[:16].ljust(16, b"\0") if b"\0" not in nm[:16] else nm[:16].ljust(16, b"\0")
+            elif tid == 601:
+                r += nm[:48].ljust(48, b"\0")
+            else:
+                r += _vlen(nm)
+            r += struct.pack(">Q", rnd.getrandbits(40))
+            f = rnd.choice(fwd)
+            r += struct.pack(">I", f) if tid == 601 else bytes([f])
+            r += _vlen(blob) if tid != 601 else blob[:20].ljust(20, b"\1")
+            r += _vlen(app) if tid != 601 else app[:6].ljust(6, b"\0")
+            recs.append(r)
+        msgs.append(ipfix_msg([dset(tid, recs)], t0 + step * (m // 3), seq=m + 2))
+    return msgs
+
+
+def test_byte_values_synthetic(dev):
+    """String keys that are one key at every wire form (fixed 16, fixed 48 and variable-length:
+    the text up to the first NUL of a fixed cell, a variable-length one as sent, so "red\\0tail"
+    sent variable-length is its own key), keys of 0 to 300 bytes; Min / Max over basicList and
+    subTemplateList (Box<[u8]> order), octet-array OR of 2 to 40 bytes (the group keeps its first
+    value's length), forwardingStatus Min / Max in its nested reason-code order -- over pushes whose
+    windows close, against the oracle."""
+    d = byte_value_stream(30, 40)
+    fields = [(0, 236, 0, OK), (0, 8, 0, OK), (0, 1, 0, ADD), (0, 89, 0, MX), (0, 291, 0, MN), (0, 292, 0, MX),
+              (0, 95, 0, OR)]
+    groups = check(fields, [d[:9], d[9:20], d[20:]], lateness_s=10)
+    keys = {g["key"][0] for g in groups}
+    assert {"red", "red\0tail", "", "x" * 300} <= keys, sorted(k[:8] for k in keys if k)
+    fields2 = [(0, 8, 0, OK), (0, 89, 0, MN), (0, 291, 0, MX), (0, 292, 0, MN), (0, 1, 0, ADD)]
+    check(fields2, [d[:15], d[15:]], lateness_s=10)
+
+
+def test_long_byte_keys_through_table_rebuilds(dev):
+    """Keys longer than 32 bytes over 24 pushes whose windows close push by push: the emitted
+    groups' tails become garbage and the table rebuild (tombstones) compacts the byte arena;
+    every push's emitted windows equal the oracle's, and so does the final flush."""
+    from netgauze_amd.aggregate import FlowAggregator
+    from netgauze_amd.flow import FlowInfoCodec
+    import ngz_oracle as O
+    fields = [(0, 82, 0, OK), (0, 1, 0, ADD)]
+    agg = FlowAggregator(fields, capacity=2000, lateness_s=0)
+    o = A.FlowAggregatorOracle(fields, 60, 0)
+    codec, oc = FlowInfoCodec(), O.FlowInfoCodec()
+    tpl = [(82, 0xFFFF), (1, 8)]
+    out = 0
+    for step in range(24):
+        recs = [_vlen(("interface-%06d-of-step-%02d-with-a-long-name" % (j, step)).encode()) +
+                struct.pack(">Q", j + 1) for j in range(900)]
+        d = [ipfix_msg(([tset(256, tpl)] if step == 0 else []) + [dset(256, recs[i:i + 300])],
+                       1_700_000_000 + 60 * step) for i in range(0, 900, 300)]
+        agg.push(codec.decode_datagrams(d))
+        A.aggregate_datagrams(fields, d, agg=o, codec=oc)
+        got = agg.emit()
+        same_groups(got, o.emit())
+        out += len(got)
+    assert out == 23 * 900
     same_groups(agg.flush(), o.flush())
 
 

@@ -108,6 +108,30 @@ def test_float_and_enum_orders():
     assert A.reduce_value(tcp, A.OP_MIN, 0x02, 0x01) == 0x02  # {SYN} < {FIN}
 
 
+def test_nested_and_byte_orders():
+    """forwardingStatus (nested reason codes, generator_sub_registries.rs:96-140): the outer
+    variant per 64-value group, then the reason enum's discriminant (Unassigned(x) = last
+    declared reason + 1), then x; values from 256 are the outer Unassigned(x), after every
+    group.  Box<[u8]> (lists) order lexicographically, a prefix first; octet-array OR keeps
+    the group's length (zip)."""
+    import ngz_oracle as O
+    fwd = O.REGISTRY.lookup(0, 89)
+    assert fwd.subreg["kind"] == "nested"
+    mn = lambda a, b: A.reduce_value(fwd, A.OP_MIN, a, b)  # noqa: E731
+    mx = lambda a, b: A.reduce_value(fwd, A.OP_MAX, a, b)  # noqa: E731
+    assert mn(69, 68) == 68          # Forwarded: reason 68 < Unassigned(69)
+    assert mn(100, 128) == 100       # Forwarded(..) < Dropped(..)
+    assert mx(300, 255) == 300       # Unassigned(300) after Consumed(Unassigned(255))
+    assert mn(3, 64) == 3            # Unknown(Unassigned(3)) < Forwarded(Unknown)
+    assert mx(144, 143) == 144       # Dropped: Unassigned(144) > Hardware (143)
+    blist = O.REGISTRY.lookup(0, 291)
+    assert A.reduce_value(blist, A.OP_MIN, b"\x01\x02", b"\x01") == b"\x01"      # a prefix is less
+    assert A.reduce_value(blist, A.OP_MAX, b"\x02", b"\x01\xff\xff") == b"\x02"  # first byte decides
+    octets = O.REGISTRY.lookup(0, 210)
+    assert A.reduce_value(octets, A.OP_OR, b"\x01\x00", b"\x10\x20\x30") == b"\x11\x20"
+    assert A.reduce_value(octets, A.OP_OR, b"\x01\x00\x00", b"\x02") == b"\x03\x00\x00"
+
+
 def run_oracle_scenario(sc):
     """Pushes of a kats_agg scenario through the oracle (one codec per peer address, one shard)."""
     import ngz_oracle as O
