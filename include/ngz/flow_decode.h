@@ -196,6 +196,16 @@ int ngz_decode_batch_host(ngz_ctx *ctx, const uint8_t *bytes, uint64_t bytes_siz
  * 0 the generic kernel, 2 the generic kernel while its own compiles. */
 int ngz_slot_kernel(ngz_ctx *ctx, uint32_t slot);
 
+/* How the last batch ran (bits): NGZ_BATCH_PREDICTED decode launched without a host round trip
+ * (steady state), NGZ_BATCH_SPLIT split framing (the record walk of variable-length sets on a
+ * second stream beside the fixed-length sets' framing and decode), NGZ_BATCH_RERUN a pass was
+ * repeated (buffer growth, a template slot without a count row, a record error split framing
+ * went past).  Returns the bits, or NGZ_E_INVALID. */
+#define NGZ_BATCH_PREDICTED 1
+#define NGZ_BATCH_SPLIT 2
+#define NGZ_BATCH_RERUN 4
+int ngz_last_batch_info(ngz_ctx *ctx);
+
 /* Column layout of a batch slot (valid with the last batch). */
 int ngz_slot_fields(ngz_ctx *ctx, uint32_t slot, ngz_field_info *fields, uint32_t cap);
 

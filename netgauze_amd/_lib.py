@@ -22,8 +22,10 @@ ABI_FUNCTIONS = [
     "ngz_templates_json", "ngz_template_counts", "ngz_last_timing", "ngz_ctx_set_option",
     "ngz_template_kernel", "ngz_group_kernel", "ngz_columns_to_host", "ngz_dgram_json", "ngz_batch_json",
     "ngz_dgram_error", "ngz_template_counts_device", "ngz_slot_kernel", "ngz_rtc_drain", "ngz_abi_version",
+    "ngz_last_batch_info",
 ]
 NGZ_ABI_VERSION = 3
+NGZ_BATCH_PREDICTED, NGZ_BATCH_SPLIT, NGZ_BATCH_RERUN = 1, 2, 4  # ngz_last_batch_info
 NGZ_AGG_ABI_VERSION = 3
 # ngz_error.kind / .layer (flow_decode.h)
 ERR_KINDS = ["NONE", "UNSUPPORTED_VERSION", "INVALID_LENGTH", "UNEXPECTED_EOF", "INVALID_PADDING_LENGTH",
@@ -215,6 +217,8 @@ def load():
     lib.ngz_batch_json.restype = ctypes.c_int64
     lib.ngz_slot_kernel.argtypes = [P, U32]
     lib.ngz_slot_kernel.restype = I
+    lib.ngz_last_batch_info.argtypes = [P]
+    lib.ngz_last_batch_info.restype = I
     lib.ngz_dgram_error.argtypes = [P, U32, ctypes.POINTER(Error)]
     lib.ngz_dgram_error.restype = I
     lib.ngz_template_counts_device.argtypes = [P, I, P, U32, I, P]

@@ -36,6 +36,9 @@ extern "C" int ngz_launch_scan(void *temp, size_t temp_bytes, const uint32_t *in
 extern "C" int ngz_launch_layout_emit(const BatchDev *B, const uint32_t *hf_flag, const uint32_t *hf_first,
                                       hipStream_t st);
 extern "C" int ngz_launch_decode_generic(const BatchDev *B, uint32_t grid, hipStream_t st);
+extern "C" int ngz_launch_frame_vlen(const BatchDev *B, hipStream_t st);
+extern "C" int ngz_launch_layout(const BatchDev *B, hipStream_t st);
+extern "C" int ngz_launch_emit(const BatchDev *B, hipStream_t st);
 void *ngz_rtc_kernel(int device, const DevPlan &P);
 int ngz_rtc_kernel_async(int device, const DevPlan &P, void **fn, void **entry);
 int ngz_rtc_poll(void *entry, void **fn);
@@ -844,14 +847,59 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
     // overflow bit 8 and the batch runs again with a row for every slot
     const bool few_rows = ctx->pred_valid && ctx->pred_versions == ctx->slot_version && !hf && !ctx->rows_all &&
                           ctx->pred_active.size() == S;
-    std::vector<uint16_t> rows(S, (uint16_t)NGZ_NO_ROW);
-    uint32_t A = 0;
+    bool any_vlen = false;
+    uint32_t min_vlen_rec = 0xFFFFFFFFu;
+    std::vector<uint8_t> is_v(S, 0);  // a variable-length template (records walked one by one)
+    for (uint32_t s = 0; s < S; ++s) {
+        const DevPlan &P = ctx->versions[ctx->slot_version[s]].plan;
+        if (P.has_vlen && P.rpl) {
+            any_vlen = true;
+            is_v[s] = 1;
+            min_vlen_rec = std::min<uint32_t>(min_vlen_rec, P.rec_len);
+        }
+    }
+    // Records of variable-length sets found by k_frame's walk reach k_emit as a list of
+    // record offsets per datagram (2 bytes per record, written in order by the walking
+    // thread; no per-batch zeroing).  Every such record spans at least min_record_length
+    // bytes (ipfix.rs:193-214), so datagram d's list fits from entry offsets[d] / that + d.
+    // Templates whose records may be shorter than 8 bytes use the record-start bitmap (one
+    // bit per batch byte, zeroed per batch).  NGZ_RECMAP: 0 walk twice, 1 bitmap, 2 lists.
+    static const int recmap_env = getenv("NGZ_RECMAP") ? atoi(getenv("NGZ_RECMAP")) : -1;
+    const bool lists = any_vlen && recmap_env != 0 && recmap_env != 1 && min_vlen_rec >= 8;
+    // Split framing (steady state, every active template with its compiled kernel, record-offset
+    // lists): the record walk of the variable-length sets -- one thread per datagram through a
+    // chain of dependent length-prefix loads, latency-bound -- runs on a second stream (phase B)
+    // beside the framing, layout and decode of the fixed-length sets (phase A, bandwidth-bound),
+    // then lays out, emits and decodes its own templates there; the two join before the counts.
+    // Config 4 (NFv9 + variable-length IPFIX): k_frame was 0.61 of the 2.39 ms step.
+    const int split_env = getenv("NGZ_SPLIT") ? atoi(getenv("NGZ_SPLIT")) : 1;  // per batch (tests)
+    bool split = false;
+    if (split_env && few_rows && lists && ctx->specialize) {
+        bool any_v = false, any_f = false, all_spec = true;
+        for (uint32_t s = 0; s < S; ++s) {
+            if (!ctx->pred_active[s]) continue;
+            (is_v[s] ? any_v : any_f) = true;
+            all_spec = all_spec && ctx->versions[ctx->slot_version[s]].rtc_state == 1;
+        }
+        split = any_v && any_f && all_spec && ctx->split_skip == 0;
+    }
+    if (ctx->split_skip) --ctx->split_skip;
+    if (ctx->pipeline_runs++) ctx->batch_info |= NGZ_BATCH_RERUN;
+    if (split) ctx->batch_info |= NGZ_BATCH_SPLIT;
+    else ctx->batch_info &= ~(uint32_t)NGZ_BATCH_SPLIT;
+    std::vector<uint16_t> rows(S, (uint16_t)NGZ_NO_ROW), rows2(S, (uint16_t)NGZ_NO_ROW);
+    uint32_t A = 0, A2 = 0;
     for (uint32_t s = 0; s < S; ++s)
-        if (!few_rows || ctx->pred_active[s]) rows[s] = (uint16_t)A++;
-    const uint64_t n_items = (uint64_t)(2 * A + 1) * N + 1;
-    if (n_items > 0x7FFFFFF0ull) return fail(ctx, NGZ_E_LIMIT, "batch too large for the count matrix");
-    size_t scan_tmp = 0;
+        if (!few_rows || ctx->pred_active[s]) {
+            if (split && is_v[s]) rows2[s] = (uint16_t)A2++;
+            else rows[s] = (uint16_t)A++;
+        }
+    const uint64_t n_items = (uint64_t)(2 * A + 1) * N + 1, n_items2 = (uint64_t)(2 * A2 + 1) * N + 1;
+    if (n_items > 0x7FFFFFF0ull || n_items2 > 0x7FFFFFF0ull)
+        return fail(ctx, NGZ_E_LIMIT, "batch too large for the count matrix");
+    size_t scan_tmp = 0, scan_tmp2 = 0;
     if (ngz_scan_temp_bytes(n_items, &scan_tmp)) return fail(ctx, NGZ_E_DEVICE, "scan temp size");
+    if (split && ngz_scan_temp_bytes(n_items2, &scan_tmp2)) return fail(ctx, NGZ_E_DEVICE, "scan temp size");
     // capacities (overflow is detected on device and retried with more room)
     uint64_t chunk_cap = std::max<uint64_t>(ctx->d_chunks.cap, in->bytes_size / 4096 + 3ull * N + 1024);
     uint64_t set_cap = std::max<uint64_t>(ctx->d_sets.cap, 2ull * N + 1024);
@@ -876,6 +924,20 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
     if (rows != ctx->slot_row_host || ctx->d_slot_row.p != old_rows) {  // changed, or a new buffer
         if (S) HIPCHK(hipMemcpy(ctx->d_slot_row.p, rows.data(), S * 2, hipMemcpyHostToDevice));
         ctx->slot_row_host = rows;
+    }
+    if (split) {
+        const uint16_t *old2 = ctx->d_slot_row2.p;
+        if (ctx->d_counts2.ensure(n_items2) || ctx->d_scan2.ensure(n_items2) || ctx->d_scan_tmp2.ensure(scan_tmp2 + 1) ||
+            ctx->d_slot_row2.ensure(std::max<uint32_t>(S, 1)))
+            return fail(ctx, NGZ_E_NOMEM, "device alloc (split framing)");
+        if (rows2 != ctx->slot_row2_host || ctx->d_slot_row2.p != old2) {
+            HIPCHK(hipMemcpy(ctx->d_slot_row2.p, rows2.data(), S * 2, hipMemcpyHostToDevice));
+            ctx->slot_row2_host = rows2;
+        }
+        if (!ctx->split_stream) {
+            HIPCHK(hipStreamCreateWithFlags(&ctx->split_stream, hipStreamNonBlocking));
+            for (auto &e : ctx->split_ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        }
     }
     const int par = ctx->parity;
     BatchSummary *d_sum = ctx->d_summary.p + par;
@@ -944,24 +1006,9 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
     }
     B.recoff = nullptr;
     B.recoff_div = 0;
-    bool any_vlen = false;
-    uint32_t min_vlen_rec = 0xFFFFFFFFu;
-    for (uint32_t s = 0; s < S; ++s) {
-        const DevPlan &P = ctx->versions[ctx->slot_version[s]].plan;
-        if (P.has_vlen && P.rpl) {
-            any_vlen = true;
-            min_vlen_rec = std::min<uint32_t>(min_vlen_rec, P.rec_len);
-        }
-    }
-    // Records of variable-length sets found by k_frame's walk reach k_emit as a list of
-    // record offsets per datagram (2 bytes per record, written in order by the walking
-    // thread; no per-batch zeroing).  Every such record spans at least min_record_length
-    // bytes (ipfix.rs:193-214), so datagram d's list fits from entry offsets[d] / that + d.
-    // Templates whose records may be shorter than 8 bytes use the record-start bitmap (one
-    // bit per batch byte, zeroed per batch).  NGZ_RECMAP: 0 walk twice, 1 bitmap, 2 lists.
-    static const int recmap_env = getenv("NGZ_RECMAP") ? atoi(getenv("NGZ_RECMAP")) : -1;
+    B.split = 0;
     if (any_vlen && recmap_env != 0) {
-        if (recmap_env != 1 && min_vlen_rec >= 8) {
+        if (lists) {
             if (ctx->d_recoff.ensure(in->bytes_size / min_vlen_rec + 8ull * N + 16))
                 return fail(ctx, NGZ_E_NOMEM, "device alloc (record offsets)");
             B.recoff = ctx->d_recoff.p;
@@ -972,6 +1019,19 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
         }
     }
     B.summary = d_sum;
+    // split framing: phase B has its own count matrix, scan and rows and writes the record-offset
+    // lists; phase A defers the variable-length sets
+    BatchDev B2 = B;
+    if (split) {
+        B2.split = 2;
+        B2.counts = ctx->d_counts2.p;
+        B2.scan = ctx->d_scan2.p;
+        B2.slot_row = ctx->d_slot_row2.p;
+        B2.n_rows = A2;
+        B2.dsum = nullptr;
+        B.split = 1;
+        B.recoff = nullptr;
+    }
 
     HIPCHK(hipEventRecord(ctx->ev[0], st));
     // k_frame zeroes the count matrix itself; the summary and increments of
@@ -1005,10 +1065,28 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
         ctx->clean[par ^ 1] = true;
         return 0;
     };
+    const hipStream_t ss = split ? ctx->split_stream : st;
+    if (split) {
+        // phase B starts with the batch (the summary zeroed, the plans uploaded)
+        HIPCHK(hipEventRecord(ctx->split_ev[0], st));
+        HIPCHK(hipStreamWaitEvent(ss, ctx->split_ev[0], 0));
+        if (ngz_launch_frame_vlen(&B2, ss)) return fail(ctx, NGZ_E_DEVICE, "k_frame_vlen launch");
+        if (ngz_launch_scan(ctx->d_scan_tmp2.p, scan_tmp2, ctx->d_counts2.p, ctx->d_scan2.p, n_items2, ss))
+            return fail(ctx, NGZ_E_DEVICE, "scan launch (phase B)");
+    }
     if (ngz_launch_frame(&B, hf_flag, hf_first, st)) return fail(ctx, NGZ_E_DEVICE, "k_frame launch");
     if (ngz_launch_scan(ctx->d_scan_tmp.p, scan_tmp, ctx->d_counts.p, ctx->d_scan.p, n_items, st))
         return fail(ctx, NGZ_E_DEVICE, "scan launch");
-    if (ngz_launch_layout_emit(&B, hf_flag, hf_first, st)) return fail(ctx, NGZ_E_DEVICE, "layout/emit launch");
+    if (!split) {
+        if (ngz_launch_layout_emit(&B, hf_flag, hf_first, st)) return fail(ctx, NGZ_E_DEVICE, "layout/emit launch");
+    } else {
+        // phase B lays its templates out after phase A's (and reads phase A's headers in k_emit)
+        if (ngz_launch_layout(&B, st)) return fail(ctx, NGZ_E_DEVICE, "layout launch");
+        HIPCHK(hipEventRecord(ctx->split_ev[1], st));
+        if (ngz_launch_emit(&B, st)) return fail(ctx, NGZ_E_DEVICE, "emit launch");
+        HIPCHK(hipStreamWaitEvent(ss, ctx->split_ev[1], 0));
+        if (ngz_launch_layout(&B2, ss) || ngz_launch_emit(&B2, ss)) return fail(ctx, NGZ_E_DEVICE, "layout/emit launch (phase B)");
+    }
     // Decode launches.  The record counts per slot are known on the device
     // only; reading them back costs a host round trip in the middle of the
     // pipeline.  In steady state (same slots as the previous batch) the
@@ -1018,6 +1096,8 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
     // records is decoded then, and processed counts / statuses are redone.
     const uint32_t grid = (uint32_t)ctx->n_cus * ctx->blocks_per_cu;  // 256-thread blocks
     const bool predict = ctx->pred_valid && ctx->pred_versions == ctx->slot_version && !hf;
+    if (predict) ctx->batch_info |= NGZ_BATCH_PREDICTED;
+    else ctx->batch_info &= ~(uint32_t)NGZ_BATCH_PREDICTED;
     // launch the decode of slot s (rt: its counts when known)
     auto launch_slot = [&](uint32_t s, const SlotRT *rt, bool &generic, hipStream_t ls) -> int {
         const Version &v = ctx->versions[ctx->slot_version[s]];
@@ -1039,7 +1119,8 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
                     g = std::min<uint32_t>(grid, (units + 3) / 4);
                 }
             }
-            if (g && ngz_rtc_launch(v.rtc_fn, &B, s, g, block, ls)) return fail(ctx, NGZ_E_DEVICE, "specialised decode launch");
+            if (g && ngz_rtc_launch(v.rtc_fn, split && is_v[s] ? &B2 : &B, s, g, block, split && is_v[s] ? ss : ls))
+                return fail(ctx, NGZ_E_DEVICE, "specialised decode launch");
         } else {
             generic = true;
         }
@@ -1049,6 +1130,7 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
         ctx->summary = *ctx->h_summary;
         if (ctx->summary.overflow) {
             if (ctx->summary.overflow & 8) ctx->rows_all = true;  // a slot without a count row had a set
+            if (ctx->summary.overflow & 16) ctx->split_skip = 64;  // a record error phase A went past
             if (ctx->summary.overflow & 1) ctx->d_arena.ensure(ctx->summary.arena_used + 4096);
             if (ctx->summary.overflow & 2) ctx->d_chunks.ensure(ctx->summary.n_chunks + 1024);
             if (ctx->summary.overflow & 4) ctx->d_sets.ensure(ctx->summary.n_sets + 1024);
@@ -1126,7 +1208,7 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
     // several active templates: their kernels run side by side on the context's
     // auxiliary streams (fork/join with events), so one kernel's tail overlaps
     // the next one's start instead of draining the GPU between templates
-    const uint32_t n_aux = todo.size() >= 2 ? std::min<uint32_t>(ctx->n_aux, (uint32_t)todo.size() - 1) : 0;
+    const uint32_t n_aux = todo.size() >= 2 && !split ? std::min<uint32_t>(ctx->n_aux, (uint32_t)todo.size() - 1) : 0;
     if (n_aux) {
         HIPCHK(hipEventRecord(ctx->fork_ev, st));
         for (uint32_t i = 0; i < n_aux; ++i) HIPCHK(hipStreamWaitEvent(ctx->aux[i], ctx->fork_ev, 0));
@@ -1136,6 +1218,10 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
         if (launch_slot(todo[k].first, todo[k].second, generic, ls)) return -1;
     }
     if (generic && ngz_launch_decode_generic(&B, grid, st)) return fail(ctx, NGZ_E_DEVICE, "decode launch");
+    if (split) {  // join phase B before the counts
+        HIPCHK(hipEventRecord(ctx->split_ev[2], ss));
+        HIPCHK(hipStreamWaitEvent(st, ctx->split_ev[2], 0));
+    }
     for (uint32_t i = 0; i < n_aux; ++i) {
         HIPCHK(hipEventRecord(ctx->join_ev[i], ctx->aux[i]));
         HIPCHK(hipStreamWaitEvent(st, ctx->join_ev[i], 0));
@@ -1350,6 +1436,13 @@ void ngz_ctx_destroy(ngz_ctx *ctx) {
     ctx->d_slots.release(); ctx->d_chunks.release(); ctx->d_sets.release(); ctx->d_arena.release();
     ctx->d_proc.release(); ctx->d_summary.release(); ctx->d_recmap.release(); ctx->d_recoff.release(); ctx->d_dsum.release(); ctx->d_slot_row.release(); ctx->d_in_bytes.release(); ctx->d_in_off.release();
     ctx->d_in_len.release();
+    ctx->d_counts2.release(); ctx->d_scan2.release(); ctx->d_scan_tmp2.release(); ctx->d_slot_row2.release();
+    if (ctx->split_stream) {
+        hipStreamSynchronize(ctx->split_stream);
+        hipStreamDestroy(ctx->split_stream);
+    }
+    for (auto &e : ctx->split_ev)
+        if (e) hipEventDestroy(e);
     for (auto &e : ctx->ev) hipEventDestroy(e);
     for (uint32_t i = 0; i < ctx->n_aux; ++i) {
         hipStreamSynchronize(ctx->aux[i]);
@@ -1408,6 +1501,8 @@ int ngz_decode_batch(ngz_ctx *ctx, const ngz_batch_in *in, ngz_batch_out *out, v
     ctx->tmpl_sets.clear();
     ctx->batch_serial++;
     ctx->json_view.reset();
+    ctx->batch_info = 0;
+    ctx->pipeline_runs = 0;
     memset(out, 0, sizeof *out);
     int rc = ctx->assigned_gen == ctx->tmpl_gen ? 0 : assign_slots(ctx, {});
     if (rc) return rc;
@@ -1623,6 +1718,8 @@ int ngz_slot_fields(ngz_ctx *ctx, uint32_t slot, ngz_field_info *fields, uint32_
     }
     return (int)n;
 }
+
+int ngz_last_batch_info(ngz_ctx *ctx) { return ctx ? (int)ctx->batch_info : NGZ_E_INVALID; }
 
 int ngz_slot_kernel(ngz_ctx *ctx, uint32_t slot) {
     if (!ctx || slot >= ctx->slot_spec.size()) return NGZ_E_INVALID;

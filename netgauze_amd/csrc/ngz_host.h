@@ -309,6 +309,17 @@ struct ngz_ctx {
     bool rows_all = false;
     std::vector<uint16_t> slot_row_host;  // what d_slot_row holds
     ngzh::DevBuf<uint16_t> d_slot_row;
+    // split framing (run_pipeline): phase B's count matrix, scan and rows (the variable-length
+    // slots), its stream and fork / join events; split_skip: batches left without splitting after
+    // phase B met a record error
+    ngzh::DevBuf<uint32_t> d_counts2, d_scan2;
+    ngzh::DevBuf<uint8_t> d_scan_tmp2;
+    ngzh::DevBuf<uint16_t> d_slot_row2;
+    std::vector<uint16_t> slot_row2_host;
+    hipStream_t split_stream = nullptr;
+    hipEvent_t split_ev[3] = {};
+    uint32_t split_skip = 0;
+    uint32_t batch_info = 0, pipeline_runs = 0;  // ngz_last_batch_info
     std::vector<ngzh::TemplateSetJson> tmpl_sets;  // template sets of the last batch, (dgram, set_pos) order
     uint64_t batch_serial = 0;                      // bumped by every ngz_decode_batch
     std::shared_ptr<ngzh::JsonView> json_view;      // ngz_dgram_json cache of the last batch

@@ -257,7 +257,8 @@ struct BatchSummary {    // device -> host at the end of a batch
     uint32_t n_chunks;
     uint32_t n_sets;
     uint32_t n_host;        // datagrams needing host framing (template sets)
-    uint32_t overflow;      // 1: arena, 2: chunks, 4: sets, 8: a set of a slot without a count row
+    uint32_t overflow;      // 1: arena, 2: chunks, 4: sets, 8: a set of a slot without a count row,
+                            // 16: split framing met a record error in a variable-length set (run again whole)
     uint32_t n_unsupported;
     uint64_t arena_used;
 };
@@ -293,7 +294,9 @@ struct BatchDev {        // device pointers of one batch
     unsigned long long *proc_counts; // [n_slots] processed_count increments
     BatchSummary *summary;
     uint32_t cap_pad_windows;  // extra workgroup windows of capacity per slot (column placement tuning)
-    uint32_t reserved_b;
+    uint32_t split;            // split framing (ngz_host.cpp run_pipeline): 0 off; 1 phase A, the sets of
+                               // variable-length templates deferred (counted as sets, no records walked);
+                               // 2 phase B, only those sets (record walk, row tables), on another stream
     uint32_t *recmap;          // variable-length slots: 1 bit per batch byte, set at every complete record
                                // (used when recoff is null)
     uint16_t *recoff;          // variable-length slots: per datagram, the offsets of its complete records

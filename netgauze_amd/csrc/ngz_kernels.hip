@@ -282,6 +282,9 @@ struct CountVis {
     }
     uint64_t sum = 0;  // the first data set: set_pos | slot << 16 | n << 32 | (end - set_pos, or 1) << 48
     uint64_t dg_end = 0;  // batch offset past the datagram
+    uint32_t split = 0;    // BatchDev::split
+    bool deferred = false;  // phase A: a variable-length set was left to phase B
+    bool vlen_err = false;  // phase B: a variable-length set's record walk failed
     // record-start marks of the word being filled (record starts only ever move forward)
     uint64_t mw = ~0ull;
     uint32_t mbits = 0;
@@ -293,7 +296,17 @@ struct CountVis {
         else atomicOr(&recmap[mw], mbits);
     }
     __device__ uint32_t vlen(const uint8_t *p, uint32_t pos, uint32_t end, uint32_t, const DevPlan &pl, uint64_t *err) {
+        if (split == 1) {  // phase B walks it
+            deferred = true;
+            return 0;
+        }
         if (!sets) sum = (uint64_t)(end - (pos - 4)) << 48;
+        const uint64_t e0 = *err;
+        const uint32_t n = walk_records(p, pos, end, pl, err);
+        vlen_err = vlen_err || *err != e0;
+        return n;
+    }
+    __device__ uint32_t walk_records(const uint8_t *p, uint32_t pos, uint32_t end, const DevPlan &pl, uint64_t *err) {
         return ngz_vlen_walk(p, pos, end, pl, err, [this](uint32_t, uint32_t at) {
             if (ro) {  // the record's offset in the datagram, appended to the datagram's list
                 ro_push(at);
@@ -312,6 +325,15 @@ struct CountVis {
     const uint16_t *row;
     BatchSummary *summary;
     __device__ void on_set(uint32_t set_pos, uint32_t slot, uint32_t n, uint32_t, uint32_t) {
+        if (split) {
+            // phase A counts the records of fixed-length sets only, phase B of variable-length ones;
+            // both count every set (the set table's order)
+            const bool v = plans[slot].has_vlen && plans[slot].rpl;
+            if (v == (split == 1)) {
+                sets += 1;
+                return;
+            }
+        }
         if (!sets) sum = (sum ? sum : 1ull << 48) | set_pos | ((uint64_t)slot << 16) | ((uint64_t)(n & 0xFFFF) << 32);
         const uint32_t r = row[slot];
         if (r == NGZ_NO_ROW) {
@@ -334,6 +356,7 @@ __global__ void __launch_bounds__(kFrameBlock) k_frame(BatchDev B, const uint32_
     vis.row = B.slot_row;
     vis.summary = B.summary;
     vis.dg_end = vis.dg_off + B.lengths[d];
+    vis.split = B.split;
     if (B.recoff) vis.ro = ngz_ro_list(B, vis.dg_off, d);
     WalkOut o;
     walk_datagram(B, hf_flag, hf_first, d, o, vis);
@@ -347,7 +370,7 @@ __global__ void __launch_bounds__(kFrameBlock) k_frame(BatchDev B, const uint32_
     // one data set, parsed cleanly: k_emit takes it from here instead of walking the datagram again
     if (B.dsum)
         B.dsum[d] = (o.status == NGZ_FR_OK && o.err == NGZ_NO_ERR && vis.sets == 1 && !(hf_flag && hf_flag[d]) &&
-                     ((vis.sum >> 32) & 0xFFFF) < 0xFFFF)
+                     ((vis.sum >> 32) & 0xFFFF) < 0xFFFF && !vis.deferred)
                         ? vis.sum
                         : 0ull;
     ngz_dgram_hdr h;
@@ -366,6 +389,29 @@ __global__ void __launch_bounds__(kFrameBlock) k_frame(BatchDev B, const uint32_
     if (o.status == NGZ_FR_UNSUPPORTED) atomicAdd(&B.summary->n_unsupported, 1u);
 }
 
+// Split framing, phase B (BatchDev::split 2, on its own stream beside phase A's fixed-length
+// decode): the record walk of the variable-length sets, into phase B's own count matrix (rows of
+// the variable-length slots, every set counted for the set order) and the record-offset lists.
+// Phase A (k_frame with split 1) wrote the headers; a record error here, which phase A did not
+// see, sends the batch round again unsplit (overflow bit 16).
+__global__ void __launch_bounds__(kFrameBlock) k_frame_vlen(BatchDev B) {
+    const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d >= B.n) return;
+    for (uint32_t r = 0; r < 2 * B.n_rows; ++r) B.counts[(uint64_t)r * B.n + d] = 0;
+    if (d == 0) B.counts[(uint64_t)(2 * B.n_rows + 1) * B.n] = 0;
+    CountVis vis{B.counts, B.n, B.n_rows, d, 0, B.plans, nullptr, B.offsets[d]};
+    vis.row = B.slot_row;
+    vis.summary = B.summary;
+    vis.dg_end = vis.dg_off + B.lengths[d];
+    vis.split = 2;
+    vis.ro = ngz_ro_list(B, vis.dg_off, d);
+    WalkOut o;
+    walk_datagram(B, nullptr, nullptr, d, o, vis);
+    vis.ro_finish();
+    B.counts[(uint64_t)(2 * B.n_rows) * B.n + d] = vis.sets;
+    if (vis.vlen_err) atomicOr(&B.summary->overflow, 16u);
+}
+
 // Column layout: slot-major rows of the scanned count matrix give each slot a
 // dense, stream-ordered row range; columns of a slot are laid out
 // column-major inside one 256-byte aligned block of cap*row_bytes bytes.
@@ -374,8 +420,11 @@ __global__ void k_layout(BatchDev B) {
     const uint64_t N = B.n;
     const uint32_t S = B.n_slots, A = B.n_rows;
     const uint32_t chunk_base = B.scan[(uint64_t)A * N];
-    uint64_t off = 0;
+    // split framing: phase A lays out the fixed-length slots from the arena start, phase B the
+    // variable-length ones after them (it runs once phase A's layout is done)
+    uint64_t off = B.split == 2 ? B.summary->arena_used : 0;
     for (uint32_t s = 0; s < S; ++s) {
+        if (B.split && (B.plans[s].has_vlen && B.plans[s].rpl) != (B.split == 2)) continue;  // the other phase's
         const uint32_t r = B.slot_row[s];
         const bool has = r != NGZ_NO_ROW;
         // a slot without a row has no records in this batch (else the batch runs again)
@@ -416,15 +465,21 @@ __global__ void k_layout(BatchDev B) {
     const uint32_t rec_total = chunk_base;
     const uint32_t chunks = B.scan[(uint64_t)(2 * A) * N] - chunk_base;
     const uint32_t sets = B.scan[(uint64_t)(2 * A + 1) * N] - B.scan[(uint64_t)(2 * A) * N];
-    B.summary->n_records_total = rec_total;
-    B.summary->n_chunks = chunks;
-    B.summary->n_sets = sets;
+    if (B.split == 2) {  // phase A's summary plus the variable-length slots
+        B.summary->n_records_total += rec_total;
+    } else {
+        B.summary->n_records_total = rec_total;
+        B.summary->n_chunks = chunks;
+        B.summary->n_sets = sets;
+    }
     B.summary->arena_used = off;
-    uint32_t ov = B.summary->overflow & 8u;  // k_frame's: a set of a slot without a row
+    // bits only ever set (the summary starts the batch zeroed): the other framing phase and
+    // k_frame (bit 8) may be setting theirs
+    uint32_t ov = 0;
     if (off > B.arena_cap) ov |= 1;
-    if (chunks > B.chunk_cap) ov |= 2;
-    if (sets > B.set_cap) ov |= 4;
-    B.summary->overflow = ov;
+    if (B.split != 2 && chunks > B.chunk_cap) ov |= 2;  // phase B's rows only count records
+    if (B.split != 2 && sets > B.set_cap) ov |= 4;
+    if (ov) atomicOr(&B.summary->overflow, ov);
 }
 
 // Row-mode record tables of variable-length slots are staged per workgroup:
@@ -447,6 +502,7 @@ struct EmitVis {
     const uint16_t *ro;        // the datagram's record-offset list (k_frame), at its next set's first record
     uint64_t *lrs;             // LDS row tables
     uint32_t *lrd;
+    uint32_t split;            // BatchDev::split: phase A emits the fixed-length sets, phase B the others
     // row mode: every record's batch offset and datagram, rows rec0.. of this set
     __device__ uint64_t *rowsrc(uint32_t slot) const { return (uint64_t *)(B->arena + B->slots[slot].rows); }
     __device__ uint32_t *rowdg(uint32_t slot) const {
@@ -454,6 +510,7 @@ struct EmitVis {
     }
     __device__ uint32_t vlen(const uint8_t *p, uint32_t pos, uint32_t end, uint32_t slot, const DevPlan &pl,
                              uint64_t *err) {
+        if (split == 1) return 0;  // phase B's
         const uint32_t rec0 = B->scan[(uint64_t)B->slot_row[slot] * B->n + d] - B->slots[slot].base;
         uint64_t *rs = rowsrc(slot) + rec0;
         uint32_t *rd = rowdg(slot) + rec0;
@@ -532,6 +589,10 @@ struct EmitVis {
     }
     __device__ void on_set(uint32_t set_pos, uint32_t slot, uint32_t n, uint32_t payload_pos, uint32_t rl) {
         const uint64_t N = B->n;
+        if (split && (B->plans[slot].has_vlen && B->plans[slot].rpl) != (split == 2)) {
+            ++set_at;  // the other phase writes this set's entry
+            return;
+        }
         const uint32_t row = B->slot_row[slot];
         uint32_t *cell = &B->scan[(uint64_t)row * N + d];
         const uint32_t rec0 = *cell - B->slots[slot].base;
@@ -635,6 +696,7 @@ __global__ void __launch_bounds__(256) k_emit(BatchDev B, const uint32_t *hf_fla
         vis.ntab = ntab;
         vis.lrs = st_rs;
         vis.lrd = st_rd;
+        vis.split = B.split;
         vis.ro = B.recoff ? ngz_ro_list(B, vis.dg_off, d) : nullptr;
         const unsigned long long sm = B.dsum ? B.dsum[d] : 0ull;
         if (sm) {
@@ -903,6 +965,12 @@ extern "C" int ngz_launch_frame(const BatchDev *B, const uint32_t *hf_flag, cons
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+extern "C" int ngz_launch_frame_vlen(const BatchDev *B, hipStream_t st) {
+    const uint32_t nb = (B->n + kFrameBlock - 1) / kFrameBlock;
+    if (nb) hipLaunchKernelGGL(k_frame_vlen, dim3(nb), dim3(kFrameBlock), 0, st, *B);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 extern "C" int ngz_scan_temp_bytes(uint64_t n_items, size_t *bytes) {
     *bytes = 0;
     return hipcub::DeviceScan::ExclusiveSum(nullptr, *bytes, (uint32_t *)nullptr, (uint32_t *)nullptr, (int)n_items) ==
@@ -921,6 +989,17 @@ extern "C" int ngz_launch_layout_emit(const BatchDev *B, const uint32_t *hf_flag
     hipLaunchKernelGGL(k_layout, dim3(1), dim3(64), 0, st, *B);
     const uint32_t nb = (B->n + 255) / 256;
     if (nb) hipLaunchKernelGGL(k_emit, dim3(nb), dim3(256), 0, st, *B, hf_flag, hf_first);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int ngz_launch_layout(const BatchDev *B, hipStream_t st) {
+    hipLaunchKernelGGL(k_layout, dim3(1), dim3(64), 0, st, *B);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int ngz_launch_emit(const BatchDev *B, hipStream_t st) {
+    const uint32_t nb = (B->n + 255) / 256;
+    if (nb) hipLaunchKernelGGL(k_emit, dim3(nb), dim3(256), 0, st, *B, nullptr, nullptr);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

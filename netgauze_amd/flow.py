@@ -266,6 +266,10 @@ class FlowInfoCodec:
             self._check(n)
         return n
 
+    def last_batch_info(self):
+        """ngz_last_batch_info bits: 1 predicted launches, 2 split framing, 4 a pass repeated."""
+        return lib().ngz_last_batch_info(self._ctx)
+
     def last_timing(self):
         a, b = ctypes.c_float(), ctypes.c_float()
         lib().ngz_last_timing(self._ctx, ctypes.byref(a), ctypes.byref(b))

@@ -565,6 +565,49 @@ def test_reference_field_kats(dev):
     assert stats["err"] == 0 and stats["ok"] == 2 * len(good) and stats["records"] == 3 * len(good)
 
 
+def test_cfg4_split_framing_steady_state(dev, kernel_path):
+    """Steady-state config-4 batches (NFv9 313 + IPFIX variable-length 900): from the second
+    batch on, the record walk of the variable-length sets runs on its own stream beside the
+    NFv9 framing and decode (split framing, specialised kernels); every batch equals the
+    oracle, processed counts included.  A batch with a variable-length record that runs past
+    its set (the UnexpectedEof only the split walk sees; phase A went past it) runs again
+    unsplit and equals the oracle too, and so does the batch after it."""
+    from netgauze_amd import synth
+    dg = synth.cfg4_datagrams(9000)
+    codec = new_codec()
+    oc = O.FlowInfoCodec()
+    codec.decode_datagrams(dg[:2])
+    parity.oracle_datagrams(dg[:2], oc)
+    data = dg[2:]
+    third = len(data) // 3
+    infos = []
+    for k in range(3):
+        part = data[k * third:(k + 1) * third]
+        batch = codec.decode_datagrams(part)
+        oracle, _ = parity.oracle_datagrams(part, oc)
+        stats = parity.check_batch(batch, oracle)
+        assert stats["err"] == 0 and stats["records"] > 0
+        infos.append(codec.last_batch_info())
+    if kernel_path == "specialized":
+        assert infos[1] & L.NGZ_BATCH_SPLIT and infos[2] & L.NGZ_BATCH_SPLIT, infos
+    else:
+        assert not any(i & L.NGZ_BATCH_SPLIT for i in infos), infos
+    bad = list(data[:400])
+    i = next(j for j, d in enumerate(bad) if d[1] == 10 and j > 40)
+    b = bytearray(bad[i])
+    b[28:32] = b"\xff\xff\xff\xff"  # the first record's first string: 0xFF escape, length 2^24 - 1
+    bad[i] = bytes(b)
+    for part in (bad, data[400:800]):
+        batch = codec.decode_datagrams(part)
+        oracle, _ = parity.oracle_datagrams(part, oc)
+        stats = parity.check_batch(batch, oracle)
+        assert stats["err"] == (1 if part is bad else 0)
+        if part is bad and kernel_path == "specialized":
+            assert codec.last_batch_info() & L.NGZ_BATCH_RERUN
+    assert codec.template_counts(10) == {900: oc.ipfix_templates[900].processed_count}
+    assert codec.template_counts(9) == {313: oc.netflow_templates[313].processed_count}
+
+
 def test_cfg4_netflow_v9_and_variable_length(dev):
     """Config 4 shape: NetFlow v9 (the reference capture's template 313, 130 B)
     interleaved with IPFIX records carrying variable-length strings/octets and
