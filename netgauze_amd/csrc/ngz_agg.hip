@@ -1444,31 +1444,51 @@ __global__ __launch_bounds__(256) void k_agg_part_hist(const RecCtx C, const uin
     for (uint32_t i = threadIdx.x; i < n_part; i += blockDim.x) counts[(uint64_t)i * gridDim.x + blockIdx.x] = h[i];
 }
 
-// Payload of one record (pb bytes): {group, export time, sys-up time, slot | info << 16}, then
-// the operands of aggregated fields 0..n_vals-1 (u64 each; zero when absent or ordered)
+// Payload of one record (pb = 16 NP bytes): {group, export time, sys-up time, slot | info << 16},
+// then the operands of aggregated fields 0..n_vals-1 (u64 each; zero when absent or ordered).
+// A wave's 64 payloads are staged in LDS and stored record by record: NP consecutive lanes write
+// one record's NP 16-byte pieces, so a store instruction moves 64 / NP whole payloads, each one
+// contiguous run (stored per lane, a payload went out as NP separate 16-byte pieces: 113 bytes of
+// WRITE_SIZE per 80-byte payload, the 8 of the 12.7 ms of a protocol + port push)
+template <uint32_t NP>
 __global__ __launch_bounds__(256) void k_agg_part_scatter(const RecCtx C, const AggParams P, const uint32_t *__restrict__ rec_g,
                                                           uint32_t n_part, const uint32_t *__restrict__ offs,
-                                                          uint8_t *__restrict__ pay, uint32_t pb) {
+                                                          uint8_t *__restrict__ pay) {
     extern __shared__ uint32_t cur[];
+    __shared__ uint4 stage[4][64 * NP];
+    __shared__ uint32_t spos[4][64];
     for (uint32_t i = threadIdx.x; i < n_part; i += blockDim.x) cur[i] = offs[(uint64_t)i * gridDim.x + blockIdx.x];
     __syncthreads();
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint64_t t0 = (uint64_t)blockIdx.x * PART_TILE, t1 = min(t0 + PART_TILE, C.n_rec);
-    for (uint64_t t = t0 + threadIdx.x; t < t1; t += blockDim.x) {
-        const uint32_t g = rec_g[t];
-        if (g == NONE) continue;
-        const Rec r = rec_of(C, t, nullptr);
-        const uint32_t pos = atomicAdd(&cur[g >> PART_SHIFT], 1u);
-        uint4 *d = (uint4 *)(pay + (uint64_t)pos * pb);
-        d[0] = make_uint4(g, r.ts, r.sysup, r.slot | ((uint32_t)r.info << 16));
-        const AggSlotPlan &sp = C.plans[r.slot];
-        uint64_t x[8];
+    for (uint64_t base = t0; base < t1; base += blockDim.x) {  // uniform over the workgroup
+        const uint64_t t = base + threadIdx.x;
+        const uint32_t g = t < t1 ? rec_g[t] : NONE;
+        uint32_t pos = NONE;
+        if (g != NONE) {
+            const Rec r = rec_of(C, t, nullptr);
+            pos = atomicAdd(&cur[g >> PART_SHIFT], 1u);
+            uint4 *d = &stage[w][lane * NP];
+            d[0] = make_uint4(g, r.ts, r.sysup, r.slot | ((uint32_t)r.info << 16));
+            const AggSlotPlan &sp = C.plans[r.slot];
+            uint64_t x[8];
 #pragma unroll
-        for (int v = 0; v < 8; ++v)
-            x[v] = v < (int)P.n_vals && sp.val_col[v] && !vc_ordered(P.val_vc[v]) ? value_operand(sp, P, v, r.row) : 0ull;
+            for (int v = 0; v < 8; ++v)
+                x[v] = v < (int)P.n_vals && sp.val_col[v] && !vc_ordered(P.val_vc[v]) ? value_operand(sp, P, v, r.row) : 0ull;
 #pragma unroll
-        for (int v = 0; v < 8; v += 2)
-            if (v < (int)P.n_vals)
-                d[1 + v / 2] = make_uint4((uint32_t)x[v], (uint32_t)(x[v] >> 32), (uint32_t)x[v + 1], (uint32_t)(x[v + 1] >> 32));
+            for (uint32_t k = 1; k < NP; ++k)
+                d[k] = make_uint4((uint32_t)x[2 * k - 2], (uint32_t)(x[2 * k - 2] >> 32), (uint32_t)x[2 * k - 1],
+                                  (uint32_t)(x[2 * k - 1] >> 32));
+        }
+        spos[w][lane] = pos;
+        __syncthreads();
+#pragma unroll
+        for (uint32_t i = lane; i < 64 * NP; i += 64) {
+            const uint32_t rec = i / NP, k = i % NP;
+            const uint32_t p = spos[w][rec];
+            if (p != NONE) *(uint4 *)(pay + (uint64_t)p * (16 * NP) + 16 * k) = stage[w][i];
+        }
+        __syncthreads();
     }
 }
 
@@ -3479,7 +3499,13 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, const ngz_p
             AGG_HIP(a, hipMemsetAsync(counts + nc - 1, 0, 4, st));
             hipLaunchKernelGGL(k_agg_part_hist, dim3(nt), dim3(256), 4 * np, st, C, rec_g, np, counts);
             AGG_HIP(a, hipcub::DeviceScan::ExclusiveSum(stmp, stb, counts, offs, (int)nc, st));
-            hipLaunchKernelGGL(k_agg_part_scatter, dim3(nt), dim3(256), 4 * np, st, C, P, rec_g, np, offs, pay, pb);
+            switch (pb / 16) {
+            case 1: hipLaunchKernelGGL(k_agg_part_scatter<1>, dim3(nt), dim3(256), 4 * np, st, C, P, rec_g, np, offs, pay); break;
+            case 2: hipLaunchKernelGGL(k_agg_part_scatter<2>, dim3(nt), dim3(256), 4 * np, st, C, P, rec_g, np, offs, pay); break;
+            case 3: hipLaunchKernelGGL(k_agg_part_scatter<3>, dim3(nt), dim3(256), 4 * np, st, C, P, rec_g, np, offs, pay); break;
+            case 4: hipLaunchKernelGGL(k_agg_part_scatter<4>, dim3(nt), dim3(256), 4 * np, st, C, P, rec_g, np, offs, pay); break;
+            default: hipLaunchKernelGGL(k_agg_part_scatter<5>, dim3(nt), dim3(256), 4 * np, st, C, P, rec_g, np, offs, pay); break;
+            }
             hipLaunchKernelGGL(k_agg_part_reduce, dim3(np), dim3(256), 0, st, P, a->plans, offs, nt, pay, pb, a->rows);
         } else if (P.own && !split && groups * 8 > (uint64_t)n_rec) {
 

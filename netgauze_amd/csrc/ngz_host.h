@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdio>
 #include <memory>
 #include <string>
 #include <map>
@@ -145,9 +146,13 @@ struct DevBuf {
         if (p) hipFree(p);
         p = nullptr;
         size_t c = std::max(n, cap + cap / 2);
-        if (contiguous && hipExtMallocWithFlags((void **)&p, c * sizeof(T) + 64, hipDeviceMallocContiguous) == hipSuccess) {
-            cap = c;
-            return 0;
+        if (contiguous) {  // an experiment knob (NGZ_ARENA_CONTIG): say what was granted
+            const bool ok = hipExtMallocWithFlags((void **)&p, c * sizeof(T) + 64, hipDeviceMallocContiguous) == hipSuccess;
+            fprintf(stderr, "[ngz] contiguous allocation of %zu bytes: %s\n", c * sizeof(T) + 64, ok ? "granted" : "refused");
+            if (ok) {
+                cap = c;
+                return 0;
+            }
         }
         p = nullptr;
         if (hipMalloc((void **)&p, c * sizeof(T) + 64) != hipSuccess) {
