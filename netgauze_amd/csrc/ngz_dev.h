@@ -22,6 +22,16 @@
 #include "ngz/flow_decode.h"
 #include "ngz_internal.h"
 
+// Cache policy (buffer instruction aux bits) of the generated kernels' record loads and column
+// stores: 0 by default; the generator defines them from NGZ_LD_AUX / NGZ_ST_AUX for experiments
+// (2 = nt on gfx950), and they are part of the kernel's cache signature.
+#ifndef NGZ_LD_AUX
+#define NGZ_LD_AUX 0
+#endif
+#ifndef NGZ_ST_AUX
+#define NGZ_ST_AUX 0
+#endif
+
 namespace ngzdev {
 
 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
@@ -133,7 +143,7 @@ __device__ __forceinline__ void win_load(uint32_t (&R)[WIN_DW], const Pass &P, u
     uint32_t T[NT];
 #pragma unroll
     for (int i = 0; i < NB; ++i) {
-        const v4u v = __builtin_amdgcn_raw_buffer_load_b128(P.rsrc, o16 + 16 * i, 0, 0);
+        const v4u v = __builtin_amdgcn_raw_buffer_load_b128(P.rsrc, o16 + 16 * i, 0, NGZ_LD_AUX);
         T[4 * i] = v[0];
         T[4 * i + 1] = v[1];
         T[4 * i + 2] = v[2];
@@ -141,7 +151,7 @@ __device__ __forceinline__ void win_load(uint32_t (&R)[WIN_DW], const Pass &P, u
     }
     T[NT - 1] = 0;
     // the byte shift reads dword ND; with dsh = 3 it is block dword ND + 3
-    if (P.any_sh && ND + 3 >= 4 * NB) T[NT - 1] = __builtin_amdgcn_raw_buffer_load_b32(P.rsrc, o16 + 16 * NB, 0, 0);
+    if (P.any_sh && ND + 3 >= 4 * NB) T[NT - 1] = __builtin_amdgcn_raw_buffer_load_b32(P.rsrc, o16 + 16 * NB, 0, NGZ_LD_AUX);
     // per-lane dword shift by dsh (bitwise selects: a ternary on array
     // elements would become a dynamically indexed, scratch-allocated array)
     const uint32_t m0 = 0u - ((o >> 2) & 1u), m1 = 0u - ((o >> 3) & 1u);
@@ -190,21 +200,21 @@ struct ColGlb {
     __device__ __forceinline__ ColGlb(const Pass &P, uint32_t col_off, uint32_t width)
         : r(__builtin_amdgcn_make_buffer_rsrc(pass_col(P, col_off, width), (short)0, 0x7FFFFFF0, 0x00020000)) {}
     __device__ __forceinline__ void b8(uint32_t off, uint32_t v) const {
-        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, r, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, r, off, 0, NGZ_ST_AUX);
     }
     __device__ __forceinline__ void b16(uint32_t off, uint32_t v) const {
-        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)v, r, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b16((uint16_t)v, r, off, 0, NGZ_ST_AUX);
     }
     __device__ __forceinline__ void b32(uint32_t off, uint32_t v) const {
-        __builtin_amdgcn_raw_buffer_store_b32(v, r, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(v, r, off, 0, NGZ_ST_AUX);
     }
     __device__ __forceinline__ void b64(uint32_t off, uint32_t lo, uint32_t hi) const {
         v2u x = {lo, hi};
-        __builtin_amdgcn_raw_buffer_store_b64(x, r, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(x, r, off, 0, NGZ_ST_AUX);
     }
     __device__ __forceinline__ void b128(uint32_t off, uint32_t a, uint32_t b, uint32_t c, uint32_t d) const {
         v4u x = {a, b, c, d};
-        __builtin_amdgcn_raw_buffer_store_b128(x, r, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(x, r, off, 0, NGZ_ST_AUX);
     }
     // one value of `width` bytes (1/2/4/8) at row lrow
     __device__ __forceinline__ void w(uint32_t lrow, uint32_t width, uint64_t v) const {
@@ -261,7 +271,7 @@ __device__ __forceinline__ void lds_flush(uint8_t *dst, uint32_t at, uint32_t ld
     if (lane < lanes) {
         const v4u x = *(const v4u *)&ngz_lds[lds_off + 16 * lane];
         const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, 0x7FFFFFF0, 0x00020000);
-        __builtin_amdgcn_raw_buffer_store_b128(x, r, at + 16 * lane, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(x, r, at + 16 * lane, 0, NGZ_ST_AUX);
     }
 }
 #endif

@@ -871,8 +871,13 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
     // chain of dependent length-prefix loads, latency-bound -- runs on a second stream (phase B)
     // beside the framing, layout and decode of the fixed-length sets (phase A, bandwidth-bound),
     // then lays out, emits and decodes its own templates there; the two join before the counts.
-    // Config 4 (NFv9 + variable-length IPFIX): k_frame was 0.61 of the 2.39 ms step.
-    const int split_env = getenv("NGZ_SPLIT") ? atoi(getenv("NGZ_SPLIT")) : 1;  // per batch (tests)
+    // Measured on config 4 (NFv9 + variable-length IPFIX, r4b): 2.69 ms per step split against
+    // 2.51 unsplit on the same box.  Phase A's framing without the walk took 0.72 ms beside phase
+    // B's walk (0.66 ms) -- the whole k_frame took 0.61 alone --, both emits slowed, and the two
+    // decodes side by side took 1.55 ms against 1.50 in turn: framing is bound by the memory
+    // system's scattered line requests, as the decode is by bandwidth, not by load latency that
+    // another stream could fill.  Off unless NGZ_SPLIT=1 (read per batch).
+    const int split_env = getenv("NGZ_SPLIT") ? atoi(getenv("NGZ_SPLIT")) : 0;
     bool split = false;
     if (split_env && few_rows && lists && ctx->specialize) {
         bool any_v = false, any_f = false, all_spec = true;

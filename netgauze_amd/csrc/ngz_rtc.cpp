@@ -55,9 +55,19 @@ struct Item {           // one extraction step of the generated pass body
     uint32_t d0, d1;    // record dwords touched (inclusive), types 0-2
 };
 
+// Cache-policy defines of the generated source (NGZ_LD_AUX / NGZ_ST_AUX, experiments only; ngz_dev.h)
+std::string cpol_defines() {
+    std::string s;
+    if (const char *e = getenv("NGZ_LD_AUX")) s += "#define NGZ_LD_AUX " + std::to_string(atoi(e)) + "\n";
+    if (const char *e = getenv("NGZ_ST_AUX")) s += "#define NGZ_ST_AUX " + std::to_string(atoi(e)) + "\n";
+    return s;
+}
+
 std::string signature(const DevPlan &P) {
     std::string s = "rl" + std::to_string(P.rec_len) + "lw" + std::to_string(P.lds_waves) + "dm" +
                     std::to_string(P.reserved0);
+    if (const char *e = getenv("NGZ_LD_AUX")) s += "la" + std::to_string(atoi(e));
+    if (const char *e = getenv("NGZ_ST_AUX")) s += "sa" + std::to_string(atoi(e));
     char b[96];
     for (uint32_t f = 0; f < P.n_fields; ++f) {
         const DevField &d = P.f[f];
@@ -325,7 +335,7 @@ std::string generate(const DevPlan &P) {
         src += "#define NGZ_LDS_WAVES " + std::to_string(lw) + "\n";
         src += "#define NGZ_LDS_ROWB " + std::to_string(F.rowb) + "\n";
     }
-    src += "#include \"ngz_dev.h\"\nusing namespace ngzdev;\n";
+    src += cpol_defines() + "#include \"ngz_dev.h\"\nusing namespace ngzdev;\n";
     src += "extern \"C\" __global__ void __launch_bounds__(" + std::to_string(lw ? 64 * lw : 256) +
            ") ngz_tpl(BatchDev B, uint32_t slot) {\n";
     src += "    if (sload(&B.summary->overflow)) return;\n";
@@ -362,7 +372,7 @@ std::string generate_group(const DevPlan *const *plans, uint32_t n) {
         lds = std::max<uint32_t>(lds, NGZ_REG_WINDOW * parts.back().lw * parts.back().rowb);
     }
     src += "#define NGZ_LDS_BYTES " + std::to_string(std::max<uint32_t>(lds, 16)) + "\n";
-    src += "#include \"ngz_dev.h\"\nusing namespace ngzdev;\n";
+    src += cpol_defines() + "#include \"ngz_dev.h\"\nusing namespace ngzdev;\n";
     for (uint32_t k = 0; k < n; ++k) {
         const FixedParts &F = parts[k];
         const std::string L = std::to_string(F.rpl) + ", " + (F.consec ? "true" : "false");
@@ -566,7 +576,7 @@ std::string generate_vlen(const DevPlan &P) {
     }
     std::string src;
     src += "// generated by ngz_rtc.cpp for plan " + signature(P) + "\n";
-    src += "#define NGZ_VSTAGE 1\n#include \"ngz_dev.h\"\nusing namespace ngzdev;\n";
+    src += cpol_defines() + "#define NGZ_VSTAGE 1\n#include \"ngz_dev.h\"\nusing namespace ngzdev;\n";
     src += "extern \"C\" __global__ void __launch_bounds__(256) ngz_tpl(BatchDev B, uint32_t slot) {\n";
     src += "    if (sload(&B.summary->overflow)) return;\n";
     src += "    auto pass = [&](const Pass (&P)[1]) {\n";

@@ -565,14 +565,16 @@ def test_reference_field_kats(dev):
     assert stats["err"] == 0 and stats["ok"] == 2 * len(good) and stats["records"] == 3 * len(good)
 
 
-def test_cfg4_split_framing_steady_state(dev, kernel_path):
-    """Steady-state config-4 batches (NFv9 313 + IPFIX variable-length 900): from the second
-    batch on, the record walk of the variable-length sets runs on its own stream beside the
-    NFv9 framing and decode (split framing, specialised kernels); every batch equals the
+def test_cfg4_split_framing_steady_state(dev, kernel_path, monkeypatch):
+    """Steady-state config-4 batches (NFv9 313 + IPFIX variable-length 900) with split framing
+    (NGZ_SPLIT=1; off by default, it measured slower): from the second batch on, the record
+    walk of the variable-length sets runs on its own stream beside the NFv9 framing and decode
+    (specialised kernels); every batch equals the
     oracle, processed counts included.  A batch with a variable-length record that runs past
     its set (the UnexpectedEof only the split walk sees; phase A went past it) runs again
     unsplit and equals the oracle too, and so does the batch after it."""
     from netgauze_amd import synth
+    monkeypatch.setenv("NGZ_SPLIT", "1")
     dg = synth.cfg4_datagrams(9000)
     codec = new_codec()
     oc = O.FlowInfoCodec()

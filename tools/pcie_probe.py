@@ -4,6 +4,7 @@ streams (duplex), for the host-to-host decode path (bench.py --e2e).  Prints one
 usage: python tools/pcie_probe.py [--mb 640] [--reps 5]"""
 import argparse
 import json
+import os
 import time
 
 import torch
@@ -52,11 +53,26 @@ def main():
             with torch.cuda.stream(s1 if i % 2 == 0 else s2):
                 d_a[i * c:(i + 1) * c].copy_(h_src[i * c:(i + 1) * c], non_blocking=True)
 
-    t1, t2, t3, t4 = timed(h2d), timed(d2h), timed(both), timed(h2d_split)
+    ss = [torch.cuda.Stream(dev) for _ in range(4)]
+
+    def both_four(k=8):
+        # both directions cut in k pieces over four streams (does the runtime spread them over engines?)
+        c = n // k
+        for i in range(k):
+            with torch.cuda.stream(ss[i % 4]):
+                if i % 2 == 0:
+                    d_a[i * c:(i + 1) * c].copy_(h_src[i * c:(i + 1) * c], non_blocking=True)
+                    d_a[(i + 1) * c:(i + 2) * c].copy_(h_src[(i + 1) * c:(i + 2) * c], non_blocking=True)
+                else:
+                    h_dst[(i - 1) * c:i * c].copy_(d_b[(i - 1) * c:i * c], non_blocking=True)
+                    h_dst[i * c:(i + 1) * c].copy_(d_b[i * c:(i + 1) * c], non_blocking=True)
+
+    t1, t2, t3, t4, t5 = timed(h2d), timed(d2h), timed(both), timed(h2d_split), timed(both_four)
     gb = n / 1e9
     print(json.dumps({"bytes": n, "h2d_gbps": gb / t1, "d2h_gbps": gb / t2, "duplex_gbps": 2 * gb / t3,
                       "duplex_ms": t3 * 1e3, "h2d_ms": t1 * 1e3, "d2h_ms": t2 * 1e3,
-                      "h2d_two_streams_gbps": gb / t4}), flush=True)
+                      "h2d_two_streams_gbps": gb / t4, "duplex_four_streams_gbps": 2 * gb / t5,
+                      "HSA_ENABLE_SDMA": os.environ.get("HSA_ENABLE_SDMA")}), flush=True)
 
 
 if __name__ == "__main__":
