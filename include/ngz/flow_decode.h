@@ -40,9 +40,9 @@
 extern "C" {
 #endif
 
-#define NGZ_ABI_VERSION 3  /* 2: ngz_slot_info.n_fields is 32-bit (no field cap), ngz_dgram_error,
+#define NGZ_ABI_VERSION 4  /* 2: ngz_slot_info.n_fields is 32-bit (no field cap), ngz_dgram_error,
                               ngz_template_counts_device; 3: ngz_abi_version, ngz_ctx_destroy joins the
-                              context's background compiles */
+                              context's background compiles; 4: ngz_columns_to_host_async */
 
 /* return codes */
 #define NGZ_OK 0
@@ -324,6 +324,16 @@ int ngz_last_timing(ngz_ctx *ctx, float *decode_ms, float *pipeline_ms);
  * multiple of 256 bytes.  Copied on the context's stream; returns the bytes
  * written, or <0 (NGZ_E_INVALID: cap too small). */
 int64_t ngz_columns_to_host(ngz_ctx *ctx, void *dst, uint64_t cap);
+
+/* ngz_columns_to_host queued on hip_stream (NULL = the context's stream) without waiting for it:
+ * the copy starts once the last batch's decode is done, and the context's next ngz_decode_batch /
+ * ngz_decode_batch_host waits for the copy before it reuses the columns.  Returns the bytes queued.
+ * flags: NGZ_D2H_KERNEL copies with a kernel whose stores cross PCIe to dst (dst must be pinned host
+ * memory mapped for the device: hipHostMalloc, or hipHostRegister with hipHostRegisterMapped;
+ * NGZ_E_INVALID otherwise), leaving the copy engines to the next batch's host-to-device copy so the
+ * link carries both directions at once; 0 uses a copy engine. */
+#define NGZ_D2H_KERNEL 1u
+int64_t ngz_columns_to_host_async(ngz_ctx *ctx, void *dst, uint64_t cap, void *hip_stream, uint32_t flags);
 
 /* Introspection (no device needed): the per-template decode kernel for one
  * IPFIX template record (template id u16, field count u16, field specifiers;

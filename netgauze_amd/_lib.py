@@ -20,11 +20,11 @@ ABI_FUNCTIONS = [
     "ngz_ctx_create", "ngz_ctx_destroy", "ngz_last_error", "ngz_decode_batch",
     "ngz_decode_batch_host", "ngz_slot_fields", "ngz_dgram_error_json",
     "ngz_templates_json", "ngz_template_counts", "ngz_last_timing", "ngz_ctx_set_option",
-    "ngz_template_kernel", "ngz_group_kernel", "ngz_columns_to_host", "ngz_dgram_json", "ngz_batch_json",
+    "ngz_template_kernel", "ngz_group_kernel", "ngz_columns_to_host", "ngz_columns_to_host_async", "ngz_dgram_json", "ngz_batch_json",
     "ngz_dgram_error", "ngz_template_counts_device", "ngz_slot_kernel", "ngz_rtc_drain", "ngz_abi_version",
     "ngz_last_batch_info",
 ]
-NGZ_ABI_VERSION = 3
+NGZ_ABI_VERSION = 4
 NGZ_BATCH_PREDICTED, NGZ_BATCH_SPLIT, NGZ_BATCH_RERUN = 1, 2, 4  # ngz_last_batch_info
 NGZ_AGG_ABI_VERSION = 3
 # ngz_error.kind / .layer (flow_decode.h)
@@ -205,6 +205,8 @@ def load():
     lib.ngz_last_timing.restype = I
     lib.ngz_columns_to_host.argtypes = [P, P, U64]
     lib.ngz_columns_to_host.restype = ctypes.c_int64
+    lib.ngz_columns_to_host_async.argtypes = [P, P, U64, P, ctypes.c_uint32]
+    lib.ngz_columns_to_host_async.restype = ctypes.c_int64
     lib.ngz_template_kernel.argtypes = [P, ctypes.c_size_t, I, ctypes.c_char_p, ctypes.c_size_t]
     lib.ngz_template_kernel.restype = I
     lib.ngz_group_kernel.argtypes = [P, ctypes.c_size_t, I, ctypes.c_char_p, ctypes.c_size_t]

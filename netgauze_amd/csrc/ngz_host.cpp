@@ -53,6 +53,7 @@ int ngz_rtc_compile_only(const DevPlan &P, std::string *log_out);
 int ngz_rtc_compile_source(const std::string &src, std::string *log_out);
 int ngz_rtc_launch(void *fn, const BatchDev *B, uint32_t slot, uint32_t grid, uint32_t block, hipStream_t st);
 extern "C" int ngz_launch_counts(const BatchDev *B, uint64_t set_cap, hipStream_t st);
+extern "C" int ngz_launch_to_host(const void *src, void *dst, uint64_t bytes, hipStream_t st);
 extern "C" int ngz_launch_export(const BatchDev *B, BatchSummary *h_summary, SlotRT *h_slots,
                                  unsigned long long *h_proc, BatchSummary *next_summary,
                                  unsigned long long *next_proc, unsigned long long *h_done, unsigned long long seq,
@@ -1435,6 +1436,10 @@ void ngz_ctx_destroy(ngz_ctx *ctx) {
     }
     hipSetDevice(ctx->device);
     hipStreamSynchronize(ctx->stream);
+    if (ctx->d2h_ev) {
+        hipEventSynchronize(ctx->d2h_ev);
+        hipEventDestroy(ctx->d2h_ev);
+    }
     ctx->d_plans.release(); ctx->d_fields.release(); ctx->d_cur_slot.release(); ctx->d_tl_key.release(); ctx->d_tl_dgram.release();
     ctx->d_tl_slot.release(); ctx->d_hf_flag.release(); ctx->d_hf_hdr.release(); ctx->d_hf_first.release(); ctx->d_hf_sets.release();
     ctx->d_hdr.release(); ctx->d_counts.release(); ctx->d_scan.release(); ctx->d_scan_tmp.release();
@@ -1497,11 +1502,14 @@ int ngz_ctx_set_option(ngz_ctx *ctx, int opt, int64_t value) {
     return fail(ctx, NGZ_E_INVALID, "unknown option");
 }
 
+static int wait_d2h(ngz_ctx *ctx);
+
 int ngz_decode_batch(ngz_ctx *ctx, const ngz_batch_in *in, ngz_batch_out *out, void *hip_stream) {
     if (!ctx || !in || !out) return NGZ_E_INVALID;
     if (in->n && (!in->bytes || !in->offsets || !in->lengths)) return fail(ctx, NGZ_E_INVALID, "null batch arrays");
     HIPCHK(hipSetDevice(ctx->device));
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : ctx->stream;
+    if (wait_d2h(ctx)) return NGZ_E_DEVICE;
     ctx->host_errors.clear();
     ctx->tmpl_sets.clear();
     ctx->batch_serial++;
@@ -1678,6 +1686,7 @@ int ngz_decode_batch_host(ngz_ctx *ctx, const uint8_t *bytes, uint64_t bytes_siz
                           const uint32_t *lengths, uint32_t n, ngz_batch_out *out) {
     if (!ctx || !out || (n && (!bytes || !offsets || !lengths))) return NGZ_E_INVALID;
     HIPCHK(hipSetDevice(ctx->device));
+    if (wait_d2h(ctx)) return NGZ_E_DEVICE;
     if (ctx->d_in_bytes.ensure(bytes_size + 16) || ctx->d_in_off.ensure(n + 1) || ctx->d_in_len.ensure(n + 1))
         return fail(ctx, NGZ_E_NOMEM, "device alloc (input)");
     HIPCHK(hipMemcpyAsync(ctx->d_in_bytes.p, bytes, bytes_size, hipMemcpyHostToDevice, ctx->stream));
@@ -1687,9 +1696,30 @@ int ngz_decode_batch_host(ngz_ctx *ctx, const uint8_t *bytes, uint64_t bytes_siz
     return ngz_decode_batch(ctx, &in, out, nullptr);
 }
 
-int64_t ngz_columns_to_host(ngz_ctx *ctx, void *dst, uint64_t cap) {
-    if (!ctx || (!dst && cap)) return NGZ_E_INVALID;
+// The columns of the last batch stay valid until the context's next decode: one that starts while a
+// queued copy may still read them waits for it first (host side, so no reallocation can race it)
+static int wait_d2h(ngz_ctx *ctx) {
+    if (!ctx->d2h_pending) return 0;
+    ctx->d2h_pending = false;
+    HIPCHK(hipEventSynchronize(ctx->d2h_ev));
+    return 0;
+}
+
+int64_t ngz_columns_to_host_async(ngz_ctx *ctx, void *dst, uint64_t cap, void *hip_stream, uint32_t flags) {
+    if (!ctx || (!dst && cap) || (flags & ~NGZ_D2H_KERNEL)) return NGZ_E_INVALID;
     HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t st = hip_stream ? (hipStream_t)hip_stream : ctx->stream;
+    uint8_t *to = (uint8_t *)dst;
+    if ((flags & NGZ_D2H_KERNEL) && dst) {
+        void *dp = nullptr;
+        if (hipHostGetDevicePointer(&dp, dst, 0) != hipSuccess || !dp) {
+            (void)hipGetLastError();
+            return fail(ctx, NGZ_E_INVALID, "NGZ_D2H_KERNEL: dst is not pinned host memory mapped for the device");
+        }
+        to = (uint8_t *)dp;
+    }
+    if (!ctx->d2h_ev) HIPCHK(hipEventCreateWithFlags(&ctx->d2h_ev, hipEventDisableTiming));
+    HIPCHK(hipStreamWaitEvent(st, ctx->ev[3], 0));  // the end of the last batch's pipeline
     uint64_t at = 0;
     for (size_t s = 0; s < ctx->slot_infos.size(); ++s) {
         const ngz_slot_info &si = ctx->slot_infos[s];
@@ -1697,11 +1727,24 @@ int64_t ngz_columns_to_host(ngz_ctx *ctx, void *dst, uint64_t cap) {
         const uint64_t bytes = (uint64_t)si.capacity * ctx->versions[si.version_id].plan.row_bytes;
         at = (at + 255) & ~255ull;
         if (at + bytes > cap) return fail(ctx, NGZ_E_INVALID, "ngz_columns_to_host: destination too small");
-        HIPCHK(hipMemcpyAsync((uint8_t *)dst + at, si.columns, bytes, hipMemcpyDeviceToHost, ctx->stream));
+        if (flags & NGZ_D2H_KERNEL) {
+            if (ngz_launch_to_host(si.columns, to + at, bytes, st)) return fail(ctx, NGZ_E_DEVICE, "k_to_host launch");
+        } else {
+            HIPCHK(hipMemcpyAsync(to + at, si.columns, bytes, hipMemcpyDeviceToHost, st));
+        }
         at += bytes;
     }
-    HIPCHK(hipStreamSynchronize(ctx->stream));
+    HIPCHK(hipEventRecord(ctx->d2h_ev, st));
+    ctx->d2h_pending = true;
     return (int64_t)at;
+}
+
+int64_t ngz_columns_to_host(ngz_ctx *ctx, void *dst, uint64_t cap) {
+    const int64_t n = ngz_columns_to_host_async(ctx, dst, cap, nullptr, 0);
+    if (n < 0) return n;
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    ctx->d2h_pending = false;
+    return n;
 }
 
 int ngz_slot_fields(ngz_ctx *ctx, uint32_t slot, ngz_field_info *fields, uint32_t cap) {

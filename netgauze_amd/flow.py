@@ -166,6 +166,7 @@ class DecodedBatch:
 OPT_SPECIALIZE = 1
 OPT_BLOCKS_PER_CU = 2
 OPT_RTC_SYNC = 5
+D2H_KERNEL = 1  # NGZ_D2H_KERNEL
 
 
 class FlowInfoCodec:
@@ -239,6 +240,17 @@ class FlowInfoCodec:
         """D2H of the last batch's column blocks (slot order, 256-byte aligned)
         on the context's stream; returns the bytes written."""
         n = lib().ngz_columns_to_host(self._ctx, host_ptr, cap)
+        if n < 0:
+            self._check(int(n))
+        return int(n)
+
+    def columns_to_host_async(self, host_ptr, cap, stream=None, kernel=False):
+        """ngz_columns_to_host_async: the same copy queued on `stream` (None: the context's) without
+        waiting; kernel=True stores through the CUs (host_ptr pinned and mapped: hipHostMalloc /
+        torch pin_memory) so the copy engines stay free for host-to-device copies.  The context's
+        next decode waits for it.  Returns the bytes queued."""
+        n = lib().ngz_columns_to_host_async(self._ctx, host_ptr, cap, ctypes.c_void_p(stream) if stream else None,
+                                            D2H_KERNEL if kernel else 0)
         if n < 0:
             self._check(int(n))
         return int(n)

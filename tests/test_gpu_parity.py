@@ -810,3 +810,44 @@ def test_template_counts_device(dev):
     assert codec.template_counts_device(9, table.data_ptr(), 8) == 0
     torch.cuda.synchronize()
     assert table.abs().sum().item() == 0
+
+
+def test_columns_to_host_async(dev, kernel_path):
+    """ngz_columns_to_host_async: the column blocks copied by a copy engine or by the CUs' stores
+    to pinned host memory (NGZ_D2H_KERNEL) on another stream equal the synchronous copy, and the
+    context's next decode waits for the copy before it reuses the columns."""
+    from netgauze_amd import synth
+    from netgauze_amd.flow import NgzError
+    codec = new_codec()
+    dgrams = synth.cfg4_datagrams(4000) + t20_stream(5000)  # three templates, NFv9 and IPFIX
+    batch = codec.decode_datagrams(dgrams)
+    assert sum(1 for s in batch.slots if s.n_records) == 3
+    cap = sum(s.block_bytes() + 256 for s in batch.slots)
+    side = torch.cuda.Stream(dev)
+    again = t20_stream(3000)[1:]
+    for kernel in (True, False):
+        ref = np.zeros(cap, dtype=np.uint8)
+        n = codec.columns_to_host(ref.ctypes.data, cap)
+        assert n > 0
+        out = torch.zeros(cap + 64, dtype=torch.uint8).pin_memory()
+        for shift in (0, 3):  # 16-byte and byte copies
+            out.zero_()
+            got = codec.columns_to_host_async(out.data_ptr() + shift, cap, stream=side.cuda_stream, kernel=kernel)
+            assert got == n
+            side.synchronize()
+            assert np.array_equal(out.numpy()[shift:shift + n], ref[:n])
+        # queued, then straight into the next decode on the same context: the copy still sees this
+        # batch's columns (the decode waits for it)
+        out.zero_()
+        codec.columns_to_host_async(out.data_ptr(), cap, stream=side.cuda_stream, kernel=kernel)
+        b2 = codec.decode_datagrams(again)
+        assert b2.n_records == 3000
+        side.synchronize()
+        assert np.array_equal(out.numpy()[:n], ref[:n])
+        batch = codec.decode_datagrams(dgrams[2:])  # the same records, templates known
+        cap = max(cap, sum(s.block_bytes() + 256 for s in batch.slots))
+    with pytest.raises(NgzError):
+        codec.columns_to_host_async(out.data_ptr(), 16, stream=side.cuda_stream, kernel=True)  # too small
+    pageable = np.zeros(cap, dtype=np.uint8)
+    with pytest.raises(NgzError):
+        codec.columns_to_host_async(pageable.ctypes.data, cap, kernel=True)  # not mapped for the device
