@@ -145,6 +145,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--e2e-contexts", type=int, default=3, help="--e2e: contexts (host threads) in flight")
     ap.add_argument("--e2e-ranges", type=int, default=12, help="--e2e: message ranges per batch")
+    ap.add_argument("--e2e-duplex-contexts", type=int, default=6, help="--e2e duplex modes: contexts")
+    ap.add_argument("--e2e-duplex-ranges", type=int, default=24, help="--e2e duplex modes: message ranges")
     ap.add_argument("--e2e", action="store_true",
                     help="host-to-host rate instead: pinned host datagrams -> H2D -> decode -> D2H of all columns")
     ap.add_argument("--agg", choices=["proto_dir", "dport", "5tuple"], default=None,
@@ -187,6 +189,10 @@ def main():
         rec = synth.t20_records(n, seed=synth.SEED_CFG2 + rank, device=dev, first=0)
         buf, offs, lens = synth.ipfix_data_stream(rec, 64)
         del rec
+        if os.environ.get("NGZ_BENCH_INPUT_MB"):  # experiment: the batch at the start of a larger allocation
+            big = torch.empty(max(buf.numel(), int(os.environ["NGZ_BENCH_INPUT_MB"]) << 20), dtype=torch.uint8, device=dev)
+            big[:buf.numel()].copy_(buf)
+            buf = big[:buf.numel()]
         rec_bytes = {256: 64}
     elif args.workload in ("mixed8", "cfg5"):
         tpls = synth.CFG3_TEMPLATES if args.workload == "mixed8" else synth.CFG5_TEMPLATES
@@ -463,7 +469,7 @@ def main_e2e(args):
     # (stream d) are queued before the decode of range k, so PCIe carries both directions at once
     # while the GPU decodes.  Contexts round robin (a context's columns stay valid until its next
     # decode: the D2H that reads them is waited for first), device inputs double buffered.
-    KD = args.e2e_ranges
+    KD = args.e2e_duplex_ranges
     cuts = [nmsg * k // KD for k in range(KD + 1)]
     dranges = []
     for k in range(KD):
@@ -478,7 +484,7 @@ def main_e2e(args):
     max_m = max(r[3] for r in dranges)
     dbuf = [torch.empty(max_b, dtype=torch.uint8, device=dev) for _ in range(2)]
     dmeta = [torch.empty(12 * max_m, dtype=torch.uint8, device=dev) for _ in range(2)]
-    PD = max(2, args.e2e_contexts)
+    PD = max(2, args.e2e_duplex_contexts)
     dcodecs = []
     for _ in range(PD):
         c = FlowInfoCodec(0, rtc_sync=True)

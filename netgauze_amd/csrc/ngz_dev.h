@@ -1014,9 +1014,24 @@ struct ChunkGatherSrc {
 // would with windows dealt across all XCDs (those runs were up to 15 %
 // slower, depending on where the allocations landed).  A multi-template kernel
 // deals each template's windows this way in turn.
+// NGZ_WIN_ROT (experiment): each XCD walks its stretch from a pseudo-random phase, wrapping, so
+// the XCDs' concurrent positions are not at one fixed spacing
+#ifndef NGZ_WIN_ROT
+#define NGZ_WIN_ROT 0
+#endif
 struct WinSeq {
     uint32_t first, step, end;
+    uint32_t base, len, rot;
     __device__ __forceinline__ uint32_t at(uint32_t i) const { return first + i * step; }
+    __device__ __forceinline__ uint32_t map(uint32_t W) const {
+#if NGZ_WIN_ROT
+        uint32_t r = W - base + rot;
+        if (r >= len) r -= len;
+        return base + r;
+#else
+        return W;
+#endif
+    }
 };
 
 __device__ __forceinline__ WinSeq win_seq(uint32_t nwin) {
@@ -1024,9 +1039,23 @@ __device__ __forceinline__ WinSeq win_seq(uint32_t nwin) {
     const uint32_t X = (G % 8 == 0 && G >= 8) ? 8u : 1u;
     const uint32_t x = blockIdx.x % X, l = blockIdx.x / X;
     const uint32_t per = (nwin + X - 1) / X;
-    const uint32_t start = x * per;
+    const uint32_t start = min(nwin, x * per);
     const uint32_t end = min(nwin, start + per);
-    return WinSeq{start + l, G / X, end};
+    const uint32_t len = end - start;
+    const uint32_t rot = len ? (uint32_t)(((uint64_t)((x * (uint32_t)NGZ_WIN_ROT * 2654435761u) >> 8) & 0xFFFFFF) * len >> 24) : 0;
+    return WinSeq{start + l, G / X, end, start, len, rot};
+}
+
+// NGZ_TRACE diagnostics: the constant-rate clock (100 MHz) at a window's start and end
+__device__ __forceinline__ unsigned long long win_clock(const BatchDev &B) {
+    return B.trace ? (unsigned long long)__builtin_amdgcn_s_memrealtime() : 0ull;
+}
+__device__ __forceinline__ void win_trace(const BatchDev &B, uint32_t slot, uint32_t W, unsigned long long t0) {
+    if (B.trace && threadIdx.x == 0 && W < NGZ_TRACE_WINDOWS) {
+        unsigned long long *t = B.trace + 2ull * ((uint64_t)slot * NGZ_TRACE_WINDOWS + W);
+        t[0] = t0;
+        t[1] = (unsigned long long)__builtin_amdgcn_s_memrealtime();
+    }
 }
 
 template <int RPL, bool CONSEC, uint32_t LW, class Shape, class PassFn, class StoreFn>
@@ -1047,20 +1076,23 @@ __device__ __forceinline__ void run_lds(const BatchDev &B, uint32_t slot, Shape 
     if (rt.mode == NGZ_MODE_ROW) {
         const uint64_t *rs = (const uint64_t *)(B.arena + rt.rows);
         const uint32_t *rd = (const uint32_t *)(B.arena + rt.rows + 8ull * rt.cap);
-        for (uint32_t W = ws.first; W < ws.end; W += ws.step) {
+        for (uint32_t W0 = ws.first; W0 < ws.end; W0 += ws.step) {
+            const uint32_t W = ws.map(W0);
+            const unsigned long long t0 = win_clock(B);
             const uint32_t s = W * LW + q;
             if (s < nsub) row_window<RPL, CONSEC>(B, RowTableSrc{rs, rd}, total, s, W * ROWS, P, pass);
             __syncthreads();
             store(W, blk, rt.cap);
             __syncthreads();
+            win_trace(B, slot, W, t0);
         }
         return;
     }
     // window-table entries [cb, ce) of this wave's sub-windows i0 .. i0+63 (lane i)
     auto wt_fetch = [&](uint32_t i0, uint32_t &ta, uint32_t &tb) {
         const uint32_t Wl = ws.at(i0 + lane);
-        const uint32_t sl = Wl * LW + q;
         const bool in = Wl < ws.end;
+        const uint32_t sl = (in ? ws.map(Wl) : Wl) * LW + q;
         ta = in && sl < nsub ? wt[sl] : c_end;
         tb = in && sl + 1 < nsub ? wt[sl + 1] : c_end;
     };
@@ -1078,7 +1110,9 @@ __device__ __forceinline__ void run_lds(const BatchDev &B, uint32_t slot, Shape 
     wt_fetch(0, ta, tb);
     desc_fetch(lane_u32(ta, 0), lane_u32(tb, 0), n0, n1);
     uint32_t i = 0;
-    for (uint32_t W = ws.first; W < ws.end; W += ws.step, ++i) {
+    for (uint32_t W0 = ws.first; W0 < ws.end; W0 += ws.step, ++i) {
+        const uint32_t W = ws.map(W0);
+        const unsigned long long t0 = win_clock(B);
         const uint32_t s = W * LW + q;
         const uint32_t cb = lane_u32(ta, i & 63), ce = lane_u32(tb, i & 63);
         const uint4 e0 = n0, e1 = n1;
@@ -1104,6 +1138,7 @@ __device__ __forceinline__ void run_lds(const BatchDev &B, uint32_t slot, Shape 
         __syncthreads();
         store(W, blk, rt.cap);
         __syncthreads();
+        win_trace(B, slot, W, t0);
     }
 }
 #endif

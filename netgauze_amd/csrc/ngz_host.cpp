@@ -839,6 +839,8 @@ struct HostFramed {
     Timeline tl;
 };
 
+static void trace_report(ngz_ctx *ctx, uint32_t S, hipStream_t st);
+
 int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const HostFramed *hf) {
     const uint32_t N = in->n;
     const uint32_t S = (uint32_t)ctx->slot_version.size();
@@ -920,6 +922,8 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
     uint64_t arena_cap = (uint64_t)(ratio * (double)in->bytes_size) +
                          (uint64_t)S * (1 + ctx->cap_pad_windows) * (maxwin_row + 256) + 4096;
     arena_cap = std::max<uint64_t>(arena_cap + ctx->arena_shift, ctx->d_arena.cap);
+    static const uint64_t arena_min = getenv("NGZ_ARENA_MIN_MB") ? (uint64_t)atoll(getenv("NGZ_ARENA_MIN_MB")) << 20 : 0;
+    arena_cap = std::max(arena_cap, arena_min);  // experiment: allocation size vs placement
     const uint16_t *old_rows = ctx->d_slot_row.p;
     if (ctx->d_hdr.ensure(std::max<uint32_t>(N, 1)) || ctx->d_counts.ensure(n_items) || ctx->d_scan.ensure(n_items) ||
         ctx->d_scan_tmp.ensure(scan_tmp + 1) || ctx->d_slots.ensure(std::max<uint32_t>(S, 1)) ||
@@ -989,6 +993,13 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
     B.n_slots = S;
     B.slot_row = ctx->d_slot_row.p;
     B.n_rows = A;
+    static const bool trace_on = getenv("NGZ_TRACE") && atoi(getenv("NGZ_TRACE")) != 0;
+    if (trace_on) {
+        const uint64_t n = 2ull * NGZ_TRACE_WINDOWS * std::max<uint32_t>(S, 1);
+        if (ctx->d_trace.ensure(n)) return fail(ctx, NGZ_E_NOMEM, "trace buffer");
+        HIPCHK(hipMemsetAsync(ctx->d_trace.p, 0, n * 8, st));
+        B.trace = ctx->d_trace.p;
+    }
     B.plans = ctx->d_plans.p;
     B.cur_slot = ctx->d_cur_slot.p;
     B.hdr = ctx->d_hdr.p;
@@ -1262,6 +1273,7 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
             if (rc) return rc;
         }
     }
+    if (B.trace) trace_report(ctx, S, st);
     ctx->parity ^= 1;
     // slots with records this batch: launched without a round trip next time
     ctx->pred_versions = ctx->slot_version;
@@ -1275,6 +1287,41 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
     hipEventElapsedTime(&ctx->t_decode, ctx->ev[1], ctx->ev[2]);
     hipEventElapsedTime(&ctx->t_pipeline, ctx->ev[0], ctx->ev[3]);
     return 0;
+}
+
+// NGZ_TRACE: per slot, the windows' start / end clocks (100 MHz) summarised on stderr: the launch
+// span, the mean window time in each tenth of it, and the windows finished per tenth
+static void trace_report(ngz_ctx *ctx, uint32_t S, hipStream_t st) {
+    if (hipStreamSynchronize(st) != hipSuccess) return;
+    std::vector<unsigned long long> t(2ull * NGZ_TRACE_WINDOWS * S);
+    if (hipMemcpy(t.data(), ctx->d_trace.p, t.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
+    for (uint32_t s = 0; s < S; ++s) {
+        const unsigned long long *w = t.data() + 2ull * NGZ_TRACE_WINDOWS * s;
+        unsigned long long lo = ~0ull, hi = 0;
+        uint32_t n = 0;
+        for (uint32_t i = 0; i < NGZ_TRACE_WINDOWS; ++i)
+            if (w[2 * i + 1]) {
+                lo = std::min(lo, w[2 * i]);
+                hi = std::max(hi, w[2 * i + 1]);
+                ++n;
+            }
+        if (!n || hi <= lo) continue;
+        double sum[10] = {}, cnt[10] = {}, fin[10] = {};
+        for (uint32_t i = 0; i < NGZ_TRACE_WINDOWS; ++i)
+            if (w[2 * i + 1]) {
+                const int b0 = (int)std::min<unsigned long long>(9, (w[2 * i] - lo) * 10 / (hi - lo));
+                const int b1 = (int)std::min<unsigned long long>(9, (w[2 * i + 1] - lo) * 10 / (hi - lo));
+                sum[b0] += (double)(w[2 * i + 1] - w[2 * i]) * 0.01;
+                cnt[b0] += 1;
+                fin[b1] += 1;
+            }
+        fprintf(stderr, "[ngz] trace slot %u: %u windows over %.1f us; mean window us by start tenth:", s, n,
+                (double)(hi - lo) * 0.01);
+        for (int b = 0; b < 10; ++b) fprintf(stderr, " %.1f", cnt[b] ? sum[b] / cnt[b] : 0.0);
+        fprintf(stderr, "; finished per tenth:");
+        for (int b = 0; b < 10; ++b) fprintf(stderr, " %.0f", fin[b]);
+        fprintf(stderr, "\n");
+    }
 }
 
 // Arena placement.  The decode kernel's speed depends on where in HBM the
@@ -1413,6 +1460,7 @@ int ngz_ctx_create(int device, ngz_ctx **out) {
     if (const char *e = getenv("NGZ_SPIN")) ctx->spin_wait = atoi(e) != 0;
     if (const char *e = getenv("NGZ_ARENA_CONTIG")) ctx->d_arena.contiguous = atoi(e) != 0;
     if (const char *e = getenv("NGZ_PLACE_TRIALS")) ctx->place_trials = atoi(e);
+    if (const char *e = getenv("NGZ_CAP_PAD")) ctx->cap_pad_windows = (uint32_t)std::max(0, std::min(200000, atoi(e)));
     *ctx->h_done = 0;
     if (const char *e = getenv("NGZ_BLOCKS_PER_CU")) ctx->blocks_per_cu = std::max(1, std::min(32, atoi(e)));
     if (const char *e = getenv("NGZ_LDS_BLOCKS_PER_CU")) ctx->lds_blocks_per_cu = std::max(1, std::min(512, atoi(e)));
@@ -1446,6 +1494,7 @@ void ngz_ctx_destroy(ngz_ctx *ctx) {
     ctx->d_slots.release(); ctx->d_chunks.release(); ctx->d_sets.release(); ctx->d_arena.release();
     ctx->d_proc.release(); ctx->d_summary.release(); ctx->d_recmap.release(); ctx->d_recoff.release(); ctx->d_dsum.release(); ctx->d_slot_row.release(); ctx->d_in_bytes.release(); ctx->d_in_off.release();
     ctx->d_in_len.release();
+    ctx->d_trace.release();
     ctx->d_counts2.release(); ctx->d_scan2.release(); ctx->d_scan_tmp2.release(); ctx->d_slot_row2.release();
     if (ctx->split_stream) {
         hipStreamSynchronize(ctx->split_stream);

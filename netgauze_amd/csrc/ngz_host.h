@@ -325,6 +325,7 @@ struct ngz_ctx {
     hipEvent_t split_ev[3] = {};
     uint32_t split_skip = 0;
     uint32_t batch_info = 0, pipeline_runs = 0;  // ngz_last_batch_info
+    ngzh::DevBuf<unsigned long long> d_trace;  // NGZ_TRACE window clocks
     hipEvent_t d2h_ev = nullptr;  // ngz_columns_to_host_async: the last queued copy of the columns
     bool d2h_pending = false;
     std::vector<ngzh::TemplateSetJson> tmpl_sets;  // template sets of the last batch, (dgram, set_pos) order

@@ -311,5 +311,8 @@ struct BatchDev {        // device pointers of one batch
     const uint16_t *slot_row;  // [n_slots]: the slot's row, or NGZ_NO_ROW
     uint32_t n_rows;           // rows A: counts / scan are [(2A + 1) n + 1]
     uint32_t reserved_d;
+    unsigned long long *trace;  // NGZ_TRACE (diagnostics): per slot and window, start / end clock of the
+                                // window in the generated LDS-staged kernels (ngz_dev.h run_lds), or null
 };
+#define NGZ_TRACE_WINDOWS (1u << 17)  // windows traced per slot
 #define NGZ_NO_ROW 0xFFFFu

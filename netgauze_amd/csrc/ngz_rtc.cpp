@@ -60,6 +60,7 @@ std::string cpol_defines() {
     std::string s;
     if (const char *e = getenv("NGZ_LD_AUX")) s += "#define NGZ_LD_AUX " + std::to_string(atoi(e)) + "\n";
     if (const char *e = getenv("NGZ_ST_AUX")) s += "#define NGZ_ST_AUX " + std::to_string(atoi(e)) + "\n";
+    if (const char *e = getenv("NGZ_WIN_ROT")) s += "#define NGZ_WIN_ROT " + std::to_string(atoi(e)) + "\n";
     return s;
 }
 
@@ -68,6 +69,7 @@ std::string signature(const DevPlan &P) {
                     std::to_string(P.reserved0);
     if (const char *e = getenv("NGZ_LD_AUX")) s += "la" + std::to_string(atoi(e));
     if (const char *e = getenv("NGZ_ST_AUX")) s += "sa" + std::to_string(atoi(e));
+    if (const char *e = getenv("NGZ_WIN_ROT")) s += "wr" + std::to_string(atoi(e));
     char b[96];
     for (uint32_t f = 0; f < P.n_fields; ++f) {
         const DevField &d = P.f[f];
