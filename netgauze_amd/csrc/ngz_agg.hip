@@ -147,6 +147,7 @@ struct AggParams {
     unsigned long long *arena_used;  // device bump counter (bytes)
     const unsigned long long *rank_nested[NGZ_AGG_MAX_VALUES];  // VC_RANK of a nested sub-registry: rank of
                                                                  // values 0..255, [256]: outer Unassigned
+    uint8_t op_off[8], op_w[8];  // partitioned path: operand v's byte offset and width in a payload (0: none)
 };
 
 __device__ __forceinline__ uint64_t mix64(uint64_t h, uint64_t v) {
@@ -1444,12 +1445,14 @@ __global__ __launch_bounds__(256) void k_agg_part_hist(const RecCtx C, const uin
     for (uint32_t i = threadIdx.x; i < n_part; i += blockDim.x) counts[(uint64_t)i * gridDim.x + blockIdx.x] = h[i];
 }
 
-// Payload of one record (pb = 16 NP bytes): {group, export time, sys-up time, slot | info << 16},
-// then the operands of aggregated fields 0..n_vals-1 (u64 each; zero when absent or ordered).
-// A wave's 64 payloads are staged in LDS and stored record by record: NP consecutive lanes write
-// one record's NP 16-byte pieces, so a store instruction moves 64 / NP whole payloads, each one
-// contiguous run (stored per lane, a payload went out as NP separate 16-byte pieces: 113 bytes of
-// WRITE_SIZE per 80-byte payload, the 8 of the 12.7 ms of a protocol + port push)
+// Payload of one record (pb = 16 NP bytes, a multiple of 32): {group, export time, sys-up time,
+// slot | info << 16}, then the operands of the order-free aggregated fields at their own widths
+// (P.op_off / op_w: 8-byte operands first, then 4, 2, 1; an unsigned field's operand is its column
+// width, others 8 bytes), zero padded.  Whole 32-byte sectors per payload: a payload never shares
+// a sector with another, so a line written in pieces by several waves needs no read-modify-write
+// (the 80-byte payloads of 7 u64 operands straddled sectors).  A wave's 64 payloads are staged in
+// LDS and stored record by record: NP consecutive lanes write one record's NP 16-byte pieces, so a
+// store instruction moves 64 / NP whole payloads, each one contiguous run.
 template <uint32_t NP>
 __global__ __launch_bounds__(256) void k_agg_part_scatter(const RecCtx C, const AggParams P, const uint32_t *__restrict__ rec_g,
                                                           uint32_t n_part, const uint32_t *__restrict__ offs,
@@ -1470,15 +1473,21 @@ __global__ __launch_bounds__(256) void k_agg_part_scatter(const RecCtx C, const 
             pos = atomicAdd(&cur[g >> PART_SHIFT], 1u);
             uint4 *d = &stage[w][lane * NP];
             d[0] = make_uint4(g, r.ts, r.sysup, r.slot | ((uint32_t)r.info << 16));
+#pragma unroll
+            for (uint32_t k = 1; k < NP; ++k) d[k] = make_uint4(0, 0, 0, 0);
+            uint8_t *b = (uint8_t *)d;
             const AggSlotPlan &sp = C.plans[r.slot];
-            uint64_t x[8];
 #pragma unroll
-            for (int v = 0; v < 8; ++v)
-                x[v] = v < (int)P.n_vals && sp.val_col[v] && !vc_ordered(P.val_vc[v]) ? value_operand(sp, P, v, r.row) : 0ull;
-#pragma unroll
-            for (uint32_t k = 1; k < NP; ++k)
-                d[k] = make_uint4((uint32_t)x[2 * k - 2], (uint32_t)(x[2 * k - 2] >> 32), (uint32_t)x[2 * k - 1],
-                                  (uint32_t)(x[2 * k - 1] >> 32));
+            for (int v = 0; v < 8; ++v) {
+                const uint32_t ow = P.op_w[v];
+                if (!ow || !sp.val_col[v]) continue;
+                const uint64_t x = value_operand(sp, P, v, r.row);
+                uint8_t *o = b + P.op_off[v];
+                if (ow == 8) *(uint64_t *)o = x;
+                else if (ow == 4) *(uint32_t *)o = (uint32_t)x;
+                else if (ow == 2) *(uint16_t *)o = (uint16_t)x;
+                else *o = (uint8_t)x;
+            }
         }
         spos[w][lane] = pos;
         __syncthreads();
@@ -1512,17 +1521,15 @@ __global__ __launch_bounds__(256) void k_agg_part_reduce(const AggParams P, cons
     const uint32_t p = blockIdx.x;
     const uint64_t beg = offs[(uint64_t)p * n_tiles], end = offs[(uint64_t)(p + 1) * n_tiles];
     for (uint64_t i = beg + threadIdx.x; i < end; i += blockDim.x) {
-        const uint4 *q = (const uint4 *)(pay + i * pb);
-        const uint4 h = q[0];
+        const uint8_t *q = pay + i * pb;
+        const uint4 h = *(const uint4 *)q;
         uint64_t x[8];
 #pragma unroll
-        for (int v = 0; v < 8; v += 2) {
-            x[v] = x[v + 1] = 0;
-            if (v < (int)P.n_vals) {
-                const uint4 w = q[1 + v / 2];
-                x[v] = ((uint64_t)w.y << 32) | w.x;
-                x[v + 1] = ((uint64_t)w.w << 32) | w.z;
-            }
+        for (int v = 0; v < 8; ++v) {
+            const uint32_t ow = P.op_w[v];
+            const uint8_t *o = q + P.op_off[v];
+            x[v] = ow == 8 ? *(const uint64_t *)o : ow == 4 ? *(const uint32_t *)o : ow == 2 ? *(const uint16_t *)o
+                 : ow == 1 ? *o : 0ull;
         }
         const uint32_t e = h.x & (PART_SLOTS - 1), ts = h.y, sysup = h.z, slot = h.w & 0xFFFF, info = h.w >> 16;
         const AggSlotPlan &sp = plans[slot];
@@ -3478,7 +3485,19 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, const ngz_p
                                                          groups * 8 <= (uint64_t)n_rec));
         if (part) {
             const uint32_t nt = (uint32_t)((n_rec + PART_TILE - 1) / PART_TILE), np = (uint32_t)n_part;
-            const uint32_t pb = 16 + 16 * ((P.n_vals + 1) / 2);
+            // operand layout of the payloads (k_agg_part_scatter): widest first, from byte 16
+            uint32_t at = 16;
+            for (uint32_t wd = 8; wd; wd >>= 1)
+                for (uint32_t v = 0; v < 8; ++v) {
+                    uint32_t ow = 0;
+                    if (v < P.n_vals && !vc_ordered(P.val_vc[v]) && a->val_w[v] > 0)
+                        ow = P.val_vc[v] == VC_UINT ? (uint32_t)a->val_w[v] : 8u;
+                    if (ow != wd) continue;
+                    P.op_off[v] = (uint8_t)at;
+                    P.op_w[v] = (uint8_t)ow;
+                    at += ow;
+                }
+            const uint32_t pb = (at + 31) & ~31u;
             const uint64_t nc = (uint64_t)np * nt + 1;
             size_t stb = 0;
             hipcub::DeviceScan::ExclusiveSum(nullptr, stb, (uint32_t *)nullptr, (uint32_t *)nullptr, (int)nc, st);
@@ -3500,11 +3519,9 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, const ngz_p
             hipLaunchKernelGGL(k_agg_part_hist, dim3(nt), dim3(256), 4 * np, st, C, rec_g, np, counts);
             AGG_HIP(a, hipcub::DeviceScan::ExclusiveSum(stmp, stb, counts, offs, (int)nc, st));
             switch (pb / 16) {
-            case 1: hipLaunchKernelGGL(k_agg_part_scatter<1>, dim3(nt), dim3(256), 4 * np, st, C, P, rec_g, np, offs, pay); break;
             case 2: hipLaunchKernelGGL(k_agg_part_scatter<2>, dim3(nt), dim3(256), 4 * np, st, C, P, rec_g, np, offs, pay); break;
-            case 3: hipLaunchKernelGGL(k_agg_part_scatter<3>, dim3(nt), dim3(256), 4 * np, st, C, P, rec_g, np, offs, pay); break;
             case 4: hipLaunchKernelGGL(k_agg_part_scatter<4>, dim3(nt), dim3(256), 4 * np, st, C, P, rec_g, np, offs, pay); break;
-            default: hipLaunchKernelGGL(k_agg_part_scatter<5>, dim3(nt), dim3(256), 4 * np, st, C, P, rec_g, np, offs, pay); break;
+            default: hipLaunchKernelGGL(k_agg_part_scatter<6>, dim3(nt), dim3(256), 4 * np, st, C, P, rec_g, np, offs, pay); break;
             }
             hipLaunchKernelGGL(k_agg_part_reduce, dim3(np), dim3(256), 0, st, P, a->plans, offs, nt, pay, pb, a->rows);
         } else if (P.own && !split && groups * 8 > (uint64_t)n_rec) {
