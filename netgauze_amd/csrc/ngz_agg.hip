@@ -10,8 +10,9 @@
 //                 current_time the running max of the earlier non-late items)
 //                 and its observation-domain dictionary entry (new domains are
 //                 listed for the host, which assigns them: k_agg_domfix)
-//   hipcub sum-scan over set record counts -> k_agg_recinfo: every record's row, times, plan
-//                 and datagram info, 16 bytes (one load in the record kernels)
+//   hipcub sum-scan over set record counts -> k_agg_recinfo: every set's first row, times,
+//                 plan and datagram info (16 bytes), and the set holding every 256th record;
+//                 a record kernel finds its record's set from those (ctx_of), cached loads only
 //   k_agg_claim   one lane per record: its group's slot in the HBM table
 //                 (open addressing; a new group's first record claims a slot
 //                 with a CAS on the 64-bit tag and writes the exact key).  Keys
@@ -558,23 +559,18 @@ __global__ void k_agg_domfix(const ngz_dgram_hdr *__restrict__ hdr, const unsign
 //   x: row in the slot's columns   y: export time   z: sys-up time (NetFlow v9, else 0)
 //   w: slot (bits 0-15) | datagram info (bits 16-31, DG_VALID: aggregated)
 constexpr uint16_t DG_VALID = 0x8000;
-__global__ void k_agg_recinfo(const ngz_set_info *__restrict__ sets, const uint32_t *__restrict__ rstart,
-                              uint32_t n_sets, const ngz_dgram_hdr *__restrict__ hdr,
+// The context of each set (one thread per set): {first row, export time, sys-up time (NetFlow v9),
+// slot | datagram info << 16}; and bset[b]: the set holding record 256 b (the last set starting at
+// or before it: empty sets share their successor's start)
+__global__ void k_agg_recinfo(const ngz_set_info *__restrict__ sets, uint32_t n_sets, const ngz_dgram_hdr *__restrict__ hdr,
                               const uint16_t *__restrict__ dginfo, const AggSlotPlan *__restrict__ plans,
-                              uint32_t n_dgrams, uint32_t n_slots, uint4 *__restrict__ rinfo,
-                              unsigned int *__restrict__ err) {
-    // one wave per set writes the context of each of its records
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const uint32_t n_waves = (gridDim.x * blockDim.x) >> 6;
-    for (uint32_t s = wave; s < n_sets; s += n_waves) {
+                              uint32_t n_dgrams, uint32_t n_slots, uint4 *__restrict__ sctx, unsigned int *__restrict__ err) {
+    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < n_sets; s += gridDim.x * blockDim.x) {
         const ngz_set_info si = sets[s];
-        const uint32_t n = si.n, r0 = rstart[s];
-        if (!n) continue;
         uint32_t ts = 0, sysup = 0, w = 0;
-        if (si.dgram >= n_dgrams || si.slot >= n_slots) {
-            if (lane == 0) atomicOr(err, 16u);
-        } else {
+        if (si.n && (si.dgram >= n_dgrams || si.slot >= n_slots)) {
+            atomicOr(err, 16u);
+        } else if (si.n) {
             const ngz_dgram_hdr &h = hdr[si.dgram];
             ts = h.time;
             sysup = h.version == 9 ? h.sys_up_time : 0u;
@@ -582,16 +578,47 @@ __global__ void k_agg_recinfo(const ngz_set_info *__restrict__ sets, const uint3
             if ((info & DG_USE) && plans[si.slot].usable) info |= DG_VALID;
             w = si.slot | ((uint32_t)info << 16);
         }
-        for (uint32_t i = lane; i < n; i += 64) rinfo[r0 + i] = make_uint4(si.rec0 + i, ts, sysup, w);
+        sctx[s] = make_uint4(si.rec0, ts, sysup, w);
     }
+}
+
+// last s in [lo, hi] with rstart[s] <= t
+__device__ __forceinline__ uint32_t set_search(const uint32_t *__restrict__ rstart, uint32_t lo, uint32_t hi, uint64_t t) {
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (rstart[mid] <= t) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+__global__ void k_agg_bset(const uint32_t *__restrict__ rstart, uint32_t n_sets, uint64_t n_blocks,
+                           uint32_t *__restrict__ bset) {
+    for (uint64_t b = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; b < n_blocks; b += (uint64_t)gridDim.x * blockDim.x)
+        bset[b] = set_search(rstart, 0, n_sets - 1, b << 8);
 }
 
 // Everything the record kernels share
 struct RecCtx {
-    const uint4 *rinfo;
+    const uint4 *sctx;       // per set: {first row, export time, sys-up time, slot | info << 16}
+    const uint32_t *rstart;  // per set: its first record (exclusive scan of the set sizes)
+    const uint32_t *bset;    // per 256 records: the set holding the first
+    uint32_t n_sets;
     uint64_t n_rec;
     const AggSlotPlan *plans;
 };
+
+// Record t's context {row, export time, sys-up time, slot | info << 16}: its set is between the
+// sets of records 256 floor(t / 256) and 256 (floor(t / 256) + 1), so a wave of consecutive records
+// reads the same few cached entries (a per-record table was 16 bytes of HBM per record and pass)
+__device__ __forceinline__ uint4 ctx_of(const RecCtx &C, uint64_t t) {
+    if (t >= C.n_rec) return make_uint4(0, 0, 0, 0);
+    const uint64_t b = t >> 8;
+    const uint32_t lo = C.bset[b], hi = ((b + 1) << 8) < C.n_rec ? C.bset[b + 1] : C.n_sets - 1;
+    const uint32_t s = set_search(C.rstart, lo, hi, t);
+    const uint4 c = C.sctx[s];
+    return make_uint4(c.x + (uint32_t)(t - C.rstart[s]), c.y, c.z, c.w);
+}
 
 struct Rec {
     bool valid = false, late = false;
@@ -603,7 +630,7 @@ struct Rec {
 __device__ __forceinline__ Rec rec_of(const RecCtx &C, uint64_t t, unsigned int *) {
     Rec r;
     if (t >= C.n_rec) return r;
-    const uint4 p = C.rinfo[t];
+    const uint4 p = ctx_of(C, t);
     r.row = p.x;
     r.ts = p.y;
     r.sysup = p.z;
@@ -856,7 +883,7 @@ __global__ __launch_bounds__(256, 4) void k_agg_apply(const RecCtx C, const AggP
         const uint64_t i = tile * blockDim.x + threadIdx.x;
         t = i < n ? (list ? list[i] : i) : C.n_rec;
         g = t < C.n_rec ? rec_g[t] : NONE;
-        ctx = t < C.n_rec ? C.rinfo[t] : make_uint4(0, 0, 0, 0);
+        ctx = ctx_of(C, t);
     };
     uint64_t t_next;
     uint32_t g_next;
@@ -3302,7 +3329,9 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, const ngz_p
         hipcub::DeviceRadixSort::SortPairs(nullptr, sort_tmp, (uint32_t *)nullptr, (uint32_t *)nullptr,
                                            (uint32_t *)nullptr, (uint32_t *)nullptr, (int)std::max<uint32_t>(n_rec, 1),
                                            0, 32, st);
-    const size_t rec_need = 8 * R4 + (ordered ? 4 * R4 + al(sort_tmp) : 0);
+    const uint64_t n_blk = ((uint64_t)n_rec + 255) / 256;
+    const size_t B0 = al(16ull * NS) + al(4 * (n_blk + 1));  // set contexts, block sets
+    const size_t rec_need = B0 + 4 * R4 + (ordered ? 4 * R4 + al(sort_tmp) : 0);
     if (rec_need > a->rec_cap) {
         hipFree(a->rec_buf);
         a->rec_buf = nullptr;
@@ -3310,10 +3339,11 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, const ngz_p
         if (hipMalloc(&a->rec_buf, rec_need) != hipSuccess) { restore(); upload_domains(a); return fail(a, NGZ_E_NOMEM, "record buffers"); }
         a->rec_cap = rec_need;
     }
-    uint4 *rinfo = (uint4 *)a->rec_buf;
-    uint32_t *rec_g = (uint32_t *)(a->rec_buf + 4 * R4), *claims = (uint32_t *)(a->rec_buf + 5 * R4),
-             *list_a = (uint32_t *)(a->rec_buf + 6 * R4), *list_b = (uint32_t *)(a->rec_buf + 7 * R4);
-    const RecCtx C{rinfo, (uint64_t)n_rec, a->plans};
+    uint4 *sctx = (uint4 *)a->rec_buf;
+    uint32_t *bset = (uint32_t *)(a->rec_buf + al(16ull * NS));
+    uint32_t *rec_g = (uint32_t *)(a->rec_buf + B0), *claims = (uint32_t *)(a->rec_buf + B0 + R4),
+             *list_a = (uint32_t *)(a->rec_buf + B0 + 2 * R4), *list_b = (uint32_t *)(a->rec_buf + B0 + 3 * R4);
+    const RecCtx C{sctx, rstart, bset, NS, (uint64_t)n_rec, a->plans};
     const uint32_t blocks = (uint32_t)((n_rec + 255) / 256);
     static const uint32_t grid_cap = getenv("NGZ_AGG_GRID") ? (uint32_t)std::max(1, atoi(getenv("NGZ_AGG_GRID"))) : 4096u;
     const uint32_t ig = std::max<uint32_t>(1, std::min<uint32_t>(blocks, grid_cap));
@@ -3407,8 +3437,9 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, const ngz_p
     }
     a->last_path = "general";
     {
-    hipLaunchKernelGGL(k_agg_recinfo, dim3(grid_for(64ull * NS, 256, 4096)), dim3(256), 0, st, sets, rstart, NS, hdr,
-                       dginfo, a->plans, D, S, rinfo, a->err);
+    hipLaunchKernelGGL(k_agg_recinfo, dim3(grid_for(NS, 256, 4096)), dim3(256), 0, st, sets, NS, hdr, dginfo, a->plans, D,
+                       S, sctx, a->err);
+    if (n_blk) hipLaunchKernelGGL(k_agg_bset, dim3(grid_for(n_blk, 256, 4096)), dim3(256), 0, st, rstart, NS, n_blk, bset);
     AGG_HIP(a, hipGetLastError());
     if (P.has_bytes && n_rec) {
         // byte values longer than 32 bytes: room in the arena for every tail this push can write
@@ -3547,9 +3578,9 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, const ngz_p
                                    a->err);
         }
         if (ordered) {
-            uint32_t *sk = (uint32_t *)(a->rec_buf + 8 * R4), *sv = (uint32_t *)(a->rec_buf + 9 * R4),
-                     *sk2 = (uint32_t *)(a->rec_buf + 10 * R4), *sv2 = (uint32_t *)(a->rec_buf + 11 * R4);
-            void *stmp = a->rec_buf + 12 * R4;
+            uint32_t *sk = (uint32_t *)(a->rec_buf + B0 + 4 * R4), *sv = (uint32_t *)(a->rec_buf + B0 + 5 * R4),
+                     *sk2 = (uint32_t *)(a->rec_buf + B0 + 6 * R4), *sv2 = (uint32_t *)(a->rec_buf + B0 + 7 * R4);
+            void *stmp = a->rec_buf + B0 + 8 * R4;
             AGG_HIP(a, hipMemcpyAsync(sk, rec_g, 4ull * n_rec, hipMemcpyDeviceToDevice, st));
             hipLaunchKernelGGL(k_agg_iota, dim3(grid_for(n_rec)), dim3(256), 0, st, sv, (uint64_t)n_rec);
             int end_bit = 1;

@@ -6,8 +6,8 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-r4s}
 mkdir -p $OUT
-timeout -k 10 600 python -u -m pytest tests/test_gpu_agg.py -v -m gpu --timeout 300 --timeout-method thread \
-  -k "partitioned" > $OUT/pytest.log 2>&1 || { grep -E "FAILED|Error" $OUT/pytest.log | head -20; tail -5 $OUT/pytest.log; exit 2; }
+timeout -k 10 900 python -u -m pytest tests/test_gpu_agg.py -v -m gpu --timeout 300 --timeout-method thread \
+  > $OUT/pytest.log 2>&1 || { grep -E "FAILED|Error" $OUT/pytest.log | head -20; tail -5 $OUT/pytest.log; exit 2; }
 tail -1 $OUT/pytest.log
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/agg_dport -o run -- \
   python3 bench.py --agg dport --steps 5 --warmup 1 > $OUT/agg_dport.json 2> $OUT/agg_dport.err || { tail -5 $OUT/agg_dport.err; exit 3; }
