@@ -220,7 +220,7 @@ def main():
             exchange.step(reset=True)
         return batch
 
-    for _ in range(args.warmup):
+    for _ in range(max(1, args.warmup)):  # (one untimed step even at --warmup 0: it sizes the roofline bytes)
         b = step()
     assert b.n_records == n, (b.n_records, n)
     # algorithmic bytes per launch: wire bytes read + canonical column bytes written, per template

@@ -1529,7 +1529,7 @@ __global__ __launch_bounds__(256) void k_agg_part_scatter(const RecCtx C, const 
 #pragma unroll
             for (int v = 0; v < 8; ++v) {
                 const uint32_t ow = P.op_w[v];
-                if (!ow || !sp.val_col[v]) continue;
+                if (!ow || !sp.val_col[v] || (dbg & 2)) continue;  // 2: no operand loads (measurement only)
                 const uint64_t x = value_operand(sp, P, v, r.row);
                 uint8_t *o = b + P.op_off[v];
                 if (ow == 8) *(uint64_t *)o = x;
