@@ -1465,21 +1465,29 @@ __global__ __launch_bounds__(256) void k_agg_ordered(const RecCtx C, const AggPa
 // records within a run is not kept: only order-free reductions run here (ordered classes are
 // k_agg_ordered's).
 constexpr uint32_t PART_SLOTS = 512, PART_SHIFT = 9;
-constexpr uint32_t PART_TILE = 65536;  // records per histogram / scatter workgroup (4x larger tiles
-                                       // of 1024-thread workgroups: scatter 8.0 -> 10.9 ms)
+constexpr uint32_t PART_TILE = 65536;  // records per histogram / scatter workgroup (grid size; at most
+                                       // 2048 workgroups)
 
-// counts[p * n_tiles + tile]: the tile's records headed for partition p (a record has a group
-// only if the claim found it valid)
+// Workgroup w of the histogram and scatter passes takes rounds w, w + G, w + 2G, ... of PART_ROUND
+// records (G workgroups): at any time the grid works on one contiguous stretch of records, so the
+// operand columns are read as a few sequential streams (tiles of contiguous records per workgroup
+// made ~10 000 concurrent column streams, and the operand loads ran at under 1 TB/s)
+constexpr uint32_t PART_RPT = 4;                      // records per thread and round
+constexpr uint32_t PART_ROUND = 256 * PART_RPT;
+
+// counts[p * G + w]: workgroup w's records headed for partition p (a record has a group only if
+// the claim found it valid)
 __global__ __launch_bounds__(256) void k_agg_part_hist(const RecCtx C, const uint32_t *__restrict__ rec_g, uint32_t n_part,
                                                        uint32_t *__restrict__ counts) {
     extern __shared__ uint32_t h[];
     for (uint32_t i = threadIdx.x; i < n_part; i += blockDim.x) h[i] = 0;
     __syncthreads();
-    const uint64_t t0 = (uint64_t)blockIdx.x * PART_TILE, t1 = min(t0 + PART_TILE, C.n_rec);
-    for (uint64_t t = t0 + threadIdx.x; t < t1; t += blockDim.x) {
-        const uint32_t g = rec_g[t];
-        if (g != NONE) atomicAdd(&h[g >> PART_SHIFT], 1u);
-    }
+    for (uint64_t r0 = (uint64_t)blockIdx.x * PART_ROUND; r0 < C.n_rec; r0 += (uint64_t)gridDim.x * PART_ROUND)
+        for (uint32_t k = 0; k < PART_RPT; ++k) {
+            const uint64_t t = r0 + k * 256 + threadIdx.x;
+            const uint32_t g = t < C.n_rec ? rec_g[t] : NONE;
+            if (g != NONE) atomicAdd(&h[g >> PART_SHIFT], 1u);
+        }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < n_part; i += blockDim.x) counts[(uint64_t)i * gridDim.x + blockIdx.x] = h[i];
 }
@@ -1487,259 +1495,75 @@ __global__ __launch_bounds__(256) void k_agg_part_hist(const RecCtx C, const uin
 // Payload of one record (pb = 16 NP bytes, a multiple of 32): {group, export time, sys-up time,
 // slot | info << 16}, then the operands of the order-free aggregated fields at their own widths
 // (P.op_off / op_w: 8-byte operands first, then 4, 2, 1; an unsigned field's operand is its column
-// width, others 8 bytes), zero padded.  Whole 32-byte sectors per payload: a payload never shares
-// a sector with another, so a line written in pieces by several waves needs no read-modify-write
-// (the 80-byte payloads of 7 u64 operands straddled sectors).  A wave's 64 payloads are staged in
-// LDS and stored record by record: NP consecutive lanes write one record's NP 16-byte pieces, so a
-// store instruction moves 64 / NP whole payloads, each one contiguous run.
+// width, others 8 bytes), zero padded.  A payload fills whole 32-byte sectors, so one written in
+// pieces needs no read-modify-write in DRAM (80-byte payloads of 7 u64 operands straddled sectors:
+// 113 bytes of WRITE_SIZE per payload).  Each thread builds PART_RPT payloads a round, every load of
+// the round issued before the first payload is assembled, and stores each as NP 16-byte pieces.
 template <uint32_t NP>
 __global__ __launch_bounds__(256) void k_agg_part_scatter(const RecCtx C, const AggParams P, const uint32_t *__restrict__ rec_g,
                                                           uint32_t n_part, const uint32_t *__restrict__ offs,
                                                           uint8_t *__restrict__ pay, uint32_t dbg) {
     extern __shared__ uint32_t cur[];
-    __shared__ uint4 stage[4][64 * NP];
-    __shared__ uint32_t spos[4][64];
     for (uint32_t i = threadIdx.x; i < n_part; i += blockDim.x) cur[i] = offs[(uint64_t)i * gridDim.x + blockIdx.x];
     __syncthreads();
-    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const uint64_t t0 = (uint64_t)blockIdx.x * PART_TILE, t1 = min(t0 + PART_TILE, C.n_rec);
-    // the next round's group and record context are loaded while this round's payloads are built
-    // and stored (the round is otherwise a chain of dependent loads: group, set, context, operands)
-    uint32_t g_next = t0 + threadIdx.x < t1 ? rec_g[t0 + threadIdx.x] : NONE;
-    uint4 c_next = g_next != NONE ? ctx_of(C, t0 + threadIdx.x) : make_uint4(0, 0, 0, 0);
-    for (uint64_t base = t0; base < t1; base += blockDim.x) {  // uniform over the workgroup
-        const uint64_t t = base + threadIdx.x;
-        const uint32_t g = g_next;
-        const uint4 c = c_next;
-        {
-            const uint64_t tn = t + blockDim.x;
-            g_next = tn < t1 ? rec_g[tn] : NONE;
-            c_next = g_next != NONE ? ctx_of(C, tn) : make_uint4(0, 0, 0, 0);
-        }
-        uint32_t pos = NONE;
-        if (g != NONE) {
-            const Rec r = rec_from(c);
-            pos = dbg & 1 ? (uint32_t)t : atomicAdd(&cur[g >> PART_SHIFT], 1u);  // 1: measurement only
-            uint4 *d = &stage[w][lane * NP];
-            d[0] = make_uint4(g, r.ts, r.sysup, r.slot | ((uint32_t)r.info << 16));
+    for (uint64_t r0 = (uint64_t)blockIdx.x * PART_ROUND; r0 < C.n_rec; r0 += (uint64_t)gridDim.x * PART_ROUND) {
+        uint32_t g[PART_RPT];
+        uint4 c[PART_RPT];
 #pragma unroll
-            for (uint32_t k = 1; k < NP; ++k) d[k] = make_uint4(0, 0, 0, 0);
-            uint8_t *b = (uint8_t *)d;
-            const AggSlotPlan &sp = C.plans[r.slot];
+        for (uint32_t k = 0; k < PART_RPT; ++k) {
+            const uint64_t t = r0 + k * 256 + threadIdx.x;
+            g[k] = t < C.n_rec ? rec_g[t] : NONE;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < PART_RPT; ++k)
+            c[k] = g[k] != NONE ? ctx_of(C, r0 + k * 256 + threadIdx.x) : make_uint4(0, 0, 0, 0);
+        uint64_t x[PART_RPT][8];
+#pragma unroll
+        for (uint32_t k = 0; k < PART_RPT; ++k) {
+            const uint32_t slot = c[k].w & 0xFFFF;
+            const AggSlotPlan &sp = C.plans[slot];
+#pragma unroll
+            for (int v = 0; v < 8; ++v)
+                x[k][v] = g[k] != NONE && P.op_w[v] && sp.val_col[v] && !(dbg & 2) ? value_operand(sp, P, v, c[k].x) : 0ull;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < PART_RPT; ++k) {
+            if (g[k] == NONE) continue;
+            const uint32_t pos = dbg & 1 ? (uint32_t)(r0 + k * 256 + threadIdx.x)  // 1: measurement only
+                                         : atomicAdd(&cur[g[k] >> PART_SHIFT], 1u);
+            uint32_t wd[NP * 4];
+            wd[0] = g[k];
+            wd[1] = c[k].y;
+            wd[2] = c[k].z;
+            wd[3] = c[k].w;
+#pragma unroll
+            for (uint32_t j = 4; j < NP * 4; ++j) wd[j] = 0;
 #pragma unroll
             for (int v = 0; v < 8; ++v) {
                 const uint32_t ow = P.op_w[v];
-                if (!ow || !sp.val_col[v] || (dbg & 2)) continue;  // 2: no operand loads (measurement only)
-                const uint64_t x = value_operand(sp, P, v, r.row);
-                uint8_t *o = b + P.op_off[v];
-                if (ow == 8) *(uint64_t *)o = x;
-                else if (ow == 4) *(uint32_t *)o = (uint32_t)x;
-                else if (ow == 2) *(uint16_t *)o = (uint16_t)x;
-                else *o = (uint8_t)x;
+                if (!ow) continue;
+                const uint64_t xv = x[k][v];
+                const uint32_t o = P.op_off[v], j0 = o >> 2, sh = 8 * (o & 3);
+                const uint32_t lo = ow >= 4 ? (uint32_t)xv : ow == 2 ? ((uint32_t)xv & 0xFFFFu) << sh : ((uint32_t)xv & 0xFFu) << sh;
+#pragma unroll
+                for (uint32_t j = 4; j < NP * 4; ++j) {
+                    if (j == j0) wd[j] |= lo;
+                    if (ow == 8 && j == j0 + 1) wd[j] = (uint32_t)(xv >> 32);
+                }
             }
-        }
-        spos[w][lane] = pos;
-        __syncthreads();
+            uint4 *d = (uint4 *)(pay + (uint64_t)pos * (16 * NP));
 #pragma unroll
-        for (uint32_t i = lane; i < 64 * NP; i += 64) {
-            const uint32_t rec = i / NP, k = i % NP;
-            const uint32_t p = spos[w][rec];
-            if (p != NONE) *(uint4 *)(pay + (uint64_t)p * (16 * NP) + 16 * k) = stage[w][i];
-        }
-        __syncthreads();
-    }
-}
-
-// ---- Two-level partitioning: payloads reach their partition runs in whole chunks ----
-// The one-pass scatter stores every payload alone at its partition's cursor: with ~2048 partitions
-// those are 64-byte stores to random places, a DRAM row opened per payload (the scatter of a
-// protocol + port push ran at ~1.5 TB/s).  Here a workgroup appends payloads to per-bucket chunk
-// buffers in LDS and stores a bucket's chunk (CH payloads, one contiguous run) once it fills, its
-// place claimed with one global atomic.  Level 1 buckets records by partition group (NB groups of F
-// partitions), level 2 re-buckets each group's run by partition; with NB >= partitions level 1
-// alone does it.  Chunks land in a run in claim order: only order-free reductions use this path.
-constexpr uint32_t PB_LDS = 65536;  // bytes of chunk buffers per bucketing workgroup
-
-// the partition totals (a tile's LDS histogram added into tot[])
-__global__ __launch_bounds__(256) void k_agg_part_tot(const RecCtx C, const uint32_t *__restrict__ rec_g, uint32_t n_part,
-                                                      uint32_t *__restrict__ tot) {
-    extern __shared__ uint32_t h[];
-    for (uint32_t i = threadIdx.x; i < n_part; i += blockDim.x) h[i] = 0;
-    __syncthreads();
-    const uint64_t t0 = (uint64_t)blockIdx.x * PART_TILE, t1 = min(t0 + PART_TILE, C.n_rec);
-    for (uint64_t t = t0 + threadIdx.x; t < t1; t += blockDim.x) {
-        const uint32_t g = rec_g[t];
-        if (g != NONE) atomicAdd(&h[g >> PART_SHIFT], 1u);
-    }
-    __syncthreads();
-    for (uint32_t i = threadIdx.x; i < n_part; i += blockDim.x)
-        if (h[i]) atomicAdd(&tot[i], h[i]);
-}
-
-// cursors: gcur[b] = start of partition group b's run, fcur[p] = start of partition p's run
-__global__ void k_agg_part_cur(const uint32_t *__restrict__ pstart, uint32_t n_part, uint32_t nb, uint32_t F,
-                               uint32_t *__restrict__ gcur, uint32_t *__restrict__ fcur) {
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n_part; i += gridDim.x * blockDim.x) {
-        fcur[i] = pstart[i];
-        if (i < nb) gcur[i] = pstart[min(i * F, n_part)];
-    }
-}
-
-// record t's payload in registers (layout of k_agg_part_scatter): header, operands at P.op_off
-template <uint32_t NP>
-__device__ __forceinline__ void build_payload(const RecCtx &C, const AggParams &P, uint64_t t, uint32_t g,
-                                              uint32_t (&wd)[NP * 4]) {
-    const Rec r = rec_of(C, t, nullptr);
-    wd[0] = g;
-    wd[1] = r.ts;
-    wd[2] = r.sysup;
-    wd[3] = r.slot | ((uint32_t)r.info << 16);
-#pragma unroll
-    for (uint32_t j = 4; j < NP * 4; ++j) wd[j] = 0;
-    const AggSlotPlan &sp = C.plans[r.slot];
-#pragma unroll
-    for (int v = 0; v < 8; ++v) {
-        const uint32_t ow = P.op_w[v];
-        if (!ow || !sp.val_col[v]) continue;
-        const uint64_t x = value_operand(sp, P, v, r.row);
-        const uint32_t o = P.op_off[v], j0 = o >> 2, sh = 8 * (o & 3);
-        const uint32_t lo = ow == 8 ? (uint32_t)x : ow == 4 ? (uint32_t)x : ow == 2 ? ((uint32_t)x & 0xFFFFu) << sh
-                                                                             : ((uint32_t)x & 0xFFu) << sh;
-#pragma unroll
-        for (uint32_t j = 4; j < NP * 4; ++j) {
-            if (j == j0) wd[j] |= lo;
-            if (ow == 8 && j == j0 + 1) wd[j] = (uint32_t)(x >> 32);
+            for (uint32_t j = 0; j < NP; ++j) d[j] = make_uint4(wd[4 * j], wd[4 * j + 1], wd[4 * j + 2], wd[4 * j + 3]);
         }
     }
-}
-
-// The chunk buffers of one bucketing workgroup: bucket b holds cnt[b] payloads (at most 2 CH) in
-// buf[b * 2CH ...].  add(): a payload into its bucket (or straight to the run when the buffer is
-// full: skewed pushes stay correct); flush(): every bucket holding a chunk stores CH payloads;
-// drain(): what is left, at the end of the workgroup's records.
-template <uint32_t NP>
-struct ChunkBuckets {
-    uint4 *buf;
-    uint32_t *cnt, *full, *fbase, *nfull;
-    uint32_t nb, ch;
-    uint32_t *cur;  // global run cursors, one per bucket
-    uint8_t *out;   // payload array of the runs
-    __device__ void add(uint32_t b, const uint32_t (&wd)[NP * 4]) {
-        const uint32_t s = atomicAdd(&cnt[b], 1u);
-        uint4 *d;
-        if (s < 2 * ch) {
-            d = buf + ((uint64_t)b * 2 * ch + s) * NP;
-        } else {
-            const uint32_t at = atomicAdd(&cur[b], 1u);
-            d = (uint4 *)(out + (uint64_t)at * 16 * NP);
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < NP; ++k) d[k] = make_uint4(wd[4 * k], wd[4 * k + 1], wd[4 * k + 2], wd[4 * k + 3]);
-    }
-    // call with the whole workgroup, after the adds (and a barrier)
-    __device__ void flush(bool all) {
-        for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) {
-            const uint32_t c = min(cnt[b], 2 * ch);
-            cnt[b] = c;
-            const uint32_t take = all ? c : (c >= ch ? ch : 0u);
-            if (take) {
-                const uint32_t i = atomicAdd(nfull, 1u);
-                full[i] = b | (take << 16);
-                fbase[i] = atomicAdd(&cur[b], take);
-            }
-        }
-        __syncthreads();
-        const uint32_t nf = *nfull;
-        const uint32_t per = ch * NP;  // 16-byte pieces of one chunk
-        for (uint32_t k = threadIdx.x; k < nf * per; k += blockDim.x) {
-            const uint32_t i = k / per, r = k % per, b = full[i] & 0xFFFF, take = full[i] >> 16;
-            if (r < take * NP) ((uint4 *)(out + (uint64_t)fbase[i] * 16 * NP))[r] = buf[(uint64_t)b * 2 * ch * NP + r];
-        }
-        __syncthreads();
-        if (!all)  // the rest of a flushed bucket (< CH payloads) to its front
-            for (uint32_t k = threadIdx.x; k < nf * per; k += blockDim.x) {
-                const uint32_t i = k / per, r = k % per, b = full[i] & 0xFFFF;
-                if (r < (cnt[b] - ch) * NP) buf[(uint64_t)b * 2 * ch * NP + r] = buf[((uint64_t)b * 2 * ch + ch) * NP + r];
-            }
-        __syncthreads();
-        for (uint32_t i = threadIdx.x; i < nf; i += blockDim.x) {
-            const uint32_t b = full[i] & 0xFFFF;
-            cnt[b] -= full[i] >> 16;
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) *nfull = 0;
-        __syncthreads();
-    }
-};
-
-// Level 1: a tile of records, bucketed by partition group (g >> PART_SHIFT) / F into NB chunk buffers
-template <uint32_t NP>
-__global__ __launch_bounds__(256) void k_agg_part_l1(const RecCtx C, const AggParams P, const uint32_t *__restrict__ rec_g,
-                                                     uint32_t nb, uint32_t F, uint32_t ch, uint32_t *__restrict__ gcur,
-                                                     uint8_t *__restrict__ out) {
-    extern __shared__ uint4 sbuf[];
-    __shared__ uint32_t cnt[256], full[256], fbase[256], nfull;
-    for (uint32_t b = threadIdx.x; b < nb; b += blockDim.x) cnt[b] = 0;
-    if (threadIdx.x == 0) nfull = 0;
-    __syncthreads();
-    ChunkBuckets<NP> K{sbuf, cnt, full, fbase, &nfull, nb, ch, gcur, out};
-    const uint64_t t0 = (uint64_t)blockIdx.x * PART_TILE, t1 = min(t0 + PART_TILE, C.n_rec);
-    for (uint64_t base = t0; base < t1; base += blockDim.x) {
-        const uint64_t t = base + threadIdx.x;
-        const uint32_t g = t < t1 ? rec_g[t] : NONE;
-        if (g != NONE) {
-            uint32_t wd[NP * 4];
-            build_payload<NP>(C, P, t, g, wd);
-            K.add((g >> PART_SHIFT) / F, wd);
-        }
-        __syncthreads();
-        K.flush(false);
-    }
-    K.flush(true);
-}
-
-// Level 2: a slice of partition group b's run, bucketed by partition into F chunk buffers
-template <uint32_t NP>
-__global__ __launch_bounds__(256) void k_agg_part_l2(const uint8_t *__restrict__ in, const uint32_t *__restrict__ pstart,
-                                                     uint32_t n_part, uint32_t F, uint32_t slices, uint32_t ch,
-                                                     uint32_t *__restrict__ fcur, uint8_t *__restrict__ out) {
-    extern __shared__ uint4 sbuf[];
-    __shared__ uint32_t cnt[256], full[256], fbase[256], nfull;
-    const uint32_t b = blockIdx.x / slices, k = blockIdx.x % slices;
-    const uint32_t p0 = min(b * F, n_part), p1 = min(p0 + F, n_part);
-    for (uint32_t i = threadIdx.x; i < F; i += blockDim.x) cnt[i] = 0;
-    if (threadIdx.x == 0) nfull = 0;
-    __syncthreads();
-    ChunkBuckets<NP> K{sbuf, cnt, full, fbase, &nfull, p1 - p0, ch, fcur + p0, out};
-    const uint64_t r0 = pstart[p0], r1 = pstart[p1], len = r1 - r0;
-    const uint64_t s0 = r0 + len * k / slices, s1 = r0 + len * (k + 1) / slices;
-    for (uint64_t base = s0; base < s1; base += blockDim.x) {
-        const uint64_t i = base + threadIdx.x;
-        if (i < s1) {
-            const uint4 *q = (const uint4 *)(in + i * 16 * NP);
-            uint32_t wd[NP * 4];
-#pragma unroll
-            for (uint32_t j = 0; j < NP; ++j) {
-                const uint4 v = q[j];
-                wd[4 * j] = v.x;
-                wd[4 * j + 1] = v.y;
-                wd[4 * j + 2] = v.z;
-                wd[4 * j + 3] = v.w;
-            }
-            K.add((wd[0] >> PART_SHIFT) - p0, wd);
-        }
-        __syncthreads();
-        K.flush(false);
-    }
-    K.flush(true);
 }
 
 // One workgroup per partition: its run reduced into an LDS table indexed by slot, then every
 // touched row updated in place (the reductions of FlowCacheRecord::reduce, aggregator.rs:159-198)
+template <uint32_t NP>
 __global__ __launch_bounds__(256) void k_agg_part_reduce(const AggParams P, const AggSlotPlan *__restrict__ plans,
                                                          const uint32_t *__restrict__ offs, uint32_t n_tiles,
-                                                         const uint8_t *__restrict__ pay, uint32_t pb,
-                                                         uint8_t *__restrict__ rows) {
+                                                         const uint8_t *__restrict__ pay, uint8_t *__restrict__ rows) {
     __shared__ uint32_t e_cnt[PART_SLOTS], e_tmin[PART_SLOTS], e_tmax[PART_SLOTS], e_smax[PART_SLOTS], e_vp[PART_SLOTS];
     __shared__ unsigned long long e_tpl[PART_SLOTS], e_d0[PART_SLOTS], e_d1[PART_SLOTS];
     __shared__ unsigned long long e_val[8][PART_SLOTS];
@@ -1753,26 +1577,27 @@ __global__ __launch_bounds__(256) void k_agg_part_reduce(const AggParams P, cons
     __syncthreads();
     const uint32_t p = blockIdx.x;
     const uint64_t beg = offs[(uint64_t)p * n_tiles], end = offs[(uint64_t)(p + 1) * n_tiles];
-    // each lane's next payload is loaded (whole 16-byte pieces) while the current one is reduced:
-    // the loop is a chain of dependent loads otherwise
-    const uint32_t np16 = pb / 16;
-    uint4 nxt[6];
-    auto load = [&](uint64_t i, uint4 (&w)[6]) {
+    // PART_RPT payloads per thread and round, all loaded before the first is reduced (one round
+    // trip per round, not per record)
+    for (uint64_t i0 = beg; i0 < end; i0 += (uint64_t)PART_RPT * blockDim.x) {
+        uint4 q[PART_RPT][NP];
 #pragma unroll
-        for (uint32_t j = 0; j < 6; ++j)
-            w[j] = i < end && j < np16 ? ((const uint4 *)(pay + i * pb))[j] : make_uint4(0, 0, 0, 0);
-    };
-    load(beg + threadIdx.x, nxt);
-    for (uint64_t i = beg + threadIdx.x; i < end; i += blockDim.x) {
-        uint32_t wd[24];
+        for (uint32_t k = 0; k < PART_RPT; ++k) {
+            const uint64_t i = i0 + k * blockDim.x + threadIdx.x;
 #pragma unroll
-        for (uint32_t j = 0; j < 6; ++j) {
-            wd[4 * j] = nxt[j].x;
-            wd[4 * j + 1] = nxt[j].y;
-            wd[4 * j + 2] = nxt[j].z;
-            wd[4 * j + 3] = nxt[j].w;
+            for (uint32_t j = 0; j < NP; ++j) q[k][j] = i < end ? ((const uint4 *)(pay + i * 16 * NP))[j] : make_uint4(0, 0, 0, 0);
         }
-        load(i + blockDim.x, nxt);
+#pragma unroll
+        for (uint32_t k = 0; k < PART_RPT; ++k) {
+        if (i0 + k * blockDim.x + threadIdx.x >= end) continue;
+        uint32_t wd[NP * 4];
+#pragma unroll
+        for (uint32_t j = 0; j < NP; ++j) {
+            wd[4 * j] = q[k][j].x;
+            wd[4 * j + 1] = q[k][j].y;
+            wd[4 * j + 2] = q[k][j].z;
+            wd[4 * j + 3] = q[k][j].w;
+        }
         const uint4 h = make_uint4(wd[0], wd[1], wd[2], wd[3]);
         uint64_t x[8];
 #pragma unroll
@@ -1780,7 +1605,7 @@ __global__ __launch_bounds__(256) void k_agg_part_reduce(const AggParams P, cons
             const uint32_t ow = P.op_w[v], o = P.op_off[v], j0 = o >> 2, sh = 8 * (o & 3);
             uint32_t lo = 0, hi = 0;
 #pragma unroll
-            for (uint32_t j = 4; j < 24; ++j) {
+            for (uint32_t j = 4; j < NP * 4; ++j) {
                 if (j == j0) lo = wd[j];
                 if (j == j0 + 1) hi = wd[j];
             }
@@ -1790,26 +1615,34 @@ __global__ __launch_bounds__(256) void k_agg_part_reduce(const AggParams P, cons
         const uint32_t e = h.x & (PART_SLOTS - 1), ts = h.y, sysup = h.z, slot = h.w & 0xFFFF, info = h.w >> 16;
         const AggSlotPlan &sp = plans[slot];
         const uint32_t db = (info >> 2) & 0x7F;
+        // Min / Max / Or only move one way: an entry the record cannot change (read first) takes no
+        // atomic.  After a group's first records that is most of them, and the LDS atomics (a dozen
+        // per record, 64-bit ones at half rate) were what bounded this kernel
         atomicAdd(&e_cnt[e], 1u);
-        atomicMin(&e_tmin[e], ts);
-        atomicMax(&e_tmax[e], ts);
-        if (sysup) atomicMax(&e_smax[e], sysup);
-        atomicOr(&e_tpl[e], (unsigned long long)sp.tpl_bit);
-        atomicOr(db < 64 ? &e_d0[e] : &e_d1[e], 1ull << (db & 63));
+        if (ts < e_tmin[e]) atomicMin(&e_tmin[e], ts);
+        if (ts > e_tmax[e]) atomicMax(&e_tmax[e], ts);
+        if (sysup > e_smax[e]) atomicMax(&e_smax[e], sysup);
+        const unsigned long long tb = sp.tpl_bit;
+        if ((e_tpl[e] & tb) != tb) atomicOr(&e_tpl[e], tb);
+        unsigned long long *dd = db < 64 ? &e_d0[e] : &e_d1[e];
+        const unsigned long long dbit = 1ull << (db & 63);
+        if (!(*dd & dbit)) atomicOr(dd, dbit);
         uint32_t hv = 0;
 #pragma unroll
         for (int v = 0; v < 8; ++v) {
             if (v >= (int)P.n_vals || !sp.val_col[v] || vc_ordered(P.val_vc[v])) continue;
             hv |= 1u << v;
             unsigned long long *c = &e_val[v][e];
+            const unsigned long long xv = x[v];
             switch (P.val_op[v]) {
-            case NGZ_AGG_ADD: if (x[v]) atomicAdd(c, (unsigned long long)x[v]); break;
-            case NGZ_AGG_MIN: atomicMin(c, (unsigned long long)x[v]); break;
-            case NGZ_AGG_MAX: atomicMax(c, (unsigned long long)x[v]); break;
-            default: atomicOr(c, (unsigned long long)x[v]); break;
+            case NGZ_AGG_ADD: if (xv) atomicAdd(c, xv); break;
+            case NGZ_AGG_MIN: if (xv < *c) atomicMin(c, xv); break;
+            case NGZ_AGG_MAX: if (xv > *c) atomicMax(c, xv); break;
+            default: if ((*c | xv) != *c) atomicOr(c, xv); break;
             }
         }
-        if (hv) atomicOr(&e_vp[e], hv);
+        if ((e_vp[e] & hv) != hv) atomicOr(&e_vp[e], hv);
+        }
     }
     __syncthreads();
     for (uint32_t e = threadIdx.x; e < PART_SLOTS; e += blockDim.x) {
@@ -3744,7 +3577,8 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, const ngz_p
         const bool part = part_ok && (part_env == 1 || (part_env != 0 && n_rec >= (1u << 20) && groups > 4096 &&
                                                          groups * 8 <= (uint64_t)n_rec));
         if (part) {
-            const uint32_t nt = (uint32_t)((n_rec + PART_TILE - 1) / PART_TILE), np = (uint32_t)n_part;
+            const uint32_t nt = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((n_rec + PART_TILE - 1) / PART_TILE, 2048)),
+                           np = (uint32_t)n_part;
             // operand layout of the payloads (k_agg_part_scatter): widest first, from byte 16
             uint32_t at = 16;
             for (uint32_t wd = 8; wd; wd >>= 1)
@@ -3761,12 +3595,10 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, const ngz_p
             // NGZ_AGG_SCATTER_DBG=1: payloads stored in record order (wrong results; timing of the
             // scatter without its scattered stores)
             static const uint32_t sc_dbg = getenv("NGZ_AGG_SCATTER_DBG") ? (uint32_t)atoi(getenv("NGZ_AGG_SCATTER_DBG")) : 0u;
-            // NGZ_AGG_PART2=1: two-level partitioning (k_agg_part_l1 / l2: payloads stored as whole chunks)
-            const bool two = getenv("NGZ_AGG_PART2") && atoi(getenv("NGZ_AGG_PART2")) != 0;
-            const uint64_t nc = two ? (uint64_t)np + 1 : (uint64_t)np * nt + 1;
+            const uint64_t nc = (uint64_t)np * nt + 1;
             size_t stb = 0;
             hipcub::DeviceScan::ExclusiveSum(nullptr, stb, (uint32_t *)nullptr, (uint32_t *)nullptr, (int)nc, st);
-            const size_t need = 2 * al(4 * nc) + al(stb) + (size_t)n_rec * pb * (two ? 2 : 1) + (two ? 2 * al(4ull * np) : 0);
+            const size_t need = 2 * al(4 * nc) + al(stb) + (size_t)n_rec * pb;
             if (need > a->part_cap) {
                 hipFree(a->part_buf);
                 a->part_buf = nullptr;
@@ -3780,35 +3612,6 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, const ngz_p
             uint32_t *counts = (uint32_t *)a->part_buf, *offs = (uint32_t *)(a->part_buf + al(4 * nc));
             void *stmp = a->part_buf + 2 * al(4 * nc);
             uint8_t *pay = a->part_buf + 2 * al(4 * nc) + al(stb);
-            if (two) {
-                uint8_t *pay2 = pay + (size_t)n_rec * pb;
-                uint32_t *gcur = (uint32_t *)(pay2 + (size_t)n_rec * pb), *fcur = gcur + al(4ull * np) / 4;
-                const uint32_t nb = np <= 64 ? np : 64, F = (np + nb - 1) / nb, ng = (np + F - 1) / F;
-                const uint32_t ch1 = std::max<uint32_t>(1, PB_LDS / (2 * ng * pb)), ch2 = std::max<uint32_t>(1, PB_LDS / (2 * F * pb));
-                const uint32_t slices = std::max<uint32_t>(1, 2048 / ng);
-                AGG_HIP(a, hipMemsetAsync(counts, 0, 4 * nc, st));
-                hipLaunchKernelGGL(k_agg_part_tot, dim3(nt), dim3(256), 4 * np, st, C, rec_g, np, counts);
-                AGG_HIP(a, hipcub::DeviceScan::ExclusiveSum(stmp, stb, counts, offs, (int)nc, st));
-                hipLaunchKernelGGL(k_agg_part_cur, dim3(grid_for(np)), dim3(256), 0, st, offs, np, ng, F, gcur, fcur);
-                const size_t l1 = (size_t)2 * ng * ch1 * pb, l2 = (size_t)2 * F * ch2 * pb;
-                uint8_t *run = F > 1 ? pay : pay2;  // level 1's output: the partition runs when F == 1
-                switch (pb / 16) {
-                case 2:
-                    hipLaunchKernelGGL(k_agg_part_l1<2>, dim3(nt), dim3(256), l1, st, C, P, rec_g, ng, F, ch1, gcur, run);
-                    if (F > 1) hipLaunchKernelGGL(k_agg_part_l2<2>, dim3(ng * slices), dim3(256), l2, st, pay, offs, np, F, slices, ch2, fcur, pay2);
-                    break;
-                case 4:
-                    hipLaunchKernelGGL(k_agg_part_l1<4>, dim3(nt), dim3(256), l1, st, C, P, rec_g, ng, F, ch1, gcur, run);
-                    if (F > 1) hipLaunchKernelGGL(k_agg_part_l2<4>, dim3(ng * slices), dim3(256), l2, st, pay, offs, np, F, slices, ch2, fcur, pay2);
-                    break;
-                default:
-                    hipLaunchKernelGGL(k_agg_part_l1<6>, dim3(nt), dim3(256), l1, st, C, P, rec_g, ng, F, ch1, gcur, run);
-                    if (F > 1) hipLaunchKernelGGL(k_agg_part_l2<6>, dim3(ng * slices), dim3(256), l2, st, pay, offs, np, F, slices, ch2, fcur, pay2);
-                    break;
-                }
-                hipLaunchKernelGGL(k_agg_part_reduce, dim3(np), dim3(256), 0, st, P, a->plans, offs, 1u, pay2, pb, a->rows);
-                goto part_done;
-            }
             AGG_HIP(a, hipMemsetAsync(counts + nc - 1, 0, 4, st));
             hipLaunchKernelGGL(k_agg_part_hist, dim3(nt), dim3(256), 4 * np, st, C, rec_g, np, counts);
             AGG_HIP(a, hipcub::DeviceScan::ExclusiveSum(stmp, stb, counts, offs, (int)nc, st));
@@ -3817,8 +3620,11 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, const ngz_p
             case 4: hipLaunchKernelGGL(k_agg_part_scatter<4>, dim3(nt), dim3(256), 4 * np, st, C, P, rec_g, np, offs, pay, sc_dbg); break;
             default: hipLaunchKernelGGL(k_agg_part_scatter<6>, dim3(nt), dim3(256), 4 * np, st, C, P, rec_g, np, offs, pay, sc_dbg); break;
             }
-            hipLaunchKernelGGL(k_agg_part_reduce, dim3(np), dim3(256), 0, st, P, a->plans, offs, nt, pay, pb, a->rows);
-        part_done:;
+            switch (pb / 16) {
+            case 2: hipLaunchKernelGGL(k_agg_part_reduce<2>, dim3(np), dim3(256), 0, st, P, a->plans, offs, nt, pay, a->rows); break;
+            case 4: hipLaunchKernelGGL(k_agg_part_reduce<4>, dim3(np), dim3(256), 0, st, P, a->plans, offs, nt, pay, a->rows); break;
+            default: hipLaunchKernelGGL(k_agg_part_reduce<6>, dim3(np), dim3(256), 0, st, P, a->plans, offs, nt, pay, a->rows); break;
+            }
         } else if (P.own && !split && groups * 8 > (uint64_t)n_rec) {
 
             // owners reduce their rows first, the records k_agg_apply_own lists apply atomics after

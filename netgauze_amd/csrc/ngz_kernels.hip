@@ -241,6 +241,74 @@ __device__ bool has_template_sets(const BatchDev &B, uint32_t d) {
 
 constexpr uint32_t kFrameBlock = 256;
 
+// 64 bytes of a datagram for the record walk, in this thread's 64-byte LDS slot (the window starts
+// at a 16-byte aligned address): the length prefixes of a variable-length record lie 20-40 bytes
+// apart, so most of them come out of the window already loaded instead of from a byte load of their
+// own.  Each byte load was a round trip on the walk's dependent chain (k_frame spent 86 % of its wave
+// cycles waiting); a window is four independent 16-byte loads, one round trip.  LDS, not registers:
+// k_frame has no VGPRs to spare for 16 more.
+struct WalkWin {
+    uint4 *slot;         // this thread's 64 bytes of LDS
+    uintptr_t base = 0;  // address the window starts at; 0 = empty
+    // the byte at address q; lim: end of the batch buffer (no window reaches past it)
+    __device__ __forceinline__ uint32_t byte(const uint8_t *q, const uint8_t *lim) {
+        const uintptr_t a = (uintptr_t)q;
+        if (!slot) return *q;
+        if (!base || a < base || a >= base + 64) {
+            const uintptr_t b0 = a & ~(uintptr_t)15;
+            if (b0 + 64 > (uintptr_t)lim) return *q;
+            const uint4 *v = (const uint4 *)b0;
+            const uint4 x0 = v[0], x1 = v[1], x2 = v[2], x3 = v[3];
+            slot[0] = x0;
+            slot[1] = x1;
+            slot[2] = x2;
+            slot[3] = x3;
+            base = b0;
+        }
+        return ((const uint8_t *)slot)[a - base];
+    }
+};
+
+// ngz_vlen_walk's fast form (ngz_internal.h) with the length prefixes read through a WalkWin; a
+// record the fast steps cannot complete goes to the exact form from its start, as there
+template <class F>
+__device__ uint32_t vlen_walk_win(const uint8_t *p, uint32_t pos, uint32_t end, const DevPlan &pl, uint64_t *err,
+                                  const uint8_t *lim, uint4 *slot, F &&on_rec) {
+    if (pl.walk_nv > NGZ_WALK_MAX) return ngz_vlen_walk_exact(p, pos, end, pl, err, on_rec);
+    const uint32_t minlen = pl.rec_len, nv = pl.walk_nv;
+    uint32_t fx[NGZ_WALK_MAX + 1];
+#pragma unroll
+    for (uint32_t k = 0; k <= NGZ_WALK_MAX; ++k) fx[k] = pl.walk_fixed[k];
+    WalkWin W{slot};
+    uint32_t n = 0;
+    while (minlen > 0 && end - pos >= minlen) {
+        const uint32_t start = pos;
+        bool ok = end - pos >= fx[0];
+        pos += fx[0];
+#pragma unroll
+        for (uint32_t k = 0; k < NGZ_WALK_MAX; ++k) {
+            if (k < nv && ok) {
+                uint32_t len = 0, hdr = 1;
+                ok = end - pos >= 1;
+                if (ok) {
+                    len = W.byte(p + pos, lim);
+                    if (len == 255) {
+                        ok = end - pos >= 4;
+                        if (ok) len = ((uint32_t)p[pos + 1] << 16) | ((uint32_t)p[pos + 2] << 8) | p[pos + 3];
+                        hdr = 4;
+                    }
+                }
+                ok = ok && end - pos - hdr >= len && end - pos - hdr - len >= fx[k + 1];
+                pos += hdr + len + fx[k + 1];
+            }
+        }
+        if (!ok) return n + ngz_vlen_walk_exact(p, start, end, pl, err, on_rec, n);
+        on_rec(n, start);
+        ++n;
+    }
+    return n;
+}
+
 // Datagram d's record-offset list: 16-byte aligned, at entry ceil8(offsets[d] / div + 8 d).  A
 // datagram of L bytes has at most L / div records (+ the terminator), so the lists of datagrams
 // whose bytes do not overlap do not overlap either, whole 16-byte pieces included
@@ -306,8 +374,10 @@ struct CountVis {
         vlen_err = vlen_err || *err != e0;
         return n;
     }
+    const uint8_t *lim = nullptr;  // end of the batch buffer (WalkWin loads stay inside it)
+    uint4 *win = nullptr;          // this thread's WalkWin slot in LDS
     __device__ uint32_t walk_records(const uint8_t *p, uint32_t pos, uint32_t end, const DevPlan &pl, uint64_t *err) {
-        return ngz_vlen_walk(p, pos, end, pl, err, [this](uint32_t, uint32_t at) {
+        return vlen_walk_win(p, pos, end, pl, err, lim, win, [this](uint32_t, uint32_t at) {
             if (ro) {  // the record's offset in the datagram, appended to the datagram's list
                 ro_push(at);
                 return;
@@ -357,6 +427,9 @@ __global__ void __launch_bounds__(kFrameBlock) k_frame(BatchDev B, const uint32_
     vis.summary = B.summary;
     vis.dg_end = vis.dg_off + B.lengths[d];
     vis.split = B.split;
+    vis.lim = B.bytes + B.bytes_size;
+    __shared__ uint4 wwin[kFrameBlock * 4];
+    vis.win = &wwin[threadIdx.x * 4];
     if (B.recoff) vis.ro = ngz_ro_list(B, vis.dg_off, d);
     WalkOut o;
     walk_datagram(B, hf_flag, hf_first, d, o, vis);
@@ -404,6 +477,9 @@ __global__ void __launch_bounds__(kFrameBlock) k_frame_vlen(BatchDev B) {
     vis.summary = B.summary;
     vis.dg_end = vis.dg_off + B.lengths[d];
     vis.split = 2;
+    vis.lim = B.bytes + B.bytes_size;
+    __shared__ uint4 wwin[kFrameBlock * 4];
+    vis.win = &wwin[threadIdx.x * 4];
     vis.ro = ngz_ro_list(B, vis.dg_off, d);
     WalkOut o;
     walk_datagram(B, nullptr, nullptr, d, o, vis);

@@ -470,26 +470,21 @@ def test_stale_batch_is_refused(dev):
     [(0, 4, 0, OK), (0, 11, 0, OK)],                    # protocol + destination port (bench key dport)
     [(0, 8, 0, OK), (0, 12, 0, OK), (0, 7, 0, OK), (0, 11, 0, OK), (0, 4, 0, OK)],
 ])
-@pytest.mark.parametrize("two", ["0", "1"])
-def test_partitioned_reduction(dev, keys, two, monkeypatch):
+def test_partitioned_reduction(dev, keys, monkeypatch):
     """The partitioned reduction (slot-range partitions reduced in LDS, rows updated in place),
-    forced with NGZ_AGG_PART=1, on the T20 streams with late messages and closing windows; one
-    pass of scattered payloads, or two passes of whole chunks (NGZ_AGG_PART2=1)."""
+    forced with NGZ_AGG_PART=1, on the T20 streams with late messages and closing windows."""
     monkeypatch.setenv("NGZ_AGG_PART", "1")
-    monkeypatch.setenv("NGZ_AGG_PART2", two)
     times = [1_700_000_010, 1_700_000_030, 1_700_000_015, 1_700_000_045, 1_700_000_020, 1_700_000_050,
              1_700_000_061, 1_700_000_049]
     d = t20_datagrams(6000, 100, times)
     check(keys + T20_AGG, [d[:25], d[25:]])
 
 
-@pytest.mark.parametrize("two", ["0", "1"])
-def test_partitioned_reduction_ports_captures_orders(dev, two, monkeypatch):
+def test_partitioned_reduction_ports_captures_orders(dev, monkeypatch):
     """Forced partitioned reduction: peer ports and collection times over two pushes, every
     reference capture (wide and packed keys), wrapping adds / signed min-max, and the ordered
     reductions that run after it."""
     monkeypatch.setenv("NGZ_AGG_PART", "1")
-    monkeypatch.setenv("NGZ_AGG_PART2", two)
     test_t20_multi_port_collection_times(dev)
     test_wrapping_add_and_signed_min_max(dev)
     test_ordered_reductions(dev)
@@ -523,9 +518,8 @@ def test_partitioned_equals_atomic_at_full_size(dev, monkeypatch):
     assert batch.n_records == n
     fields = [(0, 4, 0, OK), (0, 11, 0, OK)] + T20_AGG
     rows = {}
-    for mode in ("0", "1", "2"):  # atomic, partitioned in one pass, in two passes of whole chunks
-        monkeypatch.setenv("NGZ_AGG_PART", "0" if mode == "0" else "1")
-        monkeypatch.setenv("NGZ_AGG_PART2", "1" if mode == "2" else "0")
+    for mode in ("0", "1"):
+        monkeypatch.setenv("NGZ_AGG_PART", mode)
         agg = FlowAggregator(fields, capacity=1 << 20, lateness_s=60, max_peers=256)  # packed, as the bench
         for _ in range(2):
             assert agg.push(batch, 4739, 0) == 0
@@ -535,7 +529,7 @@ def test_partitioned_equals_atomic_at_full_size(dev, monkeypatch):
         raw[:, 88:92] = 0  # owner word
         rows[mode] = sorted(bytes(r) for r in raw)
     assert len(rows["1"]) > 300_000
-    assert rows["0"] == rows["1"] == rows["2"]
+    assert rows["0"] == rows["1"]
     codec.close()
 
 
