@@ -620,6 +620,29 @@ __device__ __forceinline__ uint4 ctx_of(const RecCtx &C, uint64_t t) {
     return make_uint4(c.x + (uint32_t)(t - C.rstart[s]), c.y, c.z, c.w);
 }
 
+// The slot every active lane of the wave holds (as a wave-uniform value the compiler keeps in an
+// SGPR), or NONE when they differ
+__device__ __forceinline__ uint32_t wave_uniform_slot(uint32_t slot, bool active) {
+    const uint64_t m = __ballot(active);
+    if (!m) return NONE;
+    const int l0 = __ffsll((unsigned long long)m) - 1;
+    const uint32_t s0 = (uint32_t)__shfl((int)slot, l0);
+    if (!__all(!active || slot == s0)) return NONE;
+    return __builtin_amdgcn_readfirstlane(s0);
+}
+
+// ctx_of for a caller whose lanes' records all lie in one 256-record block (t >> 8 equal across
+// the wave): the block's set bounds come through scalar loads
+__device__ __forceinline__ uint4 ctx_of_block(const RecCtx &C, uint64_t t) {
+    if (t >= C.n_rec) return make_uint4(0, 0, 0, 0);
+    const uint64_t b = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(t >> 40)) << 32) |
+                       __builtin_amdgcn_readfirstlane((uint32_t)(t >> 8));
+    const uint32_t lo = C.bset[b], hi = ((b + 1) << 8) < C.n_rec ? C.bset[b + 1] : C.n_sets - 1;
+    const uint32_t s = set_search(C.rstart, lo, hi, t);
+    const uint4 c = C.sctx[s];
+    return make_uint4(c.x + (uint32_t)(t - C.rstart[s]), c.y, c.z, c.w);
+}
+
 struct Rec {
     bool valid = false, late = false;
     uint32_t slot = 0, ts = 0, sysup = 0;
@@ -717,19 +740,23 @@ __global__ __launch_bounds__(256) void k_agg_claim(const RecCtx C, const AggPara
                                                    unsigned int *__restrict__ err) {
     for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < C.n_rec; base += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t t = base + threadIdx.x;
-        const Rec r = rec_of(C, t, err);
+        const Rec r = rec_from(ctx_of_block(C, t));  // base: a multiple of 256
         const uint64_t late_mask = __ballot(r.late);
         if ((threadIdx.x & 63) == 0 && late_mask) atomicAdd(late_count, (unsigned long long)__popcll(late_mask));
+        const uint32_t su = wave_uniform_slot(r.slot, r.valid);  // the wave's template, in an SGPR
         if (t >= C.n_rec) continue;
         uint32_t g = NONE;
         bool tentative = false, claimed = false;
         if (r.valid) {
-            const AggSlotPlan &sp = C.plans[r.slot];
-            const uint32_t ts = r.ts, win = ts - ts % 60;  // get_window_start
-            uint32_t kp;
-            KeyVal kv;
-            const uint64_t h = key_tag(sp, P, r.row, win, kp, kv);
-            g = probe<false>(sp, P, r.row, win, kp, kv, h, tags, rows, err, &tentative, &claimed);
+            auto go = [&](const AggSlotPlan &sp) {
+                const uint32_t ts = r.ts, win = ts - ts % 60;  // get_window_start
+                uint32_t kp;
+                KeyVal kv;
+                const uint64_t h = key_tag(sp, P, r.row, win, kp, kv);
+                g = probe<false>(sp, P, r.row, win, kp, kv, h, tags, rows, err, &tentative, &claimed);
+            };
+            if (su != NONE) go(C.plans[su]);
+            else go(C.plans[r.slot]);
             // every record of the group writes itself as the owner; the last store wins
             if (P.own && g != NONE) *(uint32_t *)(rows + (uint64_t)g * P.row_bytes + OWN_OFF) = (uint32_t)t;
         }
@@ -1196,14 +1223,15 @@ __global__ __launch_bounds__(256) void k_agg_apply_own(const RecCtx C, const Agg
     for (uint64_t base = wave * 64; base < C.n_rec; base += n_waves * 64) {
         const uint32_t mine = base + lane < C.n_rec ? rec_g[base + lane] : NONE;
         Rec r;
-        if (FUSED && mine != NONE) r = rec_of(C, base + lane, err);
+        if (FUSED && mine != NONE) r = rec_from(ctx_of_block(C, base + lane));  // base: a multiple of 64
         const bool owner = FUSED ? mine != NONE && r.valid : mine != NONE && (mine & OWN_BIT);
         uint64_t m = __ballot(owner);
         if (!m) continue;
         if (!FUSED && owner) rec_g[base + lane] = mine & ~OWN_BIT;  // plain group index again (k_agg_ordered sorts on it)
-        if (!FUSED && owner) r = rec_of(C, base + lane, err);
+        if (!FUSED && owner) r = rec_from(ctx_of_block(C, base + lane));
+        const uint32_t su = wave_uniform_slot(r.slot, r.valid);
         {
-            const AggSlotPlan &sp = C.plans[r.slot];
+            const AggSlotPlan &sp = su != NONE ? C.plans[su] : C.plans[r.slot];
             const uint32_t db = (r.info >> 2) & 0x7F;
             uint32_t hv = 0;
 #pragma unroll
@@ -1516,15 +1544,21 @@ __global__ __launch_bounds__(256) void k_agg_part_scatter(const RecCtx C, const 
         }
 #pragma unroll
         for (uint32_t k = 0; k < PART_RPT; ++k)
-            c[k] = g[k] != NONE ? ctx_of(C, r0 + k * 256 + threadIdx.x) : make_uint4(0, 0, 0, 0);
+            c[k] = g[k] != NONE ? ctx_of_block(C, r0 + k * 256 + threadIdx.x) : make_uint4(0, 0, 0, 0);
         uint64_t x[PART_RPT][8];
 #pragma unroll
         for (uint32_t k = 0; k < PART_RPT; ++k) {
             const uint32_t slot = c[k].w & 0xFFFF;
-            const AggSlotPlan &sp = C.plans[slot];
+            auto ops = [&](const AggSlotPlan &sp) {
 #pragma unroll
-            for (int v = 0; v < 8; ++v)
-                x[k][v] = g[k] != NONE && P.op_w[v] && sp.val_col[v] && !(dbg & 2) ? value_operand(sp, P, v, c[k].x) : 0ull;
+                for (int v = 0; v < 8; ++v)
+                    x[k][v] = g[k] != NONE && P.op_w[v] && sp.val_col[v] && !(dbg & 2) ? value_operand(sp, P, v, c[k].x) : 0ull;
+            };
+            // a wave's records nearly always share one template: its plan then comes through scalar
+            // loads (per-lane plan loads were most of this kernel's time)
+            const uint32_t su = wave_uniform_slot(slot, g[k] != NONE);
+            if (su != NONE) ops(C.plans[su]);
+            else ops(C.plans[slot]);
         }
 #pragma unroll
         for (uint32_t k = 0; k < PART_RPT; ++k) {
@@ -1613,7 +1647,8 @@ __global__ __launch_bounds__(256) void k_agg_part_reduce(const AggParams P, cons
                  : ow == 1 ? (uint64_t)((lo >> sh) & 0xFFu) : 0ull;
         }
         const uint32_t e = h.x & (PART_SLOTS - 1), ts = h.y, sysup = h.z, slot = h.w & 0xFFFF, info = h.w >> 16;
-        const AggSlotPlan &sp = plans[slot];
+        const uint32_t su = wave_uniform_slot(slot, true);
+        const AggSlotPlan &sp = su != NONE ? plans[su] : plans[slot];
         const uint32_t db = (info >> 2) & 0x7F;
         // Min / Max / Or only move one way: an entry the record cannot change (read first) takes no
         // atomic.  After a group's first records that is most of them, and the LDS atomics (a dozen
