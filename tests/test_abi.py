@@ -141,6 +141,18 @@ def test_ctx_create_without_device_fails_cleanly():
     assert not ctx.value
 
 
+def test_column_copies_reject_bad_arguments_without_device():
+    """ngz_columns_to_host / _async: a null context, a null destination with room, or an unknown
+    flag is NGZ_E_INVALID before any device call."""
+    from netgauze_amd import _lib
+    lib = _lib.load()
+    buf = ctypes.create_string_buffer(64)
+    assert lib.ngz_columns_to_host(None, buf, 64) == -1
+    assert lib.ngz_columns_to_host_async(None, buf, 64, None, 0) == -1
+    assert lib.ngz_columns_to_host_async(None, None, 64, None, 1) == -1
+    assert lib.ngz_columns_to_host_async(None, buf, 64, None, 2) == -1
+
+
 def test_product_does_not_import_oracle():
     """The product path never routes through the CPU oracle."""
     pkg = os.path.join(ROOT, "netgauze_amd")

@@ -2,10 +2,10 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
-OUT=gpurun_out/r4z
+OUT=gpurun_out/${TAG:-r4z}
 mkdir -p $OUT
 timeout -k 10 600 python -u -m pytest tests/test_gpu_agg.py -v -m gpu --timeout 300 --timeout-method thread \
-  -k "partitioned" > $OUT/pytest.log 2>&1 || { grep -E "FAILED|Error" $OUT/pytest.log | head -20; tail -5 $OUT/pytest.log; exit 2; }
+  > $OUT/pytest.log 2>&1 || { grep -E "FAILED|Error" $OUT/pytest.log | head -20; tail -5 $OUT/pytest.log; exit 2; }
 tail -1 $OUT/pytest.log
 for K in dport proto_dir 5tuple; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/agg_$K -o run -- \
