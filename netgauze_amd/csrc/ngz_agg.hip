@@ -1594,7 +1594,7 @@ __global__ __launch_bounds__(256) void k_agg_part_scatter(const RecCtx C, const 
 
 // One workgroup per partition: its run reduced into an LDS table indexed by slot, then every
 // touched row updated in place (the reductions of FlowCacheRecord::reduce, aggregator.rs:159-198)
-template <uint32_t NP>
+template <uint32_t NP, uint32_t RPT>
 __global__ __launch_bounds__(256) void k_agg_part_reduce(const AggParams P, const AggSlotPlan *__restrict__ plans,
                                                          const uint32_t *__restrict__ offs, uint32_t n_tiles,
                                                          const uint8_t *__restrict__ pay, uint8_t *__restrict__ rows) {
@@ -1611,18 +1611,18 @@ __global__ __launch_bounds__(256) void k_agg_part_reduce(const AggParams P, cons
     __syncthreads();
     const uint32_t p = blockIdx.x;
     const uint64_t beg = offs[(uint64_t)p * n_tiles], end = offs[(uint64_t)(p + 1) * n_tiles];
-    // PART_RPT payloads per thread and round, all loaded before the first is reduced (one round
+    // RPT payloads per thread and round, all loaded before the first is reduced (one round
     // trip per round, not per record)
-    for (uint64_t i0 = beg; i0 < end; i0 += (uint64_t)PART_RPT * blockDim.x) {
-        uint4 q[PART_RPT][NP];
+    for (uint64_t i0 = beg; i0 < end; i0 += (uint64_t)RPT * blockDim.x) {
+        uint4 q[RPT][NP];
 #pragma unroll
-        for (uint32_t k = 0; k < PART_RPT; ++k) {
+        for (uint32_t k = 0; k < RPT; ++k) {
             const uint64_t i = i0 + k * blockDim.x + threadIdx.x;
 #pragma unroll
             for (uint32_t j = 0; j < NP; ++j) q[k][j] = i < end ? ((const uint4 *)(pay + i * 16 * NP))[j] : make_uint4(0, 0, 0, 0);
         }
 #pragma unroll
-        for (uint32_t k = 0; k < PART_RPT; ++k) {
+        for (uint32_t k = 0; k < RPT; ++k) {
         if (i0 + k * blockDim.x + threadIdx.x >= end) continue;
         uint32_t wd[NP * 4];
 #pragma unroll
@@ -3655,10 +3655,15 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, const ngz_p
             case 4: hipLaunchKernelGGL(k_agg_part_scatter<4>, dim3(nt), dim3(256), 4 * np, st, C, P, rec_g, np, offs, pay, sc_dbg); break;
             default: hipLaunchKernelGGL(k_agg_part_scatter<6>, dim3(nt), dim3(256), 4 * np, st, C, P, rec_g, np, offs, pay, sc_dbg); break;
             }
-            switch (pb / 16) {
-            case 2: hipLaunchKernelGGL(k_agg_part_reduce<2>, dim3(np), dim3(256), 0, st, P, a->plans, offs, nt, pay, a->rows); break;
-            case 4: hipLaunchKernelGGL(k_agg_part_reduce<4>, dim3(np), dim3(256), 0, st, P, a->plans, offs, nt, pay, a->rows); break;
-            default: hipLaunchKernelGGL(k_agg_part_reduce<6>, dim3(np), dim3(256), 0, st, P, a->plans, offs, nt, pay, a->rows); break;
+            // payloads per thread and round in the reduce (NGZ_AGG_RED_RPT 1 or 4; A/B knob)
+            static const uint32_t red_rpt = getenv("NGZ_AGG_RED_RPT") && atoi(getenv("NGZ_AGG_RED_RPT")) == 1 ? 1u : 4u;
+            switch (pb / 16 * 8 + red_rpt) {
+            case 17: hipLaunchKernelGGL((k_agg_part_reduce<2, 1>), dim3(np), dim3(256), 0, st, P, a->plans, offs, nt, pay, a->rows); break;
+            case 20: hipLaunchKernelGGL((k_agg_part_reduce<2, 4>), dim3(np), dim3(256), 0, st, P, a->plans, offs, nt, pay, a->rows); break;
+            case 33: hipLaunchKernelGGL((k_agg_part_reduce<4, 1>), dim3(np), dim3(256), 0, st, P, a->plans, offs, nt, pay, a->rows); break;
+            case 36: hipLaunchKernelGGL((k_agg_part_reduce<4, 4>), dim3(np), dim3(256), 0, st, P, a->plans, offs, nt, pay, a->rows); break;
+            case 49: hipLaunchKernelGGL((k_agg_part_reduce<6, 1>), dim3(np), dim3(256), 0, st, P, a->plans, offs, nt, pay, a->rows); break;
+            default: hipLaunchKernelGGL((k_agg_part_reduce<6, 4>), dim3(np), dim3(256), 0, st, P, a->plans, offs, nt, pay, a->rows); break;
             }
         } else if (P.own && !split && groups * 8 > (uint64_t)n_rec) {
 
