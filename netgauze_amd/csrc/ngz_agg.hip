@@ -460,6 +460,29 @@ __host__ __device__ __forceinline__ uint32_t bitrev8(uint32_t x) {
 // sub-registry (forwardingStatus) orders by its outer variant (one per 64-value group, then
 // Unassigned), then by the reason enum's discriminant, then by the value: a host-built table
 // (rank_nested, the value in the low 32 bits).
+// value_operand from a cell's bytes already loaded (raw: the w-byte cell, little-endian, zero-extended)
+__device__ __forceinline__ uint64_t operand_of_raw(const AggSlotPlan &sp, const AggParams &P, uint32_t v, uint64_t raw) {
+    const uint8_t vc = P.val_vc[v];
+    const uint32_t w = sp.val_w[v];
+    uint64_t x = raw;
+    if (vc == VC_DTFRAC) x = (raw << 32) | (raw >> 32);  // {u32 secs, u32 nanos} -> (secs, nanos), as load_value
+    else if (vc == VC_SINT && w < 8) {
+        const uint32_t sh = 64 - 8 * w;
+        x = (uint64_t)(((int64_t)(x << sh)) >> sh);
+    }
+    if (vc == VC_SINT && (P.val_op[v] == NGZ_AGG_MIN || P.val_op[v] == NGZ_AGG_MAX)) x ^= 1ull << 63;
+    if (vc == VC_RANK) {
+        if (P.val_tcp[v]) x = bitrev8((uint32_t)x & 0xFF);
+        else if (const unsigned long long *nr = P.rank_nested[v]) x = x < 256 ? nr[x] : nr[256] | x;
+        else {
+            const uint32_t *known = P.rank_known[v];
+            const bool reg = x < 65536 && known && ((known[x >> 5] >> (x & 31)) & 1);
+            if (!reg) x |= 1ull << 32;
+        }
+    }
+    return x;
+}
+
 __device__ __forceinline__ uint64_t value_operand(const AggSlotPlan &sp, const AggParams &P, uint32_t v, uint64_t row) {
     const uint8_t vc = P.val_vc[v];
     uint64_t x = load_value(sp.val_col[v] + row * sp.val_w[v], sp.val_w[v], vc == VC_RANK ? VC_UINT : vc);
@@ -1534,36 +1557,83 @@ __global__ __launch_bounds__(256) void k_agg_part_scatter(const RecCtx C, const 
     extern __shared__ uint32_t cur[];
     for (uint32_t i = threadIdx.x; i < n_part; i += blockDim.x) cur[i] = offs[(uint64_t)i * gridDim.x + blockIdx.x];
     __syncthreads();
+    // thread i of a round takes records r0 + 4i .. r0 + 4i + 3 (a wave: one aligned 256-record
+    // block): its group ids come in one 16-byte load and, when the four are consecutive rows of one
+    // template, each operand column in one load of 4 cells (4, 8, 16 or 2x16 bytes) -- a quarter of
+    // the load instructions of a record per lane
     for (uint64_t r0 = (uint64_t)blockIdx.x * PART_ROUND; r0 < C.n_rec; r0 += (uint64_t)gridDim.x * PART_ROUND) {
+        const uint64_t t0 = r0 + PART_RPT * threadIdx.x;
         uint32_t g[PART_RPT];
         uint4 c[PART_RPT];
+        if (t0 + PART_RPT <= C.n_rec) {
+            const uint4 gg = *(const uint4 *)(rec_g + t0);
+            g[0] = gg.x;
+            g[1] = gg.y;
+            g[2] = gg.z;
+            g[3] = gg.w;
+        } else {
 #pragma unroll
-        for (uint32_t k = 0; k < PART_RPT; ++k) {
-            const uint64_t t = r0 + k * 256 + threadIdx.x;
-            g[k] = t < C.n_rec ? rec_g[t] : NONE;
+            for (uint32_t k = 0; k < PART_RPT; ++k) g[k] = t0 + k < C.n_rec ? rec_g[t0 + k] : NONE;
         }
 #pragma unroll
         for (uint32_t k = 0; k < PART_RPT; ++k)
-            c[k] = g[k] != NONE ? ctx_of_block(C, r0 + k * 256 + threadIdx.x) : make_uint4(0, 0, 0, 0);
+            c[k] = g[k] != NONE ? ctx_of_block(C, t0 + k) : make_uint4(0, 0, 0, 0);
         uint64_t x[PART_RPT][8];
+        const uint32_t slot0 = c[0].w & 0xFFFF;
+        bool quad = (dbg & 2) == 0;
 #pragma unroll
-        for (uint32_t k = 0; k < PART_RPT; ++k) {
-            const uint32_t slot = c[k].w & 0xFFFF;
-            auto ops = [&](const AggSlotPlan &sp) {
+        for (uint32_t k = 0; k < PART_RPT; ++k)
+            quad = quad && g[k] != NONE && (c[k].w & 0xFFFF) == slot0 && c[k].x == c[0].x + k;
+        quad = quad && (c[0].x & 3) == 0;
+        const uint32_t suq = wave_uniform_slot(slot0, quad);
+        if (quad && suq != NONE) {
+            const AggSlotPlan &sp = C.plans[suq];
+#pragma unroll
+            for (int v = 0; v < 8; ++v) {
+                uint64_t raw[PART_RPT] = {0, 0, 0, 0};
+                const uint32_t wv = sp.val_w[v];
+                if (P.op_w[v] && sp.val_col[v] && wv != 1 && wv != 2 && wv != 4 && wv != 8) {
+                    // other widths (byte-wise OR of a 3..7-byte cell): cell by cell
+#pragma unroll
+                    for (uint32_t k = 0; k < PART_RPT; ++k) x[k][v] = value_operand(sp, P, v, c[k].x);
+                    continue;
+                }
+                if (P.op_w[v] && sp.val_col[v]) {
+                    const uint32_t w = wv;
+                    const uint8_t *b = sp.val_col[v] + (uint64_t)c[0].x * w;
+                    if (w == 1) {
+                        const uint32_t q = *(const uint32_t *)b;
+                        raw[0] = q & 0xFF; raw[1] = (q >> 8) & 0xFF; raw[2] = (q >> 16) & 0xFF; raw[3] = q >> 24;
+                    } else if (w == 2) {
+                        const uint2 q = *(const uint2 *)b;
+                        raw[0] = q.x & 0xFFFF; raw[1] = q.x >> 16; raw[2] = q.y & 0xFFFF; raw[3] = q.y >> 16;
+                    } else if (w == 4) {
+                        const uint4 q = *(const uint4 *)b;
+                        raw[0] = q.x; raw[1] = q.y; raw[2] = q.z; raw[3] = q.w;
+                    } else {
+                        const uint4 q0 = *(const uint4 *)b, q1 = *(const uint4 *)(b + 16);
+                        raw[0] = ((uint64_t)q0.y << 32) | q0.x; raw[1] = ((uint64_t)q0.w << 32) | q0.z;
+                        raw[2] = ((uint64_t)q1.y << 32) | q1.x; raw[3] = ((uint64_t)q1.w << 32) | q1.z;
+                    }
+                }
+#pragma unroll
+                for (uint32_t k = 0; k < PART_RPT; ++k)
+                    x[k][v] = P.op_w[v] && sp.val_col[v] ? operand_of_raw(sp, P, v, raw[k]) : 0ull;
+            }
+        } else {
+#pragma unroll
+            for (uint32_t k = 0; k < PART_RPT; ++k) {
+                const uint32_t slot = c[k].w & 0xFFFF;
+                const AggSlotPlan &sp = C.plans[slot];
 #pragma unroll
                 for (int v = 0; v < 8; ++v)
                     x[k][v] = g[k] != NONE && P.op_w[v] && sp.val_col[v] && !(dbg & 2) ? value_operand(sp, P, v, c[k].x) : 0ull;
-            };
-            // a wave's records nearly always share one template: its plan then comes through scalar
-            // loads (per-lane plan loads were most of this kernel's time)
-            const uint32_t su = wave_uniform_slot(slot, g[k] != NONE);
-            if (su != NONE) ops(C.plans[su]);
-            else ops(C.plans[slot]);
+            }
         }
 #pragma unroll
         for (uint32_t k = 0; k < PART_RPT; ++k) {
             if (g[k] == NONE) continue;
-            const uint32_t pos = dbg & 1 ? (uint32_t)(r0 + k * 256 + threadIdx.x)  // 1: measurement only
+            const uint32_t pos = dbg & 1 ? (uint32_t)(t0 + k)  // 1: measurement only
                                          : atomicAdd(&cur[g[k] >> PART_SHIFT], 1u);
             uint32_t wd[NP * 4];
             wd[0] = g[k];
@@ -1595,7 +1665,7 @@ __global__ __launch_bounds__(256) void k_agg_part_scatter(const RecCtx C, const 
 // One workgroup per partition: its run reduced into an LDS table indexed by slot, then every
 // touched row updated in place (the reductions of FlowCacheRecord::reduce, aggregator.rs:159-198)
 template <uint32_t NP, uint32_t RPT>
-__global__ __launch_bounds__(256) void k_agg_part_reduce(const AggParams P, const AggSlotPlan *__restrict__ plans,
+__global__ __launch_bounds__(1024) void k_agg_part_reduce(const AggParams P, const AggSlotPlan *__restrict__ plans,
                                                          const uint32_t *__restrict__ offs, uint32_t n_tiles,
                                                          const uint8_t *__restrict__ pay, uint8_t *__restrict__ rows) {
     __shared__ uint32_t e_cnt[PART_SLOTS], e_tmin[PART_SLOTS], e_tmax[PART_SLOTS], e_smax[PART_SLOTS], e_vp[PART_SLOTS];
@@ -3657,13 +3727,16 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, const ngz_p
             }
             // payloads per thread and round in the reduce (NGZ_AGG_RED_RPT 1 or 4; A/B knob)
             static const uint32_t red_rpt = getenv("NGZ_AGG_RED_RPT") && atoi(getenv("NGZ_AGG_RED_RPT")) == 1 ? 1u : 4u;
+            // threads per partition workgroup (one LDS table per workgroup: more threads, more waves
+            // per CU on the same LDS; NGZ_AGG_RED_THREADS A/B knob)
+            static const uint32_t red_thr = getenv("NGZ_AGG_RED_THREADS") ? (uint32_t)std::max(64, std::min(1024, atoi(getenv("NGZ_AGG_RED_THREADS")))) / 64 * 64 : 256u;
             switch (pb / 16 * 8 + red_rpt) {
-            case 17: hipLaunchKernelGGL((k_agg_part_reduce<2, 1>), dim3(np), dim3(256), 0, st, P, a->plans, offs, nt, pay, a->rows); break;
-            case 20: hipLaunchKernelGGL((k_agg_part_reduce<2, 4>), dim3(np), dim3(256), 0, st, P, a->plans, offs, nt, pay, a->rows); break;
-            case 33: hipLaunchKernelGGL((k_agg_part_reduce<4, 1>), dim3(np), dim3(256), 0, st, P, a->plans, offs, nt, pay, a->rows); break;
-            case 36: hipLaunchKernelGGL((k_agg_part_reduce<4, 4>), dim3(np), dim3(256), 0, st, P, a->plans, offs, nt, pay, a->rows); break;
-            case 49: hipLaunchKernelGGL((k_agg_part_reduce<6, 1>), dim3(np), dim3(256), 0, st, P, a->plans, offs, nt, pay, a->rows); break;
-            default: hipLaunchKernelGGL((k_agg_part_reduce<6, 4>), dim3(np), dim3(256), 0, st, P, a->plans, offs, nt, pay, a->rows); break;
+            case 17: hipLaunchKernelGGL((k_agg_part_reduce<2, 1>), dim3(np), dim3(red_thr), 0, st, P, a->plans, offs, nt, pay, a->rows); break;
+            case 20: hipLaunchKernelGGL((k_agg_part_reduce<2, 4>), dim3(np), dim3(red_thr), 0, st, P, a->plans, offs, nt, pay, a->rows); break;
+            case 33: hipLaunchKernelGGL((k_agg_part_reduce<4, 1>), dim3(np), dim3(red_thr), 0, st, P, a->plans, offs, nt, pay, a->rows); break;
+            case 36: hipLaunchKernelGGL((k_agg_part_reduce<4, 4>), dim3(np), dim3(red_thr), 0, st, P, a->plans, offs, nt, pay, a->rows); break;
+            case 49: hipLaunchKernelGGL((k_agg_part_reduce<6, 1>), dim3(np), dim3(red_thr), 0, st, P, a->plans, offs, nt, pay, a->rows); break;
+            default: hipLaunchKernelGGL((k_agg_part_reduce<6, 4>), dim3(np), dim3(red_thr), 0, st, P, a->plans, offs, nt, pay, a->rows); break;
             }
         } else if (P.own && !split && groups * 8 > (uint64_t)n_rec) {
 
