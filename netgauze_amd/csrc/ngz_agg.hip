@@ -3728,8 +3728,9 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, const ngz_p
             // payloads per thread and round in the reduce (NGZ_AGG_RED_RPT 1 or 4; A/B knob)
             static const uint32_t red_rpt = getenv("NGZ_AGG_RED_RPT") && atoi(getenv("NGZ_AGG_RED_RPT")) == 1 ? 1u : 4u;
             // threads per partition workgroup (one LDS table per workgroup: more threads, more waves
-            // per CU on the same LDS; NGZ_AGG_RED_THREADS A/B knob)
-            static const uint32_t red_thr = getenv("NGZ_AGG_RED_THREADS") ? (uint32_t)std::max(64, std::min(1024, atoi(getenv("NGZ_AGG_RED_THREADS")))) / 64 * 64 : 256u;
+            // per CU on the same LDS; dport push 11.9 -> 10.4 ms at 512, 10.7 at 1024; knob
+            // NGZ_AGG_RED_THREADS)
+            static const uint32_t red_thr = getenv("NGZ_AGG_RED_THREADS") ? (uint32_t)std::max(64, std::min(1024, atoi(getenv("NGZ_AGG_RED_THREADS")))) / 64 * 64 : 512u;
             switch (pb / 16 * 8 + red_rpt) {
             case 17: hipLaunchKernelGGL((k_agg_part_reduce<2, 1>), dim3(np), dim3(red_thr), 0, st, P, a->plans, offs, nt, pay, a->rows); break;
             case 20: hipLaunchKernelGGL((k_agg_part_reduce<2, 4>), dim3(np), dim3(red_thr), 0, st, P, a->plans, offs, nt, pay, a->rows); break;
