@@ -94,7 +94,7 @@ __device__ __forceinline__ uint16_t resolve_slot(const BatchDev &B, uint32_t pid
 // position of the first record.  Template sets end the walk with NGZ_FR_HOST.
 template <class V>
 __device__ void walk_datagram(const BatchDev &B, const uint32_t *__restrict__ hf_flag, const uint32_t *__restrict__ hf_first,
-                              uint32_t d, WalkOut &o, V &vis, const uint8_t *staged = nullptr) {
+                              uint32_t d, WalkOut &o, V &vis) {
     o.status = NGZ_FR_OK;
     o.version = o.length = o.time = o.seq = o.domain = o.sysup = o.nsets = 0;
     o.err = NGZ_NO_ERR;
@@ -112,17 +112,10 @@ __device__ void walk_datagram(const BatchDev &B, const uint32_t *__restrict__ hf
         }
         return;
     }
-    // staged: the datagram's bytes copied to LDS by k_frame (the walk reads them there)
-    const uint8_t *p = staged ? staged : B.bytes + B.offsets[d];
+    const uint8_t *p = B.bytes + B.offsets[d];
     const uint32_t dl = B.lengths[d];
     HdrWin H;
-    if (staged) {
-        H.ok = false;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) H.w[j] = 0;
-    } else {
-        hdr_window(B, p, H);
-    }
+    hdr_window(B, p, H);
     // codec.rs:197-209: need the 16-byte header and buf.len() >= u16 at [2..4]
     if (dl < 16) { o.status = NGZ_FR_NEED_MORE; return; }
     const uint32_t ver = H.ok ? hw_be16(H, 0) : be16(p), len = H.ok ? hw_be16(H, 2) : be16(p + 2);
@@ -423,9 +416,9 @@ struct CountVis {
     }
 };
 
-// One datagram's framing (k_frame's per-thread work); staged: its bytes in LDS, or null
-__device__ __forceinline__ void frame_one(const BatchDev &B, const uint32_t *hf_flag, const uint32_t *hf_first, uint32_t d,
-                                          const uint8_t *staged, uint4 *win) {
+__global__ void __launch_bounds__(kFrameBlock) k_frame(BatchDev B, const uint32_t *hf_flag, const uint32_t *hf_first) {
+    const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d >= B.n) return;
     // this datagram's column of the count matrix starts at zero (no memset pass)
     for (uint32_t r = 0; r < 2 * B.n_rows; ++r) B.counts[(uint64_t)r * B.n + d] = 0;
     if (d == 0) B.counts[(uint64_t)(2 * B.n_rows + 1) * B.n] = 0;  // the scan's trailing element
@@ -435,10 +428,11 @@ __device__ __forceinline__ void frame_one(const BatchDev &B, const uint32_t *hf_
     vis.dg_end = vis.dg_off + B.lengths[d];
     vis.split = B.split;
     vis.lim = B.bytes + B.bytes_size;
-    vis.win = staged ? nullptr : win;  // staged bytes are read in LDS directly
+    __shared__ uint4 wwin[kFrameBlock * 4];
+    vis.win = &wwin[threadIdx.x * 4];
     if (B.recoff) vis.ro = ngz_ro_list(B, vis.dg_off, d);
     WalkOut o;
-    walk_datagram(B, hf_flag, hf_first, d, o, vis, staged);
+    walk_datagram(B, hf_flag, hf_first, d, o, vis);
     vis.mark_flush();
     if (vis.ro) vis.ro_finish();  // end of the list
     // a walk that ended OK visited every set (template sets end it with HOST)
@@ -466,71 +460,6 @@ __device__ __forceinline__ void frame_one(const BatchDev &B, const uint32_t *hf_
     ((ngz_dgram_hdr *)B.hdr)[d] = h;
     if (o.status == NGZ_FR_HOST && !(hf_flag && hf_flag[d])) atomicAdd(&B.summary->n_host, 1u);
     if (o.status == NGZ_FR_UNSUPPORTED) atomicAdd(&B.summary->n_unsupported, 1u);
-}
-
-// Framing, one wave per 64 datagrams, in four rounds of 16.  Each round the wave first copies the
-// round's IPFIX datagrams of at most kStageSlot - 15 bytes into LDS with coalesced 16-byte loads,
-// then the round's 16 lanes walk them there.  The variable-length record walk reads every length
-// prefix of a datagram, one dependent load at a time; from HBM each was a scattered line request
-// per lane (k_frame spent 86 % of its wave cycles waiting), from LDS it is a short local read.
-// Other datagrams (NetFlow v9: no record walk; larger ones; host-framed) are walked in place.
-constexpr uint32_t kStageSlot = 1536, kStageGroup = 16;
-
-__global__ void __launch_bounds__(64) k_frame(BatchDev B, const uint32_t *hf_flag, const uint32_t *hf_first) {
-    __shared__ uint4 stg[kStageGroup * kStageSlot / 16];
-    __shared__ uint4 wwin[64 * 4];
-    __shared__ uint32_t pre[kStageGroup + 1];
-    __shared__ uint64_t abase[kStageGroup];
-    const uint32_t lane = threadIdx.x, d0 = blockIdx.x * 64;
-    for (uint32_t r = 0; r < 64 / kStageGroup; ++r) {
-        // lanes 0..15: may datagram d0 + 16 r + lane be staged, and from which aligned address
-        uint64_t a16 = 0;
-        uint32_t pieces = 0;
-        if (lane < kStageGroup) {
-            const uint32_t d = d0 + kStageGroup * r + lane;
-            if (d < B.n && !(hf_flag && hf_flag[d])) {
-                const uint64_t off = B.offsets[d];
-                const uint32_t len = B.lengths[d];
-                a16 = off & ~15ull;
-                const uint64_t span = off + len - a16;
-                const uint32_t pc = (uint32_t)((span + 15) / 16);
-                if (len >= 4 && span <= kStageSlot && a16 + 16ull * pc <= B.bytes_size && be16(B.bytes + off) == 10)
-                    pieces = pc;
-            }
-        }
-        // prefix of the pieces over the round's datagrams, then one flat copy loop over all of them
-        uint32_t incl = pieces;
-#pragma unroll
-        for (uint32_t sh = 1; sh < kStageGroup; sh <<= 1) {
-            const uint32_t v = (uint32_t)__shfl_up((int)incl, sh, 64);
-            if (lane >= sh && lane < kStageGroup) incl += v;
-        }
-        if (lane < kStageGroup) {
-            pre[lane + 1] = incl;
-            abase[lane] = a16;
-        }
-        if (lane == 0) pre[0] = 0;
-        __syncthreads();
-        const uint32_t total = pre[kStageGroup];
-        for (uint32_t i = lane; i < total; i += 64) {
-            uint32_t j = 0;
-#pragma unroll
-            for (uint32_t k = 1; k < kStageGroup; ++k) j += i >= pre[k] ? 1u : 0u;
-            const uint32_t k = i - pre[j];
-            stg[j * (kStageSlot / 16) + k] = ((const uint4 *)(B.bytes + abase[j]))[k];
-        }
-        __syncthreads();
-        // the round's owners: lane 16 r + j walks datagram d0 + 16 r + j
-        const uint32_t j = lane & (kStageGroup - 1);
-        const uint32_t pj = pre[j + 1] - pre[j];
-        const uint64_t aj = abase[j];
-        const uint32_t d = d0 + lane;
-        if (lane / kStageGroup == r && d < B.n) {
-            const uint8_t *staged = pj ? (const uint8_t *)&stg[j * (kStageSlot / 16)] + (B.offsets[d] - aj) : nullptr;
-            frame_one(B, hf_flag, hf_first, d, staged, &wwin[lane * 4]);
-        }
-        __syncthreads();
-    }
 }
 
 // Split framing, phase B (BatchDev::split 2, on its own stream beside phase A's fixed-length
@@ -1131,8 +1060,8 @@ __global__ void __launch_bounds__(256) k_to_host_bytes(const uint8_t *__restrict
 // launch wrappers (C linkage, used by ngz_host.cpp)
 // ---------------------------------------------------------------------------
 extern "C" int ngz_launch_frame(const BatchDev *B, const uint32_t *hf_flag, const uint32_t *hf_first, hipStream_t st) {
-    const uint32_t nb = (B->n + 63) / 64;
-    if (nb) hipLaunchKernelGGL(k_frame, dim3(nb), dim3(64), 0, st, *B, hf_flag, hf_first);
+    const uint32_t nb = (B->n + kFrameBlock - 1) / kFrameBlock;
+    if (nb) hipLaunchKernelGGL(k_frame, dim3(nb), dim3(kFrameBlock), 0, st, *B, hf_flag, hf_first);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
