@@ -1553,7 +1553,7 @@ __global__ __launch_bounds__(256) void k_agg_part_hist(const RecCtx C, const uin
 template <uint32_t NP>
 __global__ __launch_bounds__(256) void k_agg_part_scatter(const RecCtx C, const AggParams P, const uint32_t *__restrict__ rec_g,
                                                           uint32_t n_part, const uint32_t *__restrict__ offs,
-                                                          uint8_t *__restrict__ pay, uint32_t dbg) {
+                                                          uint8_t *__restrict__ pay) {
     extern __shared__ uint32_t cur[];
     for (uint32_t i = threadIdx.x; i < n_part; i += blockDim.x) cur[i] = offs[(uint64_t)i * gridDim.x + blockIdx.x];
     __syncthreads();
@@ -1580,7 +1580,7 @@ __global__ __launch_bounds__(256) void k_agg_part_scatter(const RecCtx C, const 
             c[k] = g[k] != NONE ? ctx_of_block(C, t0 + k) : make_uint4(0, 0, 0, 0);
         uint64_t x[PART_RPT][8];
         const uint32_t slot0 = c[0].w & 0xFFFF;
-        bool quad = (dbg & 2) == 0;
+        bool quad = true;
 #pragma unroll
         for (uint32_t k = 0; k < PART_RPT; ++k)
             quad = quad && g[k] != NONE && (c[k].w & 0xFFFF) == slot0 && c[k].x == c[0].x + k;
@@ -1627,14 +1627,13 @@ __global__ __launch_bounds__(256) void k_agg_part_scatter(const RecCtx C, const 
                 const AggSlotPlan &sp = C.plans[slot];
 #pragma unroll
                 for (int v = 0; v < 8; ++v)
-                    x[k][v] = g[k] != NONE && P.op_w[v] && sp.val_col[v] && !(dbg & 2) ? value_operand(sp, P, v, c[k].x) : 0ull;
+                    x[k][v] = g[k] != NONE && P.op_w[v] && sp.val_col[v] ? value_operand(sp, P, v, c[k].x) : 0ull;
             }
         }
 #pragma unroll
         for (uint32_t k = 0; k < PART_RPT; ++k) {
             if (g[k] == NONE) continue;
-            const uint32_t pos = dbg & 1 ? (uint32_t)(t0 + k)  // 1: measurement only
-                                         : atomicAdd(&cur[g[k] >> PART_SHIFT], 1u);
+            const uint32_t pos = atomicAdd(&cur[g[k] >> PART_SHIFT], 1u);
             uint32_t wd[NP * 4];
             wd[0] = g[k];
             wd[1] = c[k].y;
@@ -2027,7 +2026,7 @@ __host__ __device__ constexpr size_t lc_lds_bytes(uint32_t nv) {
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_agg_lc_part(
     const LcSet *__restrict__ descs, uint32_t n_sets, const AggSlotPlan *__restrict__ plans, const AggParams P,
     uint32_t key_bits, LcEntry *__restrict__ out, unsigned int *__restrict__ n_out, uint32_t cap,
-    unsigned int *__restrict__ flag, uint32_t dbg) {
+    unsigned int *__restrict__ flag) {
     extern __shared__ unsigned long long lc_cells[];
     const uint32_t nv = P.n_vals, lane = threadIdx.x, cl = lane & (LC_CELLS - 1);
     unsigned int *lc_cnt = (unsigned int *)(lc_cells + (size_t)(LC_NK + 1) * nv * LC_CELLS);
@@ -2193,9 +2192,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_
             // field by field: the field's loads for the block in flight together, then its
             // LDS updates (the width's own instantiation; a runtime loop over the fields)
             for (uint32_t v = 0; v < nv; ++v) {
-                if (!((hv >> v) & 1) || (dbg & 1)) continue;
+                if (!((hv >> v) & 1)) continue;
                 const uint32_t w = sp.val_w[v];
-                const __amdgpu_buffer_rsrc_t r = lc_rsrc((dbg & 2) ? nullptr : sp.val_col[v], w, A, end);
+                const __amdgpu_buffer_rsrc_t r = lc_rsrc(sp.val_col[v], w, A, end);
                 unsigned long long *cv = lc_cells + v * LC_CELLS;
                 switch (w) {
                 case 8: lc_reduce_field<8>(r, P, v, lane, cell, cv); break;
@@ -3572,13 +3571,11 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, const ngz_p
         }
         uint32_t kb = 0;
         for (uint32_t k = 0; k < P.n_keys; ++k) kb += 1 + 8 * P.key_pw[k];
-        // measurement only (wrong results): 1 skips the LDS updates, 2 the value loads
-        static const uint32_t lc_dbg = getenv("NGZ_AGG_LC_DBG") ? (uint32_t)atoi(getenv("NGZ_AGG_LC_DBG")) : 0u;
         AGG_HIP(a, hipMemsetAsync(a->lc_cnt, 0, 16, st));
         hipLaunchKernelGGL(k_agg_lc_sets, dim3(grid_for(NS)), dim3(256), 0, st, sets, NS, hdr, dginfo, a->plans, D, S,
                            a->lc_sets, a->late, a->err);
         hipLaunchKernelGGL(k_agg_lc_part, dim3(rg), dim3(64), lds, st, a->lc_sets, NS, a->plans, P, kb, a->lc,
-                           a->lc_cnt, cap, a->lc_cnt + 1, lc_dbg);
+                           a->lc_cnt, cap, a->lc_cnt + 1);
         AGG_HIP(a, hipGetLastError());
         const uint64_t room = a->limit - std::min(a->live, a->limit);
         hipLaunchKernelGGL(k_agg_lc_merge, dim3(LCM_BLOCKS), dim3(LCM_THREADS), 0, st, a->lc, cap, a->lc + cap,
@@ -3697,9 +3694,6 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, const ngz_p
                     at += ow;
                 }
             const uint32_t pb = (at + 31) & ~31u;
-            // NGZ_AGG_SCATTER_DBG=1: payloads stored in record order (wrong results; timing of the
-            // scatter without its scattered stores)
-            static const uint32_t sc_dbg = getenv("NGZ_AGG_SCATTER_DBG") ? (uint32_t)atoi(getenv("NGZ_AGG_SCATTER_DBG")) : 0u;
             const uint64_t nc = (uint64_t)np * nt + 1;
             size_t stb = 0;
             hipcub::DeviceScan::ExclusiveSum(nullptr, stb, (uint32_t *)nullptr, (uint32_t *)nullptr, (int)nc, st);
@@ -3721,9 +3715,9 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, const ngz_p
             hipLaunchKernelGGL(k_agg_part_hist, dim3(nt), dim3(256), 4 * np, st, C, rec_g, np, counts);
             AGG_HIP(a, hipcub::DeviceScan::ExclusiveSum(stmp, stb, counts, offs, (int)nc, st));
             switch (pb / 16) {
-            case 2: hipLaunchKernelGGL(k_agg_part_scatter<2>, dim3(nt), dim3(256), 4 * np, st, C, P, rec_g, np, offs, pay, sc_dbg); break;
-            case 4: hipLaunchKernelGGL(k_agg_part_scatter<4>, dim3(nt), dim3(256), 4 * np, st, C, P, rec_g, np, offs, pay, sc_dbg); break;
-            default: hipLaunchKernelGGL(k_agg_part_scatter<6>, dim3(nt), dim3(256), 4 * np, st, C, P, rec_g, np, offs, pay, sc_dbg); break;
+            case 2: hipLaunchKernelGGL(k_agg_part_scatter<2>, dim3(nt), dim3(256), 4 * np, st, C, P, rec_g, np, offs, pay); break;
+            case 4: hipLaunchKernelGGL(k_agg_part_scatter<4>, dim3(nt), dim3(256), 4 * np, st, C, P, rec_g, np, offs, pay); break;
+            default: hipLaunchKernelGGL(k_agg_part_scatter<6>, dim3(nt), dim3(256), 4 * np, st, C, P, rec_g, np, offs, pay); break;
             }
             // payloads per thread and round in the reduce (NGZ_AGG_RED_RPT 1 or 4; A/B knob)
             static const uint32_t red_rpt = getenv("NGZ_AGG_RED_RPT") && atoi(getenv("NGZ_AGG_RED_RPT")) == 1 ? 1u : 4u;
