@@ -23,13 +23,16 @@
 #include "ngz_internal.h"
 
 // Cache policy (buffer instruction aux bits) of the generated kernels' record loads and column
-// stores: 0 by default; the generator defines them from NGZ_LD_AUX / NGZ_ST_AUX for experiments
-// (2 = nt on gfx950), and they are part of the kernel's cache signature.
+// stores.  Column stores are nontemporal (2 = nt on gfx950): the columns are written once and not
+// read back by the decode, and streaming them past the caches measured 1-2 % faster (T20 2.138 ->
+// 2.098 ms, config 3 4.27 -> 4.22 ms, same box); nt record loads were 1.4-2x slower, so loads keep the
+// default.  The generator overrides either from NGZ_LD_AUX / NGZ_ST_AUX (experiments), and an
+// override is part of the kernel's cache signature.
 #ifndef NGZ_LD_AUX
 #define NGZ_LD_AUX 0
 #endif
 #ifndef NGZ_ST_AUX
-#define NGZ_ST_AUX 0
+#define NGZ_ST_AUX 2
 #endif
 
 namespace ngzdev {
