@@ -45,9 +45,10 @@
 extern "C" {
 #endif
 
-#define NGZ_AGG_ABI_VERSION 3 /* 2: ngz_agg_create takes max_peers, ngz_agg_push a const ngz_peer * (the
+#define NGZ_AGG_ABI_VERSION 4 /* 2: ngz_agg_create takes max_peers, ngz_agg_push a const ngz_peer * (the
                                  exporter's address; 1 took a uint16 port); 3: byte-valued keys and values
-                                 of any length (kkind 3, vclass 8 / 9, ngz_agg_row_bytes) */
+                                 of any length (kkind 3, vclass 8 / 9, ngz_agg_row_bytes); 4:
+                                 ngz_agg_set_option */
 
 /* NGZ_AGG_ABI_VERSION the library was built with (checked by hosts like ngz_abi_version). */
 int ngz_agg_abi_version(void);
@@ -113,7 +114,9 @@ const char *ngz_agg_last_error(ngz_agg *a);
  * (min/max_collection_time).  Records of failed messages are not pushed (they yield no
  * FlowInfo).  *late_records (may be NULL) receives the records dropped as late.
  * hip_stream: the stream the batch was decoded on (NULL = the context's stream is
- * synchronised by ngz_decode_batch already). */
+ * synchronised by ngz_decode_batch already).  Variable-length key / value cells point into the
+ * batch's input bytes (NGZ_K_VLEN): the bytes given to ngz_decode_batch must stay valid and
+ * unchanged until ngz_agg_push returns (a host that recycles its H2D buffers pushes first). */
 int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, const ngz_peer *peer,
                  int64_t collection_time_ms, uint64_t *late_records, void *hip_stream);
 
@@ -139,7 +142,7 @@ typedef struct {
 } ngz_agg_row;
 
 /* Row layout of ngz_agg_flush output: row_bytes per group (a multiple of 128: whole
- * cache lines in the device table; 16 with NGZ_AGG_ROW_PACK set); the
+ * cache lines in the device table); the
  * ngz_agg_row header, 8 bytes of device bookkeeping, then key field k at key_off[k]
  * (column width of the IE, rounded to 4; width in key_width[k]: 0 if the
  * field never appeared), value v at val_off[v] (8 bytes; OR of byte fields: width
@@ -215,7 +218,10 @@ int ngz_agg_value_info(ngz_agg *a, uint32_t v, ngz_agg_value_desc *out);
 
 /* The whole byte value of key k (is_value 0, kkind 3) or aggregated field v (is_value 1,
  * vclass 8 / 9) of an output row of the last ngz_agg_flush / ngz_agg_emit call: up to cap
- * bytes into dst (may be NULL); returns the value's length, or NGZ_E_INVALID. */
+ * bytes into dst (may be NULL); returns the value's length, or NGZ_E_INVALID.  Byte values can be
+ * read only until the next flush / emit: the tails come from that call's copy.  A row of an
+ * earlier call whose tail lies outside the copy is NGZ_E_INVALID (and ngz_agg_flowinfo_json then
+ * fails with NGZ_E_INVALID instead of printing the value empty); one inside it reads other bytes. */
 int64_t ngz_agg_row_bytes(ngz_agg *a, const void *row, int is_value, uint32_t index, uint8_t *dst, uint64_t cap);
 
 /* AggFlowInfo::into_flowinfo_with_extra_fields (aggregator.rs:203-277) of output rows,
@@ -236,6 +242,20 @@ int64_t ngz_agg_row_bytes(ngz_agg *a, const void *row, int is_value, uint32_t in
  * rows rendered or <0. */
 int64_t ngz_agg_flowinfo_json(ngz_agg *a, const void *rows, uint64_t n, uint32_t shard_id, uint32_t seq0,
                               int64_t export_time_ms, ngz_json_line_fn fn, void *user);
+
+/* Aggregator options (ngz_agg_set_option).  They choose how a push reduces, never what it
+ * computes: every choice gives the same groups (tests/test_gpu_agg.py runs them against each
+ * other and the oracle).  The library reads no tuning from the environment. */
+#define NGZ_AGG_OPT_LOWCARD 1    /* -1 (default): the low-cardinality path from 2^16 records; 0 never;
+                                    1 at any size (where the config allows it) */
+#define NGZ_AGG_OPT_PARTITION 2  /* -1 (default): the partitioned reduction for many groups with at least 8
+                                    records each per push; 0 never; 1 whenever the config allows it */
+#define NGZ_AGG_OPT_OWNER 3      /* 1 (default): per-record owner rows where groups get few records per
+                                    push; 0 never */
+#define NGZ_AGG_OPT_HASH_BITS 4  /* 0 (default): the full 64-bit hash of hashed keys; 1..63: only that many
+                                    bits, so distinct keys collide (tests of the exact key compare).  Only
+                                    while the aggregator holds no group (NGZ_E_INVALID otherwise). */
+int ngz_agg_set_option(ngz_agg *a, int opt, int64_t value);
 
 /* Device time of the last push (HIP events around its kernels), milliseconds. */
 int ngz_agg_last_timing(ngz_agg *a, float *push_ms);

@@ -170,6 +170,16 @@ const char *ngz_last_error(ngz_ctx *ctx);
                                    generic kernel decodes its records until it is ready (a new template on
                                    one peer never stalls a batch); 1: the first batch after a template
                                    definition waits for its compile (deterministic kernel choice) */
+#define NGZ_OPT_SPLIT 6         /* 1: split framing in steady state -- the record walk of variable-length
+                                   sets on a second stream beside the fixed-length sets' framing and
+                                   decode (measured slower on config 4); 0 (default) */
+#define NGZ_OPT_GROUP 7         /* 1: one multi-template decode launch per workgroup shape for the
+                                   LDS-staged templates of a batch (ngz_group_kernel); 0 (default): one
+                                   launch per template */
+#define NGZ_OPT_PLACE_TRIALS 8  /* column arenas tried for a context's first large batch, the fastest
+                                   kept (1..16, default 6; 1 = no trials, DESIGN.md §2 "Arena placement") */
+/* Options change how a batch runs, never its results.  The library reads no tuning from the
+ * environment (only NGZ_DEBUG, stderr traces). */
 int ngz_ctx_set_option(ngz_ctx *ctx, int opt, int64_t value);
 
 /* Wait for every background template compile of the process (NGZ_OPT_RTC_SYNC 0) to finish

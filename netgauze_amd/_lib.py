@@ -10,6 +10,10 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libngz.so")
+# NGZ_EXPERIMENTS=1 (tools only): the experiment build, libngz_exp.so (tools/build_experiments.sh),
+# whose knobs are read from NGZ_<name> variables for A/B measurements.  Never the product path.
+if os.environ.get("NGZ_EXPERIMENTS") == "1":
+    LIB_PATH = os.path.join(HERE, "libngz_exp.so")
 
 NGZ_DG_OK, NGZ_DG_NEED_MORE, NGZ_DG_ERROR, NGZ_DG_UNSUPPORTED = 0, 1, 2, 3
 (K_UINT, K_TCPFLAGS, K_SINT, K_BOOL, K_BYTES, K_U256, K_DTMS, K_DTFRAC, K_STR,
@@ -26,7 +30,10 @@ ABI_FUNCTIONS = [
 ]
 NGZ_ABI_VERSION = 4
 NGZ_BATCH_PREDICTED, NGZ_BATCH_SPLIT, NGZ_BATCH_RERUN = 1, 2, 4  # ngz_last_batch_info
-NGZ_AGG_ABI_VERSION = 3
+# ngz_ctx_set_option
+(NGZ_OPT_SPECIALIZE, NGZ_OPT_BLOCKS_PER_CU, NGZ_OPT_ARENA_SHIFT, NGZ_OPT_CAP_PAD, NGZ_OPT_RTC_SYNC, NGZ_OPT_SPLIT,
+ NGZ_OPT_GROUP, NGZ_OPT_PLACE_TRIALS) = range(1, 9)
+NGZ_AGG_ABI_VERSION = 4
 # ngz_error.kind / .layer (flow_decode.h)
 ERR_KINDS = ["NONE", "UNSUPPORTED_VERSION", "INVALID_LENGTH", "UNEXPECTED_EOF", "INVALID_PADDING_LENGTH",
              "INVALID_SET_ID", "NO_TEMPLATE", "INVALID_PADDING_VALUE", "INVALID_COUNT", "INVALID_TEMPLATE_ID",
@@ -44,10 +51,11 @@ AGG_FUNCTIONS = [
     "ngz_agg_create", "ngz_agg_destroy", "ngz_agg_last_error", "ngz_agg_push", "ngz_agg_layout",
     "ngz_agg_groups", "ngz_agg_flush", "ngz_agg_closed", "ngz_agg_emit", "ngz_agg_reset", "ngz_agg_sets",
     "ngz_agg_key_info", "ngz_agg_value_info", "ngz_agg_flowinfo_json", "ngz_agg_last_timing", "ngz_agg_peer", "ngz_agg_last_path",
-    "ngz_agg_abi_version", "ngz_agg_row_bytes",
+    "ngz_agg_abi_version", "ngz_agg_row_bytes", "ngz_agg_set_option",
 ]
 NGZ_AGG_KEY, NGZ_AGG_ADD, NGZ_AGG_MIN, NGZ_AGG_MAX, NGZ_AGG_OR = range(5)
 NGZ_AGG_E_OVERFLOW, NGZ_AGG_E_COLLISION, NGZ_AGG_E_POISONED = -10, -11, -12
+NGZ_AGG_OPT_LOWCARD, NGZ_AGG_OPT_PARTITION, NGZ_AGG_OPT_OWNER, NGZ_AGG_OPT_HASH_BITS = 1, 2, 3, 4
 # ngz_agg_key_desc.kkind / ngz_agg_value_desc.vclass
 AGG_KK_FIXED, AGG_KK_BYTES = 0, 3
 (AGG_VC_UINT, AGG_VC_SINT, AGG_VC_DTFRAC, AGG_VC_BYTES, AGG_VC_RANK, AGG_VC_F32, AGG_VC_F64, AGG_VC_IPV6,
@@ -274,6 +282,8 @@ def load():
     lib.ngz_agg_peer.restype = I
     lib.ngz_agg_last_path.argtypes = [P]
     lib.ngz_agg_last_path.restype = ctypes.c_char_p
+    lib.ngz_agg_set_option.argtypes = [P, I, ctypes.c_int64]
+    lib.ngz_agg_set_option.restype = I
     # ingest (flow_ingest.h)
     lib.ngz_pcap_open.argtypes = [ctypes.c_char_p, ctypes.POINTER(P)]
     lib.ngz_pcap_open.restype = I

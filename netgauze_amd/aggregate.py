@@ -78,11 +78,13 @@ def _datetime_ms(ms):
 class FlowAggregator:
     DEFAULT_PEER = "192.0.2.1"  # TEST-NET-1: the exporter of pushes that name none
 
-    def __init__(self, transform, window_s=60, lateness_s=10, capacity=1 << 20, device=0, kinds=None, max_peers=0):
+    def __init__(self, transform, window_s=60, lateness_s=10, capacity=1 << 20, device=0, kinds=None, max_peers=0,
+                 options=None):
         """max_peers: distinct exporter IPs the aggregator takes between flushes (0: the library's
         NGZ_AGG_MAX_PEERS, 65536).  Entries are kept until flush / reset, as each peer's event time
         is; a push from a new IP beyond it fails (AggError, NGZ_AGG_E_OVERFLOW).  A smaller bound
-        leaves more bits of the exact 63-bit group tag to the key fields (flow_aggregate.h)."""
+        leaves more bits of the exact 63-bit group tag to the key fields (flow_aggregate.h).
+        options: {NGZ_AGG_OPT_*: value} for ngz_agg_set_option (how pushes reduce, never what)."""
         self.fields = unify(transform) if isinstance(transform, dict) else list(transform)
         self.key_fields = [f for f in self.fields if f[3] == _lib.NGZ_AGG_KEY]
         self.val_fields = [f for f in self.fields if f[3] != _lib.NGZ_AGG_KEY]
@@ -95,6 +97,13 @@ class FlowAggregator:
         self._h = h
         # optional override of the rendering per (pen, ie_id): "sint" | "uint" | "bytes" | "str"
         self.kinds = kinds or {}
+        for opt, value in (options or {}).items():
+            self.set_option(opt, value)
+
+    def set_option(self, opt, value):
+        """ngz_agg_set_option: NGZ_AGG_OPT_LOWCARD / _PARTITION (-1 auto, 0 never, 1 always),
+        _OWNER (0 / 1), _HASH_BITS (0 full hash; 1..63, only while no group is held)."""
+        self._check(lib().ngz_agg_set_option(self._h, opt, int(value)))
 
     def close(self):
         if getattr(self, "_h", None) and self._h.value:

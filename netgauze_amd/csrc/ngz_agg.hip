@@ -102,6 +102,12 @@ enum : uint8_t {
 // first 32 bytes zero padded.  Values longer than 32 bytes keep their tail in the aggregator's
 // byte arena (bump-allocated per group, compacted when the table is rebuilt, emptied by flush).
 constexpr uint32_t BVAL_BYTES = 40, BVAL_INLINE = 32;
+// Arena bytes a BVAL value of n > 32 bytes takes: its tail, rounded to 8 bytes.  Row offsets are
+// in 8-byte units (a u32 addresses 32 GiB of arena; a push that would pass it fails, NGZ_E_LIMIT)
+constexpr uint64_t ARENA_MAX = 1ull << 35;
+__host__ __device__ __forceinline__ uint64_t tail_span(uint32_t n) {
+    return n > BVAL_INLINE ? ((uint64_t)(n - BVAL_INLINE) + 7) & ~7ull : 0;
+}
 
 struct AggSlotPlan {            // per batch slot, built on the host every push
     const uint8_t *key_col[NGZ_AGG_MAX_KEYS];   // null: the record has no such field (None)
@@ -135,7 +141,7 @@ struct AggParams {
     uint64_t coll_flip;         // collection time ms, sign bit flipped (unsigned order == signed order)
     uint32_t lds_ok;            // 1: no byte-wise OR values (wave results may be combined in LDS)
     uint32_t packed;            // 1: the whole group key packs into 63 bits (exact tag)
-    uint64_t hash_mask;         // hashed keys: bits of the hash kept (tests force collisions with NGZ_AGG_HASH_BITS)
+    uint64_t hash_mask;         // hashed keys: bits of the hash kept (NGZ_AGG_OPT_HASH_BITS: tests force collisions)
     uint32_t own;               // 1: one record per group and push (its owner) reduces with plain stores
     uint32_t kw_n;              // hashed keys of at most 8 words: their count (key words held in registers), else 0
     uint8_t kw_key[8], kw_idx[8];  // key word j: its key field and its word within the field
@@ -239,7 +245,7 @@ struct BRef {
 
 __device__ __forceinline__ BRef bval_ref(const uint8_t *slot, const AggParams &P) {
     const uint32_t n = *(const uint32_t *)slot, off = *(const uint32_t *)(slot + 4);
-    return BRef{slot + 8, P.arena + off, BVAL_INLINE, n};
+    return BRef{slot + 8, P.arena + ((uint64_t)off << 3), BVAL_INLINE, n};
 }
 
 // Box<[u8]> / [u8] Ord: lexicographic, then by length
@@ -262,14 +268,14 @@ __device__ __forceinline__ void bval_write(uint8_t *slot, const Span s, const Ag
 #pragma unroll
     for (uint32_t j = 0; j < BVAL_INLINE / 4; ++j) d[2 + j] = span_word(s.p, min(s.n, BVAL_INLINE), j);
     if (s.n > BVAL_INLINE) {
-        const uint64_t need = s.n - BVAL_INLINE;
+        const uint64_t need = tail_span(s.n);
         const uint64_t off = atomicAdd(P.arena_used, (unsigned long long)need);
         if (off + need > P.arena_cap) {
             atomicOr(err, 64u);
             return;
         }
-        for (uint32_t i = 0; i < need; ++i) P.arena[off + i] = s.p[BVAL_INLINE + i];
-        d[1] = (uint32_t)off;
+        for (uint32_t i = 0; i < s.n - BVAL_INLINE; ++i) P.arena[off + i] = s.p[BVAL_INLINE + i];
+        d[1] = (uint32_t)(off >> 3);
     }
 }
 
@@ -391,7 +397,7 @@ __device__ __forceinline__ bool key_equal(const uint8_t *R, const AggSlotPlan &s
             for (uint32_t j = 0; j < BVAL_INLINE / 4 && same; ++j)
                 same = rk[2 + j] == span_word(s.p, min(s.n, BVAL_INLINE), j);
             if (same && s.n > BVAL_INLINE) {
-                const uint8_t *t = P.arena + rk[1];
+                const uint8_t *t = P.arena + ((uint64_t)rk[1] << 3);
                 for (uint32_t i = BVAL_INLINE; i < s.n && same; ++i) same = t[i - BVAL_INLINE] == s.p[i];
             }
             continue;
@@ -1422,7 +1428,7 @@ __global__ __launch_bounds__(256) void k_agg_ordered(const RecCtx C, const AggPa
 #pragma unroll
                     for (uint32_t q = 0; q < BVAL_INLINE / 4; ++q) inl[q] |= span_word(s.p, min(m, BVAL_INLINE), q);
                     if (m > BVAL_INLINE) {
-                        uint8_t *t = P.arena + d[1];
+                        uint8_t *t = P.arena + ((uint64_t)d[1] << 3);
                         for (uint32_t b = BVAL_INLINE; b < m; ++b) t[b - BVAL_INLINE] |= s.p[b];
                     }
                 }
@@ -2517,10 +2523,11 @@ __global__ void k_agg_rehash(const unsigned long long *__restrict__ tags, const 
 }
 
 // ---- byte values (BVAL) longer than 32 bytes: their tails in the byte arena ----
-// Tail bytes a push can write at most: every present BVAL key and value of every valid record
-// beyond its first 32 bytes (a group's claim or its ordered fold writes at most one record's)
+// Tail bytes a push can write at most: need[0] the tails of every present BVAL key and value of
+// every valid record, need[1] the longest one (a group's claim writes one tail per key field, its
+// ordered fold at most one per value field, so a push writes at most slots x fields x longest)
 __global__ void k_agg_tail_need(const RecCtx C, const AggParams P, unsigned long long *__restrict__ need) {
-    uint64_t mine = 0;
+    uint64_t mine = 0, longest = 0;
     for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < C.n_rec; t += (uint64_t)gridDim.x * blockDim.x) {
         const Rec r = rec_of(C, t, nullptr);
         if (!r.valid) continue;
@@ -2528,16 +2535,24 @@ __global__ void k_agg_tail_need(const RecCtx C, const AggParams P, unsigned long
         for (uint32_t k = 0; k < P.n_keys; ++k)
             if (P.key_kind[k] == KK_BYTES && sp.key_col[k]) {
                 const Span s = key_span(sp, P, k, r.row);
-                if (s.n > BVAL_INLINE) mine += s.n - BVAL_INLINE;
+                mine += tail_span(s.n);
+                longest = max(longest, tail_span(s.n));
             }
         for (uint32_t v = 0; v < P.n_vals; ++v)
             if ((P.val_vc[v] == VC_VBYTES || P.val_vc[v] == VC_VLIST) && sp.val_col[v]) {
                 const Span s = val_span(sp, v, r.row);
-                if (s.n > BVAL_INLINE) mine += s.n - BVAL_INLINE;
+                mine += tail_span(s.n);
+                longest = max(longest, tail_span(s.n));
             }
     }
-    for (int m = 32; m >= 1; m >>= 1) mine += (uint64_t)__shfl_xor((long long)mine, m);
-    if ((threadIdx.x & 63) == 0 && mine) atomicAdd(need, (unsigned long long)mine);
+    for (int m = 32; m >= 1; m >>= 1) {
+        mine += (uint64_t)__shfl_xor((long long)mine, m);
+        longest = max(longest, (uint64_t)__shfl_xor((long long)longest, m));
+    }
+    if ((threadIdx.x & 63) == 0 && mine) {
+        atomicAdd(need, (unsigned long long)mine);
+        atomicMax(need + 1, (unsigned long long)longest);
+    }
 }
 
 // Moves the tails of one row's BVAL keys / values from arena `from` to `to` (bump cursor),
@@ -2548,10 +2563,10 @@ __device__ __forceinline__ void move_tails(uint8_t *R, const AggParams &P, const
     auto one = [&](uint8_t *slot) {
         uint32_t *d = (uint32_t *)slot;
         if (d[0] <= BVAL_INLINE) return;
-        const uint64_t n = d[0] - BVAL_INLINE;
-        const uint64_t off = atomicAdd(cursor, (unsigned long long)n);
-        for (uint64_t i = 0; i < n; ++i) to[off + i] = from[d[1] + i];
-        d[1] = (uint32_t)off;
+        const uint64_t n = d[0] - BVAL_INLINE, src = (uint64_t)d[1] << 3;
+        const uint64_t off = atomicAdd(cursor, (unsigned long long)tail_span(d[0]));
+        for (uint64_t i = 0; i < n; ++i) to[off + i] = from[src + i];
+        d[1] = (uint32_t)(off >> 3);
     };
     for (uint32_t k = 0; k < P.n_keys; ++k)
         if (P.key_kind[k] == KK_BYTES && ((kp >> k) & 1)) one(R + P.key_off[k]);
@@ -2641,6 +2656,9 @@ struct ngz_agg {
     LcSet *lc_sets = nullptr;     // ... the push's set descriptors
     uint32_t lc_sets_cap = 0;
     const char *last_path = "";   // the reduction path of the last push ("lowcard" / "general")
+    int opt_lowcard = -1;         // NGZ_AGG_OPT_LOWCARD: -1 by size, 0 never, 1 at any size
+    int opt_partition = -1;       // NGZ_AGG_OPT_PARTITION: -1 by groups and records, 0 never, 1 always
+    bool opt_owner = true;        // NGZ_AGG_OPT_OWNER
     uint32_t lc_skip = 0;         // pushes left before the low-cardinality scan is tried again
 };
 
@@ -2814,8 +2832,11 @@ int rehash(ngz_agg *a) {
 // Byte arena: room for `need` more bytes after the ones in use (grown to at least twice its size,
 // the bytes in use moved over)
 int arena_reserve(ngz_agg *a, uint64_t need) {
+    // row offsets are u32 counts of 8-byte units (tail_span): the arena ends at 32 GiB
+    if (a->arena_mark + need > ARENA_MAX)
+        return fail(a, NGZ_E_LIMIT, "byte arena: the push could need more than 32 GiB of value tails");
     if (a->arena_mark + need <= a->arena_cap) return NGZ_OK;
-    const uint64_t cap = std::max<uint64_t>({a->arena_mark + need, 2 * a->arena_cap, 1u << 20});
+    const uint64_t cap = std::min<uint64_t>(ARENA_MAX, std::max<uint64_t>({a->arena_mark + need, 2 * a->arena_cap, 1u << 20}));
     uint8_t *p = nullptr;
     if (hipMalloc(&p, cap) != hipSuccess) return fail(a, NGZ_E_NOMEM, "byte arena");
     if (a->arena_mark) AGG_HIP(a, hipMemcpyAsync(p, a->arena, a->arena_mark, hipMemcpyDeviceToDevice, a->stream));
@@ -3050,7 +3071,7 @@ int ngz_agg_create(int device, const ngz_agg_field *fields, uint32_t n_fields, u
     // whole 128-byte lines: a row at a random slot then touches ceil(row/128) lines, not one
     // more when it straddles (176-byte rows at a 176-byte stride cover 2.4 lines on average);
     // NGZ_AGG_ROW_PACK keeps whole 16-byte pieces only (k_agg_apply_own's unit)
-    P.row_bytes = getenv("NGZ_AGG_ROW_PACK") ? (off + 15) & ~15u : (off + 127) & ~127u;
+    P.row_bytes = ngz_knob("NGZ_AGG_ROW_PACK", 0) ? (off + 15) & ~15u : (off + 127) & ~127u;
     P.peer_bits = 0;
     while ((1u << P.peer_bits) < a->max_peers) ++P.peer_bits;
     {
@@ -3060,7 +3081,7 @@ int ngz_agg_create(int device, const ngz_agg_field *fields, uint32_t n_fields, u
             ok = ok && P.key_pw[k] != 0;
             bits += 1 + 8 * P.key_pw[k];
         }
-        P.packed = ok && bits <= 63 && getenv("NGZ_AGG_NO_PACK") == nullptr;
+        P.packed = ok && bits <= 63 && !ngz_knob("NGZ_AGG_NO_PACK", 0);
     }
     P.lds_ok = 1;
     for (uint32_t v = 0; v < P.n_vals; ++v)
@@ -3070,7 +3091,7 @@ int ngz_agg_create(int device, const ngz_agg_field *fields, uint32_t n_fields, u
         uint32_t nw = 0;
         for (uint32_t k = 0; k < P.n_keys; ++k) nw += P.key_slot[k] / 4;
         P.kw_n = 0;
-        if (!P.packed && nw <= 8 && getenv("NGZ_AGG_NO_KW") == nullptr) {
+        if (!P.packed && nw <= 8 && !ngz_knob("NGZ_AGG_NO_KW", 0)) {
             uint32_t j = 0;
             for (uint32_t k = 0; k < P.n_keys; ++k)
                 for (uint32_t i = 0; i < P.key_slot[k] / 4; ++i, ++j) {
@@ -3081,7 +3102,7 @@ int ngz_agg_create(int device, const ngz_agg_field *fields, uint32_t n_fields, u
         }
     }
     // owner path: rows of up to 256 bytes, no byte-wise ORs, aggregated fields 0-7
-    P.own = P.lds_ok && P.row_bytes <= 256 && P.n_vals <= 8 && getenv("NGZ_AGG_NO_OWN") == nullptr;
+    P.own = P.lds_ok && P.row_bytes <= 256 && P.n_vals <= 8;  // NGZ_AGG_OPT_OWNER 0 turns it off per push
     {
         uint8_t op[32] = {}, src[32] = {};
         op[1] = U_VP;                                   // val_present (high word of key_present's unit)
@@ -3108,10 +3129,6 @@ int ngz_agg_create(int device, const ngz_agg_field *fields, uint32_t n_fields, u
         }
     }
     P.hash_mask = ~0ull;
-    if (const char *hb = getenv("NGZ_AGG_HASH_BITS")) {  // test knob: a narrow hash makes distinct keys collide
-        const int b = atoi(hb);
-        if (b > 0 && b < 64) P.hash_mask = (1ull << b) - 1;
-    }
     if (capacity > (1ull << 30)) { delete a; return NGZ_E_LIMIT; }  // slot indexes stay below OWN_BIT
     uint64_t slots = 1024;
     while (slots < 2 * std::max<uint64_t>(capacity, 1)) slots <<= 1;
@@ -3139,9 +3156,9 @@ int ngz_agg_create(int device, const ngz_agg_field *fields, uint32_t n_fields, u
         hipMalloc(&a->newdom, NEWDOM_SLOTS * 8) != hipSuccess || hipMalloc(&a->err, 4) != hipSuccess ||
         hipMalloc(&a->late, 8) != hipSuccess || hipMalloc(&a->cursor, 8) != hipSuccess ||
         hipMalloc(&a->n_claims, 8) != hipSuccess || hipMalloc(&a->n_coll, 4) != hipSuccess ||
-        hipMalloc(&a->used, 32) != hipSuccess || hipMalloc(&a->arena_used, 16) != hipSuccess)
+        hipMalloc(&a->used, 32) != hipSuccess || hipMalloc(&a->arena_used, 24) != hipSuccess)
         return bail(NGZ_E_NOMEM, "hipMalloc (group table)");
-    hipMemset(a->arena_used, 0, 16);
+    hipMemset(a->arena_used, 0, 24);
     P.arena_used = a->arena_used;
     if (ranks) {
         // sub-registry ranks: which values are registered variants (known bitmap per value)
@@ -3437,7 +3454,7 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, const ngz_p
     // few, hot groups the wave / workgroup pre-aggregation of k_agg_apply serves them better
     // and the owner stores and checks would only add traffic.  Decided from the groups held
     // before the push (an empty table: the first push of any key).
-    P.own = P.own && (a->live == 0 || a->live * 8 > (uint64_t)out->n_records);
+    P.own = P.own && a->opt_owner && (a->live == 0 || a->live * 8 > (uint64_t)out->n_records);
     AGG_HIP(a, hipEventRecord(a->ev0, st));
     AGG_HIP(a, hipMemsetAsync(has_rec, 0, 4ull * D, st));
     AGG_HIP(a, hipMemsetAsync(a->late, 0, 8, st));
@@ -3511,7 +3528,7 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, const ngz_p
              *list_a = (uint32_t *)(a->rec_buf + B0 + 2 * R4), *list_b = (uint32_t *)(a->rec_buf + B0 + 3 * R4);
     const RecCtx C{sctx, rstart, bset, NS, (uint64_t)n_rec, a->plans};
     const uint32_t blocks = (uint32_t)((n_rec + 255) / 256);
-    static const uint32_t grid_cap = getenv("NGZ_AGG_GRID") ? (uint32_t)std::max(1, atoi(getenv("NGZ_AGG_GRID"))) : 4096u;
+    static const uint32_t grid_cap = (uint32_t)std::max<int64_t>(1, ngz_knob("NGZ_AGG_GRID", 4096));
     const uint32_t ig = std::max<uint32_t>(1, std::min<uint32_t>(blocks, grid_cap));
     unsigned long long n_claims = 0;
     auto rollback = [&](int rc, const std::string &why) {
@@ -3528,10 +3545,9 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, const ngz_p
     // every record in one pass into per-wave partial groups, k_agg_lc_merge combines them
     // per tag, claims and applies.  A wave with more than LC_NK key tuples in one window
     // context, or more than LC_MAX_TAGS tags in the push, sends the push to the general
-    // path below, with nothing claimed or applied (NGZ_AGG_LC: 0 never, 1 at any size;
+    // path below, with nothing claimed or applied (NGZ_AGG_OPT_LOWCARD: 0 never, 1 at any size;
     // default from 2^16 records).
-    static const int lc_env = getenv("NGZ_AGG_LC") ? atoi(getenv("NGZ_AGG_LC")) : -1;
-    const int lc_now = getenv("NGZ_AGG_LC") ? atoi(getenv("NGZ_AGG_LC")) : lc_env;  // read per push (tests)
+    const int lc_now = a->opt_lowcard;  // NGZ_AGG_OPT_LOWCARD
     // a push that found too many key tuples sends the next 15 pushes of the aggregator
     // straight to the general path (high-cardinality keys pay for one try in 16)
     const bool lc_try = lc_now == 1 || (lc_now != 0 && n_rec >= (1u << 16) && (a->lc_skip == 0 || --a->lc_skip == 0));
@@ -3606,13 +3622,20 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, const ngz_p
     if (n_blk) hipLaunchKernelGGL(k_agg_bset, dim3(grid_for(n_blk, 256, 4096)), dim3(256), 0, st, rstart, NS, n_blk, bset);
     AGG_HIP(a, hipGetLastError());
     if (P.has_bytes && n_rec) {
-        // byte values longer than 32 bytes: room in the arena for every tail this push can write
-        // (key claims and ordered folds write at most one record's per group and field)
-        unsigned long long need = 0;
-        AGG_HIP(a, hipMemsetAsync(a->arena_used + 1, 0, 8, st));
+        // byte values longer than 32 bytes: room in the arena for every tail this push can write.
+        // Key claims and ordered folds write at most one tail per group and field, and a push
+        // touches at most every slot of the table: the bound is the smaller of the records' tails
+        // and slots x byte fields x the longest tail (10^8 records of a 64-byte key over a few
+        // groups reserve 2 slots per group's worth, not 3 GB)
+        unsigned long long nd[2] = {0, 0};
+        AGG_HIP(a, hipMemsetAsync(a->arena_used + 1, 0, 16, st));
         hipLaunchKernelGGL(k_agg_tail_need, dim3(grid_for(n_rec, 256, 4096)), dim3(256), 0, st, C, P, a->arena_used + 1);
-        AGG_HIP(a, hipMemcpyAsync(&need, a->arena_used + 1, 8, hipMemcpyDeviceToHost, st));
+        AGG_HIP(a, hipMemcpyAsync(nd, a->arena_used + 1, 16, hipMemcpyDeviceToHost, st));
         AGG_HIP(a, hipStreamSynchronize(st));
+        uint32_t n_bval = 0;
+        for (uint32_t k = 0; k < P.n_keys; ++k) n_bval += P.key_kind[k] == KK_BYTES;
+        for (uint32_t v = 0; v < P.n_vals; ++v) n_bval += P.val_vc[v] == VC_VBYTES || P.val_vc[v] == VC_VLIST;
+        const uint64_t need = std::min<uint64_t>(nd[0], a->slots * n_bval * nd[1]);
         if (int r = arena_reserve(a, need)) { restore(); upload_domains(a); return r; }
         P.arena = a->P.arena;
         P.arena_cap = a->P.arena_cap;
@@ -3670,10 +3693,10 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, const ngz_p
         // groups (a first push of a low-cardinality key included) would list almost every record
         // for k_agg_apply, one counter atomic per wave on a single word (142 ms for 12 groups
         // and 10^8 records), so the owner test stays in k_agg_apply there.
-        static const bool split = getenv("NGZ_AGG_OWN_SPLIT") != nullptr;  // A/B: the owner test in k_agg_apply
+        static const bool split = ngz_knob("NGZ_AGG_OWN_SPLIT", 0) != 0;  // A/B: the owner test in k_agg_apply
         // partitioned reduction: more groups than LDS tables hold, at least 8 records per group
-        // (NGZ_AGG_PART: 0 never, 1 whenever the config allows it)
-        const int part_env = getenv("NGZ_AGG_PART") ? atoi(getenv("NGZ_AGG_PART")) : -1;  // read per push (tests)
+        // (NGZ_AGG_OPT_PARTITION: 0 never, 1 whenever the config allows it)
+        const int part_env = a->opt_partition;  // NGZ_AGG_OPT_PARTITION
         const uint64_t groups = a->live + n_claims, n_part = a->slots / PART_SLOTS;
         const bool part_ok = P.lds_ok && P.n_vals <= 8 && a->slots >= PART_SLOTS && n_part <= 8192;
         const bool part = part_ok && (part_env == 1 || (part_env != 0 && n_rec >= (1u << 20) && groups > 4096 &&
@@ -3720,11 +3743,11 @@ int ngz_agg_push(ngz_agg *a, ngz_ctx *ctx, const ngz_batch_out *out, const ngz_p
             default: hipLaunchKernelGGL(k_agg_part_scatter<6>, dim3(nt), dim3(256), 4 * np, st, C, P, rec_g, np, offs, pay); break;
             }
             // payloads per thread and round in the reduce (NGZ_AGG_RED_RPT 1 or 4; A/B knob)
-            static const uint32_t red_rpt = getenv("NGZ_AGG_RED_RPT") && atoi(getenv("NGZ_AGG_RED_RPT")) == 1 ? 1u : 4u;
+            static const uint32_t red_rpt = ngz_knob("NGZ_AGG_RED_RPT", 4) == 1 ? 1u : 4u;
             // threads per partition workgroup (one LDS table per workgroup: more threads, more waves
             // per CU on the same LDS; dport push 11.9 -> 10.4 ms at 512, 10.7 at 1024; knob
             // NGZ_AGG_RED_THREADS)
-            static const uint32_t red_thr = getenv("NGZ_AGG_RED_THREADS") ? (uint32_t)std::max(64, std::min(1024, atoi(getenv("NGZ_AGG_RED_THREADS")))) / 64 * 64 : 512u;
+            static const uint32_t red_thr = (uint32_t)std::max<int64_t>(64, std::min<int64_t>(1024, ngz_knob("NGZ_AGG_RED_THREADS", 512))) / 64 * 64;
             switch (pb / 16 * 8 + red_rpt) {
             case 17: hipLaunchKernelGGL((k_agg_part_reduce<2, 1>), dim3(np), dim3(red_thr), 0, st, P, a->plans, offs, nt, pay, a->rows); break;
             case 20: hipLaunchKernelGGL((k_agg_part_reduce<2, 4>), dim3(np), dim3(red_thr), 0, st, P, a->plans, offs, nt, pay, a->rows); break;
@@ -3901,6 +3924,32 @@ int ngz_agg_peer(ngz_agg *a, uint32_t index, ngz_peer *out) {
 
 const char *ngz_agg_last_path(ngz_agg *a) { return a ? a->last_path : ""; }
 
+int ngz_agg_set_option(ngz_agg *a, int opt, int64_t value) {
+    if (!a) return NGZ_E_INVALID;
+    switch (opt) {
+    case NGZ_AGG_OPT_LOWCARD:
+        if (value < -1 || value > 1) return fail(a, NGZ_E_INVALID, "NGZ_AGG_OPT_LOWCARD takes -1, 0 or 1");
+        a->opt_lowcard = (int)value;
+        a->lc_skip = 0;
+        return NGZ_OK;
+    case NGZ_AGG_OPT_PARTITION:
+        if (value < -1 || value > 1) return fail(a, NGZ_E_INVALID, "NGZ_AGG_OPT_PARTITION takes -1, 0 or 1");
+        a->opt_partition = (int)value;
+        return NGZ_OK;
+    case NGZ_AGG_OPT_OWNER:
+        if (value < 0 || value > 1) return fail(a, NGZ_E_INVALID, "NGZ_AGG_OPT_OWNER takes 0 or 1");
+        a->opt_owner = value != 0;
+        return NGZ_OK;
+    case NGZ_AGG_OPT_HASH_BITS:
+        // groups sit at their hash's slot: only an empty table may change the hash
+        if (value < 0 || value > 63) return fail(a, NGZ_E_INVALID, "NGZ_AGG_OPT_HASH_BITS takes 0..63");
+        if (a->live || a->tombs) return fail(a, NGZ_E_INVALID, "NGZ_AGG_OPT_HASH_BITS: the aggregator holds groups");
+        a->P.hash_mask = value ? (1ull << value) - 1 : ~0ull;
+        return NGZ_OK;
+    }
+    return fail(a, NGZ_E_INVALID, "unknown option");
+}
+
 int ngz_agg_last_timing(ngz_agg *a, float *push_ms) {
     if (!a) return NGZ_E_INVALID;
     if (push_ms) *push_ms = a->t_push;
@@ -3928,10 +3977,11 @@ int64_t ngz_agg_row_bytes(ngz_agg *a, const void *row, int is_value, uint32_t in
         off = a->P.key_off[index];
     }
     const uint8_t *slot = (const uint8_t *)row + off;
-    uint32_t n, toff;
+    uint32_t n, toff8;
     memcpy(&n, slot, 4);
-    memcpy(&toff, slot + 4, 4);
-    if (n > BVAL_INLINE && (uint64_t)toff + (n - BVAL_INLINE) > a->out_tails.size()) return NGZ_E_INVALID;
+    memcpy(&toff8, slot + 4, 4);
+    const uint64_t toff = (uint64_t)toff8 << 3;  // 8-byte units (tail_span)
+    if (n > BVAL_INLINE && toff + (n - BVAL_INLINE) > a->out_tails.size()) return NGZ_E_INVALID;
     if (dst)
         for (uint64_t i = 0; i < n && i < cap; ++i)
             dst[i] = i < BVAL_INLINE ? slot[8 + i] : a->out_tails[toff + i - BVAL_INLINE];

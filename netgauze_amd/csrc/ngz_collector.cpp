@@ -603,7 +603,7 @@ int ngz_collector_push(ngz_collector *c, const ngz_peer_key *key, const uint8_t 
             return c->fail(rc, "ngz_ctx_create");
         }
         // per-template kernels only for templates that carry volume (captures are mostly short)
-        if (!getenv("NGZ_SPECIALIZE")) ngz_ctx_set_option(p->ctx, NGZ_OPT_SPECIALIZE, 2);
+        if (ngz_knob("NGZ_SPECIALIZE", -1) < 0) ngz_ctx_set_option(p->ctx, NGZ_OPT_SPECIALIZE, 2);
         p->prefix = "{\"source_address\":\"" + socket_addr(k.src, k.src_port, k.family) +
                     "\",\"destination_address\":\"" + socket_addr(k.dst, k.dst_port, k.family) + "\",\"info\":";
         c->index.emplace(k, c->peers.size());

@@ -327,15 +327,15 @@ void build_plan(Version &v) {
     if (rl <= NGZ_MAX_REC_LEN) P.rpl = 1;
     // per-template kernels stage the columns of 256*lds_waves rows in LDS
     // (NGZ_LDS=0: direct column stores, for A/B measurements)
-    static const bool lds_on = !getenv("NGZ_LDS") || atoi(getenv("NGZ_LDS")) != 0;
+    static const bool lds_on = ngz_knob("NGZ_LDS", 1) != 0;
     // LDS budget per workgroup (gfx950 allows up to 160 KiB) and waves per window
-    static const uint32_t lds_budget = getenv("NGZ_LDS_BUDGET") ? (uint32_t)atoi(getenv("NGZ_LDS_BUDGET")) : NGZ_LDS_BUDGET;
-    static const uint32_t lds_maxw = getenv("NGZ_LDS_MAXW") ? (uint32_t)atoi(getenv("NGZ_LDS_MAXW")) : 4u;
+    static const uint32_t lds_budget = (uint32_t)ngz_knob("NGZ_LDS_BUDGET", NGZ_LDS_BUDGET);
+    static const uint32_t lds_maxw = (uint32_t)ngz_knob("NGZ_LDS_MAXW", 4);
     // columns at least lds_direct bytes wide skip LDS (stored directly; 0 = stage every column).
     // Default: rows too wide for 4 staged waves in the budget send their 8- and 16-byte columns
     // direct (config 5: 4.35 -> 4.12 ms per 10^8 records); narrower rows stage everything
     // (T20 stays at its 1024-row windows).
-    static const int lds_direct_env = getenv("NGZ_LDS_DIRECT_MIN") ? atoi(getenv("NGZ_LDS_DIRECT_MIN")) : -1;
+    static const int lds_direct_env = (int)ngz_knob("NGZ_LDS_DIRECT_MIN", -1);
     const uint32_t lds_direct = lds_direct_env >= 0 ? (uint32_t)lds_direct_env
                                 : (NGZ_REG_WINDOW * 4 * P.row_bytes > lds_budget ? 8u : 0u);
     uint32_t staged = 0;
@@ -867,7 +867,7 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
     // bytes (ipfix.rs:193-214), so datagram d's list fits from entry offsets[d] / that + d.
     // Templates whose records may be shorter than 8 bytes use the record-start bitmap (one
     // bit per batch byte, zeroed per batch).  NGZ_RECMAP: 0 walk twice, 1 bitmap, 2 lists.
-    static const int recmap_env = getenv("NGZ_RECMAP") ? atoi(getenv("NGZ_RECMAP")) : -1;
+    static const int recmap_env = (int)ngz_knob("NGZ_RECMAP", -1);
     const bool lists = any_vlen && recmap_env != 0 && recmap_env != 1 && min_vlen_rec >= 8;
     // Split framing (steady state, every active template with its compiled kernel, record-offset
     // lists): the record walk of the variable-length sets -- one thread per datagram through a
@@ -880,7 +880,7 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
     // decodes side by side took 1.55 ms against 1.50 in turn: framing is bound by the memory
     // system's scattered line requests, as the decode is by bandwidth, not by load latency that
     // another stream could fill.  Off unless NGZ_SPLIT=1 (read per batch).
-    const int split_env = getenv("NGZ_SPLIT") ? atoi(getenv("NGZ_SPLIT")) : 0;
+    const int split_env = ctx->split_framing;
     bool split = false;
     if (split_env && few_rows && lists && ctx->specialize) {
         bool any_v = false, any_f = false, all_spec = true;
@@ -922,7 +922,7 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
     uint64_t arena_cap = (uint64_t)(ratio * (double)in->bytes_size) +
                          (uint64_t)S * (1 + ctx->cap_pad_windows) * (maxwin_row + 256) + 4096;
     arena_cap = std::max<uint64_t>(arena_cap + ctx->arena_shift, ctx->d_arena.cap);
-    static const uint64_t arena_min = getenv("NGZ_ARENA_MIN_MB") ? (uint64_t)atoll(getenv("NGZ_ARENA_MIN_MB")) << 20 : 0;
+    static const uint64_t arena_min = (uint64_t)ngz_knob("NGZ_ARENA_MIN_MB", 0) << 20;
     arena_cap = std::max(arena_cap, arena_min);  // experiment: allocation size vs placement
     const uint16_t *old_rows = ctx->d_slot_row.p;
     if (ctx->d_hdr.ensure(std::max<uint32_t>(N, 1)) || ctx->d_counts.ensure(n_items) || ctx->d_scan.ensure(n_items) ||
@@ -993,7 +993,7 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
     B.n_slots = S;
     B.slot_row = ctx->d_slot_row.p;
     B.n_rows = A;
-    static const bool trace_on = getenv("NGZ_TRACE") && atoi(getenv("NGZ_TRACE")) != 0;
+    static const bool trace_on = ngz_knob("NGZ_TRACE", 0) != 0;
     if (trace_on) {
         const uint64_t n = 2ull * NGZ_TRACE_WINDOWS * std::max<uint32_t>(S, 1);
         if (ctx->d_trace.ensure(n)) return fail(ctx, NGZ_E_NOMEM, "trace buffer");
@@ -1016,7 +1016,7 @@ int run_pipeline(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, const Hos
     B.cap_pad_windows = ctx->cap_pad_windows;
     B.recmap = nullptr;
     B.dsum = nullptr;
-    static const bool dsum_on = !getenv("NGZ_DSUM") || atoi(getenv("NGZ_DSUM")) != 0;
+    static const bool dsum_on = ngz_knob("NGZ_DSUM", 1) != 0;
     if (dsum_on && N) {
         if (ctx->d_dsum.ensure(N)) return fail(ctx, NGZ_E_NOMEM, "device alloc (datagram summaries)");
         B.dsum = ctx->d_dsum.p;
@@ -1357,7 +1357,7 @@ int place_arena(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st) {
         ms.push_back(ctx->t_decode);
     }
     const size_t best = (size_t)(std::min_element(ms.begin(), ms.end()) - ms.begin());
-    if (getenv("NGZ_DEBUG")) {
+    if (ngz_debug()) {
         fprintf(stderr, "[ngz] arena placement:");
         for (float m : ms) fprintf(stderr, " %.3f", m);
         fprintf(stderr, " ms -> %zu\n", best);
@@ -1433,7 +1433,7 @@ int ngz_ctx_create(int device, ngz_ctx **out) {
         return NGZ_E_DEVICE;
     }
     for (auto &e : ctx->ev) hipEventCreate(&e);
-    if (const char *e = getenv("NGZ_DECODE_STREAMS")) ctx->n_aux = (uint32_t)std::max(0, std::min(NGZ_MAX_AUX, atoi(e) - 1));
+    if (const int64_t e = ngz_knob("NGZ_DECODE_STREAMS", 0)) ctx->n_aux = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(NGZ_MAX_AUX, e - 1));
     for (uint32_t i = 0; i < ctx->n_aux; ++i) {
         if (hipStreamCreateWithFlags(&ctx->aux[i], hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&ctx->join_ev[i], hipEventDisableTiming) != hipSuccess) {
@@ -1456,15 +1456,16 @@ int ngz_ctx_create(int device, ngz_ctx **out) {
         ngz_ctx_destroy(ctx);
         return NGZ_E_NOMEM;
     }
-    if (const char *e = getenv("NGZ_SPECIALIZE")) ctx->specialize = atoi(e);
-    if (const char *e = getenv("NGZ_SPIN")) ctx->spin_wait = atoi(e) != 0;
-    if (const char *e = getenv("NGZ_ARENA_CONTIG")) ctx->d_arena.contiguous = atoi(e) != 0;
-    if (const char *e = getenv("NGZ_PLACE_TRIALS")) ctx->place_trials = atoi(e);
-    if (const char *e = getenv("NGZ_CAP_PAD")) ctx->cap_pad_windows = (uint32_t)std::max(0, std::min(200000, atoi(e)));
+    // defaults; hosts choose through ngz_ctx_set_option (experiment builds also read NGZ_<name>)
+    ctx->specialize = (int)ngz_knob("NGZ_SPECIALIZE", ctx->specialize);
+    ctx->spin_wait = ngz_knob("NGZ_SPIN", ctx->spin_wait) != 0;
+    ctx->d_arena.contiguous = ngz_knob("NGZ_ARENA_CONTIG", ctx->d_arena.contiguous) != 0;
+    ctx->place_trials = (int)ngz_knob("NGZ_PLACE_TRIALS", ctx->place_trials);
+    ctx->cap_pad_windows = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(200000, ngz_knob("NGZ_CAP_PAD", ctx->cap_pad_windows)));
     *ctx->h_done = 0;
-    if (const char *e = getenv("NGZ_BLOCKS_PER_CU")) ctx->blocks_per_cu = std::max(1, std::min(32, atoi(e)));
-    if (const char *e = getenv("NGZ_LDS_BLOCKS_PER_CU")) ctx->lds_blocks_per_cu = std::max(1, std::min(512, atoi(e)));
-    if (const char *e = getenv("NGZ_GROUP")) ctx->group_launch = atoi(e) != 0;
+    ctx->blocks_per_cu = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(32, ngz_knob("NGZ_BLOCKS_PER_CU", ctx->blocks_per_cu)));
+    ctx->lds_blocks_per_cu = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(512, ngz_knob("NGZ_LDS_BLOCKS_PER_CU", ctx->lds_blocks_per_cu)));
+    ctx->group_launch = ngz_knob("NGZ_GROUP", ctx->group_launch) != 0;
     *out = ctx;
     return NGZ_OK;
 }
@@ -1546,6 +1547,18 @@ int ngz_ctx_set_option(ngz_ctx *ctx, int opt, int64_t value) {
     case NGZ_OPT_BLOCKS_PER_CU:
         if (value < 1 || value > 32) return fail(ctx, NGZ_E_INVALID, "NGZ_OPT_BLOCKS_PER_CU takes 1..32");
         ctx->blocks_per_cu = (uint32_t)value;
+        return NGZ_OK;
+    case NGZ_OPT_SPLIT:
+        if (value < 0 || value > 1) return fail(ctx, NGZ_E_INVALID, "NGZ_OPT_SPLIT takes 0 or 1");
+        ctx->split_framing = (int)value;
+        return NGZ_OK;
+    case NGZ_OPT_GROUP:
+        if (value < 0 || value > 1) return fail(ctx, NGZ_E_INVALID, "NGZ_OPT_GROUP takes 0 or 1");
+        ctx->group_launch = value != 0;
+        return NGZ_OK;
+    case NGZ_OPT_PLACE_TRIALS:
+        if (value < 1 || value > 16) return fail(ctx, NGZ_E_INVALID, "NGZ_OPT_PLACE_TRIALS takes 1..16");
+        ctx->place_trials = (int)value;
         return NGZ_OK;
     }
     return fail(ctx, NGZ_E_INVALID, "unknown option");
@@ -1687,7 +1700,7 @@ int ngz_decode_batch(ngz_ctx *ctx, const ngz_batch_in *in, ngz_batch_out *out, v
         }
         rc = upload_slots(ctx, cur0, st);
         if (rc) return rc;
-        if (getenv("NGZ_DEBUG")) {
+        if (ngz_debug()) {
             fprintf(stderr, "[ngz] slow path round %d: host dgrams %zu, slots %zu, timeline %zu\n", round,
                     host_idx.size(), ctx->slot_version.size(), hf.tl.key.size());
             for (size_t i = 0; i < hf.tl.key.size(); ++i)
@@ -1706,7 +1719,7 @@ int ngz_decode_batch(ngz_ctx *ctx, const ngz_batch_in *in, ngz_batch_out *out, v
         std::vector<ngz_dgram_hdr> h2(N);
         HIPCHK(hipMemcpy(h2.data(), ctx->d_hdr.p, N * sizeof(ngz_dgram_hdr), hipMemcpyDeviceToHost));
         bool redo = false;
-        if (getenv("NGZ_DEBUG"))
+        if (ngz_debug())
             for (size_t i = 0; i < host_idx.size(); ++i)
                 fprintf(stderr, "[ngz]   host dgram %u flag %u status %u err %016llx limit %u defs %zu\n", host_idx[i],
                         hf.flag[host_idx[i]], h2[host_idx[i]].status, (unsigned long long)h2[host_idx[i]].err_key,
@@ -1767,17 +1780,31 @@ int64_t ngz_columns_to_host_async(ngz_ctx *ctx, void *dst, uint64_t cap, void *h
         }
         to = (uint8_t *)dp;
     }
+    // the whole size first: a copy too large for dst queues nothing
+    uint64_t total = 0;
+    for (size_t s = 0; s < ctx->slot_infos.size(); ++s) {
+        const ngz_slot_info &si = ctx->slot_infos[s];
+        if (si.n_records)
+            total = ((total + 255) & ~255ull) + (uint64_t)si.capacity * ctx->versions[si.version_id].plan.row_bytes;
+    }
+    if (total > cap) return fail(ctx, NGZ_E_INVALID, "ngz_columns_to_host: destination too small");
     if (!ctx->d2h_ev) HIPCHK(hipEventCreateWithFlags(&ctx->d2h_ev, hipEventDisableTiming));
     HIPCHK(hipStreamWaitEvent(st, ctx->ev[3], 0));  // the end of the last batch's pipeline
+    // one event covers every queued copy: a copy queued earlier on another stream is waited for
+    // by this one's stream before the event is recorded again (the next decode waits on it)
+    if (ctx->d2h_pending) HIPCHK(hipStreamWaitEvent(st, ctx->d2h_ev, 0));
     uint64_t at = 0;
     for (size_t s = 0; s < ctx->slot_infos.size(); ++s) {
         const ngz_slot_info &si = ctx->slot_infos[s];
         if (!si.n_records) continue;
         const uint64_t bytes = (uint64_t)si.capacity * ctx->versions[si.version_id].plan.row_bytes;
         at = (at + 255) & ~255ull;
-        if (at + bytes > cap) return fail(ctx, NGZ_E_INVALID, "ngz_columns_to_host: destination too small");
         if (flags & NGZ_D2H_KERNEL) {
-            if (ngz_launch_to_host(si.columns, to + at, bytes, st)) return fail(ctx, NGZ_E_DEVICE, "k_to_host launch");
+            if (ngz_launch_to_host(si.columns, to + at, bytes, st)) {
+                ctx->d2h_pending = at > 0 || ctx->d2h_pending;
+                if (ctx->d2h_pending) (void)hipEventRecord(ctx->d2h_ev, st);
+                return fail(ctx, NGZ_E_DEVICE, "k_to_host launch");
+            }
         } else {
             HIPCHK(hipMemcpyAsync(to + at, si.columns, bytes, hipMemcpyDeviceToHost, st));
         }
@@ -1791,7 +1818,8 @@ int64_t ngz_columns_to_host_async(ngz_ctx *ctx, void *dst, uint64_t cap, void *h
 int64_t ngz_columns_to_host(ngz_ctx *ctx, void *dst, uint64_t cap) {
     const int64_t n = ngz_columns_to_host_async(ctx, dst, cap, nullptr, 0);
     if (n < 0) return n;
-    HIPCHK(hipStreamSynchronize(ctx->stream));
+    // the event covers this copy and every copy queued before it on any stream
+    HIPCHK(hipEventSynchronize(ctx->d2h_ev));
     ctx->d2h_pending = false;
     return n;
 }

@@ -274,14 +274,15 @@ struct ngz_ctx {
     uint32_t lds_blocks_per_cu = 8;             // LDS-staged decode grid (2 resident per CU at 64 KB)
     // multi-template decode launches (ngz_rtc.cpp generate_group): one kernel for the
     // LDS-staged specialised templates of a batch that share a workgroup shape, per set of
-    // template versions; NGZ_GROUP=1 turns it on (default: one launch per template)
+    // template versions; NGZ_OPT_GROUP 1 turns it on (default: one launch per template)
     struct GroupKernel {
         int state = 0;  // 0 not looked up, 1 ready, 2 unavailable, 3 compiling
         void *fn = nullptr;
         void *entry = nullptr;
     };
     std::map<std::vector<int32_t>, GroupKernel> group_kernels;
-    bool group_launch = false;
+    bool group_launch = false;                  // NGZ_OPT_GROUP
+    int split_framing = 0;                      // NGZ_OPT_SPLIT
     // device summary / processed_count increments alternate between two
     // parities: a batch's k_export zeroes the other parity for the next one
     int parity = 0;
@@ -296,7 +297,7 @@ struct ngz_ctx {
     unsigned long long *h_done = nullptr, *dh_done = nullptr;  // k_export completion word (pinned)
     unsigned long long export_seq = 0;
     uint32_t cap_pad_windows = 0;               // NGZ_OPT_CAP_PAD
-    int place_trials = 6;                       // arena placement trials on the first large batch (NGZ_PLACE_TRIALS)
+    int place_trials = 6;                       // arena placement trials on the first large batch (NGZ_OPT_PLACE_TRIALS)
     bool placed = false;
     uint64_t arena_shift = 0;                   // NGZ_OPT_ARENA_SHIFT: columns start this far into the arena
     bool spin_wait = true;                      // wait for a batch by spinning on h_done (NGZ_SPIN=0: stream sync)

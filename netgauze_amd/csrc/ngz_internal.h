@@ -17,6 +17,15 @@
 #define NGZ_REG_WINDOW 256    // records per chunk window (4 passes of 64 lanes)
 #define NGZ_LDS_BUDGET 65536  // LDS bytes one workgroup may stage columns in
 
+#ifndef __HIPCC_RTC__
+// Experiment knobs (ngz_knobs.cpp): `dflt` in the product library; NGZ_<name> from the
+// environment only in a -DNGZ_EXPERIMENTS build.  ngz_debug(): NGZ_DEBUG stderr traces.
+int64_t ngz_knob(const char *name, int64_t dflt);
+const char *ngz_knob_str(const char *name, const char *dflt);
+bool ngz_debug();
+extern "C" int ngz_experiments_build();  // 1 in a -DNGZ_EXPERIMENTS build (tests check the product is not)
+#endif
+
 // Workgroup window of the LDS-staged per-template kernels: a workgroup
 // decodes lds_waves consecutive 256-row windows (one per wave) into LDS,
 // column-major, then writes every column's 256*lds_waves rows as one

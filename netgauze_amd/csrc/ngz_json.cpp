@@ -562,12 +562,13 @@ void put_bytes(std::string &o, uint32_t pen, uint16_t id, const std::vector<uint
     put_field(o, s, fd, cell, b.data());
 }
 
-// the whole byte value of a row's BVAL key / value
-std::vector<uint8_t> row_bytes(ngz_agg *a, const uint8_t *R, int is_value, uint32_t i) {
+// the whole byte value of a row's BVAL key / value; false when the row's tail is not in the
+// tails of the last flush / emit (a row of an earlier call): the caller fails, NGZ_E_INVALID
+bool row_bytes(ngz_agg *a, const uint8_t *R, int is_value, uint32_t i, std::vector<uint8_t> &b) {
     const int64_t n = ngz_agg_row_bytes(a, R, is_value, i, nullptr, 0);
-    std::vector<uint8_t> b(n > 0 ? (size_t)n : 0);
-    if (n > 0) ngz_agg_row_bytes(a, R, is_value, i, b.data(), b.size());
-    return b;
+    if (n < 0) return false;
+    b.assign((size_t)n, 0);
+    return n == 0 || ngz_agg_row_bytes(a, R, is_value, i, b.data(), b.size()) == n;
 }
 
 }  // namespace
@@ -618,7 +619,9 @@ extern "C" int64_t ngz_agg_flowinfo_json(ngz_agg *a, const void *rows, uint64_t 
             sep();
             const uint8_t *c = R + ko[k];
             if (kd[k].kkind == 3) {  // a byte value of any length
-                put_bytes(o, keys[k].pen, keys[k].ie_id, row_bytes(a, R, 0, k));
+                std::vector<uint8_t> b;
+                if (!row_bytes(a, R, 0, k, b)) return NGZ_E_INVALID;
+                put_bytes(o, keys[k].pen, keys[k].ie_id, b);
             } else {
                 put_cell(o, keys[k].pen, keys[k].ie_id, kd[k].kind, kd[k].width, c);
             }
@@ -642,7 +645,12 @@ extern "C" int64_t ngz_agg_flowinfo_json(ngz_agg *a, const void *rows, uint64_t 
             case 6: put_cell(o, vals[v].pen, vals[v].ie_id, NGZ_K_UINT, 8, c); break;
             case 7: put_cell(o, vals[v].pen, vals[v].ie_id, NGZ_K_BYTES, 16, c); break;
             case 8:
-            case 9: put_bytes(o, vals[v].pen, vals[v].ie_id, row_bytes(a, R, 1, v)); break;
+            case 9: {
+                std::vector<uint8_t> b;
+                if (!row_bytes(a, R, 1, v, b)) return NGZ_E_INVALID;
+                put_bytes(o, vals[v].pen, vals[v].ie_id, b);
+                break;
+            }
             default: put_cell(o, vals[v].pen, vals[v].ie_id, vd[v].kind, vd[v].width, c); break;
             }
         }

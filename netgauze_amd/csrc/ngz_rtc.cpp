@@ -58,18 +58,17 @@ struct Item {           // one extraction step of the generated pass body
 // Cache-policy defines of the generated source (NGZ_LD_AUX / NGZ_ST_AUX, experiments only; ngz_dev.h)
 std::string cpol_defines() {
     std::string s;
-    if (const char *e = getenv("NGZ_LD_AUX")) s += "#define NGZ_LD_AUX " + std::to_string(atoi(e)) + "\n";
-    if (const char *e = getenv("NGZ_ST_AUX")) s += "#define NGZ_ST_AUX " + std::to_string(atoi(e)) + "\n";
-    if (const char *e = getenv("NGZ_WIN_ROT")) s += "#define NGZ_WIN_ROT " + std::to_string(atoi(e)) + "\n";
+    for (const char *k : {"NGZ_LD_AUX", "NGZ_ST_AUX", "NGZ_WIN_ROT"})
+        if (const int64_t v = ngz_knob(k, -1); v >= 0) s += std::string("#define ") + k + " " + std::to_string(v) + "\n";
     return s;
 }
 
 std::string signature(const DevPlan &P) {
     std::string s = "rl" + std::to_string(P.rec_len) + "lw" + std::to_string(P.lds_waves) + "dm" +
                     std::to_string(P.reserved0);
-    if (const char *e = getenv("NGZ_LD_AUX")) s += "la" + std::to_string(atoi(e));
-    if (const char *e = getenv("NGZ_ST_AUX")) s += "sa" + std::to_string(atoi(e));
-    if (const char *e = getenv("NGZ_WIN_ROT")) s += "wr" + std::to_string(atoi(e));
+    if (const int64_t v = ngz_knob("NGZ_LD_AUX", -1); v >= 0) s += "la" + std::to_string(v);
+    if (const int64_t v = ngz_knob("NGZ_ST_AUX", -1); v >= 0) s += "sa" + std::to_string(v);
+    if (const int64_t v = ngz_knob("NGZ_WIN_ROT", -1); v >= 0) s += "wr" + std::to_string(v);
     char b[96];
     for (uint32_t f = 0; f < P.n_fields; ++f) {
         const DevField &d = P.f[f];
@@ -171,9 +170,9 @@ FixedParts fixed_parts(const DevPlan &P) {
     // span), where 4 consecutive rows per lane spread it over 4x as many
     // cache lines; T20 at 10^8 records decoded in 2.15 ms (r1) vs 2.55 ms
     // (c4) on the same box (profiles/r1e).
-    const char *layout = getenv("NGZ_RTC_LAYOUT");
-    if (!layout && P.lds_waves) layout = getenv("NGZ_RTC_LDS_LAYOUT") ? getenv("NGZ_RTC_LDS_LAYOUT") : "r1";
-    if (!layout && P.rec_len > 76) layout = getenv("NGZ_RTC_LONG") ? getenv("NGZ_RTC_LONG") : "r1";
+    const char *layout = ngz_knob_str("NGZ_RTC_LAYOUT", nullptr);
+    if (!layout && P.lds_waves) layout = ngz_knob_str("NGZ_RTC_LDS_LAYOUT", "r1");
+    if (!layout && P.rec_len > 76) layout = ngz_knob_str("NGZ_RTC_LONG", "r1");
     if (layout) {
         if (layout[0] == 'c' || layout[0] == 'r') {
             consec = layout[0] == 'c';
@@ -298,7 +297,7 @@ FixedParts fixed_parts(const DevPlan &P) {
             }
         }
         // NGZ_RTC_EXP=1: no store step (timing experiments only; output invalid)
-        if (getenv("NGZ_RTC_EXP") && (atoi(getenv("NGZ_RTC_EXP")) & 1)) per_wave.assign(lw, "");
+        if (ngz_knob("NGZ_RTC_EXP", 0) & 1) per_wave.assign(lw, "");
         std::string st;
         st += "    auto store = [&](uint32_t W, uint8_t *blk, uint32_t cap) {\n";
         st += "        const uint32_t q = sgpr(threadIdx.x >> 6);\n";
@@ -708,7 +707,7 @@ bool compile(const std::string &src, std::vector<char> &code, std::string &log) 
 void build(Entry *e, int device, const std::string &src, const std::string &sig, const char *kname) {
     std::vector<char> code;
     std::string log;
-    if (getenv("NGZ_RTC_DUMP")) fprintf(stderr, "[ngz rtc] source:\n%s\n", src.c_str());
+    if (ngz_debug()) fprintf(stderr, "[ngz rtc] source:\n%s\n", src.c_str());
     if (!compile(src, code, log)) {
         fprintf(stderr, "[ngz rtc] compile failed for %s:\n%s\n", sig.c_str(), log.c_str());
         e->state.store(3, std::memory_order_release);

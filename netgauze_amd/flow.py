@@ -166,15 +166,19 @@ class DecodedBatch:
 OPT_SPECIALIZE = 1
 OPT_BLOCKS_PER_CU = 2
 OPT_RTC_SYNC = 5
+OPT_SPLIT = 6         # split framing (flow_decode.h NGZ_OPT_SPLIT)
+OPT_GROUP = 7         # multi-template decode launches
+OPT_PLACE_TRIALS = 8  # column arenas tried for the first large batch
 D2H_KERNEL = 1  # NGZ_D2H_KERNEL
 
 
 class FlowInfoCodec:
-    def __init__(self, device=0, specialize=None, rtc_sync=None):
+    def __init__(self, device=0, specialize=None, rtc_sync=None, options=None):
         """specialize: None (library default: per-template kernels, compiled in
         the background), True (per-template kernels, each template's first batch
         waits for its compile: deterministic kernel choice), False (generic
-        kernel only).  rtc_sync overrides the waiting."""
+        kernel only).  rtc_sync overrides the waiting.  options: {OPT_*: value}
+        for ngz_ctx_set_option (how batches run, never their results)."""
         self.generation = 0  # batches decoded so far (DecodedBatch.generation)
         ctx = ctypes.c_void_p()
         rc = lib().ngz_ctx_create(device, ctypes.byref(ctx))
@@ -186,6 +190,8 @@ class FlowInfoCodec:
         if rtc_sync is None:
             rtc_sync = bool(specialize)
         self.set_option(OPT_RTC_SYNC, 1 if rtc_sync else 0)
+        for opt, value in (options or {}).items():
+            self.set_option(opt, value)
 
     def set_option(self, opt, value):
         self._check(lib().ngz_ctx_set_option(self._ctx, opt, int(value)))

@@ -129,6 +129,60 @@ def reduce_value(ie, op, lhs, rhs):
     return lhs | rhs
 
 
+# IE::supports_{arithmetic,comparison,bitwise}_ops (ipfix-code-generator/src/generator.rs:1176-1272)
+_NUMERIC = {"signed8", "signed16", "signed32", "signed64", "unsigned8", "unsigned16", "unsigned32", "unsigned64",
+            "float32", "float64"}
+_CMP_TYPES = _NUMERIC | {"dateTimeSeconds", "dateTimeMilliseconds", "dateTimeMicroseconds", "dateTimeNanoseconds",
+                         "ipv4Address", "ipv6Address", "basicList", "subTemplateList", "subTemplateMultiList"}
+_BIT_TYPES = (_NUMERIC - {"float32", "float64"}) | {"octetArray", "boolean", "macAddress", "ipv4Address",
+                                                    "ipv6Address", "unsigned256"}
+_SEMANTICS = None
+
+
+def _semantics(ie):
+    global _SEMANTICS
+    if _SEMANTICS is None:
+        import json
+        with open(O._REG_PATH) as f:
+            _SEMANTICS = {(r["pen"], r["id"]): r.get("semantics") for r in json.load(f)["ies"]}
+    return _SEMANTICS.get((ie.pen, ie.id)) if ie.kind in ("iana", "vendor") else None
+
+
+def supports(ie, op):
+    """generator.rs:1176-1272.  Arithmetic: a numeric type (unsigned256 excluded) without a
+    sub-registry and without identifier / flags dataTypeSemantics; comparison and bitwise by data
+    type alone."""
+    if op == OP_ADD:
+        if _semantics(ie) in ("identifier", "flags") or ie.subreg is not None:
+            return False
+        return ie.dtype in _NUMERIC
+    if op in (OP_MIN, OP_MAX):
+        return ie.dtype in _CMP_TYPES
+    if op == OP_OR:
+        return ie.dtype in _BIT_TYPES
+    raise ValueError(op)
+
+
+class FieldOperationError(Exception):
+    """FieldOperationError::Inapplicable{Add,Min,Max,Bitwise}(IE, IE) (generator.rs:801-807; the
+    vendor enums' own variants map into it, :2476-2492)."""
+    VARIANT = {OP_ADD: "InapplicableAdd", OP_MIN: "InapplicableMin", OP_MAX: "InapplicableMax",
+               OP_OR: "InapplicableBitwise"}
+
+    def __init__(self, op, lhs_ie, rhs_ie):
+        super().__init__(self.VARIANT[op], lhs_ie, rhs_ie)
+        self.variant, self.lhs, self.rhs = self.VARIANT[op], lhs_ie, rhs_ie
+
+
+def field_op(op, lhs_ie, lhs, rhs_ie, rhs):
+    """Field::{add,min,max,bitwise_or}_field (generator.rs:812-880, vendor Field :2514-2580): the
+    generated match has an arm for (IE x, IE x) of every IE whose type supports the op; any other
+    pair -- two different IEs, or an IE without the op -- falls to Inapplicable*(lhs.ie(), rhs.ie())."""
+    if lhs_ie != rhs_ie or not supports(lhs_ie, op):
+        raise FieldOperationError(op, lhs_ie, rhs_ie)
+    return reduce_value(lhs_ie, op, lhs, rhs)
+
+
 def map_fields(fields):
     """FieldRef::map_fields (types.rs:82-100): (IE key, occurrence index) -> Field."""
     seen, out = {}, {}

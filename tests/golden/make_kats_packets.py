@@ -6,7 +6,7 @@ Run in the build container, where the reference checkout exists:
 
 Only the *input* byte arrays are extracted (data, not source): every
 `let NAME = [ ... ];` / `const NAME: &[u8] = &[ ... ];` literal inside the
-listed test functions, keyed "file:function:variable", with the line it was
+listed test functions (and `let NAME: Vec<u8> = vec![ ... ];`), keyed "file:function:variable", with the line it was
 found on.  The expected results those tests assert are restated by hand in
 tests/kats_packets.py next to the citation of each assertion.
 """
@@ -16,6 +16,7 @@ import re
 import sys
 
 FILES = [
+    "crates/flow-pkt/src/codec.rs",
     "crates/flow-pkt/src/wire/tests/mod.rs",
     "crates/flow-pkt/src/wire/tests/ipfix.rs",
     "crates/flow-pkt/src/wire/tests/netflow.rs",
@@ -24,7 +25,7 @@ FILES = [
 ]
 
 _FN = re.compile(r"^\s*(?:pub\s+)?fn\s+(\w+)\s*\(")
-_LET = re.compile(r"^\s*(?:let\s+(?:mut\s+)?(\w+)\s*=\s*|const\s+(\w+)\s*:\s*&\[u8\]\s*=\s*&)\[(.*)$")
+_LET = re.compile(r"^\s*(?:let\s+(?:mut\s+)?(\w+)\s*(?::\s*Vec<u8>\s*=\s*vec!|=\s*)|const\s+(\w+)\s*:\s*&\[u8\]\s*=\s*&)\[(.*)$")
 _NUM = re.compile(r"0x[0-9a-fA-F]+|\d+")
 
 

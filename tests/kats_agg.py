@@ -354,3 +354,101 @@ FLOWINFO_EXPECTED_FIELDS = [
     {"NetGauze": {"originalTemplateId": 256}}, {"NetGauze": {"originalTemplateId": 257}},
     {"originalExporterIPv4Address": FLOWINFO_PEER},  # actor.rs:222-225
 ]
+
+
+# ---------------------------------------------------------------------------------------------
+# Field arithmetic KATs of crates/flow-pkt/src/lib.rs:359-615: Field::{add,min,max,bitwise_or}_field
+# (and the *_assign_field forms, same results) on two fields of one IE, and the
+# FieldOperationError::Inapplicable* pair for a field of another IE.  IEs as (pen, id, name):
+# VMware (PEN 6876) averageLatency 958 unsigned32, algControlFlowId 955 unsigned64 identifier.
+# Each entry: (test, src, op, ie, lhs, rhs, expected, other_ie, error variant).
+# ---------------------------------------------------------------------------------------------
+IE_OCTETS = (0, 1, "octetDeltaCount")
+IE_PACKETS = (0, 2, "packetDeltaCount")
+IE_TCP_FLAGS = (0, 6, "tcpControlBits")
+IE_PROTOCOL = (0, 4, "protocolIdentifier")
+IE_VMW_LATENCY = (6876, 958, "averageLatency")
+IE_VMW_ALG_FLOW = (6876, 955, "algControlFlowId")
+ICMP, IGMP = 1, 2  # protocolIdentifier::ICMP / IGMP
+
+FIELD_OP_KATS = [
+    ("test_field_add", "lib.rs:359-382", OP_ADD, IE_OCTETS, 100, 200, 300, IE_PACKETS, "InapplicableAdd"),
+    ("test_field_min", "lib.rs:383-406", OP_MIN, IE_OCTETS, 100, 200, 100, IE_PACKETS, "InapplicableMin"),
+    ("test_field_max", "lib.rs:407-430", OP_MAX, IE_OCTETS, 100, 200, 200, IE_PACKETS, "InapplicableMax"),
+    ("test_field_bitwise_or", "lib.rs:431-454", OP_OR, IE_OCTETS, 100, 200, 236, IE_PACKETS, "InapplicableBitwise"),
+    ("test_field_bitwise_or_tcp_control_bits", "lib.rs:455-478", OP_OR, IE_TCP_FLAGS, 0x01, 0x02, 0x03, IE_PACKETS,
+     "InapplicableBitwise"),
+    ("test_field_bitwise_or_protocol_identifier", "lib.rs:479-502", OP_OR, IE_PROTOCOL, ICMP, IGMP, 0x03, IE_PACKETS,
+     "InapplicableBitwise"),
+    ("test_vmware_ops", "lib.rs:503-526", OP_ADD, IE_VMW_LATENCY, 100, 200, 300, IE_VMW_ALG_FLOW, "InapplicableAdd"),
+    ("test_vendor_field_add", "lib.rs:527-548", OP_ADD, IE_VMW_LATENCY, 100, 200, 300, IE_VMW_ALG_FLOW,
+     "InapplicableAdd"),
+    ("test_vendor_field_min", "lib.rs:549-570", OP_MIN, IE_VMW_LATENCY, 100, 200, 100, IE_VMW_ALG_FLOW,
+     "InapplicableMin"),
+    ("test_vendor_field_max", "lib.rs:571-592", OP_MAX, IE_VMW_LATENCY, 100, 200, 200, IE_VMW_ALG_FLOW,
+     "InapplicableMax"),
+    ("test_vendor_field_bitwise_or", "lib.rs:593-615", OP_OR, IE_VMW_ALG_FLOW, 100, 200, 236, IE_VMW_LATENCY,
+     "InapplicableBitwise"),
+]
+
+# IE::supports_{arithmetic,bitwise,comparison}_ops asserts of lib.rs:267-358, by IE name:
+# (arithmetic, bitwise, comparison); None where the reference test asserts nothing.
+SUPPORTS_KATS = {
+    "mplsLabelStackSection": (False, True, False), "paddingOctets": (False, True, False),
+    "destinationIPv4PrefixLength": (True, True, True), "flowActiveTimeout": (True, True, True),
+    "distinctCountOfSourceIPv4Address": (True, True, True), "postMCastPacketDeltaCount": (True, True, True),
+    "ipv6ExtensionHeadersFull": (False, True, False), "mibObjectValueInteger": (True, True, True),
+    "absoluteError": (True, None, None),
+    "ipClassOfService": (False, True, True), "egressInterface": (False, True, True),
+    "forwardingStatus": (False, True, True), "dataRecordsReliability": (False, True, False),
+    "observationTimeSeconds": (False, False, True), "observationTimeMilliseconds": (False, False, True),
+    "observationTimeNanoseconds": (False, False, True), "observationTimeMicroseconds": (False, False, True),
+    "sourceIPv4Address": (False, True, True), "sourceIPv6Address": (False, True, True),
+    "bgpSourceCommunityList": (False, None, None), "ipv6ExtensionHeaderTypeCountList": (False, None, None),
+    "subTemplateMultiList": (False, None, None),
+}
+
+_WIDTH = {(0, 1): 8, (0, 2): 8, (0, 6): 2, (0, 4): 1, (6876, 958): 4, (6876, 955): 8}
+
+
+def etset(tid, fields):
+    """An IPFIX template set of (pen, id, length) specifiers (enterprise bit set for pen != 0)."""
+    spec = b"".join(struct.pack(">HH", i | 0x8000, n) + struct.pack(">I", p) if p else struct.pack(">HH", i, n)
+                    for p, i, n in fields)
+    body = struct.pack(">HH", tid, len(fields)) + spec
+    return struct.pack(">HH", 2, 4 + len(body)) + body
+
+
+def _field_record(ie, v):
+    w = _WIDTH[ie[:2]]
+    return struct.pack(">I", k_10_1) + v.to_bytes(w, "big")
+
+
+def field_op_scenario(kat):
+    """One FIELD_OP_KATS entry as two records of one group: key sourceIPv4Address, the IE under the
+    KAT's op; lhs arrives first (Ord::min keeps it on equality, Ord::max takes the rhs).  Then the
+    Inapplicable pair: an aggregator with the op on both IEs, one record carrying only the first
+    IE and one only the other -- the reduce never combines two IEs (FieldRef lookup, types.rs:82-100;
+    aggregator.rs:159-198), so each keeps its own value."""
+    name, src, op, ie, lhs, rhs, exp, other, _err = kat
+    p, i, _ = ie
+    tpl = [(0, SRC4, 4), (p, i, _WIDTH[ie[:2]])]
+    msg = ipfix_msg([etset(300, tpl), dset(300, [_field_record(ie, lhs), _field_record(ie, rhs)])], T10, 1, 100)
+    same = _s("fieldop_" + name, src, [(0, SRC4, 0, OP_KEY), (p, i, 0, op)],
+              [(P192_1, 9995, T10_MS, [msg])],
+              [G(P192_1, T10, (k_10_1,), (exp,), count=2, coll_ms=T10_MS, templates={(10, 300)}, ports={9995},
+                 domains={100})])
+    op2 = other[:2]
+    # algControlFlowId has identifier semantics: no Add (generator.rs:1176-1181); Max there instead
+    other_op = OP_MAX if (op == OP_ADD and other == IE_VMW_ALG_FLOW) else op
+    tpl2 = [(0, SRC4, 4), (op2[0], op2[1], _WIDTH[op2])]
+    msg2 = ipfix_msg([etset(300, tpl), etset(301, tpl2), dset(300, [_field_record(ie, lhs)]),
+                      dset(301, [_field_record(other, rhs)])], T10, 2, 100)
+    pair = _s("fieldop_pair_" + name, src, [(0, SRC4, 0, OP_KEY), (p, i, 0, op), (op2[0], op2[1], 0, other_op)],
+              [(P192_1, 9995, T10_MS, [msg2])],
+              [G(P192_1, T10, (k_10_1,), (lhs, rhs), count=2, coll_ms=T10_MS, templates={(10, 300), (10, 301)},
+                 ports={9995}, domains={100})])
+    return [same, pair]
+
+
+FIELD_OP_SCENARIOS = [s for kat in FIELD_OP_KATS for s in field_op_scenario(kat)]

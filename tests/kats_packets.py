@@ -584,3 +584,12 @@ READER_KATS = [
 READER_SHORTENED = [bytes([0xAB, 0xCD]), bytes([0x00, 0xAB, 0xCD]), bytes([0x00, 0x00, 0xAB, 0xCD])]
 # reader.rs:430-439, 511-520: len beyond the width is rejected before consuming
 READER_TOO_WIDE = [("uint64", 9, ("pad", 0, 9, 8)), ("uint32", 5, ("pad", 0, 5, 4))]
+
+
+# --- FlowInfoCodec::decode KAT (crates/flow-pkt/src/codec.rs:226-249) ---------------------------
+# test_decode_partial_messages: one codec, two decode calls on their own buffers.  value1 is an
+# IPFIX header announcing 116 bytes followed by 2 of them (18 bytes), value2 a single byte (shorter
+# than the 16-byte header gate, codec.rs:197-201): both Ok(None) -- NGZ_DG_NEED_MORE at the C ABI --
+# and neither consumes a byte (the gates return before the buffer is touched, codec.rs:197-207).
+C_ = "codec.rs:test_decode_partial_messages:"
+CODEC_PARTIAL = [(C_ + "value1", None), (C_ + "value2", None)]  # (wire, expected decode result)

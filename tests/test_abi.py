@@ -120,6 +120,29 @@ def test_agg_config_validation_without_device():
             assert rc == -4, ((pen, ie), op, rc)
 
 
+def test_agg_config_follows_reference_supports_kats():
+    """The IE::supports_{arithmetic,bitwise,comparison}_ops asserts of lib.rs:267-358
+    (tests/kats_agg.py SUPPORTS_KATS) through ngz_agg_create's validation: an op the reference
+    supports is accepted (the call goes on to the device: no GPU here), one it does not is
+    NGZ_E_INVALID."""
+    import json
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import kats_agg as K
+    from netgauze_amd import _lib
+    lib = _lib.load()
+    reg = json.load(open(os.path.join(ROOT, "netgauze_amd", "data", "ie_registry.json")))
+    ids = {r["name"]: r["id"] for r in reg["ies"] if r["pen"] == 0}
+    for name, (arith, bit, cmp_) in K.SUPPORTS_KATS.items():
+        for op, want in ((_lib.NGZ_AGG_ADD, arith), (_lib.NGZ_AGG_OR, bit), (_lib.NGZ_AGG_MIN, cmp_),
+                         (_lib.NGZ_AGG_MAX, cmp_)):
+            if want is None:
+                continue
+            arr = (_lib.AggField * 1)(_lib.AggField(0, ids[name], 0, op))
+            h = ctypes.c_void_p()
+            rc = lib.ngz_agg_create(0, arr, 1, 60000, 10000, 1024, 0, ctypes.byref(h))
+            assert (rc != -1) == want, (name, op, rc)
+
 def test_library_exports_every_declared_symbol():
     from netgauze_amd import _lib
     if not os.path.exists(_lib.LIB_PATH):

@@ -25,6 +25,19 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 
 OK, ADD, MN, MX, OR = K.OP_KEY, K.OP_ADD, K.OP_MIN, K.OP_MAX, K.OP_OR
+# ngz_agg_set_option values a test forces on every aggregator it creates (monkeypatch.setitem);
+# they choose the reduction path, never the result
+AGG_OPTIONS = {}
+
+
+def new_agg(*args, **kw):
+    from netgauze_amd.aggregate import FlowAggregator
+    return FlowAggregator(*args, options=dict(AGG_OPTIONS), **kw)
+
+
+def _opt(name):
+    from netgauze_amd import _lib
+    return getattr(_lib, name)
 
 
 @pytest.fixture(scope="module")
@@ -77,7 +90,7 @@ def run_device(fields, batches, port=4739, coll=1_700_000_000_000, lateness_s=10
     from netgauze_amd.flow import FlowInfoCodec
     codec = FlowInfoCodec()
     # one peer: 8 peer bits (max_peers 256) keep keys up to 35 bits in the exact packed tag
-    agg = FlowAggregator(fields, lateness_s=lateness_s, capacity=capacity, max_peers=256)
+    agg = new_agg(fields, lateness_s=lateness_s, capacity=capacity, max_peers=256)
     late = 0
     emitted = []
     for b in batches:
@@ -156,7 +169,7 @@ def test_wrapping_add_and_signed_min_max(dev):
     from netgauze_amd.aggregate import FlowAggregator
     from netgauze_amd.flow import FlowInfoCodec
     codec = FlowInfoCodec()
-    agg = FlowAggregator(fields)
+    agg = new_agg(fields)
     agg.push(codec.decode_datagrams(d))
     (g,) = agg.flush()
     assert g["vals"] == ((200 + 100 + 250) & 0xFF, -9, 7, 6)
@@ -202,7 +215,7 @@ def test_t20_multi_port_collection_times(dev):
     keys = [(0, 4, 0, OK)]
     d = t20_datagrams(3000, 300, [1_700_000_000])
     codec = FlowInfoCodec()
-    agg = FlowAggregator(keys + T20_AGG)
+    agg = new_agg(keys + T20_AGG)
     agg.push(codec.decode_datagrams(d[:6]), 1000, 5_000)
     agg.push(codec.decode_datagrams(d[6:]), 2000, 9_000)
     o = A.FlowAggregatorOracle(keys + T20_AGG)
@@ -261,7 +274,7 @@ def test_wave_preaggregation_bytes_and_presence(dev):
     from netgauze_amd.aggregate import FlowAggregator
     from netgauze_amd.flow import FlowInfoCodec
     codec = FlowInfoCodec()
-    agg = FlowAggregator(fields)
+    agg = new_agg(fields)
     agg.push(codec.decode_datagrams(d))
     got = norm(agg.flush())
     ref = norm(A.aggregate_datagrams(fields, d, collection_ms=0).flush())
@@ -279,11 +292,11 @@ def test_table_full_and_flush_buffer_errors(dev):
     from netgauze_amd.flow import FlowInfoCodec
     d = t20_datagrams(5000, 500, [1_700_000_000])
     codec = FlowInfoCodec()
-    agg = FlowAggregator([(0, 8, 0, OK), (0, 12, 0, OK)] + T20_AGG, capacity=16)
+    agg = new_agg([(0, 8, 0, OK), (0, 12, 0, OK)] + T20_AGG, capacity=16)
     with pytest.raises(AggError, match="capacity|table full"):
         agg.push(codec.decode_datagrams(d))
     assert agg.n_groups() == 0 and agg.flush() == []
-    agg2 = FlowAggregator([(0, 4, 0, OK)] + T20_AGG)
+    agg2 = new_agg([(0, 4, 0, OK)] + T20_AGG)
     agg2.push(codec.decode_datagrams(d[:3]))
     n = agg2.n_groups()
     assert n == 6  # 3 protocols x 2 minute windows (the two data messages are 60 s apart)
@@ -318,7 +331,7 @@ def test_hash_collisions_stay_exact(dev, monkeypatch):
     """A 3-bit key hash makes nearly every distinct 5-tuple collide: groups are still exact
     (keys compared, collided records re-probed), where the previous design returned
     NGZ_AGG_E_COLLISION."""
-    monkeypatch.setenv("NGZ_AGG_HASH_BITS", "3")
+    monkeypatch.setitem(AGG_OPTIONS, _opt("NGZ_AGG_OPT_HASH_BITS"), 3)
     d = t20_datagrams(3000, 100, [1_700_000_010, 1_700_000_070])
     g = check(FIVE_TUPLE + T20_AGG, [d[:10], d[10:]])
     assert len(g) > 1000
@@ -351,7 +364,7 @@ def test_peer_ports_across_flush_cycles(dev):
     from netgauze_amd.flow import FlowInfoCodec
     d = t20_datagrams(200, 100, [1_700_000_000])  # two data messages, one minute apart
     codec = FlowInfoCodec()
-    agg = FlowAggregator([(0, 4, 0, OK), (0, 1, 0, ADD)], lateness_s=60)  # nothing late, no window closes
+    agg = new_agg([(0, 4, 0, OK), (0, 1, 0, ADD)], lateness_s=60)  # nothing late, no window closes
     for cycle in range(8):
         for i in range(10):
             agg.push(codec.decode_datagrams(d), 10000 + 10 * cycle + i, 0)
@@ -368,7 +381,7 @@ def test_closed_windows_free_dictionary_entries(dev):
     import ngz_oracle as O
     fields = [(0, 4, 0, OK), (0, 1, 0, ADD), (0, 2, 0, MX)]
     codec, oc = FlowInfoCodec(), O.FlowInfoCodec()
-    agg = FlowAggregator(fields, lateness_s=10, capacity=64)
+    agg = new_agg(fields, lateness_s=10, capacity=64)
     o = A.FlowAggregatorOracle(fields, 60, 10)
     tmpl = t20_datagrams(100, 100, [1_700_000_000])[0]
     oc.decode(bytearray(tmpl))
@@ -394,7 +407,7 @@ def test_failed_push_leaves_the_aggregator_unchanged(dev):
     codec = FlowInfoCodec()
     o = A.aggregate_datagrams(fields, a, peer_port=1, collection_ms=5)
     n_a = len(o.groups) + len(o.closed)
-    agg = FlowAggregator(fields, capacity=n_a + 10)
+    agg = new_agg(fields, capacity=n_a + 10)
     agg.push(codec.decode_datagrams(a), 1, 5)
     with pytest.raises(AggError, match="capacity|table full"):
         agg.push(codec.decode_datagrams(b), 2, 9)
@@ -437,7 +450,7 @@ def test_flowinfo_rendering(dev):
     d = [K.nf_packet(), ipfix] + t20_datagrams(500, 100, [1_700_000_000])
     fields = K.NF_FIELDS + [(0, 6, 0, OR), (0, 22, 0, MN)]
     codec = FlowInfoCodec()
-    agg = FlowAggregator(fields, lateness_s=10 ** 6 // 1000, window_s=10 ** 6 // 1000)
+    agg = new_agg(fields, lateness_s=10 ** 6 // 1000, window_s=10 ** 6 // 1000)
     agg.push(codec.decode_datagrams(d), 9995, K.T_2025_01_01_10_MS)
     hdr, raw = agg.flush_raw()
     groups = agg.render(hdr, raw)
@@ -460,7 +473,7 @@ def test_stale_batch_is_refused(dev):
     d = t20_datagrams(200, 100, [1_700_000_000])
     old = codec.decode_datagrams(d)
     codec.decode_datagrams(d[1:])
-    agg = FlowAggregator([(0, 4, 0, OK), (0, 1, 0, ADD)])
+    agg = new_agg([(0, 4, 0, OK), (0, 1, 0, ADD)])
     with pytest.raises(AggError, match="stale"):
         agg.push(old)
 
@@ -472,8 +485,8 @@ def test_stale_batch_is_refused(dev):
 ])
 def test_partitioned_reduction(dev, keys, monkeypatch):
     """The partitioned reduction (slot-range partitions reduced in LDS, rows updated in place),
-    forced with NGZ_AGG_PART=1, on the T20 streams with late messages and closing windows."""
-    monkeypatch.setenv("NGZ_AGG_PART", "1")
+    forced with NGZ_AGG_OPT_PARTITION 1, on the T20 streams with late messages and closing windows."""
+    monkeypatch.setitem(AGG_OPTIONS, _opt("NGZ_AGG_OPT_PARTITION"), 1)
     times = [1_700_000_010, 1_700_000_030, 1_700_000_015, 1_700_000_045, 1_700_000_020, 1_700_000_050,
              1_700_000_061, 1_700_000_049]
     d = t20_datagrams(6000, 100, times)
@@ -484,7 +497,7 @@ def test_partitioned_reduction_ports_captures_orders(dev, monkeypatch):
     """Forced partitioned reduction: peer ports and collection times over two pushes, every
     reference capture (wide and packed keys), wrapping adds / signed min-max, and the ordered
     reductions that run after it."""
-    monkeypatch.setenv("NGZ_AGG_PART", "1")
+    monkeypatch.setitem(AGG_OPTIONS, _opt("NGZ_AGG_OPT_PARTITION"), 1)
     test_t20_multi_port_collection_times(dev)
     test_wrapping_add_and_signed_min_max(dev)
     test_ordered_reductions(dev)
@@ -519,8 +532,8 @@ def test_partitioned_equals_atomic_at_full_size(dev, monkeypatch):
     fields = [(0, 4, 0, OK), (0, 11, 0, OK)] + T20_AGG
     rows = {}
     for mode in ("0", "1"):
-        monkeypatch.setenv("NGZ_AGG_PART", mode)
-        agg = FlowAggregator(fields, capacity=1 << 20, lateness_s=60, max_peers=256)  # packed, as the bench
+        monkeypatch.setitem(AGG_OPTIONS, _opt("NGZ_AGG_OPT_PARTITION"), int(mode))
+        agg = new_agg(fields, capacity=1 << 20, lateness_s=60, max_peers=256)  # packed, as the bench
         for _ in range(2):
             assert agg.push(batch, 4739, 0) == 0
         _, raw = agg.flush_raw()
@@ -536,7 +549,7 @@ def test_partitioned_equals_atomic_at_full_size(dev, monkeypatch):
 def test_owner_path_equals_atomic_5tuple(dev, monkeypatch):
     """10^7 T20 records by the 5-tuple (about one group per record), two pushes: the owner
     path (each group's owner record reduces its row with plain stores, k_agg_apply_own) and
-    the per-record atomics (NGZ_AGG_NO_OWN) give byte-identical rows, owner word aside."""
+    the per-record atomics (NGZ_AGG_OPT_OWNER 0) give byte-identical rows, owner word aside."""
     import numpy as np
     from netgauze_amd import synth
     from netgauze_amd.aggregate import FlowAggregator
@@ -558,8 +571,8 @@ def test_owner_path_equals_atomic_5tuple(dev, monkeypatch):
     rows = {}
     for mode in ("own", "atomic"):
         if mode == "atomic":
-            monkeypatch.setenv("NGZ_AGG_NO_OWN", "1")
-        agg = FlowAggregator(fields, capacity=n, lateness_s=60)
+            monkeypatch.setitem(AGG_OPTIONS, _opt("NGZ_AGG_OPT_OWNER"), 0)
+        agg = new_agg(fields, capacity=n, lateness_s=60)
         for _ in range(2):
             assert agg.push(batch, 4739, 0) == 0
         _, raw = agg.flush_raw()
@@ -577,7 +590,7 @@ def run_device_scenario(sc):
     FlowInfoCodec), one aggregator for the shard."""
     from netgauze_amd.aggregate import FlowAggregator
     from netgauze_amd.flow import FlowInfoCodec
-    agg = FlowAggregator(sc["fields"], window_s=sc["window_s"], lateness_s=sc["lateness_s"], capacity=1024)
+    agg = new_agg(sc["fields"], window_s=sc["window_s"], lateness_s=sc["lateness_s"], capacity=1024)
     codecs, emits, late = {}, [], 0
     for ip, port, coll, dgrams in sc["pushes"]:
         codec = codecs.setdefault((ip, port), FlowInfoCodec())
@@ -592,10 +605,11 @@ def _sorted(groups):
     return sorted(groups, key=lambda g: repr((g["peer"], g["window_start"], g["flow_type"], g["key"])))
 
 
-@pytest.mark.parametrize("sc", K.SCENARIOS + K.WINDOW_SCENARIOS, ids=lambda s: s["name"])
+@pytest.mark.parametrize("sc", K.SCENARIOS + K.WINDOW_SCENARIOS + K.FIELD_OP_SCENARIOS, ids=lambda s: s["name"])
 def test_reference_scenarios(dev, sc):
-    """aggregator/tests.rs (:72-1377) and the analytics window tests (aggregation.rs:498-788) as
-    wire-level scenarios on the device: the expected groups of every push's closed windows and of
+    """aggregator/tests.rs (:72-1377), the analytics window tests (aggregation.rs:498-788) and the
+    Field arithmetic KATs (flow-pkt lib.rs:359-615, two records of one group per KAT plus the
+    Inapplicable pair kept apart) as wire-level scenarios on the device: the expected groups of every push's closed windows and of
     the flush, the late records, and each group's FlowInfo text equal to the oracle's."""
     import test_oracle_agg as T
     agg, emits, (flushed, raw), late = run_device_scenario(sc)
@@ -651,7 +665,7 @@ def test_thousand_peers_one_aggregator(dev):
     b = bytes(buf.numpy())
     msgs = [bytearray(b[o:o + ln]) for o, ln in zip(offs.tolist(), lens.tolist())]
     peers = ["10.%d.%d.1" % (i // 250, i % 250) if i % 3 else "2001:db8::%x" % (i + 1) for i in range(n_peers)]
-    agg = FlowAggregator(fields, capacity=1 << 16, lateness_s=10, max_peers=1024)
+    agg = new_agg(fields, capacity=1 << 16, lateness_s=10, max_peers=1024)
     o = A.FlowAggregatorOracle(fields, 60, 10)
     codecs, ocodecs = {}, {}
     tm = synth.template_message()
@@ -766,7 +780,7 @@ def test_long_byte_keys_through_table_rebuilds(dev):
     from netgauze_amd.flow import FlowInfoCodec
     import ngz_oracle as O
     fields = [(0, 82, 0, OK), (0, 1, 0, ADD)]
-    agg = FlowAggregator(fields, capacity=2000, lateness_s=0)
+    agg = new_agg(fields, capacity=2000, lateness_s=0)
     o = A.FlowAggregatorOracle(fields, 60, 0)
     codec, oc = FlowInfoCodec(), O.FlowInfoCodec()
     tpl = [(82, 0xFFFF), (1, 8)]
@@ -785,6 +799,40 @@ def test_long_byte_keys_through_table_rebuilds(dev):
     same_groups(agg.flush(), o.flush())
 
 
+def test_wide_byte_key_large_batch(dev):
+    """A 200-byte variable-length string key over 10^6 records in one batch, five distinct keys,
+    pushed three times: the byte arena is reserved per group and field (table slots x
+    byte fields x the longest tail), not per record (10^6 x 168 B), and tail offsets are 8-byte
+    units (no 4 GiB wrap).  Groups, counts and sums equal the numpy reference of the same records."""
+    import numpy as np
+    from netgauze_amd.flow import FlowInfoCodec
+    n, per = 1_000_000, 300
+    keys = [(b"%d-" % i) + bytes([65 + i]) * 198 for i in range(5)]
+    rng = np.random.default_rng(5)
+    ki = rng.integers(0, 5, n)
+    octets = rng.integers(1, 1 << 40, n, dtype=np.uint64)
+    rec = np.zeros((n, 209), np.uint8)
+    rec[:, 0] = 200
+    rec[:, 1:201] = np.frombuffer(b"".join(keys), np.uint8).reshape(5, 200)[ki]
+    rec[:, 201:] = octets.astype(">u8").view(np.uint8).reshape(n, 8)
+    tpl = [(82, 0xFFFF), (1, 8)]
+    dgrams = [ipfix_msg([tset(256, tpl)], 1_700_000_000)]
+    for i in range(0, n, per):
+        dgrams.append(ipfix_msg([dset(256, [rec[i:i + per].tobytes()])], 1_700_000_000, seq=2 + i // per))
+    codec = FlowInfoCodec(0)
+    batch = codec.decode_datagrams(dgrams)
+    assert batch.n_records == n
+    agg = new_agg([(0, 82, 0, OK), (0, 1, 0, ADD)], capacity=1024, lateness_s=60)
+    for _ in range(3):
+        assert agg.push(batch) == 0
+    got = {g["key"][0]: (g["record_count"], g["vals"][0]) for g in agg.flush()}
+    want = {}
+    for i, k in enumerate(keys):
+        m = ki == i
+        want[k.decode()] = (3 * int(m.sum()), int((3 * octets[m].astype(object)).sum()) % (1 << 64))
+    assert got == want
+
+
 def test_tombstones_do_not_fill_the_table(dev):
     """windows emitted push after push leave tombstones; pushes keep succeeding while
     the live groups stay within the capacity (the table is rebuilt before a push when tombstones
@@ -793,7 +841,7 @@ def test_tombstones_do_not_fill_the_table(dev):
     from netgauze_amd.flow import FlowInfoCodec
     import ngz_oracle as O
     fields = [(0, 8, 0, OK), (0, 12, 0, OK), (0, 1, 0, ADD)]
-    agg = FlowAggregator(fields, capacity=2000, lateness_s=0)
+    agg = new_agg(fields, capacity=2000, lateness_s=0)
     o = A.FlowAggregatorOracle(fields, 60, 0)
     codec, oc = FlowInfoCodec(), O.FlowInfoCodec()
     tpl = [(8, 4), (12, 4), (1, 8)]
@@ -821,7 +869,7 @@ def test_lowcard_path_equals_oracle(dev, keys, monkeypatch):
     no per-record atomics) on T20 streams whose export times go back and forth (late
     messages dropped, windows closed push by push), equal to the oracle; the path is checked
     to be the one taken."""
-    monkeypatch.setenv("NGZ_AGG_LC", "1")
+    monkeypatch.setitem(AGG_OPTIONS, _opt("NGZ_AGG_OPT_LOWCARD"), 1)
     from netgauze_amd.aggregate import FlowAggregator
     from netgauze_amd.flow import FlowInfoCodec
     import ngz_oracle as O
@@ -830,7 +878,7 @@ def test_lowcard_path_equals_oracle(dev, keys, monkeypatch):
     d = t20_datagrams(6000, 100, times)
     fields = keys + T20_AGG
     codec, oc = FlowInfoCodec(), O.FlowInfoCodec()
-    agg = FlowAggregator(fields, lateness_s=10)
+    agg = new_agg(fields, lateness_s=10)
     o = A.FlowAggregatorOracle(fields, 60, 10)
     late = 0
     for part in (d[:25], d[25:40], d[40:]):
@@ -850,7 +898,7 @@ def test_lowcard_path_many_peers(dev, max_peers, monkeypatch):
     the low-cardinality path, with max_peers 4 / 1024 / 65536 (2, 10 and 16 peer bits of the
     packed tag): every push's emitted windows and the final flush equal the oracle's, groups
     land on their own peer and close at that peer's own event time."""
-    monkeypatch.setenv("NGZ_AGG_LC", "1")
+    monkeypatch.setitem(AGG_OPTIONS, _opt("NGZ_AGG_OPT_LOWCARD"), 1)
     from netgauze_amd import synth
     from netgauze_amd.aggregate import FlowAggregator
     from netgauze_amd.flow import FlowInfoCodec
@@ -862,7 +910,7 @@ def test_lowcard_path_many_peers(dev, max_peers, monkeypatch):
     buf, offs, lens = synth.ipfix_data_stream(rec, 64, rec_per_msg=per_msg)
     b = bytes(buf.numpy())
     msgs = [bytearray(b[o:o + ln]) for o, ln in zip(offs.tolist(), lens.tolist())]
-    agg = FlowAggregator(fields, capacity=1 << 12, lateness_s=10, max_peers=max_peers)
+    agg = new_agg(fields, capacity=1 << 12, lateness_s=10, max_peers=max_peers)
     o = A.FlowAggregatorOracle(fields, 60, 10)
     codecs, ocodecs = {}, {}
     tm = synth.template_message()
@@ -896,14 +944,14 @@ def test_lowcard_falls_back_on_many_key_tuples(dev, monkeypatch):
     wave of k_agg_lc_part raise the overflow flag: k_agg_lc_merge does nothing and the push runs
     the general path from scratch (nothing claimed), and every reference capture still equals
     the oracle."""
-    monkeypatch.setenv("NGZ_AGG_LC", "1")
+    monkeypatch.setitem(AGG_OPTIONS, _opt("NGZ_AGG_OPT_LOWCARD"), 1)
     from netgauze_amd.aggregate import FlowAggregator
     from netgauze_amd.flow import FlowInfoCodec
     paths = set()
     for name in [c[0] for c in golden_io.cases()]:
         for key, dgrams in peers_of(name).items():
             codec = FlowInfoCodec()
-            agg = FlowAggregator(GOLDEN_AGG_PACKED, lateness_s=60, max_peers=256)  # 8 peer bits: packed tags
+            agg = new_agg(GOLDEN_AGG_PACKED, lateness_s=60, max_peers=256)  # 8 peer bits: packed tags
             h = len(dgrams) // 2
             emitted = []
             for part in (dgrams[:h], dgrams[h:]):
@@ -940,8 +988,8 @@ def test_lowcard_equals_general_at_full_size(dev, monkeypatch):
     fields = [(0, 4, 0, OK), (0, 61, 0, OK)] + T20_AGG
     rows = {}
     for mode in ("0", "1"):
-        monkeypatch.setenv("NGZ_AGG_LC", mode)
-        agg = FlowAggregator(fields, capacity=1 << 10, lateness_s=60)
+        monkeypatch.setitem(AGG_OPTIONS, _opt("NGZ_AGG_OPT_LOWCARD"), int(mode))
+        agg = new_agg(fields, capacity=1 << 10, lateness_s=60)
         for _ in range(2):
             assert agg.push(batch, 4739, 0) == 0
             assert agg.last_path() == ("lowcard" if mode == "1" else "general")

@@ -161,3 +161,23 @@ def test_bench_data_only_steady_state(dev, specialize):
         oracle_codec_step(oc, data)
     assert codec.template_counts(10) == {t: v.processed_count for t, v in oc.ipfix_templates.items()}
     assert codec.template_counts(10)[1024] == 1 + 64
+
+
+def test_codec_partial_messages_kat(dev, specialize):
+    """codec.rs:226-249 (test_decode_partial_messages) through the C ABI: the 18-byte IPFIX buffer
+    whose header announces 116 bytes, then the 1-byte buffer, each decoded as its own batch on one
+    context, are NGZ_DG_NEED_MORE (Ok(None)) with nothing consumed and no template state touched;
+    so is the pair as one batch, and a complete message decodes normally afterwards."""
+    from netgauze_amd.flow import FlowInfoCodec
+    codec = FlowInfoCodec(0, specialize=specialize)
+    oc = O.FlowInfoCodec()
+    wires = [K.WIRES[k] for k, _ in K.CODEC_PARTIAL]
+    for w in wires:
+        assert product_step(codec, w) == oracle_codec_step(oc, w) == (L.NGZ_DG_NEED_MORE, None, 0)
+    batch = codec.decode_datagrams(wires)
+    assert [int(s) for s in batch.dgram_headers()["status"]] == [L.NGZ_DG_NEED_MORE] * 2
+    assert batch.json_lines() == []
+    assert codec.template_counts(10) == {} and codec.template_counts(9) == {}
+    full = bytes.fromhex("000a0010583de05900000ee400000000")  # the same header, length 16, no sets
+    assert product_step(codec, full) == oracle_codec_step(oc, full)
+    assert product_step(codec, full)[0] == L.NGZ_DG_OK

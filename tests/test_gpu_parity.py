@@ -38,9 +38,14 @@ def kernel_path(request):
     _SPECIALIZE[0] = True
 
 
+# ngz_ctx_set_option values a test forces on every context it creates (monkeypatch.setitem);
+# they choose how a batch runs, never its results
+CTX_OPTIONS = {}
+
+
 def new_codec():
     from netgauze_amd.flow import FlowInfoCodec
-    return FlowInfoCodec(0, specialize=_SPECIALIZE[0])
+    return FlowInfoCodec(0, specialize=_SPECIALIZE[0], options=dict(CTX_OPTIONS))
 
 
 def run_both(dgrams):
@@ -352,8 +357,8 @@ def test_cfg5_shard_full_size(dev):
 def test_cfg3_mixed_templates_oracle(dev, group, monkeypatch):
     """Config 3 shape (8 templates, 40-153 B records, interleaved messages)
     against the oracle, every field; one launch per template or one
-    multi-template launch per workgroup shape (NGZ_GROUP)."""
-    monkeypatch.setenv("NGZ_GROUP", group)
+    multi-template launch per workgroup shape (NGZ_OPT_GROUP)."""
+    monkeypatch.setitem(CTX_OPTIONS, L.NGZ_OPT_GROUP, int(group))
     from netgauze_amd import synth
     b, o, ln, _ = synth.mixed_stream(24_000)
     bb = bytes(b.numpy())
@@ -368,8 +373,8 @@ def test_cfg5_sixteen_templates_sharded(dev, group, monkeypatch):
     """Config 5 shape (16 templates: config 3 + width permutations) against
     the oracle, decoded as two shards on two contexts (ranks) as bench.py
     --gpus N does; the shards' processed counts add up to the oracle's.  One
-    launch per template or per workgroup shape (NGZ_GROUP)."""
-    monkeypatch.setenv("NGZ_GROUP", group)
+    launch per template or per workgroup shape (NGZ_OPT_GROUP)."""
+    monkeypatch.setitem(CTX_OPTIONS, L.NGZ_OPT_GROUP, int(group))
     from netgauze_amd import dist, synth
     b, o, ln, _ = synth.mixed_stream(32_000, templates=synth.CFG5_TEMPLATES, seed=synth.SEED_CFG5)
     bb = bytes(b.numpy())
@@ -396,8 +401,8 @@ def test_cfg5_sixteen_templates_sharded(dev, group, monkeypatch):
 def test_cfg3_mixed_templates_1e7(dev, group, monkeypatch):
     """Config 3 at 10^7 records (1.25e6 per template): every column of every
     template compared on the GPU with the wire bytes re-laid, one launch per
-    template or per workgroup shape (NGZ_GROUP)."""
-    monkeypatch.setenv("NGZ_GROUP", group)
+    template or per workgroup shape (NGZ_OPT_GROUP)."""
+    monkeypatch.setitem(CTX_OPTIONS, L.NGZ_OPT_GROUP, int(group))
     from netgauze_amd import synth
     codec = new_codec()
     codec.decode_datagrams([synth.templates_message(synth.CFG3_TEMPLATES)])
@@ -567,14 +572,14 @@ def test_reference_field_kats(dev):
 
 def test_cfg4_split_framing_steady_state(dev, kernel_path, monkeypatch):
     """Steady-state config-4 batches (NFv9 313 + IPFIX variable-length 900) with split framing
-    (NGZ_SPLIT=1; off by default, it measured slower): from the second batch on, the record
+    (NGZ_OPT_SPLIT 1; off by default, it measured slower): from the second batch on, the record
     walk of the variable-length sets runs on its own stream beside the NFv9 framing and decode
     (specialised kernels); every batch equals the
     oracle, processed counts included.  A batch with a variable-length record that runs past
     its set (the UnexpectedEof only the split walk sees; phase A went past it) runs again
     unsplit and equals the oracle too, and so does the batch after it."""
     from netgauze_amd import synth
-    monkeypatch.setenv("NGZ_SPLIT", "1")
+    monkeypatch.setitem(CTX_OPTIONS, L.NGZ_OPT_SPLIT, 1)
     dg = synth.cfg4_datagrams(9000)
     codec = new_codec()
     oc = O.FlowInfoCodec()
@@ -851,3 +856,35 @@ def test_columns_to_host_async(dev, kernel_path):
     pageable = np.zeros(cap, dtype=np.uint8)
     with pytest.raises(NgzError):
         codec.columns_to_host_async(pageable.ctypes.data, cap, kernel=True)  # not mapped for the device
+
+
+def test_columns_to_host_async_two_streams_then_decode(dev):
+    """Two queued column copies of one batch on two different streams (one by the CUs, one by a
+    copy engine), then the context's next decode: the decode waits for both (one event chained
+    over every queued copy), so both buffers hold the first batch's columns.  A too-small
+    destination queues nothing and leaves the earlier copies tracked; the synchronous copy after
+    an asynchronous one on another stream waits for both."""
+    from netgauze_amd.flow import NgzError
+    codec = new_codec()
+    first = t20_stream(400_000)
+    batch = codec.decode_datagrams(first)
+    cap = sum(s.block_bytes() + 256 for s in batch.slots)
+    ref = np.zeros(cap, dtype=np.uint8)
+    n = codec.columns_to_host(ref.ctypes.data, cap)
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    a = torch.zeros(cap, dtype=torch.uint8).pin_memory()
+    b = torch.zeros(cap, dtype=torch.uint8).pin_memory()
+    assert codec.columns_to_host_async(a.data_ptr(), cap, stream=s1.cuda_stream, kernel=True) == n
+    assert codec.columns_to_host_async(b.data_ptr(), cap, stream=s2.cuda_stream, kernel=False) == n
+    with pytest.raises(NgzError):
+        codec.columns_to_host_async(b.data_ptr(), 16, stream=s2.cuda_stream)
+    b2 = codec.decode_datagrams(t20_stream(300_000, seed=99)[1:])  # other records into the same columns
+    assert b2.n_records == 300_000
+    assert np.array_equal(a.numpy()[:n], ref[:n]) and np.array_equal(b.numpy()[:n], ref[:n])
+    # synchronous copy after an asynchronous one on another stream
+    batch = codec.decode_datagrams(first[1:])
+    a.zero_()
+    codec.columns_to_host_async(a.data_ptr(), cap, stream=s1.cuda_stream, kernel=True)
+    c = np.zeros(cap, dtype=np.uint8)
+    assert codec.columns_to_host(c.ctypes.data, cap) == n
+    assert np.array_equal(a.numpy()[:n], ref[:n]) and np.array_equal(c[:n], ref[:n])

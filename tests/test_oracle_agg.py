@@ -197,3 +197,41 @@ def test_into_flowinfo_with_extra_fields(flow_type):
     assert st["Data"]["id"] == 65535 and rec["scope_fields"] == []
     key = lambda f: json.dumps(f, sort_keys=True)  # noqa: E731
     assert sorted(rec["fields"], key=key) == sorted(K.FLOWINFO_EXPECTED_FIELDS, key=key)
+
+
+def _ie(pen, ie_id):
+    import ngz_oracle as O
+    return O.REGISTRY.lookup(pen, ie_id | (0x8000 if pen else 0))
+
+
+@pytest.mark.parametrize("kat", K.FIELD_OP_KATS, ids=lambda k: k[0])
+def test_field_op_kats(kat):
+    """lib.rs:359-615: Field::{add,min,max,bitwise_or}_field of two fields of one IE gives the
+    test's value; with a field of another IE it is FieldOperationError::Inapplicable*(lhs IE,
+    rhs IE) -- for the VMware fields too, whose vendor error maps into the same variant."""
+    name, src, op, ie, lhs, rhs, exp, other, err = kat
+    a, b = _ie(*ie[:2]), _ie(*other[:2])
+    assert (a.name, b.name) == (ie[2], other[2])
+    assert A.field_op(op, a, lhs, a, rhs) == exp
+    with pytest.raises(A.FieldOperationError) as e:
+        A.field_op(op, a, lhs, b, rhs)
+    assert (e.value.variant, e.value.lhs, e.value.rhs) == (err, a, b)
+
+
+def test_supports_ops_kats():
+    """IE::supports_{arithmetic,bitwise,comparison}_ops asserts of lib.rs:267-358 on the oracle's
+    restatement (generator.rs:1176-1272)."""
+    import ngz_oracle as O
+    by_name = {ie.name: ie for ie in O.REGISTRY.by_key.values() if ie.pen == 0}
+    for name, (arith, bit, cmp_) in K.SUPPORTS_KATS.items():
+        ie = by_name[name]
+        for op, want in ((K.OP_ADD, arith), (K.OP_OR, bit), (K.OP_MIN, cmp_), (K.OP_MAX, cmp_)):
+            if want is not None:
+                assert A.supports(ie, op) == want, (name, op)
+
+
+@pytest.mark.parametrize("sc", K.FIELD_OP_SCENARIOS, ids=lambda s: s["name"])
+def test_field_op_scenarios(sc):
+    """The field-op KATs as two-record aggregation scenarios on the oracle."""
+    agg, _emits, flushed = run_oracle_scenario(sc)
+    assert _sorted(flushed) == _sorted(sc["flush"])

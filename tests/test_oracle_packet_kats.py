@@ -125,3 +125,14 @@ def test_wrapped_item_kats_at_packet_level(name):
             assert val == exp, (name, i, val, exp)
             if st == "ok":
                 assert consumed == len(dgram)
+
+
+def test_codec_partial_messages_kat():
+    """codec.rs:226-249 on the oracle codec: Ok(None) for both partial buffers, nothing consumed."""
+    oc = O.FlowInfoCodec()
+    for key, want in K.CODEC_PARTIAL:
+        buf = bytearray(K.WIRES[key])
+        n0 = len(buf)
+        assert oc.decode(buf) is want
+        assert len(buf) == n0
+    assert len(K.WIRES[K.CODEC_PARTIAL[0][0]]) == 18 and K.WIRES[K.CODEC_PARTIAL[1][0]] == b"\x01"
