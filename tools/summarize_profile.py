@@ -2,10 +2,10 @@
 """Summarize a tools/gpu_profile.sh output directory.
 
   * per-kernel rocprofv3 --kernel-trace --stats of the bench command;
-  * the decode kernel's average duration over the TIMED steps only (the last
-    `steps` dispatches in the per-dispatch kernel trace: warm-up launches and
-    the first batch's arena placement trials are excluded), to compare with the
-    bench line's HIP-event kernel_ms of the same run;
+  * the decode kernel time per TIMED step (every decode dispatch from the
+    k_frame that starts the first timed step on: warm-up steps and the first
+    batch's arena placement trials are excluded), to compare with the bench
+    line's HIP-event kernel_ms of the same run; it must not exceed ms_per_step;
   * per-launch HBM traffic of the decode kernel from the separate --pmc passes
     (FETCH_SIZE doubled on gfx950 per MI355X_MICROARCH.md §HBM; both KiB).
 
@@ -39,23 +39,36 @@ for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"])):
     short = r["Name"].replace("(anonymous namespace)::", "").split("(")[0]
     print("%-44s %8s %14.0f %14s" % (short[:44], r["Calls"], float(r["AverageNs"]), r["TotalDurationNs"]))
 
-timed = None
+timed, per_step_disp = None, None
 traces = glob.glob(os.path.join(d, "trace", "*kernel_trace.csv"))
 if traces and bench:
-    disp = []
+    disp, frames = [], []
     for r in csv.DictReader(open(traces[0])):
+        t0, t1 = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
         if any(k in r["Kernel_Name"] for k in DECODE):
-            disp.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
+            disp.append((t0, t1 - t0))
+        if "k_frame" in r["Kernel_Name"]:
+            frames.append(t0)
     disp.sort()
+    frames.sort()
     steps = bench["steps"]
-    # one step may launch several decode kernels (one per active template): group by step is not
-    # needed for the average per step; take the last `steps` steps' worth of dispatches
-    per_step = max(1, round(len(disp) / max(1, bench["steps"] + bench["warmup"])))
-    last = disp[-steps * per_step:]
+    # Each ngz_decode_batch starts with its k_frame dispatch, so the timed steps are the last
+    # `steps` k_frame starts onwards: warm-up steps and the first batch's placement trials (extra
+    # decode dispatches without a k_frame of their own) fall before them.  (r4 guessed the
+    # dispatches per step from the total count, which the trials inflate.)
+    if len(frames) < steps:
+        sys.exit("summarize_profile: %d k_frame dispatches for %d timed steps" % (len(frames), steps))
+    start = frames[-steps]
+    last = [x for t, x in disp if t >= start]
     if last:
-        timed = sum(x for _, x in last) / steps / 1e6  # ms of decode kernel per step
-        print("== decode kernel over the %d timed steps: %.4f ms/step (%d dispatches); bench kernel_ms %.4f"
-              % (steps, timed, len(last), bench["roofline"]["kernel_ms"]))
+        timed = sum(last) / steps / 1e6  # ms of decode kernel per step
+        per_step_disp = len(last) / steps
+        print("== decode kernel over the %d timed steps: %.4f ms/step (%d dispatches, %.2f per step); "
+              "bench kernel_ms %.4f, ms_per_step %.4f"
+              % (steps, timed, len(last), per_step_disp, bench["roofline"]["kernel_ms"], bench["ms_per_step"]))
+        if timed > bench["ms_per_step"]:
+            sys.exit("summarize_profile: decode time per step %.4f ms exceeds the step %.4f ms -- the step "
+                     "delimiting is wrong" % (timed, bench["ms_per_step"]))
 
 out = {}
 for c in ("FETCH_SIZE", "WRITE_SIZE"):
@@ -85,7 +98,8 @@ if "FETCH_SIZE" in out and "WRITE_SIZE" in out:
                "records": bench["config"]["records_per_gpu"] if bench else None,
                "workload": bench["config"]["workload"] if bench else None,
                "alg_bytes_per_launch": alg, "traffic_over_alg": (fetch + write) / alg if alg else None,
-               "timed_kernel_ms_trace": timed, "bench_kernel_ms": bench["roofline"]["kernel_ms"] if bench else None,
+               "timed_kernel_ms_trace": timed, "timed_dispatches_per_step": per_step_disp,
+               "ms_per_step_trace_run": bench["ms_per_step"] if bench else None, "bench_kernel_ms": bench["roofline"]["kernel_ms"] if bench else None,
                "source_hash": buildinfo.source_hash(), "decode_source_hash": buildinfo.decode_source_hash(),
                "git_sha": os.environ.get("GIT_SHA"),
                "kernel": "decode (every decode dispatch of one step)",
