@@ -857,14 +857,15 @@ struct StageBytes {
 // relative to the lane's rsrc / image base as P.rbase is
 __device__ __forceinline__ bool utf8_valid_v(const Pass &P, uint32_t rel, uint32_t len, bool stop_at_nul) {
     if (P.img == 0xFFFFFFFFu) return utf8_valid_global(P.rsrc, rel, len, stop_at_nul);
-    const uint32_t end = rel + len;
-    uint32_t acc = 0;
-    for (uint32_t a = rel & ~3u; a < end; a += 4) {
-        uint32_t m = 0xFFFFFFFFu;
-        if (a < rel) m <<= 8 * (rel - a);
-        if (a + 4 > end) m &= 0xFFFFFFFFu >> (8 * (a + 4 - end));
-        acc |= ngz_vstage[P.img + (a >> 2)] & m;
-    }
+    if (len == 0) return true;
+    // ASCII fast path: no byte of [rel, rel + len) has its high bit set.  Only the first and the
+    // last dword need masks; the ones between are ORed whole (two LDS dwords per read), so the
+    // loop body is a read and an OR (the per-dword mask version cost ~15 VALU per dword).
+    const uint32_t end = rel + len, d0 = rel >> 2, d1 = (end - 1) >> 2;
+    const uint32_t mf = 0xFFFFFFFFu << (8 * (rel & 3)), ml = 0xFFFFFFFFu >> (8 * (3 - ((end - 1) & 3)));
+    const uint32_t *img = &ngz_vstage[P.img];
+    uint32_t acc = d0 == d1 ? img[d0] & mf & ml : (img[d0] & mf) | (img[d1] & ml);
+    for (uint32_t d = d0 + 1; d < d1; ++d) acc |= img[d];
     if (!(acc & 0x80808080u)) return true;
     return utf8_valid_prefix(StageBytes{rel, P.img}, len, stop_at_nul);
 }

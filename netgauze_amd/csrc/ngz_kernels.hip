@@ -241,31 +241,38 @@ __device__ bool has_template_sets(const BatchDev &B, uint32_t d) {
 
 constexpr uint32_t kFrameBlock = 256;
 
-// 64 bytes of a datagram for the record walk, in this thread's 64-byte LDS slot (the window starts
+// 64 bytes of a datagram for the record walk, in this thread's 16 LDS dwords (the window starts
 // at a 16-byte aligned address): the length prefixes of a variable-length record lie 20-40 bytes
 // apart, so most of them come out of the window already loaded instead of from a byte load of their
 // own.  Each byte load was a round trip on the walk's dependent chain (k_frame spent 86 % of its wave
 // cycles waiting); a window is four independent 16-byte loads, one round trip.  LDS, not registers:
-// k_frame has no VGPRs to spare for 16 more.
+// k_frame has no VGPRs to spare for 16 more.  The slots are transposed -- dword j of thread t at
+// col[j * kFrameBlock + t] -- so a wave's window stores and its byte reads (every lane its own
+// dword) touch 64 different banks: thread-contiguous 64-byte slots put the lanes 16 banks apart
+// (4-16-way conflicts, 3.6e7 conflict cycles per config-4 k_frame, profiles/r5/cfg4).
 struct WalkWin {
-    uint4 *slot;         // this thread's 64 bytes of LDS
+    uint32_t *col;       // this thread's column of the transposed window table
     uintptr_t base = 0;  // address the window starts at; 0 = empty
     // the byte at address q; lim: end of the batch buffer (no window reaches past it)
     __device__ __forceinline__ uint32_t byte(const uint8_t *q, const uint8_t *lim) {
         const uintptr_t a = (uintptr_t)q;
-        if (!slot) return *q;
+        if (!col) return *q;
         if (!base || a < base || a >= base + 64) {
             const uintptr_t b0 = a & ~(uintptr_t)15;
             if (b0 + 64 > (uintptr_t)lim) return *q;
             const uint4 *v = (const uint4 *)b0;
-            const uint4 x0 = v[0], x1 = v[1], x2 = v[2], x3 = v[3];
-            slot[0] = x0;
-            slot[1] = x1;
-            slot[2] = x2;
-            slot[3] = x3;
+            const uint4 x[4] = {v[0], v[1], v[2], v[3]};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                col[(4 * j + 0) * kFrameBlock] = x[j].x;
+                col[(4 * j + 1) * kFrameBlock] = x[j].y;
+                col[(4 * j + 2) * kFrameBlock] = x[j].z;
+                col[(4 * j + 3) * kFrameBlock] = x[j].w;
+            }
             base = b0;
         }
-        return ((const uint8_t *)slot)[a - base];
+        const uint32_t o = (uint32_t)(a - base);
+        return (col[(o >> 2) * kFrameBlock] >> (8 * (o & 3))) & 0xFFu;
     }
 };
 
@@ -273,7 +280,7 @@ struct WalkWin {
 // record the fast steps cannot complete goes to the exact form from its start, as there
 template <class F>
 __device__ uint32_t vlen_walk_win(const uint8_t *p, uint32_t pos, uint32_t end, const DevPlan &pl, uint64_t *err,
-                                  const uint8_t *lim, uint4 *slot, F &&on_rec) {
+                                  const uint8_t *lim, uint32_t *slot, F &&on_rec) {
     if (pl.walk_nv > NGZ_WALK_MAX) return ngz_vlen_walk_exact(p, pos, end, pl, err, on_rec);
     const uint32_t minlen = pl.rec_len, nv = pl.walk_nv;
     uint32_t fx[NGZ_WALK_MAX + 1];
@@ -375,7 +382,7 @@ struct CountVis {
         return n;
     }
     const uint8_t *lim = nullptr;  // end of the batch buffer (WalkWin loads stay inside it)
-    uint4 *win = nullptr;          // this thread's WalkWin slot in LDS
+    uint32_t *win = nullptr;       // this thread's WalkWin column in LDS
     __device__ uint32_t walk_records(const uint8_t *p, uint32_t pos, uint32_t end, const DevPlan &pl, uint64_t *err) {
         return vlen_walk_win(p, pos, end, pl, err, lim, win, [this](uint32_t, uint32_t at) {
             if (ro) {  // the record's offset in the datagram, appended to the datagram's list
@@ -428,8 +435,8 @@ __global__ void __launch_bounds__(kFrameBlock) k_frame(BatchDev B, const uint32_
     vis.dg_end = vis.dg_off + B.lengths[d];
     vis.split = B.split;
     vis.lim = B.bytes + B.bytes_size;
-    __shared__ uint4 wwin[kFrameBlock * 4];
-    vis.win = &wwin[threadIdx.x * 4];
+    __shared__ uint32_t wwin[16 * kFrameBlock];
+    vis.win = &wwin[threadIdx.x];
     if (B.recoff) vis.ro = ngz_ro_list(B, vis.dg_off, d);
     WalkOut o;
     walk_datagram(B, hf_flag, hf_first, d, o, vis);
@@ -478,8 +485,8 @@ __global__ void __launch_bounds__(kFrameBlock) k_frame_vlen(BatchDev B) {
     vis.dg_end = vis.dg_off + B.lengths[d];
     vis.split = 2;
     vis.lim = B.bytes + B.bytes_size;
-    __shared__ uint4 wwin[kFrameBlock * 4];
-    vis.win = &wwin[threadIdx.x * 4];
+    __shared__ uint32_t wwin[16 * kFrameBlock];
+    vis.win = &wwin[threadIdx.x];
     vis.ro = ngz_ro_list(B, vis.dg_off, d);
     WalkOut o;
     walk_datagram(B, nullptr, nullptr, d, o, vis);

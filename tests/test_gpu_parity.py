@@ -551,6 +551,42 @@ def test_variable_length_fields(dev):
     assert codec.template_counts(10) == {t: oc.ipfix_templates[t].processed_count for t in (500, 501)}
 
 
+def test_variable_length_utf8_randomized(dev):
+    """UTF-8 of variable-length strings at every byte alignment and length (0-300, both length
+    forms): ASCII, valid 2-4 byte sequences, and one invalid byte (lone continuation, truncated
+    sequence, overlong, surrogate, > U+10FFFF) placed at the first, a middle and the last byte, in
+    messages of 60 records (the staged 64-row groups) and a lone-record message (unstaged); every
+    datagram against the oracle (ipfix.rs:335-370, generator.rs:1775-1793: vlen strings are
+    UTF-8 checked over all their bytes, no NUL cut)."""
+    import random
+    rnd = random.Random(29)
+    fields = [(8, 4), (82, 65535), (7, 2), (96, 65535), (4, 1), (83, 65535)]
+    t = ipfix_msg([ipfix_set(2, tmpl(502, fields))])
+    good = ["", "a", "ab", "abc", "abcd", "gr\u00fc\u00dfe", "\u20ac\u20ac", "\U0001f600x", "\u00e9" * 40]
+    bad = [b"\x80", b"\xc3", b"\xe2\x82", b"\xc0\xaf", b"\xed\xa0\x80", b"\xf4\x90\x80\x80", b"\xff"]
+
+    def text():
+        k = rnd.random()
+        n = rnd.choice([0, 1, 2, 3, 5, 17, 40, 63, 64, 65, 254, 255, 300])
+        base = "".join(rnd.choice("abcdefghij") for _ in range(n)).encode()
+        if k < 0.5:
+            return base
+        if k < 0.75:
+            return base + rnd.choice(good).encode()
+        b = rnd.choice(bad)
+        at = rnd.choice([0, len(base) // 2, len(base)])
+        return base[:at] + b + base[at:]
+
+    def rec():
+        return (struct.pack(">I", rnd.getrandbits(32)) + vl(text()) + struct.pack(">H", rnd.getrandbits(16)) +
+                vl(text()) + bytes([rnd.getrandbits(8)]) + vl(text()))
+    dgrams = [t]
+    for m in range(40):
+        dgrams.append(ipfix_msg([ipfix_set(502, b"".join(rec() for _ in range(60 if m % 4 else 1)))]))
+    stats, batch, codec, oc = run_both(dgrams)
+    assert stats["unsupported"] == 0 and stats["err"] > 5 and stats["ok"] > 1
+
+
 def test_reference_field_kats(dev):
     """The reference's field-level unit vectors (tests/kats.py) through the
     device: each wrapped as [sourceIPv4Address, field, sourceTransportPort]

@@ -3,6 +3,7 @@
 # bench.py --agg (kernel trace), one run per env setting in CONFIGS (";"-separated).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
+export NGZ_EXPERIMENTS=1  # env knobs are read only by the experiment build (tools/build_experiments.sh)
 export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-agg_ab}
 mkdir -p $OUT

@@ -5,6 +5,7 @@
 # usage: TAG=r4c [RUNS=5] bash tools/gpu_arena.sh
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
+export NGZ_EXPERIMENTS=1  # env knobs are read only by the experiment build (tools/build_experiments.sh)
 export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-arena}
 mkdir -p $OUT

@@ -18,7 +18,7 @@ if [ "${PART:-a}" = a ]; then
 else
   TAG=$TAG WORKLOADS="mixed8 cfg5" bash tools/gpu_profile.sh || exit 5
   TAG=$TAG AGGS="proto_dir dport 5tuple" bash tools/gpu_profile_agg.sh || exit 6
-  NGZ_AGG_RED_RPT=1 timeout -k 10 300 python bench.py --agg dport --steps 10 --warmup 2 > gpurun_out/$TAG/agg_dport_rpt1.json 2> gpurun_out/$TAG/agg_dport_rpt1.err || exit 8
+  NGZ_EXPERIMENTS=1 NGZ_AGG_RED_RPT=1 timeout -k 10 300 python bench.py --agg dport --steps 10 --warmup 2 > gpurun_out/$TAG/agg_dport_rpt1.json 2> gpurun_out/$TAG/agg_dport_rpt1.err || exit 8
   python3 -c "import json; d=json.load(open('gpurun_out/$TAG/agg_dport_rpt1.json')); print('dport reduce 1 payload/thread: push %.3f ms' % d['push_kernels_ms'])"
   timeout -k 10 300 python3 bench.py --e2e --records 10000000 --steps 5 --warmup 2 > gpurun_out/$TAG/e2e_1e7.json 2> gpurun_out/$TAG/e2e.err || { tail -5 gpurun_out/$TAG/e2e.err; exit 7; }
   cat gpurun_out/$TAG/e2e_1e7.json

@@ -2,6 +2,7 @@
 # column-spacing probe sweeps.  usage: TAG=r4q bash tools/gpu_spacing.sh
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
+export NGZ_EXPERIMENTS=1  # env knobs are read only by the experiment build (tools/build_experiments.sh)
 OUT=gpurun_out/${TAG:-spacing}
 mkdir -p $OUT
 P=tools/spacing_probe

@@ -7,6 +7,7 @@
 #        [STEPS=10] TAG=r4a bash tools/gpu_sweep.sh
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
+export NGZ_EXPERIMENTS=1  # env knobs are read only by the experiment build (tools/build_experiments.sh)
 export TMPDIR=/tmp
 OUT=gpurun_out/${TAG:-sweep}
 mkdir -p $OUT
