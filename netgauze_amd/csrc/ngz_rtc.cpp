@@ -483,6 +483,9 @@ std::string generate_vlen(const DevPlan &P) {
         }
         so += d.len;
     }
+    // NGZ_RTC_EXP (experiment build only; timing attribution, output invalid): bit 1 no UTF-8
+    // checks of variable-length strings, bit 3 an empty decode (the staging copy alone)
+    const int64_t vexp = ngz_knob("NGZ_RTC_EXP", 0);
     std::string body;
     char b[640];
     body += "        const Pass &P0 = P[0];\n";
@@ -559,7 +562,7 @@ std::string generate_vlen(const DevPlan &P) {
                          "                ColSt(P0, %uu, 16).b128(P0.lrow * 16, (uint32_t)at, (uint32_t)(at >> 32), L, 0);\n",
                          it.off - wb, it.off + 1 - wb, it.off, d.col_off);
                 body += b;
-                if (d.flags & 0x80)  // string: every byte UTF-8 checked
+                if ((d.flags & 0x80) && !(vexp & 2))  // string: every byte UTF-8 checked
                     body += "                if (!utf8_valid_v(P0, rel0 + data, L, false))\n"
                             "                    rec_error(P0, data, E_REC_UTF8, " + F + "u, L);\n";
                 body += "            }\n"
@@ -582,7 +585,7 @@ std::string generate_vlen(const DevPlan &P) {
     src += "    if (sload(&B.summary->overflow)) return;\n";
     src += "    auto pass = [&](const Pass (&P)[1]) {\n";
     src += "        uint32_t R[1][WIN_DW];\n";
-    src += body;
+    src += (vexp & 8) ? std::string("        (void)P; (void)R;\n") : body;
     src += "    };\n";
     src += "    run_windows_staged(B, slot, pass);\n}\n";
     return src;
