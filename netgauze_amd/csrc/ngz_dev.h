@@ -920,17 +920,58 @@ __device__ __forceinline__ void run_windows_staged(const BatchDev &B, uint32_t s
         const uint32_t avail = avail64 > 0x7FFFFFF0ull ? 0x7FFFFFF0u : (uint32_t)avail64;
         const __amdgpu_buffer_rsrc_t r =
             __builtin_amdgcn_make_buffer_rsrc((void *)(B.bytes + base), (short)0, (int)avail, 0x00020000);
-        // copy: lane's blocks [blo, bhi) -> image pieces [pc, pc + c); 8 loads in flight per lane
-        const uint32_t g0 = (uint32_t)((blo << 4) - base);
-        const uint32_t cmax = wave_max_u32(c);
-        for (uint32_t j0 = 0; j0 < cmax; j0 += 8) {
-            v4u v[8];
+        // copy: lane l's blocks [blo, bhi) are image pieces [pc, pc + c).  Consecutive lanes whose
+        // records follow each other in the batch (cont) have consecutive blocks, so the image is a few
+        // runs of consecutive batch blocks, one per lane that does not continue its predecessor (a
+        // run head: the group's first record of each set).  The wave copies the image piece by piece
+        // -- lane l takes pieces l, l + 64, ... -- so every load instruction reads 1 KiB of
+        // consecutive blocks (a few lines; one record per lane was 64 blocks ~150 B apart, 64 lines
+        // an instruction) and every LDS store writes 1 KiB of consecutive pieces (no bank conflicts).
+        uint64_t hm = __builtin_amdgcn_ballot_w64(c != 0 && !cont);
+        const uint32_t gb = (uint32_t)(((blo << 4) - base) >> 4);  // this lane's first block, resource-relative
+        uint32_t hp[8], hb[8];  // the first 8 runs: first piece (~0: none) and first block, uniform
 #pragma unroll
-            for (uint32_t k = 0; k < 8; ++k)
-                v[k] = __builtin_amdgcn_raw_buffer_load_b128(r, j0 + k < c ? g0 + 16 * (j0 + k) : 0x80000000u, 0, 0);
+        for (uint32_t i = 0; i < 8; ++i) {
+            const uint32_t h = hm ? (uint32_t)__builtin_ctzll(hm) : 0u;
+            hp[i] = hm ? sgpr(lane_u32(pc, h)) : 0xFFFFFFFFu;
+            hb[i] = hm ? sgpr(lane_u32(gb, h)) : 0u;
+            hm &= hm - 1;
+        }
+        if (hm == 0) {
+            // rounds of 64 pieces, 5 loads in flight (the image of 64 records of ~150 B is ~10 rounds)
+            constexpr uint32_t kBatch = 5;
+            for (uint32_t k0 = 0; 64 * k0 < T; k0 += kBatch) {
+                v4u v[kBatch];
 #pragma unroll
-            for (uint32_t k = 0; k < 8; ++k)
-                if (j0 + k < c) *(v4u *)&ngz_vstage[img0 + 4 * (pc + j0 + k)] = v[k];
+                for (uint32_t k = 0; k < kBatch; ++k) {
+                    const uint32_t p = 64 * (k0 + k) + lane;
+                    uint32_t blk = 0x08000000u;  // past the image: out of the resource's range, reads 0
+                    if (p < T) {
+#pragma unroll
+                        for (uint32_t i = 0; i < 8; ++i)
+                            if (p >= hp[i]) blk = hb[i] + (p - hp[i]);
+                    }
+                    v[k] = __builtin_amdgcn_raw_buffer_load_b128(r, blk << 4, 0, 0);
+                }
+#pragma unroll
+                for (uint32_t k = 0; k < kBatch; ++k) {
+                    const uint32_t p = 64 * (k0 + k) + lane;
+                    if (p < T) *(v4u *)&ngz_vstage[img0 + 4 * p] = v[k];
+                }
+            }
+        } else {
+            // more than 8 runs (records of many short sets): each lane copies its own blocks
+            const uint32_t g0 = gb << 4;
+            const uint32_t cmax = wave_max_u32(c);
+            for (uint32_t j0 = 0; j0 < cmax; j0 += 8) {
+                v4u v[8];
+#pragma unroll
+                for (uint32_t k = 0; k < 8; ++k)
+                    v[k] = __builtin_amdgcn_raw_buffer_load_b128(r, j0 + k < c ? g0 + 16 * (j0 + k) : 0x80000000u, 0, 0);
+#pragma unroll
+                for (uint32_t k = 0; k < 8; ++k)
+                    if (j0 + k < c) *(v4u *)&ngz_vstage[img0 + 4 * (pc + j0 + k)] = v[k];
+            }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
