@@ -11,9 +11,11 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libngz.so")
 # NGZ_EXPERIMENTS=1 (tools only): the experiment build, libngz_exp.so (tools/build_experiments.sh),
-# whose knobs are read from NGZ_<name> variables for A/B measurements.  Never the product path.
-if os.environ.get("NGZ_EXPERIMENTS") == "1":
-    LIB_PATH = os.path.join(HERE, "libngz_exp.so")
+# whose knobs are read from NGZ_<name> variables for A/B measurements; NGZ_EXPERIMENTS=<name>:
+# libngz_exp_<name>.so, a variant built with extra compile-time defines.  Never the product path.
+if os.environ.get("NGZ_EXPERIMENTS"):
+    _x = os.environ["NGZ_EXPERIMENTS"]
+    LIB_PATH = os.path.join(HERE, "libngz_exp.so" if _x == "1" else "libngz_exp_%s.so" % _x)
 
 NGZ_DG_OK, NGZ_DG_NEED_MORE, NGZ_DG_ERROR, NGZ_DG_UNSUPPORTED = 0, 1, 2, 3
 (K_UINT, K_TCPFLAGS, K_SINT, K_BOOL, K_BYTES, K_U256, K_DTMS, K_DTFRAC, K_STR,

@@ -533,6 +533,7 @@ __device__ __forceinline__ void chunk_passes(const BatchDev &B, const Chunk &cur
     P[0].hdr = B.hdr;
     P[0].blk = blk;
     P[0].cap = cap;
+    P[0].img = 0xFFFFFFFFu;  // record bytes through the resource (no staged image)
     const uint64_t a0 = src & ~15ull;  // 16-byte aligned resource base (win_load)
     // buffer range checks are per dword (a dword straddling num_records reads 0),
     // so round up: the <= 3 bytes past bytes_size share the last valid byte's

@@ -346,6 +346,13 @@ void build_plan(Version &v) {
     }
     P.reserved0 = (uint8_t)std::min<uint32_t>(lds_direct, 255);
     P.lds_waves = (P.rpl && !vlen && lds_on && staged) ? ngz_lds_waves(staged, lds_budget, lds_maxw) : 0;
+    // NetFlow v9 fixed templates: exporters send a few records per packet (MTU datagrams, ~10-30),
+    // so their sets are row-mode sized; they get the staged-row kernel shape of variable-length
+    // templates (each wave copies its 64 records' image into LDS with 1 KiB loads, columns stored
+    // directly) instead of LDS column windows gathering rows across ~26 chunks: config 4's
+    // template 313 decode 669 -> ~610 us (profiles/r5/cfg4_nf313_staged).  Records of up to 160 B
+    // (64 of them fit the 10 KiB per-wave image).
+    if (P.proto == 9 && !vlen && P.rpl && rl <= NGZ_VSTAGE_REC_MAX && ngz_knob("NGZ_NF9_STAGED", 1)) P.lds_waves = 0;
     if (!P.lds_waves) P.reserved0 = 0;
 }
 

@@ -16,6 +16,7 @@
 #define NGZ_MAX_REC_LEN 65535 // longest fixed record the device decode takes
 #define NGZ_REG_WINDOW 256    // records per chunk window (4 passes of 64 lanes)
 #define NGZ_LDS_BUDGET 65536  // LDS bytes one workgroup may stage columns in
+#define NGZ_VSTAGE_REC_MAX 160 // longest fixed record of a staged-row kernel (64 records per 10 KiB image)
 
 #ifndef __HIPCC_RTC__
 // Experiment knobs (ngz_knobs.cpp): `dflt` in the product library; NGZ_<name> from the
@@ -44,6 +45,7 @@ static inline __host__ __device__ uint32_t ngz_lds_waves(uint32_t row_bytes, uin
 #define NGZ_FR_ERROR 2
 #define NGZ_FR_UNSUPPORTED 3
 #define NGZ_FR_HOST 4        // contains template sets: framed on the host
+#define NGZ_FR_PENDING 5     // k_frame internal: a variable-length set waits for the wave's cooperative walk
 
 // Error codes packed into the 64-bit error key.  Key layout (min wins =
 // first error in parse order):

@@ -79,6 +79,7 @@ std::string signature(const DevPlan &P) {
 }
 
 std::string generate_vlen(const DevPlan &P);
+bool staged_rows(const DevPlan &P);
 
 // The parts of a fixed template's generated decode: the pass body (register
 // windows, extraction, column stores through ColT / ColGlb) and, when staged
@@ -326,7 +327,7 @@ std::string fixed_lambdas(const FixedParts &F) {
 }
 
 std::string generate(const DevPlan &P) {
-    if (P.has_vlen) return generate_vlen(P);
+    if (P.has_vlen || staged_rows(P)) return generate_vlen(P);
     const FixedParts F = fixed_parts(P);
     const std::string L = std::to_string(F.rpl) + ", " + (F.consec ? "true" : "false");
     const uint32_t lw = F.lw;
@@ -415,6 +416,13 @@ std::string generate_group(const DevPlan *const *plans, uint32_t n) {
 // truncation, generator.rs:1635-1672) and moves the lane's segment start past
 // its value.  Replaces the generic kernel's field-table walk with run-time
 // register indexing for these templates.
+// Fixed templates decoded by the staged-row kernel shape (see ngz_host.cpp: NetFlow v9 templates of
+// up to NGZ_VSTAGE_REC_MAX-byte records): row-mode batches copy each 64-row group's records into LDS,
+// chunk-mode batches (sets of 64+ records on average) read them through the chunk's resource
+bool staged_rows(const DevPlan &P) {
+    return !P.has_vlen && P.rpl && !P.lds_waves && P.proto == 9 && P.rec_len <= NGZ_VSTAGE_REC_MAX;
+}
+
 std::string generate_vlen(const DevPlan &P) {
     struct Seg {
         std::vector<Item> items;   // fixed fields, offsets relative to the segment start
@@ -587,7 +595,21 @@ std::string generate_vlen(const DevPlan &P) {
     src += "        uint32_t R[1][WIN_DW];\n";
     src += (vexp & 8) ? std::string("        (void)P; (void)R;\n") : body;
     src += "    };\n";
-    src += "    run_windows_staged(B, slot, pass);\n}\n";
+    if (P.has_vlen) {
+        src += "    run_windows_staged(B, slot, pass);\n}\n";
+    } else {
+        snprintf(b, sizeof b,
+                 "    const SlotRT rt = sload(&B.slots[slot]);\n"
+                 "    if (rt.mode == NGZ_MODE_ROW) {\n"
+                 "        run_windows_staged(B, slot, pass);\n"
+                 "    } else {\n"
+                 "        auto want = [&](uint32_t s) { return s == slot; };\n"
+                 "        auto shape = [](uint32_t) { return RecShape{%uu, 0u, false}; };\n"
+                 "        run_chunks<1, false>(B, rt.chunk0, rt.chunk0 + rt.nchunks, want, shape, pass);\n"
+                 "    }\n}\n",
+                 P.rec_len);
+        src += b;
+    }
     return src;
 }
 
