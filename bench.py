@@ -143,6 +143,9 @@ def main():
                          "variable-length/enterprise IEs; cfg5: config 5, 16 templates (config 3 + 8 width "
                          "permutations), one shard per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--contexts", type=int, default=1,
+                    help="decode contexts in flight (one host thread and HIP stream each, the steps dealt round "
+                         "robin): batch k+1's framing overlaps batch k's decode")
     ap.add_argument("--e2e-contexts", type=int, default=3, help="--e2e: contexts (host threads) in flight")
     ap.add_argument("--e2e-ranges", type=int, default=12, help="--e2e: message ranges per batch")
     ap.add_argument("--e2e-duplex-contexts", type=int, default=6, help="--e2e duplex modes: contexts")
@@ -184,8 +187,10 @@ def main():
     cdev = dev if dist is None or dist.get_backend() == "nccl" else torch.device("cpu")  # collective tensors
     codec = FlowInfoCodec(local, rtc_sync=True)  # template kernels compiled when the template is learnt
     n = args.records
+    learnt = []  # the template messages every context learns before timing
     if args.workload == "t20":
-        codec.decode_datagrams([synth.template_message()])  # exporter's template, learnt before timing
+        learnt = [synth.template_message()]
+        codec.decode_datagrams(learnt)  # exporter's template, learnt before timing
         rec = synth.t20_records(n, seed=synth.SEED_CFG2 + rank, device=dev, first=0)
         buf, offs, lens = synth.ipfix_data_stream(rec, 64)
         del rec
@@ -197,13 +202,15 @@ def main():
     elif args.workload in ("mixed8", "cfg5"):
         tpls = synth.CFG3_TEMPLATES if args.workload == "mixed8" else synth.CFG5_TEMPLATES
         seed = synth.SEED_CFG3 if args.workload == "mixed8" else synth.SEED_CFG5
-        codec.decode_datagrams([synth.templates_message(tpls)])
+        learnt = [synth.templates_message(tpls)]
+        codec.decode_datagrams(learnt)
         buf, offs, lens, recs = synth.mixed_stream(n, templates=tpls, seed=seed + 64 * rank, device=dev)
         rec_bytes = {tid: r.shape[1] for tid, r in recs.items()}
         del recs
     else:
         dg = synth.cfg4_datagrams(n, seed=synth.SEED_CFG4 + 16 * rank)
-        codec.decode_datagrams(dg[:2])  # the NFv9 and IPFIX templates
+        learnt = dg[:2]
+        codec.decode_datagrams(learnt)  # the NFv9 and IPFIX templates
         buf, offs, lens = synth.host_batch(dg[2:], device=dev)
         rec_bytes = None  # variable: the data bytes of the batch stand in for record bytes
     torch.cuda.synchronize()
@@ -220,8 +227,21 @@ def main():
             exchange.step(reset=True)
         return batch
 
+    # --contexts P > 1: P codecs (contexts) on P streams, each driven by its own host thread (the
+    # decode call blocks its thread until its batch is framed and decoded; ctypes releases the GIL)
+    P = max(1, args.contexts)
+    assert P == 1 or exchange is None, "--contexts > 1 is a single-rank measurement"
+    extra = []
+    for _ in range(P - 1):
+        c = FlowInfoCodec(local, rtc_sync=True)
+        c.decode_datagrams(learnt)
+        extra.append((c, torch.cuda.Stream(dev).cuda_stream))
+    ctxs = [(codec, stream)] + extra
+
     for _ in range(max(1, args.warmup)):  # (one untimed step even at --warmup 0: it sizes the roofline bytes)
         b = step()
+        for c, st in extra:
+            c.decode_batch(buf, offs, lens, stream=st)
     assert b.n_records == n, (b.n_records, n)
     # algorithmic bytes per launch: wire bytes read + canonical column bytes written, per template
     if rec_bytes is not None:
@@ -234,9 +254,24 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-        dec_ms.append(codec.last_timing()[0])
+    if P == 1:
+        for _ in range(args.steps):
+            step()
+            dec_ms.append(codec.last_timing()[0])
+    else:
+        import threading
+
+        def drive(i):
+            c, st = ctxs[i]
+            for _ in range(i, args.steps, P):
+                c.decode_batch(buf, offs, lens, stream=st)
+                dec_ms.append(c.last_timing()[0])
+
+        th = [threading.Thread(target=drive, args=(i,)) for i in range(P)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -284,7 +319,8 @@ def main():
                 % {"t20": 2, "mixed8": 3, "cfg4": 4, "cfg5": 5}[args.workload],
         "config": {"workload": workload_desc,
                    "records_per_gpu": n, "messages_per_gpu": int(offs.numel()),
-                   "parallelism": "shard-per-gpu" if world > 1 else "single"},
+                   "parallelism": "shard-per-gpu" if world > 1 else "single",
+                   **({"contexts": P} if P > 1 else {})},
         "gbps_step": alg_bytes * world * args.steps / elapsed / 1e9,
         "templates_usage_exchange": usage,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

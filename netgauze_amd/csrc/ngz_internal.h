@@ -45,7 +45,6 @@ static inline __host__ __device__ uint32_t ngz_lds_waves(uint32_t row_bytes, uin
 #define NGZ_FR_ERROR 2
 #define NGZ_FR_UNSUPPORTED 3
 #define NGZ_FR_HOST 4        // contains template sets: framed on the host
-#define NGZ_FR_PENDING 5     // k_frame internal: a variable-length set waits for the wave's cooperative walk
 
 // Error codes packed into the 64-bit error key.  Key layout (min wins =
 // first error in parse order):

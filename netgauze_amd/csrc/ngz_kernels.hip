@@ -67,7 +67,6 @@ __device__ __forceinline__ uint32_t hw_be16(const HdrWin &H, int o) {
 struct WalkOut {
     uint32_t status, version, length, time, seq, domain, sysup, nsets;
     uint64_t err;
-    uint32_t resume;  // NGZ_FR_PENDING: position of the variable-length set waiting for its walk
 };
 
 __device__ __forceinline__ uint16_t resolve_slot(const BatchDev &B, uint32_t pidx, uint32_t id, uint32_t d) {
@@ -89,57 +88,12 @@ __device__ __forceinline__ uint16_t resolve_slot(const BatchDev &B, uint32_t pid
     return B.cur_slot[pidx * 65536u + id];
 }
 
-// The IPFIX set chain of a message from `pos` (16: the first set; a later one: resuming after a
-// variable-length set the wave walked together, k_frame) to the header length `len`.
-template <class V>
-__device__ __forceinline__ void ipfix_sets(const BatchDev &B, uint32_t d, const uint8_t *p, uint32_t pos, uint32_t len, const HdrWin *H,
-                           WalkOut &o, V &vis) {
-    while (pos < len) {  // ipfix.rs:94-96
-        const uint32_t rem = len - pos;
-        if (rem < 2) { o.status = NGZ_FR_ERROR; o.err = ngz_err_key(pos, E_SET_EOF_ID, 2, rem); return; }
-        const bool first = H && H->ok && pos == 16;  // the first set header is in the window
-        const uint32_t id = first ? hw_be16(*H, 16) : be16(p + pos);
-        if (id != 2 && id != 3 && id < 256) {  // ipfix.rs:142-150
-            o.status = NGZ_FR_ERROR; o.err = ngz_err_key(pos, E_SET_INVALID_ID, id, 0); return;
-        }
-        if (rem < 4) { o.status = NGZ_FR_ERROR; o.err = ngz_err_key(pos + 2, E_SET_EOF_LEN, 2, rem - 2); return; }
-        const uint32_t sl = first ? hw_be16(*H, 18) : be16(p + pos + 2);
-        if (sl < 4) { o.status = NGZ_FR_ERROR; o.err = ngz_err_key(pos + 2, E_SET_INVALID_LENGTH, 0, sl); return; }
-        if (sl - 4 > rem - 4) {  // take_slice (reader.rs:157-161)
-            o.status = NGZ_FR_ERROR; o.err = ngz_err_key(pos + 4, E_SET_EOF_BODY, sl - 4, rem - 4); return;
-        }
-        if (id == 2 || id == 3) { o.status = NGZ_FR_HOST; return; }
-        const uint16_t slot = resolve_slot(B, 0, id, d);
-        if (slot == NGZ_NO_SLOT) {  // ipfix.rs:184-191
-            o.status = NGZ_FR_ERROR; o.err = ngz_err_key(pos, E_SET_NO_TEMPLATE, id, 0); return;
-        }
-        const DevPlan &pl = B.plans[slot];
-        const uint32_t minlen = pl.rec_len;  // ipfix.rs:193-214 (vlen counted as 1)
-        uint64_t verr = NGZ_NO_ERR;
-        uint32_t n;
-        if (pl.has_vlen && pl.rpl) {  // :219-222 record by record: lengths come from the data
-            if (vis.defer_vlen()) {  // the wave walks its pending sets together (k_frame)
-                o.status = NGZ_FR_PENDING;
-                o.resume = pos;
-                return;
-            }
-            n = vis.vlen(p, pos + 4, pos + sl, slot, pl, &verr);
-        } else
-            n = minlen ? (sl - 4) / minlen : 0;  // :219 loop bound
-        if (n && !pl.rpl) { o.status = NGZ_FR_UNSUPPORTED; return; }
-        o.nsets++;
-        vis.on_set(pos, slot, n, pos + 4, minlen);
-        if (verr != NGZ_NO_ERR) { o.status = NGZ_FR_ERROR; o.err = verr; return; }  // first error aborts
-        pos += sl;  // leftover (padding or garbage) ignored: ipfix.rs:224-227
-    }
-}
-
 // Walk one datagram as FlowInfoCodec::decode + {Ipfix,NetFlowV9}Packet::parse
 // would, without decoding records.  For every data set reached, vis.on_set()
 // gets the set header position, the template slot, the record count and the
 // position of the first record.  Template sets end the walk with NGZ_FR_HOST.
 template <class V>
-__device__ __forceinline__ void walk_datagram(const BatchDev &B, const uint32_t *__restrict__ hf_flag, const uint32_t *__restrict__ hf_first,
+__device__ void walk_datagram(const BatchDev &B, const uint32_t *__restrict__ hf_flag, const uint32_t *__restrict__ hf_first,
                               uint32_t d, WalkOut &o, V &vis) {
     o.status = NGZ_FR_OK;
     o.version = o.length = o.time = o.seq = o.domain = o.sysup = o.nsets = 0;
@@ -177,7 +131,40 @@ __device__ __forceinline__ void walk_datagram(const BatchDev &B, const uint32_t 
         o.time = H.ok ? hw_be32(H, 4) : be32(p + 4);
         o.seq = H.ok ? hw_be32(H, 8) : be32(p + 8);
         o.domain = H.ok ? hw_be32(H, 12) : be32(p + 12);
-        ipfix_sets(B, d, p, 16, len, &H, o, vis);
+        uint32_t pos = 16;
+        while (pos < len) {  // ipfix.rs:94-96
+            const uint32_t rem = len - pos;
+            if (rem < 2) { o.status = NGZ_FR_ERROR; o.err = ngz_err_key(pos, E_SET_EOF_ID, 2, rem); return; }
+            const bool first = H.ok && pos == 16;  // the first set header is in the window
+            const uint32_t id = first ? hw_be16(H, 16) : be16(p + pos);
+            if (id != 2 && id != 3 && id < 256) {  // ipfix.rs:142-150
+                o.status = NGZ_FR_ERROR; o.err = ngz_err_key(pos, E_SET_INVALID_ID, id, 0); return;
+            }
+            if (rem < 4) { o.status = NGZ_FR_ERROR; o.err = ngz_err_key(pos + 2, E_SET_EOF_LEN, 2, rem - 2); return; }
+            const uint32_t sl = first ? hw_be16(H, 18) : be16(p + pos + 2);
+            if (sl < 4) { o.status = NGZ_FR_ERROR; o.err = ngz_err_key(pos + 2, E_SET_INVALID_LENGTH, 0, sl); return; }
+            if (sl - 4 > rem - 4) {  // take_slice (reader.rs:157-161)
+                o.status = NGZ_FR_ERROR; o.err = ngz_err_key(pos + 4, E_SET_EOF_BODY, sl - 4, rem - 4); return;
+            }
+            if (id == 2 || id == 3) { o.status = NGZ_FR_HOST; return; }
+            const uint16_t slot = resolve_slot(B, 0, id, d);
+            if (slot == NGZ_NO_SLOT) {  // ipfix.rs:184-191
+                o.status = NGZ_FR_ERROR; o.err = ngz_err_key(pos, E_SET_NO_TEMPLATE, id, 0); return;
+            }
+            const DevPlan &pl = B.plans[slot];
+            const uint32_t minlen = pl.rec_len;  // ipfix.rs:193-214 (vlen counted as 1)
+            uint64_t verr = NGZ_NO_ERR;
+            uint32_t n;
+            if (pl.has_vlen && pl.rpl)  // :219-222 record by record: lengths come from the data
+                n = vis.vlen(p, pos + 4, pos + sl, slot, pl, &verr);
+            else
+                n = minlen ? (sl - 4) / minlen : 0;  // :219 loop bound
+            if (n && !pl.rpl) { o.status = NGZ_FR_UNSUPPORTED; return; }
+            o.nsets++;
+            vis.on_set(pos, slot, n, pos + 4, minlen);
+            if (verr != NGZ_NO_ERR) { o.status = NGZ_FR_ERROR; o.err = verr; return; }  // first error aborts
+            pos += sl;  // leftover (padding or garbage) ignored: ipfix.rs:224-227
+        }
         return;
     }
     if (ver == 9) {
@@ -263,26 +250,20 @@ constexpr uint32_t kFrameBlock = 256;
 // col[j * kFrameBlock + t] -- so a wave's window stores and its byte reads (every lane its own
 // dword) touch 64 different banks: thread-contiguous 64-byte slots put the lanes 16 banks apart
 // (4-16-way conflicts, 3.6e7 conflict cycles per config-4 k_frame, profiles/r5/cfg4).
-#ifndef NGZ_WALKWIN_LOADS
-#define NGZ_WALKWIN_LOADS 4  // 16-byte loads per window refill (window bytes / 16)
-#endif
 struct WalkWin {
-    static constexpr uint32_t kLoads = NGZ_WALKWIN_LOADS, kBytes = 16 * kLoads;
     uint32_t *col;       // this thread's column of the transposed window table
     uintptr_t base = 0;  // address the window starts at; 0 = empty
     // the byte at address q; lim: end of the batch buffer (no window reaches past it)
     __device__ __forceinline__ uint32_t byte(const uint8_t *q, const uint8_t *lim) {
         const uintptr_t a = (uintptr_t)q;
         if (!col) return *q;
-        if (!base || a < base || a >= base + kBytes) {
+        if (!base || a < base || a >= base + 64) {
             const uintptr_t b0 = a & ~(uintptr_t)15;
-            if (b0 + kBytes > (uintptr_t)lim) return *q;
+            if (b0 + 64 > (uintptr_t)lim) return *q;
             const uint4 *v = (const uint4 *)b0;
-            uint4 x[kLoads];
+            const uint4 x[4] = {v[0], v[1], v[2], v[3]};
 #pragma unroll
-            for (uint32_t j = 0; j < kLoads; ++j) x[j] = v[j];
-#pragma unroll
-            for (uint32_t j = 0; j < kLoads; ++j) {
+            for (int j = 0; j < 4; ++j) {
                 col[(4 * j + 0) * kFrameBlock] = x[j].x;
                 col[(4 * j + 1) * kFrameBlock] = x[j].y;
                 col[(4 * j + 2) * kFrameBlock] = x[j].z;
@@ -402,25 +383,21 @@ struct CountVis {
     }
     const uint8_t *lim = nullptr;  // end of the batch buffer (WalkWin loads stay inside it)
     uint32_t *win = nullptr;       // this thread's WalkWin column in LDS
-    bool coop = false;             // k_frame: variable-length sets wait for the wave's cooperative walk
-    __device__ bool defer_vlen() const { return coop; }
-    // a complete record of a variable-length set starts at datagram offset `at`
-    __device__ void rec(uint32_t at) {
-        if (ro) {  // the record's offset in the datagram, appended to the datagram's list
-            ro_push(at);
-            return;
-        }
-        if (!recmap) return;
-        const uint64_t b = dg_off + at;
-        if ((b >> 5) != mw) {
-            mark_flush();
-            mw = b >> 5;
-            mbits = 0;
-        }
-        mbits |= 1u << (b & 31);
-    }
     __device__ uint32_t walk_records(const uint8_t *p, uint32_t pos, uint32_t end, const DevPlan &pl, uint64_t *err) {
-        return vlen_walk_win(p, pos, end, pl, err, lim, win, [this](uint32_t, uint32_t at) { rec(at); });
+        return vlen_walk_win(p, pos, end, pl, err, lim, win, [this](uint32_t, uint32_t at) {
+            if (ro) {  // the record's offset in the datagram, appended to the datagram's list
+                ro_push(at);
+                return;
+            }
+            if (!recmap) return;
+            const uint64_t b = dg_off + at;
+            if ((b >> 5) != mw) {
+                mark_flush();
+                mw = b >> 5;
+                mbits = 0;
+            }
+            mbits |= 1u << (b & 31);
+        });
     }
     const uint16_t *row;
     BatchSummary *summary;
@@ -446,174 +423,23 @@ struct CountVis {
     }
 };
 
-// Cooperative record walk of a wave's pending variable-length sets (k_frame).  Each walking lane
-// has one set: payload [pos, end) of its datagram p.  The walk runs in epochs: every epoch the wave
-// copies a WB-byte window of each walking lane's datagram, starting at the lane's position, into
-// this wave's LDS table -- lane L loads piece L of every round, so one load instruction reads
-// 64 / (WB/16) whole windows, a few lines, where a lane refilling its own window read 64 lines per
-// instruction (the scattered refills kept k_frame's address unit busy: profiles/r5/cfg4_attrib);
-// then each lane walks its records (ngz_vlen_walk's fast form: the walk program's fixed runs and
-// length prefixes) until its next length prefix lies past its window.  A record the fast steps
-// cannot complete goes to the exact form from its start, from global memory (it reports the
-// reference's error), and a window that would reach past the batch reads its bytes from global
-// memory.  Every lane of the wave runs this (the walking lanes are `act`).
-#ifndef NGZ_FRAME_COOP
-#define NGZ_FRAME_COOP 0  // 1: the wave walks its pending sets together (measured slower: profiles/r5/cfg4_coop_walk)
-#endif
-#ifndef NGZ_COOP_WIN
-#define NGZ_COOP_WIN 64
-#endif
-constexpr uint32_t kCoopWin = NGZ_COOP_WIN;             // window bytes per lane and epoch
-constexpr uint32_t kCoopStride = kCoopWin / 4 + 1;      // LDS dwords per lane (odd: fewer bank conflicts)
-constexpr uint32_t kCoopWaveDw = 64 * kCoopStride;      // LDS dwords per wave
-
-__device__ __forceinline__ void coop_walk(const BatchDev &B, bool act, const uint8_t *p, uint32_t pos, uint32_t end, const DevPlan *pl,
-                          uint32_t *tab, CountVis &vis, uint32_t &n_out, uint64_t &err_out) {
-    constexpr uint32_t P16 = kCoopWin / 16;
-    const uint32_t L = threadIdx.x & 63;
-    const uint32_t minlen = act ? pl->rec_len : 0u, nv = act ? pl->walk_nv : 0u;
-    uint64_t err = NGZ_NO_ERR;
-    uint32_t n = 0, start = pos, kc = 0;
-    // exact: the lane's walk ends in the exact form from `start` (no walk program, or a record
-    // the fast steps cannot complete: it reports the reference's error), after the epochs
-    bool exact = act && nv > NGZ_WALK_MAX, done = !act || exact, inrec = false;
-    // the fixed runs, two 16-bit ones per register, indexed by unrolled loop counters only
-    uint32_t fx2[(NGZ_WALK_MAX + 2) / 2];
-#pragma unroll
-    for (uint32_t k = 0; k < (NGZ_WALK_MAX + 2) / 2; ++k)
-        fx2[k] = act ? (uint32_t)pl->walk_fixed[2 * k] | ((uint32_t)pl->walk_fixed[2 * k + 1] << 16) : 0u;
-    auto fx = [&](uint32_t k) { return (fx2[k >> 1] >> (16 * (k & 1))) & 0xFFFFu; };
-    const uintptr_t lim = (uintptr_t)(B.bytes + B.bytes_size);
-    while (__builtin_amdgcn_ballot_w64(!done)) {
-        const uintptr_t a = done ? 0 : ((uintptr_t)(p + pos) & ~(uintptr_t)15);
-        const bool inwin = !done && a + kCoopWin <= lim;
-        const uint64_t wa = inwin ? (uint64_t)a : 0ull;
-        const uint32_t wlo = (uint32_t)wa, whi = (uint32_t)(wa >> 32);
-#pragma unroll
-        for (uint32_t r = 0; r < P16; ++r) {
-            const uint32_t q = r * 64 + L, owner = q / P16, j = q % P16;
-            const uint64_t ob = (uint64_t)(uint32_t)__shfl((int)wlo, (int)owner, 64) |
-                                ((uint64_t)(uint32_t)__shfl((int)whi, (int)owner, 64) << 32);
-            if (ob) {
-                const uint4 v = *(const uint4 *)(uintptr_t)(ob + 16 * j);
-                uint32_t *t = tab + owner * kCoopStride + 4 * j;
-                t[0] = v.x;
-                t[1] = v.y;
-                t[2] = v.z;
-                t[3] = v.w;
-            }
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const uint32_t w0 = (uint32_t)(a - (uintptr_t)p);  // window start, datagram offset (when inwin)
-        while (!done) {
-            if (!inrec) {
-                if (minlen == 0 || end - pos < minlen) { done = true; break; }  // ipfix.rs:193-214
-                start = pos;
-                if (end - pos < fx(0)) { exact = done = true; break; }
-                pos += fx(0);
-                kc = 0;
-                inrec = true;
-            }
-            bool ok = true, out = false;
-#pragma unroll
-            for (uint32_t k = 0; k < NGZ_WALK_MAX; ++k) {
-                if (k >= kc && k < nv && ok && !out) {
-                    uint32_t len = 0, hdr = 1;
-                    ok = end - pos >= 1;
-                    if (ok) {
-                        if (inwin) {
-                            const uint32_t o = pos - w0;
-                            out = o >= kCoopWin;  // past the window: this prefix in the next epoch
-                            if (!out) len = (tab[L * kCoopStride + (o >> 2)] >> (8 * (o & 3))) & 0xFFu;
-                        } else {
-                            len = p[pos];
-                        }
-                        if (!out && len == 255) {  // 3-byte length (generator.rs:1775-1793)
-                            ok = end - pos >= 4;
-                            if (ok) len = ((uint32_t)p[pos + 1] << 16) | ((uint32_t)p[pos + 2] << 8) | p[pos + 3];
-                            hdr = 4;
-                        }
-                    }
-                    if (out) {
-                        kc = k;
-                    } else {
-                        ok = ok && end - pos - hdr >= len && end - pos - hdr - len >= fx(k + 1);
-                        pos += hdr + len + fx(k + 1);
-                        kc = k + 1;
-                    }
-                }
-            }
-            if (out) break;
-            if (!ok) { exact = done = true; break; }
-            vis.rec(start);
-            ++n;
-            inrec = false;
-        }
-        // the next epoch rewrites the table: every lane's reads of it are done
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-    }
-    if (exact) {
-        auto on_rec = [&](uint32_t, uint32_t at) { vis.rec(at); };
-        n += ngz_vlen_walk_exact(p, start, end, *pl, &err, on_rec, n);
-    }
-    n_out = n;
-    err_out = err;
-}
-
-__global__ void __launch_bounds__(kFrameBlock) __attribute__((flatten, amdgpu_waves_per_eu(4))) k_frame(BatchDev B, const uint32_t *hf_flag, const uint32_t *hf_first) {
+__global__ void __launch_bounds__(kFrameBlock) k_frame(BatchDev B, const uint32_t *hf_flag, const uint32_t *hf_first) {
     const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool live = d < B.n;  // every lane stays for the wave's cooperative walks
-    const uint32_t dd = live ? d : 0u;
-    __shared__ uint32_t wwin[(4 * WalkWin::kLoads * kFrameBlock > (kFrameBlock / 64) * kCoopWaveDw)
-                                 ? 4 * WalkWin::kLoads * kFrameBlock
-                                 : (kFrameBlock / 64) * kCoopWaveDw];
-    CountVis vis{B.counts, B.n, B.n_rows, dd, 0, B.plans, B.recmap, B.offsets[dd]};
+    if (d >= B.n) return;
+    // this datagram's column of the count matrix starts at zero (no memset pass)
+    for (uint32_t r = 0; r < 2 * B.n_rows; ++r) B.counts[(uint64_t)r * B.n + d] = 0;
+    if (d == 0) B.counts[(uint64_t)(2 * B.n_rows + 1) * B.n] = 0;  // the scan's trailing element
+    CountVis vis{B.counts, B.n, B.n_rows, d, 0, B.plans, B.recmap, B.offsets[d]};
     vis.row = B.slot_row;
     vis.summary = B.summary;
-    vis.dg_end = vis.dg_off + B.lengths[dd];
+    vis.dg_end = vis.dg_off + B.lengths[d];
     vis.split = B.split;
     vis.lim = B.bytes + B.bytes_size;
+    __shared__ uint32_t wwin[16 * kFrameBlock];
     vis.win = &wwin[threadIdx.x];
-    vis.coop = NGZ_FRAME_COOP && B.split == 0;
+    if (B.recoff) vis.ro = ngz_ro_list(B, vis.dg_off, d);
     WalkOut o;
-    o.status = NGZ_FR_OK;
-    if (live) {
-        // this datagram's column of the count matrix starts at zero (no memset pass)
-        for (uint32_t r = 0; r < 2 * B.n_rows; ++r) B.counts[(uint64_t)r * B.n + d] = 0;
-        if (d == 0) B.counts[(uint64_t)(2 * B.n_rows + 1) * B.n] = 0;  // the scan's trailing element
-        if (B.recoff) vis.ro = ngz_ro_list(B, vis.dg_off, d);
-        walk_datagram(B, hf_flag, hf_first, d, o, vis);
-    }
-    // variable-length sets: walked by the whole wave, then the set chain resumes after them
-    uint32_t *tab = &wwin[(threadIdx.x >> 6) * kCoopWaveDw];
-    const uint8_t *p = B.bytes + vis.dg_off;
-    while (__builtin_amdgcn_ballot_w64(live && o.status == NGZ_FR_PENDING)) {
-        const bool act = live && o.status == NGZ_FR_PENDING;
-        const uint32_t pos = act ? o.resume : 0u, sl = act ? be16(p + pos + 2) : 0u;
-        const uint16_t slot = act ? resolve_slot(B, 0, be16(p + pos), d) : (uint16_t)0;
-        const DevPlan *pl = &B.plans[slot];
-        uint32_t n = 0;
-        uint64_t verr = NGZ_NO_ERR;
-        coop_walk(B, act, p, pos + 4, pos + sl, pl, tab, vis, n, verr);
-        if (act) {
-            // the rest of ipfix_sets' step for this set (CountVis::vlen's bookkeeping included)
-            if (!vis.sets) vis.sum = (uint64_t)sl << 48;
-            vis.vlen_err = vis.vlen_err || verr != NGZ_NO_ERR;
-            o.nsets++;
-            vis.on_set(pos, slot, n, pos + 4, pl->rec_len);
-            if (verr != NGZ_NO_ERR) {  // first error aborts
-                o.status = NGZ_FR_ERROR;
-                o.err = verr;
-            } else {
-                o.status = NGZ_FR_OK;
-                ipfix_sets(B, d, p, pos + sl, o.length, nullptr, o, vis);
-            }
-        }
-    }
-    if (!live) return;
+    walk_datagram(B, hf_flag, hf_first, d, o, vis);
     vis.mark_flush();
     if (vis.ro) vis.ro_finish();  // end of the list
     // a walk that ended OK visited every set (template sets end it with HOST)
@@ -659,7 +485,7 @@ __global__ void __launch_bounds__(kFrameBlock) k_frame_vlen(BatchDev B) {
     vis.dg_end = vis.dg_off + B.lengths[d];
     vis.split = 2;
     vis.lim = B.bytes + B.bytes_size;
-    __shared__ uint32_t wwin[4 * WalkWin::kLoads * kFrameBlock];
+    __shared__ uint32_t wwin[16 * kFrameBlock];
     vis.win = &wwin[threadIdx.x];
     vis.ro = ngz_ro_list(B, vis.dg_off, d);
     WalkOut o;
@@ -749,7 +575,6 @@ constexpr uint32_t kEmitStageRows = 2048;
 constexpr uint32_t kEmitStageSlots = 4;
 
 struct EmitVis {
-    __device__ bool defer_vlen() const { return false; }
     const BatchDev *B;
     uint32_t d;
     uint64_t dg_off;
