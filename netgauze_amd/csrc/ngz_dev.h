@@ -47,6 +47,9 @@ constexpr int64_t kMinMillis = -8334601315200000LL;  // days_from_civil(-262143,
 constexpr int64_t kMaxMillis = 8210266876799999LL;   // (days_from_civil(262142,12,31)+1)*86400000-1
 
 __device__ __forceinline__ uint32_t sgpr(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t sgpr64(uint64_t v) {
+    return (uint64_t)sgpr((uint32_t)v) | ((uint64_t)sgpr((uint32_t)(v >> 32)) << 32);
+}
 
 // v_readlane as an unsigned value (the builtin returns int: widening it
 // directly to 64 bits would sign-extend)
@@ -618,7 +621,7 @@ __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
         const uint64_t o = __shfl_xor(v, m, 64);
         v = o < v ? o : v;
     }
-    return v;
+    return sgpr64(v);  // every lane holds it: scalar (a buffer resource built from it needs no waterfall loop)
 }
 
 __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
@@ -627,7 +630,7 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
         const uint64_t o = __shfl_xor(v, m, 64);
         v = o > v ? o : v;
     }
-    return v;
+    return sgpr64(v);  // every lane holds it: scalar (a buffer resource built from it needs no waterfall loop)
 }
 
 // exclusive prefix sum over the wave's lanes (total: the sum over all 64)
@@ -887,6 +890,14 @@ __device__ __forceinline__ void run_windows_staged(const BatchDev &B, uint32_t s
     const uint32_t img0 = sgpr(wv * kVStageDw);
     const uint32_t total = rt.total;
     const uint32_t ngroups = (total + 63) / 64;
+    // the row entries of the wave's next group are loaded one group ahead (their round trip
+    // overlaps this group's copy and decode instead of starting each group)
+    uint64_t ent_n = 0;
+    uint32_t dg_n = 0;
+    if (wid * 64 + lane < total) {
+        ent_n = rs[wid * 64 + lane];
+        dg_n = rd[wid * 64 + lane];
+    }
     for (uint32_t g = wid; g < ngroups; g += nw) {
         Pass &Q = P[0];
         Q.img = 0xFFFFFFFFu;
@@ -896,8 +907,14 @@ __device__ __forceinline__ void run_windows_staged(const BatchDev &B, uint32_t s
         Q.lrow = lane;
         Q.row = pr0 + lane;
         Q.valid = Q.row < total;
-        const uint64_t ent = Q.valid ? rs[Q.row] : 0;
-        Q.dgram = Q.valid ? rd[Q.row] : 0;
+        const uint64_t ent = ent_n;
+        Q.dgram = dg_n;
+        {
+            const uint32_t r2 = (g + nw) * 64 + lane;
+            const bool v2 = g + nw < ngroups && r2 < total;
+            ent_n = v2 ? rs[r2] : 0;
+            dg_n = v2 ? rd[r2] : 0;
+        }
         Q.recpos = 0xFFFFFFFFu;
         Q.rec0 = Q.row;
         const uint64_t src = ent & NGZ_ROW_OFF_MASK;
@@ -939,7 +956,9 @@ __device__ __forceinline__ void run_windows_staged(const BatchDev &B, uint32_t s
             hm &= hm - 1;
         }
         if (hm == 0) {
-            // rounds of 64 pieces, 5 loads in flight (the image of 64 records of ~150 B is ~10 rounds)
+            // rounds of 64 pieces, 5 loads in flight (the image of 64 records of ~150 B is ~10 rounds).
+            // Copying by buffer_load ... lds instead (every round in flight, no VGPRs) measured the same
+            // (config 4: 580 against 571 us per staged launch, profiles/r5/cfg4_glds/ab.txt)
             constexpr uint32_t kBatch = 5;
             for (uint32_t k0 = 0; 64 * k0 < T; k0 += kBatch) {
                 v4u v[kBatch];

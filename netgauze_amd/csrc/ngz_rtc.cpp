@@ -55,7 +55,8 @@ struct Item {           // one extraction step of the generated pass body
     uint32_t d0, d1;    // record dwords touched (inclusive), types 0-2
 };
 
-// Cache-policy defines of the generated source (NGZ_LD_AUX / NGZ_ST_AUX, experiments only; ngz_dev.h)
+// Defines of the generated source from experiment knobs (NGZ_LD_AUX / NGZ_ST_AUX / NGZ_WIN_ROT; the
+// experiment build only, ngz_dev.h)
 std::string cpol_defines() {
     std::string s;
     for (const char *k : {"NGZ_LD_AUX", "NGZ_ST_AUX", "NGZ_WIN_ROT"})
