@@ -1530,6 +1530,9 @@ constexpr uint32_t PART_TILE = 65536;  // records per histogram / scatter workgr
 // operand columns are read as a few sequential streams (tiles of contiguous records per workgroup
 // made ~10 000 concurrent column streams, and the operand loads ran at under 1 TB/s)
 constexpr uint32_t PART_RPT = 4;                      // records per thread and round
+#ifndef NGZ_SCATTER_ATTRIB
+#define NGZ_SCATTER_ATTRIB 0  // timing-attribution variants of k_agg_part_scatter (experiment builds; wrong output)
+#endif
 constexpr uint32_t PART_ROUND = 256 * PART_RPT;
 
 // counts[p * G + w]: workgroup w's records headed for partition p (a record has a group only if
@@ -1583,7 +1586,11 @@ __global__ __launch_bounds__(256) void k_agg_part_scatter(const RecCtx C, const 
         }
 #pragma unroll
         for (uint32_t k = 0; k < PART_RPT; ++k)
+#if NGZ_SCATTER_ATTRIB & 1  // timing attribution (experiment variants only): no context chain
+            c[k] = g[k] != NONE ? make_uint4((uint32_t)(t0 + k), 0, 0, C.sctx[0].w) : make_uint4(0, 0, 0, 0);
+#else
             c[k] = g[k] != NONE ? ctx_of_block(C, t0 + k) : make_uint4(0, 0, 0, 0);
+#endif
         uint64_t x[PART_RPT][8];
         const uint32_t slot0 = c[0].w & 0xFFFF;
         bool quad = true;
@@ -1604,7 +1611,7 @@ __global__ __launch_bounds__(256) void k_agg_part_scatter(const RecCtx C, const 
                     for (uint32_t k = 0; k < PART_RPT; ++k) x[k][v] = value_operand(sp, P, v, c[k].x);
                     continue;
                 }
-                if (P.op_w[v] && sp.val_col[v]) {
+                if (P.op_w[v] && sp.val_col[v] && !(NGZ_SCATTER_ATTRIB & 2)) {  // (2: no operand loads)
                     const uint32_t w = wv;
                     const uint8_t *b = sp.val_col[v] + (uint64_t)c[0].x * w;
                     if (w == 1) {
@@ -1652,15 +1659,15 @@ __global__ __launch_bounds__(256) void k_agg_part_scatter(const RecCtx C, const 
                 const uint32_t ow = P.op_w[v];
                 if (!ow) continue;
                 const uint64_t xv = x[k][v];
-                const uint32_t o = P.op_off[v], j0 = o >> 2, sh = 8 * (o & 3);
+                // the operand's dword: a wave-uniform index into the payload registers (one indexed
+                // move each, not a compare and select per payload dword)
+                const uint32_t o = P.op_off[v], j0 = __builtin_amdgcn_readfirstlane(o >> 2), sh = 8 * (o & 3);
                 const uint32_t lo = ow >= 4 ? (uint32_t)xv : ow == 2 ? ((uint32_t)xv & 0xFFFFu) << sh : ((uint32_t)xv & 0xFFu) << sh;
-#pragma unroll
-                for (uint32_t j = 4; j < NP * 4; ++j) {
-                    if (j == j0) wd[j] |= lo;
-                    if (ow == 8 && j == j0 + 1) wd[j] = (uint32_t)(xv >> 32);
-                }
+                wd[j0] |= lo;
+                if (ow == 8) wd[j0 + 1] = (uint32_t)(xv >> 32);
             }
             uint4 *d = (uint4 *)(pay + (uint64_t)pos * (16 * NP));
+            if ((NGZ_SCATTER_ATTRIB & 4) && wd[0] != 0xFFFFFFFFu) continue;  // (4: no payload stores)
 #pragma unroll
             for (uint32_t j = 0; j < NP; ++j) d[j] = make_uint4(wd[4 * j], wd[4 * j + 1], wd[4 * j + 2], wd[4 * j + 3]);
         }
@@ -1711,13 +1718,9 @@ __global__ __launch_bounds__(1024) void k_agg_part_reduce(const AggParams P, con
         uint64_t x[8];
 #pragma unroll
         for (int v = 0; v < 8; ++v) {
-            const uint32_t ow = P.op_w[v], o = P.op_off[v], j0 = o >> 2, sh = 8 * (o & 3);
-            uint32_t lo = 0, hi = 0;
-#pragma unroll
-            for (uint32_t j = 4; j < NP * 4; ++j) {
-                if (j == j0) lo = wd[j];
-                if (j == j0 + 1) hi = wd[j];
-            }
+            // the operand's dwords by a wave-uniform index (k_agg_part_scatter's layout)
+            const uint32_t ow = P.op_w[v], o = P.op_off[v], j0 = __builtin_amdgcn_readfirstlane(o >> 2), sh = 8 * (o & 3);
+            const uint32_t lo = ow ? wd[j0] : 0u, hi = ow == 8 ? wd[j0 + 1] : 0u;
             x[v] = ow == 8 ? ((uint64_t)hi << 32) | lo : ow == 4 ? (uint64_t)lo : ow == 2 ? (uint64_t)((lo >> sh) & 0xFFFFu)
                  : ow == 1 ? (uint64_t)((lo >> sh) & 0xFFu) : 0ull;
         }
