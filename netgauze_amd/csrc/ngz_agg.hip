@@ -1564,6 +1564,8 @@ __global__ __launch_bounds__(256) void k_agg_part_scatter(const RecCtx C, const 
                                                           uint32_t n_part, const uint32_t *__restrict__ offs,
                                                           uint8_t *__restrict__ pay) {
     extern __shared__ uint32_t cur[];
+    __shared__ uint4 stage[256 * NP];  // per wave: 64 payload rows (the store transpose)
+    const uint32_t lane = threadIdx.x & 63;
     for (uint32_t i = threadIdx.x; i < n_part; i += blockDim.x) cur[i] = offs[(uint64_t)i * gridDim.x + blockIdx.x];
     __syncthreads();
     // thread i of a round takes records r0 + 4i .. r0 + 4i + 3 (a wave: one aligned 256-record
@@ -1645,8 +1647,8 @@ __global__ __launch_bounds__(256) void k_agg_part_scatter(const RecCtx C, const 
         }
 #pragma unroll
         for (uint32_t k = 0; k < PART_RPT; ++k) {
-            if (g[k] == NONE) continue;
-            const uint32_t pos = atomicAdd(&cur[g[k] >> PART_SHIFT], 1u);
+            const bool has = g[k] != NONE;
+            const uint32_t pos = has ? atomicAdd(&cur[g[k] >> PART_SHIFT], 1u) : 0u;
             uint32_t wd[NP * 4];
             wd[0] = g[k];
             wd[1] = c[k].y;
@@ -1666,10 +1668,30 @@ __global__ __launch_bounds__(256) void k_agg_part_scatter(const RecCtx C, const 
                 wd[j0] |= lo;
                 if (ow == 8) wd[j0 + 1] = (uint32_t)(xv >> 32);
             }
-            uint4 *d = (uint4 *)(pay + (uint64_t)pos * (16 * NP));
-            if ((NGZ_SCATTER_ATTRIB & 4) && wd[0] != 0xFFFFFFFFu) continue;  // (4: no payload stores)
+            if (NGZ_SCATTER_ATTRIB & 4) continue;  // (4: no payload stores)
+            // The payloads go out whole: lane l's row of the wave's LDS stage, then each store
+            // instruction writes 64 / NP payloads with NP consecutive lanes per payload (piece
+            // lane % NP of payload lane / NP).  A store of one piece per lane wrote 64 payloads, 64
+            // scattered lines per instruction: the stores were 70 % of this kernel (5.4 -> 1.8 ms
+            // without them, profiles/r5/agg_scatter_attrib)
+            uint4 *row = &stage[(threadIdx.x & ~63u) * NP + lane * NP];
 #pragma unroll
-            for (uint32_t j = 0; j < NP; ++j) d[j] = make_uint4(wd[4 * j], wd[4 * j + 1], wd[4 * j + 2], wd[4 * j + 3]);
+            for (uint32_t j = 0; j < NP; ++j) row[j] = make_uint4(wd[4 * j], wd[4 * j + 1], wd[4 * j + 2], wd[4 * j + 3]);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const uint64_t hm = __builtin_amdgcn_ballot_w64(has);
+            constexpr uint32_t R = 64 / NP;  // payloads per store instruction
+#pragma unroll
+            for (uint32_t s0 = 0; s0 < 64; s0 += R) {
+                const uint32_t m = s0 + lane / NP, j = lane % NP;
+                const uint32_t pm = (uint32_t)__shfl((int)pos, (int)(m & 63), 64);
+                if (lane / NP < R && m < 64 && ((hm >> m) & 1))
+                    ((uint4 *)(pay + (uint64_t)pm * (16 * NP)))[j] = stage[(threadIdx.x & ~63u) * NP + m * NP + j];
+            }
+            // the next record's rows overwrite the stage: every lane's reads of it are done
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
         }
     }
 }
