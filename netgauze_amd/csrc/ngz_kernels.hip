@@ -250,20 +250,30 @@ constexpr uint32_t kFrameBlock = 256;
 // col[j * kFrameBlock + t] -- so a wave's window stores and its byte reads (every lane its own
 // dword) touch 64 different banks: thread-contiguous 64-byte slots put the lanes 16 banks apart
 // (4-16-way conflicts, 3.6e7 conflict cycles per config-4 k_frame, profiles/r5/cfg4).
+#ifndef NGZ_FRAME_ATTRIB
+#define NGZ_FRAME_ATTRIB 0  // 1: k_frame skips the record walk (experiment builds; timing only: every
+                            // variable-length set then counts no records, so nothing reads its offsets)
+#endif
+#ifndef NGZ_WALKWIN_BYTES
+#define NGZ_WALKWIN_BYTES 64  // window bytes (a multiple of 16; the experiment variants try others)
+#endif
 struct WalkWin {
+    static constexpr uint32_t kBytes = NGZ_WALKWIN_BYTES, kLoads = kBytes / 16;
     uint32_t *col;       // this thread's column of the transposed window table
     uintptr_t base = 0;  // address the window starts at; 0 = empty
     // the byte at address q; lim: end of the batch buffer (no window reaches past it)
     __device__ __forceinline__ uint32_t byte(const uint8_t *q, const uint8_t *lim) {
         const uintptr_t a = (uintptr_t)q;
         if (!col) return *q;
-        if (!base || a < base || a >= base + 64) {
+        if (!base || a < base || a >= base + kBytes) {
             const uintptr_t b0 = a & ~(uintptr_t)15;
-            if (b0 + 64 > (uintptr_t)lim) return *q;
+            if (b0 + kBytes > (uintptr_t)lim) return *q;
             const uint4 *v = (const uint4 *)b0;
-            const uint4 x[4] = {v[0], v[1], v[2], v[3]};
+            uint4 x[kLoads];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
+            for (uint32_t j = 0; j < kLoads; ++j) x[j] = v[j];
+#pragma unroll
+            for (uint32_t j = 0; j < kLoads; ++j) {
                 col[(4 * j + 0) * kFrameBlock] = x[j].x;
                 col[(4 * j + 1) * kFrameBlock] = x[j].y;
                 col[(4 * j + 2) * kFrameBlock] = x[j].z;
@@ -283,15 +293,18 @@ __device__ uint32_t vlen_walk_win(const uint8_t *p, uint32_t pos, uint32_t end, 
                                   const uint8_t *lim, uint32_t *slot, F &&on_rec) {
     if (pl.walk_nv > NGZ_WALK_MAX) return ngz_vlen_walk_exact(p, pos, end, pl, err, on_rec);
     const uint32_t minlen = pl.rec_len, nv = pl.walk_nv;
-    uint32_t fx[NGZ_WALK_MAX + 1];
+    // the fixed runs, two 16-bit ones per register (indexed by unrolled loop counters only)
+    uint32_t fx2[(NGZ_WALK_MAX + 2) / 2];
 #pragma unroll
-    for (uint32_t k = 0; k <= NGZ_WALK_MAX; ++k) fx[k] = pl.walk_fixed[k];
+    for (uint32_t k = 0; k < (NGZ_WALK_MAX + 2) / 2; ++k)
+        fx2[k] = (uint32_t)pl.walk_fixed[2 * k] | ((uint32_t)pl.walk_fixed[2 * k + 1] << 16);
+    auto fx = [&](uint32_t k) { return (fx2[k >> 1] >> (16 * (k & 1))) & 0xFFFFu; };
     WalkWin W{slot};
     uint32_t n = 0;
     while (minlen > 0 && end - pos >= minlen) {
         const uint32_t start = pos;
-        bool ok = end - pos >= fx[0];
-        pos += fx[0];
+        bool ok = end - pos >= fx(0);
+        pos += fx(0);
 #pragma unroll
         for (uint32_t k = 0; k < NGZ_WALK_MAX; ++k) {
             if (k < nv && ok) {
@@ -305,8 +318,8 @@ __device__ uint32_t vlen_walk_win(const uint8_t *p, uint32_t pos, uint32_t end, 
                         hdr = 4;
                     }
                 }
-                ok = ok && end - pos - hdr >= len && end - pos - hdr - len >= fx[k + 1];
-                pos += hdr + len + fx[k + 1];
+                ok = ok && end - pos - hdr >= len && end - pos - hdr - len >= fx(k + 1);
+                pos += hdr + len + fx(k + 1);
             }
         }
         if (!ok) return n + ngz_vlen_walk_exact(p, start, end, pl, err, on_rec, n);
@@ -376,6 +389,7 @@ struct CountVis {
             return 0;
         }
         if (!sets) sum = (uint64_t)(end - (pos - 4)) << 48;
+        if (NGZ_FRAME_ATTRIB & 1) return 0;  // timing attribution (experiment variants): no record walk
         const uint64_t e0 = *err;
         const uint32_t n = walk_records(p, pos, end, pl, err);
         vlen_err = vlen_err || *err != e0;
@@ -423,7 +437,12 @@ struct CountVis {
     }
 };
 
-__global__ void __launch_bounds__(kFrameBlock) k_frame(BatchDev B, const uint32_t *hf_flag, const uint32_t *hf_first) {
+#ifdef NGZ_FRAME_WPE  // experiment variants: a waves-per-SIMD floor for k_frame's register allocation
+#define NGZ_FRAME_ATTR __attribute__((amdgpu_waves_per_eu(NGZ_FRAME_WPE)))
+#else
+#define NGZ_FRAME_ATTR
+#endif
+__global__ void __launch_bounds__(kFrameBlock) NGZ_FRAME_ATTR k_frame(BatchDev B, const uint32_t *hf_flag, const uint32_t *hf_first) {
     const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
     if (d >= B.n) return;
     // this datagram's column of the count matrix starts at zero (no memset pass)
@@ -435,7 +454,7 @@ __global__ void __launch_bounds__(kFrameBlock) k_frame(BatchDev B, const uint32_
     vis.dg_end = vis.dg_off + B.lengths[d];
     vis.split = B.split;
     vis.lim = B.bytes + B.bytes_size;
-    __shared__ uint32_t wwin[16 * kFrameBlock];
+    __shared__ uint32_t wwin[WalkWin::kBytes / 4 * kFrameBlock];
     vis.win = &wwin[threadIdx.x];
     if (B.recoff) vis.ro = ngz_ro_list(B, vis.dg_off, d);
     WalkOut o;
@@ -485,7 +504,7 @@ __global__ void __launch_bounds__(kFrameBlock) k_frame_vlen(BatchDev B) {
     vis.dg_end = vis.dg_off + B.lengths[d];
     vis.split = 2;
     vis.lim = B.bytes + B.bytes_size;
-    __shared__ uint32_t wwin[16 * kFrameBlock];
+    __shared__ uint32_t wwin[WalkWin::kBytes / 4 * kFrameBlock];
     vis.win = &wwin[threadIdx.x];
     vis.ro = ngz_ro_list(B, vis.dg_off, d);
     WalkOut o;

@@ -925,3 +925,52 @@ def test_columns_to_host_async_two_streams_then_decode(dev):
     assert codec.columns_to_host(c.ctypes.data, cap) == n
     # (rows past the batch's records in each column are not rewritten: compare the two copies)
     assert np.array_equal(a.numpy()[:n], c[:n])
+
+
+def test_contexts_decode_concurrently(dev):
+    """bench.py --contexts: several contexts, each on its own stream and host thread, decode the
+    same device-resident config-4 batch at once (one batch's framing beside another's decode).
+    Every context's columns, statuses and processed counts equal one context decoding alone."""
+    import threading
+    from netgauze_amd import synth
+    dg = synth.cfg4_datagrams(200_000)
+    buf, offs, lens = synth.host_batch(dg[2:], device=dev)
+    torch.cuda.synchronize()
+
+    def column_bytes(codec, batch):
+        cap = sum(s.block_bytes() + 256 for s in batch.slots)
+        h = np.zeros(cap, dtype=np.uint8)
+        n = codec.columns_to_host(h.ctypes.data, cap)
+        return h[:n]
+
+    ref = new_codec()
+    ref.decode_datagrams(dg[:2])
+    b = ref.decode_batch(buf, offs, lens)
+    assert b.n_records == 200_000
+    want = column_bytes(ref, b)
+    last = {}
+    codecs = [new_codec() for _ in range(3)]
+    for c in codecs:
+        c.decode_datagrams(dg[:2])
+    streams = [torch.cuda.Stream(dev) for _ in codecs]
+    errors = []
+
+    def drive(i):
+        try:
+            for _ in range(4):
+                last[i] = codecs[i].decode_batch(buf, offs, lens, stream=streams[i].cuda_stream)
+        except Exception as e:  # surfaced below
+            errors.append(e)
+
+    th = [threading.Thread(target=drive, args=(i,)) for i in range(len(codecs))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    torch.cuda.synchronize()
+    assert not errors, errors
+    for i, c in enumerate(codecs):
+        assert last[i].n_records == 200_000
+        assert np.array_equal(column_bytes(c, last[i]), want)
+        assert c.template_counts(10) == {900: 4 * ref.template_counts(10)[900]}
+        assert c.template_counts(9) == {313: 4 * ref.template_counts(9)[313]}
