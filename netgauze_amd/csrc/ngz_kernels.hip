@@ -1135,7 +1135,8 @@ extern "C" int ngz_launch_decode_generic(const BatchDev *B, uint32_t grid, hipSt
 }
 
 extern "C" int ngz_launch_counts(const BatchDev *B, uint64_t set_cap, hipStream_t st) {
-    // n_sets is known on device only; the grid also covers every datagram (finalize)
+    // n_sets is known on device only; the grid also covers every datagram (finalize).  At most 256
+    // blocks: one element per thread (8192 blocks on config 4) measured 110 us against 70
     const uint64_t nb = std::min<uint64_t>((std::max<uint64_t>(set_cap, B->n) + 255) / 256, 256);
     if (nb) hipLaunchKernelGGL(k_counts, dim3((uint32_t)nb), dim3(256), 0, st, *B);
     return hipGetLastError() == hipSuccess ? 0 : -1;
