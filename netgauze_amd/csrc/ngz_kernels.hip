@@ -584,13 +584,17 @@ __global__ void k_layout(BatchDev B) {
     if (ov) atomicOr(&B.summary->overflow, ov);
 }
 
-// Row-mode record tables of variable-length slots are staged per workgroup:
+#ifndef NGZ_EMIT_STAGE_ROWS
+#define NGZ_EMIT_STAGE_ROWS 3072  // rows a k_emit workgroup stages (12 B each in LDS)
+#endif
+// Row-mode record tables (variable-length slots, and fixed-length ones decoded by the staged-row
+// kernel: config 4's NetFlow v9 template) are staged per workgroup:
 // the workgroup's datagrams are consecutive, so their records of one slot are
 // one contiguous row range; each thread writes its records' rows to LDS and
 // the workgroup stores the range coalesced.  (Written per thread straight to
 // HBM, 8- and 4-byte entries 64 lanes apart, they went out as partial-line
 // writes: 1.1 GB of WRITE_SIZE for 0.12 GB of rows on config 4.)
-constexpr uint32_t kEmitStageRows = 2048;
+constexpr uint32_t kEmitStageRows = NGZ_EMIT_STAGE_ROWS;
 constexpr uint32_t kEmitStageSlots = 4;
 
 struct EmitVis {
@@ -712,6 +716,11 @@ struct EmitVis {
             if (B->plans[slot].has_vlen) return;  // the walk (vlen) wrote the rows
             uint64_t *rs = rowsrc(slot) + rec0;
             uint32_t *rd = rowdg(slot) + rec0;
+            for (uint32_t k = 0; k < ntab; ++k)  // staged: the workgroup stores the range coalesced
+                if (tab[k][0] == slot) {
+                    rs = lrs + tab[k][2] + (rec0 - tab[k][1]);
+                    rd = lrd + tab[k][2] + (rec0 - tab[k][1]);
+                }
             for (uint32_t k = 0; k < n; ++k) {
                 rs[k] = ngz_row_entry(dg_off + payload_pos + (uint64_t)k * rl, rl);
                 rd[k] = d;
@@ -770,7 +779,7 @@ __global__ void __launch_bounds__(256) k_emit(BatchDev B, const uint32_t *hf_fla
     // the workgroup's row range of every variable-length row-mode slot, read
     // before any thread moves its scan cursors
     for (uint32_t s = t; s < S; s += blockDim.x) {
-        if (!B.plans[s].has_vlen || B.slots[s].mode != NGZ_MODE_ROW || B.slot_row[s] == NGZ_NO_ROW) continue;
+        if (B.slots[s].mode != NGZ_MODE_ROW || B.slot_row[s] == NGZ_NO_ROW) continue;
         const uint32_t base = B.slots[s].base, sr = B.slot_row[s];
         const uint32_t r0 = B.scan[(uint64_t)sr * N + d0] - base;
         const uint32_t r1 = B.scan[(uint64_t)sr * N + dl] - base + B.counts[(uint64_t)sr * N + dl];
@@ -787,6 +796,16 @@ __global__ void __launch_bounds__(256) k_emit(BatchDev B, const uint32_t *hf_fla
     }
     __syncthreads();
     const uint32_t ntab = min(st_cnt, kEmitStageSlots);
+    if (ntab) {
+        // every staged row is written below (k_frame counted exactly the rows this walk emits);
+        // zeroed first all the same, so no row could ever reach the decode as a stale LDS value
+        const uint32_t used = min(st_used, kEmitStageRows);
+        for (uint32_t i = t; i < used; i += blockDim.x) {
+            st_rs[i] = 0;
+            st_rd[i] = 0;
+        }
+        __syncthreads();
+    }
     if (d < B.n) {
         EmitVis vis;
         vis.B = &B;
