@@ -143,6 +143,8 @@ def main():
                          "variable-length/enterprise IEs; cfg5: config 5, 16 templates (config 3 + 8 width "
                          "permutations), one shard per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--split", action="store_true",
+                    help="split framing (NGZ_OPT_SPLIT: variable-length record walks on a second stream)")
     ap.add_argument("--contexts", type=int, default=1,
                     help="decode contexts in flight (one host thread and HIP stream each, the steps dealt round "
                          "robin): batch k+1's framing overlaps batch k's decode")
@@ -185,7 +187,9 @@ def main():
 
     dev = torch.device("cuda", local)
     cdev = dev if dist is None or dist.get_backend() == "nccl" else torch.device("cpu")  # collective tensors
-    codec = FlowInfoCodec(local, rtc_sync=True)  # template kernels compiled when the template is learnt
+    from netgauze_amd.flow import OPT_SPLIT
+    copts = {OPT_SPLIT: 1} if args.split else {}
+    codec = FlowInfoCodec(local, rtc_sync=True, options=copts)  # template kernels compiled when learnt
     n = args.records
     learnt = []  # the template messages every context learns before timing
     if args.workload == "t20":
@@ -233,7 +237,7 @@ def main():
     assert P == 1 or exchange is None, "--contexts > 1 is a single-rank measurement"
     extra = []
     for _ in range(P - 1):
-        c = FlowInfoCodec(local, rtc_sync=True)
+        c = FlowInfoCodec(local, rtc_sync=True, options=copts)
         c.decode_datagrams(learnt)
         extra.append((c, torch.cuda.Stream(dev).cuda_stream))
     ctxs = [(codec, stream)] + extra
@@ -321,7 +325,7 @@ def main():
         "config": {"workload": workload_desc,
                    "records_per_gpu": n, "messages_per_gpu": int(offs.numel()),
                    "parallelism": "shard-per-gpu" if world > 1 else "single",
-                   **({"contexts": P} if P > 1 else {})},
+                   **({"contexts": P} if P > 1 else {}), **({"split_framing": True} if args.split else {})},
         "gbps_step": alg_bytes * world * args.steps / elapsed / 1e9,
         "templates_usage_exchange": usage,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
