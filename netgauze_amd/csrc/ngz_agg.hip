@@ -1207,10 +1207,7 @@ __global__ __launch_bounds__(256, 4) void k_agg_apply(const RecCtx C, const AggP
 
 // Owner path ops, one per 8-byte unit of the row (AggParams::unit_op / unit_src)
 enum : uint8_t { U_KEEP = 0, U_ADD = 1, U_MIN = 2, U_MAX = 3, U_OR = 4, U_VP = 5, U_TS = 6, U_SYS = 7 };
-#ifndef NGZ_OWN_ROUNDS
-#define NGZ_OWN_ROUNDS 2
-#endif
-constexpr int OWN_ROUNDS = NGZ_OWN_ROUNDS;  // k_agg_apply_own: rounds of eight owners whose rows are in flight together
+constexpr int OWN_ROUNDS = 2;  // k_agg_apply_own: rounds of eight owners whose rows are in flight together
 // k_agg_apply_own's LDS row per record: aggregated-field operands 0-7, then export | sys-up time,
 // template bit, domain bits, present-value bits
 enum : uint32_t { OP_TS = 8, OP_TPL = 9, OP_D0 = 10, OP_D1 = 11, OP_HV = 12, OPW = 13 };
