@@ -1153,10 +1153,13 @@ extern "C" int ngz_launch_decode_generic(const BatchDev *B, uint32_t grid, hipSt
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+#ifndef NGZ_COUNTS_BLOCKS
+#define NGZ_COUNTS_BLOCKS 1024  // config 4: 128 / 256 / 512 / 1024 / 8192 blocks took 134 / 71 / 48 / 43 / 110 us
+#endif
 extern "C" int ngz_launch_counts(const BatchDev *B, uint64_t set_cap, hipStream_t st) {
-    // n_sets is known on device only; the grid also covers every datagram (finalize).  At most 256
-    // blocks: one element per thread (8192 blocks on config 4) measured 110 us against 70
-    const uint64_t nb = std::min<uint64_t>((std::max<uint64_t>(set_cap, B->n) + 255) / 256, 256);
+    // n_sets is known on device only; the grid also covers every datagram (finalize).  At most
+    // NGZ_COUNTS_BLOCKS blocks striding (profiles/r5/cfg4_counts_grid.txt)
+    const uint64_t nb = std::min<uint64_t>((std::max<uint64_t>(set_cap, B->n) + 255) / 256, NGZ_COUNTS_BLOCKS);
     if (nb) hipLaunchKernelGGL(k_counts, dim3((uint32_t)nb), dim3(256), 0, st, *B);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
