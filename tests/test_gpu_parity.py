@@ -974,3 +974,81 @@ def test_contexts_decode_concurrently(dev):
         assert np.array_equal(column_bytes(c, last[i]), want)
         assert c.template_counts(10) == {900: 4 * ref.template_counts(10)[900]}
         assert c.template_counts(9) == {313: 4 * ref.template_counts(9)[313]}
+
+
+def test_netflow_v9_record_lengths_around_staged_limit(dev):
+    """NFv9 templates whose records are 26 to 256 bytes, around NGZ_VSTAGE_REC_MAX (160): those up to
+    160 bytes decode through the LDS-staged row kernel, longer ones through the chunk kernels; all
+    in one batch, interleaved, MTU-style packets of 10 records, against the oracle (both kernel paths).
+    A fixed-length interfaceName string pads each record to its length (ASCII, some NUL-truncated)."""
+    import random
+    rnd = random.Random(913)
+    base = [(8, 4), (12, 4), (1, 8), (2, 4), (7, 2), (11, 2), (4, 1), (6, 1)]  # 26 bytes
+    lengths = [26, 130, 159, 160, 161, 200, 256]
+    tsets, tmpls = b"", {}
+    for i, rl in enumerate(lengths):
+        tid = 400 + i
+        fields = base + ([(82, rl - 26)] if rl > 26 else [])
+        body = struct.pack(">HH", tid, len(fields)) + b"".join(struct.pack(">HH", t, n) for t, n in fields)
+        tsets += body
+        tmpls[tid] = rl
+    dgrams = [nf_msg([struct.pack(">HH", 0, 4 + len(tsets)) + tsets], count=len(lengths))]
+
+    def record(rl):
+        r = struct.pack(">IIQIHHBB", rnd.getrandbits(32), rnd.getrandbits(32), rnd.getrandbits(64),
+                        rnd.getrandbits(32), rnd.getrandbits(16), rnd.getrandbits(16), rnd.choice([6, 17, 1]),
+                        rnd.getrandbits(8))
+        if rl > 26:
+            s = bytes(rnd.choice(b"abcdefghij-_.0123456789") for _ in range(rl - 26))
+            if rnd.random() < 0.3:
+                k = rnd.randrange(rl - 26)
+                s = s[:k] + b"\0" * (rl - 26 - k)
+            r += s
+        return r
+
+    for p in range(6):
+        for tid, rl in tmpls.items():
+            recs = b"".join(record(rl) for _ in range(10))
+            pad = (-len(recs)) % 4
+            dgrams.append(nf_msg([struct.pack(">HH", tid, 4 + len(recs) + pad) + recs + b"\0" * pad], count=10,
+                                 seq=100 + p))
+    # templates first, then the data as a batch of its own (the steady-state device path)
+    codec = new_codec()
+    oc = O.FlowInfoCodec()
+    codec.decode_datagrams(dgrams[:1])
+    parity.oracle_datagrams(dgrams[:1], oc)
+    batch = codec.decode_datagrams(dgrams[1:])
+    oracle, _ = parity.oracle_datagrams(dgrams[1:], oc)
+    stats = parity.check_batch(batch, oracle)
+    assert stats["err"] == 0 and stats["records"] == 6 * 10 * len(lengths)
+    assert codec.template_counts(9) == {k: v.processed_count for k, v in oc.netflow_templates.items()}
+
+
+@pytest.mark.parametrize("sizes", [(1, 10, 50, 400), (60, 90, 120)])
+def test_netflow_v9_staged_rows_large_packets(dev, sizes):
+    """The staged-row NFv9 template kernel on large packets of a 26-byte template: 1-400 records per
+    packet make the slot's layout chunk mode (the kernel's chunk branch); 60-120 keep it row mode with
+    ~25 000 rows per k_emit workgroup, past its LDS stage (3 072 rows), so the row tables go out by
+    direct stores.  Against the oracle, processed counts included."""
+    import random
+    rnd = random.Random(77 + len(sizes))
+    fields = [(8, 4), (12, 4), (1, 8), (2, 4), (7, 2), (11, 2), (4, 1), (6, 1)]
+    tset = struct.pack(">HH", 420, len(fields)) + b"".join(struct.pack(">HH", t, n) for t, n in fields)
+    dgrams = [nf_msg([struct.pack(">HH", 0, 4 + len(tset)) + tset], count=1)]
+    for p in range(900):
+        n = rnd.choice(sizes) if p % 3 else sizes[-1]
+        recs = b"".join(struct.pack(">IIQIHHBB", rnd.getrandbits(32), rnd.getrandbits(32), rnd.getrandbits(64),
+                                    rnd.getrandbits(32), rnd.getrandbits(16), rnd.getrandbits(16), 6, 2)
+                        for _ in range(n))
+        pad = (-len(recs)) % 4
+        dgrams.append(nf_msg([struct.pack(">HH", 420, 4 + len(recs) + pad) + recs + b"\0" * pad], count=n, seq=p))
+    codec = new_codec()
+    oc = O.FlowInfoCodec()
+    codec.decode_datagrams(dgrams[:1])
+    parity.oracle_datagrams(dgrams[:1], oc)
+    for part in (dgrams[1:], dgrams[1:]):  # twice: the second batch takes the steady-state launches
+        batch = codec.decode_datagrams(part)
+        oracle, _ = parity.oracle_datagrams(part, oc)
+        stats = parity.check_batch(batch, oracle)
+        assert stats["err"] == 0 and stats["records"] == sum(struct.unpack(">H", d[2:4])[0] for d in part)
+    assert codec.template_counts(9) == {k: v.processed_count for k, v in oc.netflow_templates.items()}
