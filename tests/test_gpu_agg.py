@@ -493,6 +493,22 @@ def test_partitioned_reduction(dev, keys, monkeypatch):
     check(keys + T20_AGG, [d[:25], d[25:]])
 
 
+@pytest.mark.parametrize("vals", [
+    [(0, 1, 0, ADD)],                                                        # 16 + 8 B: 2-piece payloads
+    [(0, 1, 0, ADD), (0, 2, 0, ADD), (0, 8, 0, MN), (0, 12, 0, MX), (0, 15, 0, MN),
+     (0, 22, 0, MN), (0, 21, 0, MX), (0, 14, 0, OR)],                        # 16 + 52 B: 6-piece payloads
+])
+def test_partitioned_reduction_payload_sizes(dev, vals, monkeypatch):
+    """The partitioned scatter's whole-payload stores at both ends of the payload size: 2 pieces
+    (32 payloads per store instruction) and 6 pieces (10 per instruction, four lanes idle), with the
+    operands of IPv4 Min / Max at 8 bytes and unsigned ones at their widths; forced partitioned path,
+    protocol + destination port key, against the oracle over closing windows."""
+    monkeypatch.setitem(AGG_OPTIONS, _opt("NGZ_AGG_OPT_PARTITION"), 1)
+    times = [1_700_000_010, 1_700_000_030, 1_700_000_061, 1_700_000_049]
+    d = t20_datagrams(6000, 100, times)
+    check([(0, 4, 0, OK), (0, 11, 0, OK)] + vals, [d[:25], d[25:]])
+
+
 def test_partitioned_reduction_ports_captures_orders(dev, monkeypatch):
     """Forced partitioned reduction: peer ports and collection times over two pushes, every
     reference capture (wide and packed keys), wrapping adds / signed min-max, and the ordered
