@@ -133,7 +133,8 @@ typedef struct {
     uint32_t min_export_time;   /* seconds */
     uint32_t max_export_time;
     uint32_t max_sys_up_time;
-    uint32_t reserved1;
+    uint32_t take_id;           /* which ngz_agg_flush / ngz_agg_emit call returned the row (1, 2, ...):
+                                   ngz_agg_row_bytes reads byte values of the last call's rows only */
     int64_t min_collection_ms;
     int64_t max_collection_ms;
     uint64_t template_bits;     /* DataSetId set */
@@ -220,8 +221,8 @@ int ngz_agg_value_info(ngz_agg *a, uint32_t v, ngz_agg_value_desc *out);
  * vclass 8 / 9) of an output row of the last ngz_agg_flush / ngz_agg_emit call: up to cap
  * bytes into dst (may be NULL); returns the value's length, or NGZ_E_INVALID.  Byte values can be
  * read only until the next flush / emit: the tails come from that call's copy.  A row of an
- * earlier call whose tail lies outside the copy is NGZ_E_INVALID (and ngz_agg_flowinfo_json then
- * fails with NGZ_E_INVALID instead of printing the value empty); one inside it reads other bytes. */
+ * earlier call (its take_id is not the last call's) is NGZ_E_INVALID, and ngz_agg_flowinfo_json
+ * then fails with NGZ_E_INVALID instead of printing another row's bytes. */
 int64_t ngz_agg_row_bytes(ngz_agg *a, const void *row, int is_value, uint32_t index, uint8_t *dst, uint64_t cap);
 
 /* AggFlowInfo::into_flowinfo_with_extra_fields (aggregator.rs:203-277) of output rows,

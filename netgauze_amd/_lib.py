@@ -13,9 +13,15 @@ LIB_PATH = os.path.join(HERE, "libngz.so")
 # NGZ_EXPERIMENTS=1 (tools only): the experiment build, libngz_exp.so (tools/build_experiments.sh),
 # whose knobs are read from NGZ_<name> variables for A/B measurements; NGZ_EXPERIMENTS=<name>:
 # libngz_exp_<name>.so, a variant built with extra compile-time defines.  Never the product path.
+# They are built outside the package (tools/exp/), so a stray variable in a collector's
+# environment finds nothing to load unless a developer built one, and loading one says so.
 if os.environ.get("NGZ_EXPERIMENTS"):
+    import sys as _sys
     _x = os.environ["NGZ_EXPERIMENTS"]
-    LIB_PATH = os.path.join(HERE, "libngz_exp.so" if _x == "1" else "libngz_exp_%s.so" % _x)
+    LIB_PATH = os.path.join(os.path.dirname(HERE), "tools", "exp",
+                            "libngz_exp.so" if _x == "1" else "libngz_exp_%s.so" % _x)
+    print("netgauze_amd: NGZ_EXPERIMENTS=%s loads the EXPERIMENT build %s (A/B knobs; timing variants "
+          "decode wrong on purpose) -- not the product library" % (_x, LIB_PATH), file=_sys.stderr)
 
 NGZ_DG_OK, NGZ_DG_NEED_MORE, NGZ_DG_ERROR, NGZ_DG_UNSUPPORTED = 0, 1, 2, 3
 (K_UINT, K_TCPFLAGS, K_SINT, K_BOOL, K_BYTES, K_U256, K_DTMS, K_DTFRAC, K_STR,
@@ -164,7 +170,7 @@ assert ctypes.sizeof(Peer) == 20
 AGG_ROW_DTYPE = np.dtype([("window_start", "<u4"), ("flow_type", "u1"), ("reserved0", "u1"), ("peer", "<u2"),
                           ("key_present", "<u4"), ("val_present", "<u4"), ("record_count", "<u8"),
                           ("min_export_time", "<u4"), ("max_export_time", "<u4"), ("max_sys_up_time", "<u4"),
-                          ("reserved1", "<u4"), ("min_collection_ms", "<i8"), ("max_collection_ms", "<i8"),
+                          ("take_id", "<u4"), ("min_collection_ms", "<i8"), ("max_collection_ms", "<i8"),
                           ("template_bits", "<u8"), ("port_bits", "<u8"), ("domain_bits", "<u8", 2)])
 assert AGG_ROW_DTYPE.itemsize == 88
 

@@ -2663,6 +2663,7 @@ struct ngz_agg {
     uint64_t arena_cap = 0, arena_mark = 0;
     unsigned long long *arena_used = nullptr;
     std::vector<uint8_t> out_tails;  // tails of the rows last returned by flush / emit
+    uint32_t take_id = 0;            // flush / emit calls so far: the last one's rows carry it (ngz_agg_row.take_id)
     int64_t *cut = nullptr;         // per-peer window cutoffs of ngz_agg_closed / ngz_agg_emit
     uint32_t cut_cap = 0;
     uint32_t *rank_maps = nullptr;  // one 65536-bit map per VC_RANK sub-registry value
@@ -2890,7 +2891,7 @@ void finish_rows(ngz_agg *a, uint8_t *dst, int64_t n) {
         uint64_t c;
         memcpy(&c, R + 40, 8); c ^= 1ull << 63; memcpy(R + 40, &c, 8);
         memcpy(&c, R + 48, 8); c ^= 1ull << 63; memcpy(R + 48, &c, 8);
-        memset(R + 36, 0, 4);
+        memcpy(R + 36, &a->take_id, 4);  // ngz_agg_row.take_id (the device's per-push marker there is done)
         uint32_t vp;
         memcpy(&vp, R + 12, 4);
         for (uint32_t v = 0; v < a->P.n_vals; ++v) {
@@ -2926,6 +2927,8 @@ int64_t take_rows(ngz_agg *a, void *dst, uint64_t cap, const int64_t *cut, bool 
     AGG_HIP(a, hipStreamSynchronize(a->stream));
     const uint32_t RB = a->P.row_bytes;
     if ((uint64_t)n * RB > cap || (n && !dst)) return fail(a, NGZ_E_INVALID, "output buffer too small");
+    if (++a->take_id == 0) a->take_id = 1;  // earlier rows' byte values are gone from here on
+    a->out_tails.clear();
     if (n) {
         uint8_t *tmp = nullptr;
         if (hipMalloc(&tmp, (uint64_t)n * RB) != hipSuccess) return fail(a, NGZ_E_NOMEM, "output staging");
@@ -4001,6 +4004,9 @@ int64_t ngz_agg_row_bytes(ngz_agg *a, const void *row, int is_value, uint32_t in
         if (index >= a->P.n_keys || a->P.key_kind[index] != KK_BYTES) return NGZ_E_INVALID;
         off = a->P.key_off[index];
     }
+    uint32_t take;
+    memcpy(&take, (const uint8_t *)row + 36, 4);
+    if (take == 0 || take != a->take_id) return NGZ_E_INVALID;  // a row of an earlier flush / emit
     const uint8_t *slot = (const uint8_t *)row + off;
     uint32_t n, toff8;
     memcpy(&n, slot, 4);

@@ -380,6 +380,7 @@ struct HostFrameOut {
     ngz_dgram_hdr hdr{};
     std::vector<HostSet> sets;
     std::vector<std::pair<uint32_t, int32_t>> defs;  // (set position, version) defined here
+    std::vector<std::pair<uint32_t, int32_t>> restarts;  // the defs that re-announced the current version
     std::vector<std::pair<uint32_t, std::string>> tsets;  // (set position, serde JSON) of template sets
 };
 
@@ -492,7 +493,34 @@ bool parse_scope_spec(Cur &c, Spec &out, std::string &err) {
 }
 
 
-int32_t define_template(ngz_ctx *ctx, uint8_t proto, uint16_t tid, std::vector<Spec> &&scope, std::vector<Spec> &&fields) {
+bool same_specs(const Spec &a, const Spec &b) {
+    return a.kind == b.kind && a.pen == b.pen && a.id == b.id && a.length == b.length && a.scope == b.scope;
+}
+
+// A template record (ipfix.rs:384-413, :276-327; netflow.rs:265-353): the id's new current version.
+// An exporter re-announces its templates every few packets or seconds; a re-announcement with the
+// same specifiers as the current version reuses that version (its slot, columns and kernel) instead
+// of appending one per announcement -- a batch with many refreshes stays within NGZ_MAX_SLOTS and a
+// long-lived peer's version list does not grow.  The reference replaces the map entry with a fresh
+// DecodingTemplate, so processed_count restarts: `restart` reports that (define_at records the
+// position; finish_batch resets the count and k_counts counts only later sets).
+int32_t define_template(ngz_ctx *ctx, uint8_t proto, uint16_t tid, std::vector<Spec> &&scope, std::vector<Spec> &&fields,
+                        bool *restart) {
+    const int32_t cur = ctx->cur[proto == 10 ? 0 : 1][tid];
+    if (cur >= 0) {
+        const Version &c = ctx->versions[cur];
+        bool same = c.n_scope == scope.size() && c.specs.size() == scope.size() + fields.size();
+        for (size_t i = 0; same && i < c.specs.size(); ++i) {
+            Spec s = i < scope.size() ? scope[i] : fields[i - scope.size()];
+            s.scope = i < scope.size();
+            same = same_specs(c.specs[i], s);
+        }
+        if (same) {
+            *restart = true;
+            return cur;
+        }
+    }
+    *restart = false;
     Version v;
     v.proto = proto;
     v.tid = tid;
@@ -573,7 +601,9 @@ void host_frame(ngz_ctx *ctx, const uint8_t *p, uint32_t dl, uint32_t limit, Hos
                         fields.push_back(s);
                     }
                     recs += (recs.empty() ? "" : ",") + template_record_json(tid, nullptr, fields);
-                    o.defs.push_back({toff, define_template(ctx, 10, (uint16_t)tid, {}, std::move(fields))});
+                    bool rs;
+                    o.defs.push_back({toff, define_template(ctx, 10, (uint16_t)tid, {}, std::move(fields), &rs)});
+                    if (rs) o.restarts.push_back({toff, o.defs.back().second});
                 }
                 o.tsets.push_back({pos, "{\"Template\":[" + recs + "]}"});
             } else if (id == 3) {  // ipfix.rs:169-181, OptionsTemplateRecord::parse :276-327
@@ -607,7 +637,9 @@ void host_frame(ngz_ctx *ctx, const uint8_t *p, uint32_t dl, uint32_t limit, Hos
                         (i < scount ? scope : fields).push_back(s);
                     }
                     recs += (recs.empty() ? "" : ",") + template_record_json(tid, &scope, fields);
-                    o.defs.push_back({toff, define_template(ctx, 10, (uint16_t)tid, std::move(scope), std::move(fields))});
+                    bool rs;
+                    o.defs.push_back({toff, define_template(ctx, 10, (uint16_t)tid, std::move(scope), std::move(fields), &rs)});
+                    if (rs) o.restarts.push_back({toff, o.defs.back().second});
                 }
                 for (uint32_t q = c.pos; q < c.end; ++q)  // check_padding_value (ipfix.rs:240-251)
                     if (p[q]) {
@@ -684,7 +716,9 @@ void host_frame(ngz_ctx *ctx, const uint8_t *p, uint32_t dl, uint32_t limit, Hos
                         fields.push_back(s);
                     }
                     recs += (recs.empty() ? "" : ",") + template_record_json(tid, nullptr, fields);
-                    o.defs.push_back({toff, define_template(ctx, 9, (uint16_t)tid, {}, std::move(fields))});
+                    bool rs;
+                    o.defs.push_back({toff, define_template(ctx, 9, (uint16_t)tid, {}, std::move(fields), &rs)});
+                    if (rs) o.restarts.push_back({toff, o.defs.back().second});
                 }
                 o.tsets.push_back({pos, "{\"Template\":[" + recs + "]}"});
                 i -= 1;
@@ -722,7 +756,9 @@ void host_frame(ngz_ctx *ctx, const uint8_t *p, uint32_t dl, uint32_t limit, Hos
                         fields.push_back(s);
                     }
                     recs += (recs.empty() ? "" : ",") + template_record_json(tid, &scope, fields);
-                    o.defs.push_back({toff, define_template(ctx, 9, (uint16_t)tid, std::move(scope), std::move(fields))});
+                    bool rs;
+                    o.defs.push_back({toff, define_template(ctx, 9, (uint16_t)tid, std::move(scope), std::move(fields), &rs)});
+                    if (rs) o.restarts.push_back({toff, o.defs.back().second});
                 }
                 for (uint32_t q = c.pos; q < c.end; ++q)
                     if (p[q]) {
@@ -805,6 +841,8 @@ int upload_slots(ngz_ctx *ctx, const std::vector<int32_t> cur_start[2], hipStrea
         Version &v = ctx->versions[ctx->slot_version[s]];
         plans[s] = v.plan;
         plans[s].f = ctx->d_fields.p + ftab.size();  // the slot's descriptors in the device field table
+        const auto cf = ctx->count_from.find(ctx->slot_version[s]);
+        plans[s].count_from = cf == ctx->count_from.end() ? 0 : cf->second;
         ftab.insert(ftab.end(), v.fields.begin(), v.fields.end());
         plans[s].spec = 0;
         if (ctx->specialize && rtc_eligible(v.plan)) {
@@ -1389,7 +1427,8 @@ int finish_batch(ngz_ctx *ctx, const ngz_batch_in *in, ngz_batch_out *out, hipSt
     ctx->slot_infos.resize(S);
     for (uint32_t s = 0; s < S; ++s) {
         Version &v = ctx->versions[ctx->slot_version[s]];
-        v.processed += proc[s];
+        // re-announced in this batch: the count restarted there (k_counts counted only later sets)
+        v.processed = (ctx->count_from.count(ctx->slot_version[s]) ? 0 : v.processed) + proc[s];
         v.seen_records += ctx->slot_rt[s].total;
         if (ctx->specialize == 2 && v.rtc_state == 0 && v.seen_records >= NGZ_SPECIALIZE_MIN_RECORDS)
             ctx->plans_dirty = true;  // the next batch compiles its kernel
@@ -1585,6 +1624,10 @@ int ngz_decode_batch(ngz_ctx *ctx, const ngz_batch_in *in, ngz_batch_out *out, v
     ctx->json_view.reset();
     ctx->batch_info = 0;
     ctx->pipeline_runs = 0;
+    if (!ctx->count_from.empty()) {  // the last batch's restarts are in its counts already
+        ctx->count_from.clear();
+        ctx->plans_dirty = true;
+    }
     memset(out, 0, sizeof *out);
     int rc = ctx->assigned_gen == ctx->tmpl_gen ? 0 : assign_slots(ctx, {});
     if (rc) return rc;
@@ -1646,6 +1689,7 @@ int ngz_decode_batch(ngz_ctx *ctx, const ngz_batch_in *in, ngz_batch_out *out, v
         ctx->cur[0] = cur0[0];
         ctx->cur[1] = cur0[1];
         ctx->host_errors.clear();
+        ctx->count_from.clear();
         HostFramed hf;
         hf.flag.assign(N, 0);
         hf.first.assign(N + 1, 0);
@@ -1661,6 +1705,10 @@ int ngz_decode_batch(ngz_ctx *ctx, const ngz_batch_in *in, ngz_batch_out *out, v
             per.push_back({d, std::move(o.sets)});
             defs[i] = o.defs;
             for (auto &df : o.defs) tl_entries.push_back({(uint32_t)df.second, d});
+            for (auto &rs : o.restarts) {  // the last re-announcement of a version in the batch wins
+                uint64_t &cf = ctx->count_from[rs.second];
+                cf = std::max<uint64_t>(cf, ((uint64_t)d << 16) | rs.first);
+            }
             for (auto &ts : o.tsets) tsets.push_back({d, ts.first, std::move(ts.second)});
         }
         std::vector<int32_t> extra;

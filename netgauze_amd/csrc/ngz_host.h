@@ -330,6 +330,9 @@ struct ngz_ctx {
     hipEvent_t d2h_ev = nullptr;  // ngz_columns_to_host_async: the last queued copy of the columns
     bool d2h_pending = false;
     std::vector<ngzh::TemplateSetJson> tmpl_sets;  // template sets of the last batch, (dgram, set_pos) order
+    // versions re-announced (identically) in this batch -> (datagram << 16 | template record position)
+    // of the last re-announcement: processed_count restarts there (DevPlan::count_from)
+    std::map<int32_t, uint64_t> count_from;
     uint64_t batch_serial = 0;                      // bumped by every ngz_decode_batch
     std::shared_ptr<ngzh::JsonView> json_view;      // ngz_dgram_json cache of the last batch
     // ngz_template_counts_device staging: a ring of pinned tables, each reused only after

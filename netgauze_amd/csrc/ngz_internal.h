@@ -24,6 +24,7 @@
 int64_t ngz_knob(const char *name, int64_t dflt);
 const char *ngz_knob_str(const char *name, const char *dflt);
 bool ngz_debug();
+int ngz_debug_level();  // 0 off, 1 traces (NGZ_DEBUG set), 2 also generated kernel sources (NGZ_DEBUG=2)
 extern "C" int ngz_experiments_build();  // 1 in a -DNGZ_EXPERIMENTS build (tests check the product is not)
 #endif
 
@@ -113,7 +114,78 @@ struct DevPlan {
     uint8_t walk_nv;
     uint8_t walk_pad[3];
     uint16_t walk_fixed[NGZ_WALK_MAX + 1];
+    // processed_count restarts inside this batch (an identical re-announcement of the template
+    // reuses its version, ngz_host.cpp define_template): only sets at (datagram << 16 | set
+    // position) > count_from count (k_counts); 0 = every set of the slot
+    uint64_t count_from;
 };
+
+// chrono's NaiveDateTime range in milliseconds (timestamp_millis_opt, generator.rs:1725-1746)
+#define NGZ_MIN_MILLIS (-8334601315200000LL)  // days_from_civil(-262143,1,1)*86400000
+#define NGZ_MAX_MILLIS 8210266876799999LL     // (days_from_civil(262142,12,31)+1)*86400000-1
+
+// std::str::from_utf8 of p[0, len); with stop_at_nul only the bytes up to the first NUL
+// (fixed-length strings, generator.rs:1651-1668).  The framing walk's form (host and device);
+// the decode kernels have their own register / LDS forms (ngz_dev.h utf8_valid_prefix).
+__host__ __device__ inline bool ngz_utf8_ok(const uint8_t *p, uint32_t len, bool stop_at_nul) {
+    uint32_t i = 0;
+    while (i < len) {
+        const uint32_t c = p[i];
+        if (c == 0 && stop_at_nul) return true;
+        if (c < 0x80) { ++i; continue; }
+        uint32_t need, lo = 0x80, hi = 0xBF;
+        if (c >= 0xC2 && c <= 0xDF) need = 1;
+        else if (c >= 0xE0 && c <= 0xEF) { need = 2; if (c == 0xE0) lo = 0xA0; if (c == 0xED) hi = 0x9F; }
+        else if (c >= 0xF0 && c <= 0xF4) { need = 3; if (c == 0xF0) lo = 0x90; if (c == 0xF4) hi = 0x8F; }
+        else return false;
+        for (uint32_t t = 1; t <= need; ++t) {
+            if (i + t >= len) return false;
+            const uint32_t b = p[i + t];
+            if (b < (t == 1 ? lo : 0x80u) || b > (t == 1 ? hi : 0xBFu)) return false;
+        }
+        i += need + 1;
+    }
+    return true;
+}
+
+// The record a walk stops in (UnexpectedEof, or a template-constant failure, at field stop_f):
+// DataRecord::parse read its fields before that one and Field::parse checked their values as it
+// read them (ipfix.rs:335-370, generator.rs:1635-1773), so the first value error among them is the
+// record's error -- a dateTime out of chrono's range, a nanosecond fraction of 1e9 outside a leap
+// second, a string that is not UTF-8.  The decode kernels check complete records only, so the walk
+// checks the failing one.  pos = the record's start.  Found by the differential fuzz corpus
+// (tests/test_gpu_fuzz.py: an invalid vlen string before a later field's EOF reported the EOF).
+__host__ __device__ inline uint64_t ngz_partial_record_err(const uint8_t *p, uint32_t pos, uint32_t stop_f,
+                                                           const DevPlan &pl) {
+    for (uint32_t f = 0; f < stop_f; ++f) {
+        const DevField &fd = pl.f[f];
+        if (fd.kind == NGZ_K_VLEN) {
+            uint32_t len = p[pos], hdr = 1;
+            if (len == 255) {
+                len = ((uint32_t)p[pos + 1] << 16) | ((uint32_t)p[pos + 2] << 8) | p[pos + 3];
+                hdr = 4;
+            }
+            if ((fd.flags & 0x80) && !ngz_utf8_ok(p + pos + hdr, len, false))
+                return ngz_err_key(pos + hdr, E_REC_UTF8, f, len);
+            pos += hdr + len;
+            continue;
+        }
+        if (fd.kind == NGZ_K_DTMS) {
+            uint64_t v = 0;
+            for (int i = 0; i < 8; ++i) v = (v << 8) | p[pos + i];
+            if ((int64_t)v < NGZ_MIN_MILLIS || (int64_t)v > NGZ_MAX_MILLIS) return ngz_err_key(pos, E_REC_DTMS, f, 0);
+        } else if (fd.kind == NGZ_K_DTFRAC) {
+            const uint32_t secs = ((uint32_t)p[pos] << 24) | ((uint32_t)p[pos + 1] << 16) | ((uint32_t)p[pos + 2] << 8) | p[pos + 3];
+            const uint32_t frac = ((uint32_t)p[pos + 4] << 24) | ((uint32_t)p[pos + 5] << 16) | ((uint32_t)p[pos + 6] << 8) | p[pos + 7];
+            const uint32_t ns = (uint32_t)(1000000000.0 * ((double)frac / 4294967295.0));
+            if (ns >= 1000000000u && (secs % 60u) != 59u) return ngz_err_key(pos, E_REC_DTFRAC, f, 0);
+        } else if (fd.kind == NGZ_K_STR) {
+            if (!ngz_utf8_ok(p + pos, fd.len, true)) return ngz_err_key(pos, E_REC_UTF8, f, 0);
+        }
+        pos += fd.len;
+    }
+    return NGZ_NO_ERR;
+}
 
 // Records of one IPFIX data set whose template has variable-length (65535)
 // fields, walked as Set::parse + DataRecord::parse + Field::parse would
@@ -130,33 +202,38 @@ __host__ __device__ inline uint32_t ngz_vlen_walk_exact(const uint8_t *p, uint32
     uint32_t n = 0;
     while (minlen > 0 && end - pos >= minlen) {
         const uint32_t start = pos;
+        // the record's error: a value error of an earlier field, else the failure at field f
+        auto fail = [&](uint64_t key, uint32_t f) {
+            const uint64_t ve = ngz_partial_record_err(p, start, f, pl);
+            *err = ve != NGZ_NO_ERR ? ve : key;
+        };
         for (uint32_t f = 0; f < pl.n_fields; ++f) {
             const DevField &fd = pl.f[f];
             const uint32_t rem = end - pos;
             if (fd.kind == NGZ_K_FAIL) {  // fails before reading (InvalidLength, ...)
-                *err = ngz_err_key(pos, E_REC_FAIL, f, 0);
+                fail(ngz_err_key(pos, E_REC_FAIL, f, 0), f);
                 return n;
             }
             if (fd.kind == NGZ_K_VLEN) {
-                if (rem < 1) { *err = ngz_err_key(pos, E_REC_EOF, f, 1); return n; }
+                if (rem < 1) { fail(ngz_err_key(pos, E_REC_EOF, f, 1), f); return n; }
                 uint32_t len = p[pos];
                 pos += 1;
                 if (len == 255) {  // read_unsigned32_be(3)
-                    if (end - pos < 3) { *err = ngz_err_key(pos, E_REC_EOF, f, 3); return n; }
+                    if (end - pos < 3) { fail(ngz_err_key(pos, E_REC_EOF, f, 3), f); return n; }
                     len = ((uint32_t)p[pos] << 16) | ((uint32_t)p[pos + 1] << 8) | p[pos + 2];
                     pos += 3;
                 }
-                if (end - pos < len) { *err = ngz_err_key(pos, E_REC_EOF, f, len); return n; }
+                if (end - pos < len) { fail(ngz_err_key(pos, E_REC_EOF, f, len), f); return n; }
                 pos += len;
                 continue;
             }
             if (fd.kind == NGZ_K_DTFRAC) {  // two u32 reads (generator.rs:1748-1773)
-                if (rem < 4) { *err = ngz_err_key(pos, E_REC_EOF, f, 4); return n; }
-                if (rem < 8) { *err = ngz_err_key(pos + 4, E_REC_EOF, f, 4); return n; }
+                if (rem < 4) { fail(ngz_err_key(pos, E_REC_EOF, f, 4), f); return n; }
+                if (rem < 8) { fail(ngz_err_key(pos + 4, E_REC_EOF, f, 4), f); return n; }
                 pos += 8;
                 continue;
             }
-            if (rem < fd.len) { *err = ngz_err_key(pos, E_REC_EOF, f, fd.len); return n; }
+            if (rem < fd.len) { fail(ngz_err_key(pos, E_REC_EOF, f, fd.len), f); return n; }
             pos += fd.len;
         }
         on_rec(n0 + n, start);

@@ -1009,7 +1009,8 @@ __global__ void __launch_bounds__(256) k_counts(BatchDev B) {
             const ngz_dgram_hdr h = ((const ngz_dgram_hdr *)B.hdr)[s.dgram];
             slot = s.slot;
             const DevPlan &pl = B.plans[s.slot];
-            if (h.status == NGZ_FR_NEED_MORE || h.status == NGZ_FR_UNSUPPORTED) {
+            if (h.status == NGZ_FR_NEED_MORE || h.status == NGZ_FR_UNSUPPORTED ||
+                (((uint64_t)s.dgram << 16) | s.set_pos) <= pl.count_from) {  // before a re-announcement
                 inc = 0;
             } else if (h.err_key == NGZ_NO_ERR) {
                 // the whole message parsed: +1 per IPFIX set (ipfix.rs:223), +1 per NFv9 record (netflow.rs:218)

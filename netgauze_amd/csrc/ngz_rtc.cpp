@@ -27,12 +27,15 @@
 
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <memory>
 #include <mutex>
+#include <set>
 #include <string>
 #include <thread>
 #include <utility>
@@ -64,9 +67,13 @@ std::string cpol_defines() {
     return s;
 }
 
+bool staged_rows(const DevPlan &P);
+
+// The cache key covers every input generate() branches on: the kernel shape (staged_rows
+// depends on the protocol, which the field list alone does not show) included.
 std::string signature(const DevPlan &P) {
     std::string s = "rl" + std::to_string(P.rec_len) + "lw" + std::to_string(P.lds_waves) + "dm" +
-                    std::to_string(P.reserved0);
+                    std::to_string(P.reserved0) + (staged_rows(P) ? "sr" : "") + (P.has_vlen ? "v" : "");
     if (const int64_t v = ngz_knob("NGZ_LD_AUX", -1); v >= 0) s += "la" + std::to_string(v);
     if (const int64_t v = ngz_knob("NGZ_ST_AUX", -1); v >= 0) s += "sa" + std::to_string(v);
     if (const int64_t v = ngz_knob("NGZ_WIN_ROT", -1); v >= 0) s += "wr" + std::to_string(v);
@@ -80,7 +87,6 @@ std::string signature(const DevPlan &P) {
 }
 
 std::string generate_vlen(const DevPlan &P);
-bool staged_rows(const DevPlan &P);
 
 // The parts of a fixed template's generated decode: the pass body (register
 // windows, extraction, column stores through ColT / ColGlb) and, when staged
@@ -640,46 +646,111 @@ std::map<std::pair<int, std::string>, std::unique_ptr<Entry>> g_cache;
 // function-local statics during a compile, on the worker, and those register
 // their destructors after the handler, so exit runs them first.  A dist rank
 // that exited with compiles in flight still hung in r3.  The complete rule is
-// that no compile is in flight when the exit handlers start.  Each compile's
-// thread is kept with its cache entry: ngz_ctx_destroy joins the threads of
-// every entry its context started or waits on (ngz_rtc_join), so a C / Rust
+// that no compile is in flight when the exit handlers start.  The pool keeps
+// the entries queued or compiling: ngz_ctx_destroy waits for those of every
+// entry its context started or waits on (ngz_rtc_join), so a C / Rust
 // host that destroys its contexts (the codec's drop is synchronous,
 // codec.rs:68-82) has nothing in flight when it returns from main;
-// ngz_rtc_drain joins every worker (netgauze_amd._lib registers it with
+// ngz_rtc_drain waits for every queued compile (netgauze_amd._lib registers it with
 // Python's atexit, which runs before any C exit handler).
+//
+// Compiles run on a bounded pool (kMaxCompilers threads draining one queue), not one thread
+// per template: a peer announcing hundreds of templates at once (or the differential fuzz
+// corpus, tests/test_gpu_fuzz.py: ~600 distinct layouts) used to start hundreds of
+// concurrent hiprtc compiles, each with its own LLVM context.  A pool thread ends when the
+// queue is empty; the next submit after that reaps the finished threads.
+void build(Entry *e, int device, const std::string &src, const std::string &sig, const char *kname);
+
 struct Workers {
+    static constexpr size_t kMaxCompilers = 4;
+    struct Job {
+        Entry *e;
+        int device;
+        std::string src, sig;
+        const char *kname;
+    };
     std::mutex mu;
-    std::vector<std::pair<const void *, std::thread>> th;  // (cache entry, its compile)
-    // join the workers of the given entries (all when entries is null); returns how many
-    int join(const void *const *entries, size_t n) {
-        std::vector<std::thread> v;
+    std::condition_variable cv;            // a job finished or a thread ended
+    std::deque<Job> q;                     // not started yet
+    std::vector<std::thread> th;           // pool threads, running or ended and not yet joined
+    size_t running = 0;                    // threads still draining the queue
+    std::multiset<const void *> pending;   // entries queued or compiling
+    void submit(Job j) {
+        std::vector<std::thread> ended;
         {
             std::lock_guard<std::mutex> lk(mu);
-            for (size_t i = 0; i < th.size();) {
-                bool take = entries == nullptr;
-                for (size_t k = 0; k < n && !take; ++k) take = th[i].first == entries[k];
-                if (take) {
-                    v.push_back(std::move(th[i].second));
-                    th[i] = std::move(th.back());
-                    th.pop_back();
-                } else {
-                    ++i;
-                }
+            if (running == 0) ended.swap(th);  // every earlier thread left its loop
+            pending.insert(j.e);
+            q.push_back(std::move(j));
+            if (running < kMaxCompilers) {
+                ++running;
+                th.emplace_back([this] { loop(); });
             }
         }
+        for (auto &t : ended)
+            if (t.joinable()) t.join();
+    }
+    void loop() {
+        pthread_setname_np(pthread_self(), "ngz-rtc");  // visible in /proc/<pid>/task/*/comm
+        std::unique_lock<std::mutex> lk(mu);
+        while (!q.empty()) {
+            Job j = std::move(q.front());
+            q.pop_front();
+            lk.unlock();
+            build(j.e, j.device, j.src, j.sig, j.kname);
+            lk.lock();
+            pending.erase(pending.find(j.e));
+            cv.notify_all();
+        }
+        --running;
+        cv.notify_all();
+    }
+    // wait until none of the given entries is queued or compiling; returns how many were
+    int join(const void *const *entries, size_t n) {
+        std::unique_lock<std::mutex> lk(mu);
         int k = 0;
-        for (auto &t : v)
-            if (t.joinable()) {
-                t.join();
-                ++k;
-            }
+        for (size_t i = 0; i < n; ++i) k += pending.count(entries[i]) ? 1 : 0;
+        cv.wait(lk, [&] {
+            for (size_t i = 0; i < n; ++i)
+                if (pending.count(entries[i])) return false;
+            return true;
+        });
         return k;
     }
-    int join_all() { return join(nullptr, 0); }
-    ~Workers() { join_all(); }
+    // wait for the queue to drain and every pool thread to end; returns the compiles waited for
+    int join_all() {
+        std::vector<std::thread> v;
+        int k;
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            k = (int)pending.size();
+            cv.wait(lk, [&] { return q.empty() && running == 0; });
+            v.swap(th);
+        }
+        for (auto &t : v)
+            if (t.joinable()) t.join();
+        return k;
+    }
+    // exit: compiles not started are dropped (their entries fail: nobody decodes any more)
+    void cancel_queued() {
+        std::lock_guard<std::mutex> lk(mu);
+        for (Job &j : q) {
+            j.e->state.store(3, std::memory_order_release);
+            pending.erase(pending.find(j.e));
+        }
+        q.clear();
+        cv.notify_all();
+    }
+    ~Workers() {
+        cancel_queued();
+        join_all();
+    }
 } g_workers;
 
-void join_workers_at_exit() { g_workers.join_all(); }
+void join_workers_at_exit() {
+    g_workers.cancel_queued();
+    g_workers.join_all();
+}
 
 // Loads comgr and runs hiprtc's lazy initialisation on the calling thread (one
 // program created and destroyed, nothing compiled), so that their exit-time
@@ -733,7 +804,7 @@ bool compile(const std::string &src, std::vector<char> &code, std::string &log) 
 void build(Entry *e, int device, const std::string &src, const std::string &sig, const char *kname) {
     std::vector<char> code;
     std::string log;
-    if (ngz_debug()) fprintf(stderr, "[ngz rtc] source:\n%s\n", src.c_str());
+    if (ngz_debug_level() >= 2) fprintf(stderr, "[ngz rtc] source:\n%s\n", src.c_str());
     if (!compile(src, code, log)) {
         fprintf(stderr, "[ngz rtc] compile failed for %s:\n%s\n", sig.c_str(), log.c_str());
         e->state.store(3, std::memory_order_release);
@@ -777,11 +848,7 @@ int kernel_async(int device, const std::string &sig, Gen &&gen, const char *knam
             prime_rtc_runtime();
             std::atexit(join_workers_at_exit);
         });
-        std::lock_guard<std::mutex> lk(g_workers.mu);
-        g_workers.th.emplace_back(e, std::thread([=, src = std::move(src)]() {
-            pthread_setname_np(pthread_self(), "ngz-rtc");  // visible in /proc/<pid>/task/*/comm
-            build(e, device, src, sig, kname);
-        }));
+        g_workers.submit(Workers::Job{e, device, std::move(src), sig, kname});
         return 0;
     }
     if (st == 2) {

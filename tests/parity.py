@@ -121,8 +121,10 @@ def check_error_struct(batch, d, err):
     return st
 
 
-def check_batch(batch, oracle, check_records=True, max_fail=5):
-    """Compare; returns stats dict; raises AssertionError with context."""
+def check_batch(batch, oracle, check_records=True, max_fail=5, failures=None):
+    """Compare; returns stats dict; raises AssertionError with context.  With a `failures`
+    list, a datagram that disagrees is appended as (datagram, message) and the comparison
+    goes on with the next one (the fuzz corpus wants every divergence of a batch)."""
     hdr = batch.dgram_headers()
     sets = batch.sets()
     by_dg = {}
@@ -139,61 +141,71 @@ def check_batch(batch, oracle, check_records=True, max_fail=5):
     stats = {"ok": 0, "none": 0, "err": 0, "unsupported": 0, "records": 0, "fields": 0}
     assert len(oracle) == batch.n_dgrams
     for d, (kind, val) in enumerate(oracle):
-        st = int(hdr[d]["status"])
-        if st == L.NGZ_DG_UNSUPPORTED:
-            stats["unsupported"] += 1
+        if failures is None:
+            _check_dgram(batch, d, kind, val, hdr, by_dg, col, stats, check_records)
             continue
-        if kind == "none":
-            assert st == L.NGZ_DG_NEED_MORE, "dgram %d: expected Ok(None), status %d" % (d, st)
-            stats["none"] += 1
-            continue
-        if kind == "err":
-            assert st == L.NGZ_DG_ERROR, "dgram %d: expected error %s, status %d" % (d, O.dumps(val), st)
-            got = batch.error_json(d)
-            assert got == O.dumps(val), "dgram %d error:\n got %s\n exp %s" % (d, got, O.dumps(val))
-            check_error_struct(batch, d, val)
-            stats["err"] += 1
-            continue
-        assert st == L.NGZ_DG_OK, "dgram %d: expected Ok(Some), status %d err %s" % (d, st, batch.error_json(d))
-        stats["ok"] += 1
-        h = hdr[d]
-        if isinstance(val, O.IpfixPacket):
-            assert (h["version"], h["time"], h["sequence"], h["domain"]) == (
-                10, val.export_time.secs, val.sequence_number, val.observation_domain_id), d
-        else:
-            assert (h["version"], h["sys_up_time"], h["time"], h["sequence"], h["domain"]) == (
-                9, val.sys_up_time, val.unix_time.secs, val.sequence_number, val.source_id), d
-        data_sets = [s for s in val.sets if s[0] == "Data"]
-        got_sets = by_dg.get(d, [])
-        assert len(data_sets) == len(got_sets), "dgram %d: %d data sets vs %d" % (d, len(data_sets), len(got_sets))
-        for (_, sid, recs), gs in zip(data_sets, got_sets):
-            slot = batch.slots[int(gs["slot"])]
-            assert slot.template_id == sid and int(gs["n"]) == len(recs), (d, sid, int(gs["n"]), len(recs))
-            if not check_records:
-                continue
-            rec0 = int(gs["rec0"])
-            for r, (scope, fields) in enumerate(recs):
-                allf = list(scope) + list(fields)
-                assert len(allf) == len(slot.fields)
-                for f, fv in enumerate(allf):
-                    fi = slot.fields[f]
-                    got = bytes(col(int(gs["slot"]), f)[rec0 + r])
-                    if fi.kind == L.K_VLEN:
-                        # {u64 batch offset, u32 length, u32 0} -> the value's bytes in the input batch
-                        off = int.from_bytes(got[:8], "little")
-                        ln = int.from_bytes(got[8:12], "little")
-                        assert got[12:] == bytes(4), (d, r, f, got.hex())
-                        v = fv.value
-                        exp = v.encode("utf-8") if isinstance(v, str) else bytes(v)
-                        assert batch.input_bytes(off, ln) == exp, (d, r, f, off, ln, exp[:32])
-                    elif fi.kind == L.K_STR:
-                        raw = got.split(b"\0", 1)[0]
-                        exp = fv.value.encode("utf-8")
-                        assert raw == exp, (d, r, f, raw, exp)
-                    else:
-                        exp = canon(fv, fi)
-                        assert got == exp, "dgram %d rec %d field %d kind %d: got %s exp %s" % (
-                            d, r, f, fi.kind, got.hex(), exp.hex())
-                    stats["fields"] += 1
-                stats["records"] += 1
+        try:
+            _check_dgram(batch, d, kind, val, hdr, by_dg, col, stats, check_records)
+        except AssertionError as e:
+            failures.append((d, str(e)[:1500]))
     return stats
+
+
+def _check_dgram(batch, d, kind, val, hdr, by_dg, col, stats, check_records):
+    st = int(hdr[d]["status"])
+    if st == L.NGZ_DG_UNSUPPORTED:
+        stats["unsupported"] += 1
+        return
+    if kind == "none":
+        assert st == L.NGZ_DG_NEED_MORE, "dgram %d: expected Ok(None), status %d" % (d, st)
+        stats["none"] += 1
+        return
+    if kind == "err":
+        assert st == L.NGZ_DG_ERROR, "dgram %d: expected error %s, status %d" % (d, O.dumps(val), st)
+        got = batch.error_json(d)
+        assert got == O.dumps(val), "dgram %d error:\n got %s\n exp %s" % (d, got, O.dumps(val))
+        check_error_struct(batch, d, val)
+        stats["err"] += 1
+        return
+    assert st == L.NGZ_DG_OK, "dgram %d: expected Ok(Some), status %d err %s" % (d, st, batch.error_json(d))
+    stats["ok"] += 1
+    h = hdr[d]
+    if isinstance(val, O.IpfixPacket):
+        assert (h["version"], h["time"], h["sequence"], h["domain"]) == (
+            10, val.export_time.secs, val.sequence_number, val.observation_domain_id), d
+    else:
+        assert (h["version"], h["sys_up_time"], h["time"], h["sequence"], h["domain"]) == (
+            9, val.sys_up_time, val.unix_time.secs, val.sequence_number, val.source_id), d
+    data_sets = [s for s in val.sets if s[0] == "Data"]
+    got_sets = by_dg.get(d, [])
+    assert len(data_sets) == len(got_sets), "dgram %d: %d data sets vs %d" % (d, len(data_sets), len(got_sets))
+    for (_, sid, recs), gs in zip(data_sets, got_sets):
+        slot = batch.slots[int(gs["slot"])]
+        assert slot.template_id == sid and int(gs["n"]) == len(recs), (d, sid, int(gs["n"]), len(recs))
+        if not check_records:
+            continue
+        rec0 = int(gs["rec0"])
+        for r, (scope, fields) in enumerate(recs):
+            allf = list(scope) + list(fields)
+            assert len(allf) == len(slot.fields)
+            for f, fv in enumerate(allf):
+                fi = slot.fields[f]
+                got = bytes(col(int(gs["slot"]), f)[rec0 + r])
+                if fi.kind == L.K_VLEN:
+                    # {u64 batch offset, u32 length, u32 0} -> the value's bytes in the input batch
+                    off = int.from_bytes(got[:8], "little")
+                    ln = int.from_bytes(got[8:12], "little")
+                    assert got[12:] == bytes(4), (d, r, f, got.hex())
+                    v = fv.value
+                    exp = v.encode("utf-8") if isinstance(v, str) else bytes(v)
+                    assert batch.input_bytes(off, ln) == exp, (d, r, f, off, ln, exp[:32])
+                elif fi.kind == L.K_STR:
+                    raw = got.split(b"\0", 1)[0]
+                    exp = fv.value.encode("utf-8")
+                    assert raw == exp, (d, r, f, raw, exp)
+                else:
+                    exp = canon(fv, fi)
+                    assert got == exp, "dgram %d rec %d field %d kind %d: got %s exp %s" % (
+                        d, r, f, fi.kind, got.hex(), exp.hex())
+                stats["fields"] += 1
+            stats["records"] += 1

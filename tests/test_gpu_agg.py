@@ -815,6 +815,39 @@ def test_long_byte_keys_through_table_rebuilds(dev):
     same_groups(agg.flush(), o.flush())
 
 
+def test_row_bytes_refuses_rows_of_an_earlier_take(dev):
+    """ngz_agg_row.take_id: byte values of a row returned by an earlier flush / emit
+    are NGZ_E_INVALID, not another row's bytes, and so is its FlowInfo rendering; the last
+    call's rows read their own values."""
+    import numpy as np
+    from netgauze_amd import _lib
+    from netgauze_amd.aggregate import AggError
+    from netgauze_amd.flow import FlowInfoCodec
+    fields = [(0, 82, 0, OK), (0, 1, 0, ADD)]
+    agg = new_agg(fields, capacity=2000, lateness_s=0)
+    codec = FlowInfoCodec()
+    tpl = [(82, 0xFFFF), (1, 8)]
+    raws = []
+    for step in range(3):
+        recs = [_vlen(("a-long-interface-name-%04d-of-step-%02d-padding" % (j, step)).encode()) +
+                struct.pack(">Q", j + 1) for j in range(50)]
+        d = [ipfix_msg(([tset(256, tpl)] if step == 0 else []) + [dset(256, recs)], 1_700_000_000 + 60 * step)]
+        agg.push(codec.decode_datagrams(d))
+        hdr, raw = agg.emit_raw() if step else agg.flush_raw()
+        raws.append((hdr, raw, step))
+    hdr, raw, step = raws[-1]
+    assert len(raw) and all(int(h["take_id"]) == 3 for h in hdr)
+    assert agg._row_bytes(raw[0], 0, 0).startswith(b"a-long-interface-name-")
+    old_hdr, old_raw, _ = raws[0]
+    assert len(old_raw) == 50 and all(int(h["take_id"]) == 1 for h in old_hdr)
+    for r in old_raw[:5]:
+        r = np.ascontiguousarray(r)
+        assert _lib.load().ngz_agg_row_bytes(agg._h, r.ctypes.data, 0, 0, None, 0) == -1  # NGZ_E_INVALID
+    with pytest.raises(AggError):
+        agg.flowinfo_json(old_raw)
+    assert len(agg.flowinfo_json(raw)) == len(raw)
+
+
 def test_wide_byte_key_large_batch(dev):
     """A 200-byte variable-length string key over 10^6 records in one batch, five distinct keys,
     pushed three times: the byte arena is reserved per group and field (table slots x
