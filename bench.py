@@ -192,25 +192,25 @@ def main():
     codec = FlowInfoCodec(local, rtc_sync=True, options=copts)  # template kernels compiled when learnt
     n = args.records
     learnt = []  # the template messages every context learns before timing
-    if args.workload == "t20":
-        learnt = [synth.template_message()]
-        codec.decode_datagrams(learnt)  # exporter's template, learnt before timing
-        rec = synth.t20_records(n, seed=synth.SEED_CFG2 + rank, device=dev, first=0)
-        buf, offs, lens = synth.ipfix_data_stream(rec, 64)
-        del rec
+    from netgauze_amd import dist as ndist
+    n_rank = n  # records this rank decodes per step
+    if args.workload in ("t20", "mixed8", "cfg5"):
+        # one stream of n * world records: its message index (records per message, no
+        # bytes) is cut into contiguous ranges balanced by records, and each rank builds only its
+        # range -- byte for byte the messages the whole stream has there
+        tpls = None if args.workload == "t20" else \
+            synth.CFG3_TEMPLATES if args.workload == "mixed8" else synth.CFG5_TEMPLATES
+        seed = {"t20": synth.SEED_CFG2, "mixed8": synth.SEED_CFG3, "cfg5": synth.SEED_CFG5}[args.workload]
+        learnt = [synth.template_message() if tpls is None else synth.templates_message(tpls)]
+        codec.decode_datagrams(learnt)  # the exporter's templates, learnt before timing
+        _, _, per_msg = synth.stream_index(n * world, tpls)
+        m0, m1 = ndist.shard_by_records(per_msg, rank, world)
+        buf, offs, lens, n_rank = synth.stream_range(n * world, m0, m1, tpls, seed=seed, device=dev)
         if os.environ.get("NGZ_BENCH_INPUT_MB"):  # experiment: the batch at the start of a larger allocation
             big = torch.empty(max(buf.numel(), int(os.environ["NGZ_BENCH_INPUT_MB"]) << 20), dtype=torch.uint8, device=dev)
             big[:buf.numel()].copy_(buf)
             buf = big[:buf.numel()]
-        rec_bytes = {256: 64}
-    elif args.workload in ("mixed8", "cfg5"):
-        tpls = synth.CFG3_TEMPLATES if args.workload == "mixed8" else synth.CFG5_TEMPLATES
-        seed = synth.SEED_CFG3 if args.workload == "mixed8" else synth.SEED_CFG5
-        learnt = [synth.templates_message(tpls)]
-        codec.decode_datagrams(learnt)
-        buf, offs, lens, recs = synth.mixed_stream(n, templates=tpls, seed=seed + 64 * rank, device=dev)
-        rec_bytes = {tid: r.shape[1] for tid, r in recs.items()}
-        del recs
+        rec_bytes = {256: 64} if tpls is None else {tid: synth.field_offsets(f)[1] for tid, f in tpls}
     else:
         dg = synth.cfg4_datagrams(n, seed=synth.SEED_CFG4 + 16 * rank)
         learnt = dg[:2]
@@ -220,7 +220,6 @@ def main():
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream(dev).cuda_stream
 
-    from netgauze_amd import dist as ndist
     # templates.usage: per step, both protocols' processed counts -> one device table
     # (ngz_template_counts_device, stream-ordered) -> one RCCL all-gather; no host sync
     exchange = ndist.CountExchange(codec, stream=stream) if dist is not None else None
@@ -247,7 +246,7 @@ def main():
         for c, st in extra:
             c.decode_batch(buf, offs, lens, stream=st)
     # (experiment builds may be timing-attribution variants whose output is wrong by design)
-    assert b.n_records == n or os.environ.get("NGZ_EXPERIMENTS", "0") not in ("", "0", "1"), (b.n_records, n)
+    assert b.n_records == n_rank or os.environ.get("NGZ_EXPERIMENTS", "0") not in ("", "0", "1"), (b.n_records, n_rank)
     # algorithmic bytes per launch: wire bytes read + canonical column bytes written, per template
     if rec_bytes is not None:
         read_bytes = sum(s.n_records * rec_bytes[s.template_id] for s in b.slots if s.n_records)
@@ -292,6 +291,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms_per_step = elapsed / args.steps * 1e3
+    # t20 / mixed8 / cfg5: the ranks' ranges partition one stream of n * world records; cfg4: a
+    # stream of n records per rank
     total_records = n * world * args.steps
     value = total_records / elapsed
     dec_avg = sum(dec_ms) / len(dec_ms)
@@ -304,6 +305,15 @@ def main():
                      "cfg4": "config 4: %d records/GPU, NFv9 template 313 (130 B, 10/packet) + IPFIX "
                              "template 900 (vlen strings/octets, VMware/Huawei IEs)" % n}[args.workload]
     traffic = committed_traffic(n, workload_desc)
+    # the arena placement lottery of the first large batch (ngz_placement_trials): every trial's
+    # decode time, the kept one, and the fraction the median trial would have reached
+    trials, kept = codec.placement_trials()
+    placement = None
+    if trials:
+        med = sorted(trials)[len(trials) // 2]
+        placement = {"placement_trials_ms": trials, "placement_kept": kept,
+                     "placement_median_frac": alg_bytes / (med * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                     "placement_best_frac": alg_bytes / (min(trials) * 1e-3) / 1e9 / HBM_PEAK_GBS}
     out = {
         "metric": {"t20": "IPFIX flow records/sec + GB/s (device-resident), 20-field fixed template",
                    "mixed8": "IPFIX flow records/sec (device-resident), config 3: 8 templates",
@@ -320,11 +330,15 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (splitmix64 records, seed 0x4E475A450000000%d+rank)"
-                % {"t20": 2, "mixed8": 3, "cfg4": 4, "cfg5": 5}[args.workload],
+        "data": ("synthetic (splitmix64 records, seed 0x4E475A4500000004+16*rank, a stream per rank)"
+                 if args.workload == "cfg4" else
+                 "synthetic (splitmix64 records, seed 0x4E475A450000000%d): one stream of %d records, each rank "
+                 "decodes its record-balanced message range (this rank: %d)"
+                 % ({"t20": 2, "mixed8": 3, "cfg5": 5}[args.workload], n * world, n_rank)),
         "config": {"workload": workload_desc,
                    "records_per_gpu": n, "messages_per_gpu": int(offs.numel()),
-                   "parallelism": "shard-per-gpu" if world > 1 else "single",
+                   "parallelism": ("record-balanced message ranges of one stream, one per GPU"
+                                   if args.workload != "cfg4" else "a stream per GPU") if world > 1 else "single",
                    **({"contexts": P} if P > 1 else {}), **({"split_framing": True} if args.split else {})},
         "gbps_step": alg_bytes * world * args.steps / elapsed / 1e9,
         "templates_usage_exchange": usage,
@@ -333,7 +347,7 @@ def main():
                      "traffic_src": traffic[1] if traffic else None,
                      "kernel": "ngz_tpl (per-template decode kernels)", "kernel_ms": dec_avg,
                      "alg_bytes_per_launch": alg_bytes,
-                     "read_gbps": read_bytes / (dec_avg * 1e-3) / 1e9},
+                     "read_gbps": read_bytes / (dec_avg * 1e-3) / 1e9, **(placement or {})},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.workload)

@@ -40,9 +40,10 @@
 extern "C" {
 #endif
 
-#define NGZ_ABI_VERSION 4  /* 2: ngz_slot_info.n_fields is 32-bit (no field cap), ngz_dgram_error,
+#define NGZ_ABI_VERSION 5  /* 2: ngz_slot_info.n_fields is 32-bit (no field cap), ngz_dgram_error,
                               ngz_template_counts_device; 3: ngz_abi_version, ngz_ctx_destroy joins the
-                              context's background compiles; 4: ngz_columns_to_host_async */
+                              context's background compiles; 4: ngz_columns_to_host_async;
+                              5: ngz_record_fields */
 
 /* return codes */
 #define NGZ_OK 0
@@ -211,6 +212,22 @@ int ngz_slot_kernel(ngz_ctx *ctx, uint32_t slot);
  * second stream beside the fixed-length sets' framing and decode), NGZ_BATCH_RERUN a pass was
  * repeated (buffer growth, a template slot without a count row, a record error split framing
  * went past).  Returns the bits, or NGZ_E_INVALID. */
+/* Data records each of n host-memory messages carries under the context's current templates
+ * (no device work, nothing decoded or learnt): per data set, its payload over the template's
+ * record length, or the framing's record walk for a variable-length template; sets of unknown
+ * templates count nothing.  For the multi-GPU shard plan (contiguous message
+ * ranges balanced by record count, netgauze_amd/dist.py shard_by_records), the reference's
+ * analogue being how the supervisor spreads exporter peers over actors (flow_supervisor.rs:288-305).
+ * Returns NGZ_OK or NGZ_E_INVALID. */
+int ngz_message_records(ngz_ctx *ctx, const uint8_t *bytes, const uint64_t *offsets, const uint32_t *lengths,
+                        uint32_t n, uint32_t *records);
+
+/* The arena placement of the context's first large batch (NGZ_OPT_PLACE_TRIALS, DESIGN.md §2
+ * "Arena placement"): the decode milliseconds of every trial arena, in trial order, into
+ * decode_ms[0, cap), and in *kept (may be NULL) the trial whose arena the context kept (the
+ * fastest).  Returns the number of trials: 0 before the placement ran (or with one trial). */
+int ngz_placement_trials(ngz_ctx *ctx, float *decode_ms, uint32_t cap, uint32_t *kept);
+
 #define NGZ_BATCH_PREDICTED 1
 #define NGZ_BATCH_SPLIT 2
 #define NGZ_BATCH_RERUN 4
@@ -290,6 +307,65 @@ int ngz_dgram_error(ngz_ctx *ctx, uint32_t dgram, ngz_error *err);
  * length (excluding NUL; buf is truncated to cap) or <0 (NGZ_E_INVALID for
  * NEED_MORE / UNSUPPORTED datagrams). */
 int64_t ngz_dgram_json(ngz_ctx *ctx, uint32_t dgram, char *buf, size_t cap);
+
+/* One decoded field of a record: the reference's `Field` value (DataRecord::parse ->
+ * Box<[Field]>, ipfix.rs:335-370, 419-424; NFv9 scope fields ScopeField, netflow.rs:443-475)
+ * as the IE that names its variant plus the typed value in the canonical column encoding
+ * (the NGZ_K_* list above).  A host builds the `Field` from (pen, ie_id, kind, value)
+ * without parsing JSON (INTEGRATION.md §2 `ColumnarBatch::record`). */
+#define NGZ_FV_SCOPE 1u      /* a scope field (IPFIX options scope / NFv9 ScopeField) */
+#define NGZ_FV_STRING 2u     /* NGZ_K_VLEN / NGZ_K_STR: a UTF-8 string (String), else octets (Box<[u8]>) */
+#define NGZ_FV_VENDOR 4u     /* the IE is in a vendor package (Field::<Vendor>(..), generator.rs:2915-2924) */
+#define NGZ_FV_UNKNOWN 8u    /* IE::Unknown{pen, id} or a vendor package's Unknown{id}: raw bytes */
+#define NGZ_FV_SUBREG 16u    /* the value is a sub-registry enum (From<int>, lossless) */
+#define NGZ_FV_MPLS 32u      /* an MPLS label IE ([u8; 3]) */
+#define NGZ_FV_TCPFLAGS 64u  /* tcpControlBits (TCPHeaderFlags from the low byte) */
+/* IPFIX data types (dtype; the registry's, RFC 7012 s3.1 order) */
+#define NGZ_DT_OCTET_ARRAY 0
+#define NGZ_DT_UNSIGNED8 1
+#define NGZ_DT_UNSIGNED16 2
+#define NGZ_DT_UNSIGNED32 3
+#define NGZ_DT_UNSIGNED64 4
+#define NGZ_DT_SIGNED8 5
+#define NGZ_DT_SIGNED16 6
+#define NGZ_DT_SIGNED32 7
+#define NGZ_DT_SIGNED64 8
+#define NGZ_DT_FLOAT32 9
+#define NGZ_DT_FLOAT64 10
+#define NGZ_DT_BOOLEAN 11
+#define NGZ_DT_MAC_ADDRESS 12
+#define NGZ_DT_STRING 13
+#define NGZ_DT_DATETIME_SECONDS 14
+#define NGZ_DT_DATETIME_MILLISECONDS 15
+#define NGZ_DT_DATETIME_MICROSECONDS 16
+#define NGZ_DT_DATETIME_NANOSECONDS 17
+#define NGZ_DT_IPV4_ADDRESS 18
+#define NGZ_DT_IPV6_ADDRESS 19
+#define NGZ_DT_BASIC_LIST 20
+#define NGZ_DT_SUB_TEMPLATE_LIST 21
+#define NGZ_DT_SUB_TEMPLATE_MULTI_LIST 22
+#define NGZ_DT_UNSIGNED256 23
+typedef struct {
+    uint32_t pen;          /* IE enterprise number (0 = IANA) */
+    uint16_t ie_id;        /* IE id (NFv9 scope fields: the raw scope code) */
+    uint8_t kind;          /* NGZ_K_*: the decode rule that produced `value` */
+    uint8_t dtype;         /* NGZ_DT_*: the IE's data type (octetArray for unknown IEs and NFv9 scopes) */
+    uint16_t wire_length;  /* declared length (65535 = variable length) */
+    uint16_t width;        /* column width */
+    uint32_t len;          /* bytes at `value`: the width, a fixed string's bytes before its first NUL,
+                              a variable-length field's value length */
+    uint32_t wire_offset;  /* where the value starts in its datagram (after a vlen prefix) */
+    uint32_t flags;        /* NGZ_FV_* */
+    uint32_t reserved;
+    const uint8_t *value;  /* host memory, valid until the context's next decode: the column cell, or
+                              for NGZ_K_VLEN the value's bytes in the batch input */
+} ngz_field_value;
+
+/* The fields of record `rec` of data set `set` (its index among datagram `dgram`'s data sets) of
+ * the last batch, scope fields first, into out[0, cap).  Returns the field count (> cap: only cap
+ * written), or NGZ_E_INVALID (datagram not NGZ_DG_OK, set or record out of range).  The first call
+ * after a decode copies the batch's columns to the host (as ngz_dgram_json). */
+int ngz_record_fields(ngz_ctx *ctx, uint32_t dgram, uint32_t set, uint32_t rec, ngz_field_value *out, uint32_t cap);
 
 /* Line callback of ngz_batch_json: datagram index, NGZ_DG_OK / NGZ_DG_ERROR,
  * the JSON text (not NUL-terminated), and the bytes FlowInfoCodec::decode

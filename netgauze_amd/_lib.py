@@ -34,9 +34,12 @@ ABI_FUNCTIONS = [
     "ngz_templates_json", "ngz_template_counts", "ngz_last_timing", "ngz_ctx_set_option",
     "ngz_template_kernel", "ngz_group_kernel", "ngz_columns_to_host", "ngz_columns_to_host_async", "ngz_dgram_json", "ngz_batch_json",
     "ngz_dgram_error", "ngz_template_counts_device", "ngz_slot_kernel", "ngz_rtc_drain", "ngz_abi_version",
-    "ngz_last_batch_info",
+    "ngz_last_batch_info", "ngz_record_fields", "ngz_placement_trials",
+    "ngz_message_records",
 ]
-NGZ_ABI_VERSION = 4
+NGZ_ABI_VERSION = 5
+# ngz_field_value.flags
+FV_SCOPE, FV_STRING, FV_VENDOR, FV_UNKNOWN, FV_SUBREG, FV_MPLS, FV_TCPFLAGS = 1, 2, 4, 8, 16, 32, 64
 NGZ_BATCH_PREDICTED, NGZ_BATCH_SPLIT, NGZ_BATCH_RERUN = 1, 2, 4  # ngz_last_batch_info
 # ngz_ctx_set_option
 (NGZ_OPT_SPECIALIZE, NGZ_OPT_BLOCKS_PER_CU, NGZ_OPT_ARENA_SHIFT, NGZ_OPT_CAP_PAD, NGZ_OPT_RTC_SYNC, NGZ_OPT_SPLIT,
@@ -122,6 +125,17 @@ class FieldInfo(ctypes.Structure):
     _fields_ = [("wire_offset", ctypes.c_uint16), ("wire_length", ctypes.c_uint16), ("width", ctypes.c_uint16),
                 ("kind", ctypes.c_uint8), ("is_scope", ctypes.c_uint8), ("col_off", ctypes.c_uint32),
                 ("pen", ctypes.c_uint32), ("ie_id", ctypes.c_uint16), ("reserved", ctypes.c_uint16)]
+
+
+class FieldValue(ctypes.Structure):
+    """ngz_field_value: one decoded field of a record (ngz_record_fields)."""
+    _fields_ = [("pen", ctypes.c_uint32), ("ie_id", ctypes.c_uint16), ("kind", ctypes.c_uint8),
+                ("dtype", ctypes.c_uint8), ("wire_length", ctypes.c_uint16), ("width", ctypes.c_uint16),
+                ("len", ctypes.c_uint32), ("wire_offset", ctypes.c_uint32), ("flags", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32), ("value", ctypes.c_void_p)]
+
+
+assert ctypes.sizeof(FieldValue) == 40
 
 
 class AggField(ctypes.Structure):
@@ -230,6 +244,12 @@ def load():
     lib.ngz_ctx_set_option.argtypes = [P, I, ctypes.c_int64]
     lib.ngz_ctx_set_option.restype = I
     lib.ngz_dgram_json.argtypes = [P, U32, ctypes.c_char_p, ctypes.c_size_t]
+    lib.ngz_record_fields.argtypes = [P, U32, U32, U32, ctypes.POINTER(FieldValue), U32]
+    lib.ngz_record_fields.restype = I
+    lib.ngz_placement_trials.argtypes = [P, ctypes.POINTER(ctypes.c_float), U32, ctypes.POINTER(ctypes.c_uint32)]
+    lib.ngz_placement_trials.restype = I
+    lib.ngz_message_records.argtypes = [P, P, P, P, U32, P]
+    lib.ngz_message_records.restype = I
     lib.ngz_dgram_json.restype = ctypes.c_int64
     lib.ngz_batch_json.argtypes = [P, P, JSON_LINE_FN, P]
     lib.ngz_batch_json.restype = ctypes.c_int64

@@ -1402,6 +1402,8 @@ int place_arena(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st) {
         ms.push_back(ctx->t_decode);
     }
     const size_t best = (size_t)(std::min_element(ms.begin(), ms.end()) - ms.begin());
+    ctx->place_ms = ms;
+    ctx->place_kept = (uint32_t)best;
     if (ngz_debug()) {
         fprintf(stderr, "[ngz] arena placement:");
         for (float m : ms) fprintf(stderr, " %.3f", m);
@@ -1900,6 +1902,45 @@ int ngz_slot_fields(ngz_ctx *ctx, uint32_t slot, ngz_field_info *fields, uint32_
 }
 
 int ngz_last_batch_info(ngz_ctx *ctx) { return ctx ? (int)ctx->batch_info : NGZ_E_INVALID; }
+
+int ngz_message_records(ngz_ctx *ctx, const uint8_t *bytes, const uint64_t *offsets, const uint32_t *lengths,
+                        uint32_t n, uint32_t *records) {
+    if (!ctx || (n && (!bytes || !offsets || !lengths || !records))) return NGZ_E_INVALID;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint8_t *p = bytes + offsets[i];
+        const uint32_t dl = lengths[i];
+        uint32_t r = 0, pos = 0, end = 0, pi = 0;
+        const uint32_t ver = dl >= 16 ? rd16(p) : 0, len = dl >= 16 ? rd16(p + 2) : 0;
+        if (ver == 10 && len >= 16 && dl >= len) {  // ipfix.rs:54-104: the sets up to the header length
+            pos = 16; end = len; pi = 0;
+        } else if (ver == 9 && dl >= 20) {          // netflow.rs:56-114: the sets up to the datagram end
+            pos = 20; end = dl; pi = 1;
+        }
+        while (pos + 4 <= end) {
+            const uint32_t id = rd16(p + pos), sl = rd16(p + pos + 2);
+            if (sl < 4 || sl > end - pos) break;
+            const int32_t vid = id >= 256 ? ctx->cur[pi][id] : -1;
+            if (vid >= 0) {
+                const DevPlan &P = ctx->versions[vid].plan;
+                uint64_t err = NGZ_NO_ERR;
+                if (P.has_vlen && P.rpl)  // the framing's own record walk (ipfix.rs:219-222)
+                    r += ngz_vlen_walk(p, pos + 4, pos + sl, P, &err, [](uint32_t, uint32_t) {});
+                else if (P.rec_len)
+                    r += (sl - 4) / P.rec_len;
+            }
+            pos += sl;
+        }
+        records[i] = r;
+    }
+    return NGZ_OK;
+}
+
+int ngz_placement_trials(ngz_ctx *ctx, float *decode_ms, uint32_t cap, uint32_t *kept) {
+    if (!ctx || (cap && !decode_ms)) return NGZ_E_INVALID;
+    for (size_t i = 0; i < ctx->place_ms.size() && i < cap; ++i) decode_ms[i] = ctx->place_ms[i];
+    if (kept) *kept = ctx->place_kept;
+    return (int)ctx->place_ms.size();
+}
 
 int ngz_slot_kernel(ngz_ctx *ctx, uint32_t slot) {
     if (!ctx || slot >= ctx->slot_spec.size()) return NGZ_E_INVALID;

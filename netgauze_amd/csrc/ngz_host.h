@@ -189,6 +189,9 @@ struct JsonView {
     const uint8_t *bytes = nullptr;          // batch bytes (host)
     std::vector<uint64_t> offs;
     std::vector<uint32_t> lens;
+    // ngz_record_fields: record offsets (in the datagram) of variable-length data sets, by set
+    // index, walked on first use
+    std::map<uint32_t, std::vector<uint32_t>> rec_pos;
 };
 
 }  // namespace ngzh
@@ -299,6 +302,8 @@ struct ngz_ctx {
     uint32_t cap_pad_windows = 0;               // NGZ_OPT_CAP_PAD
     int place_trials = 6;                       // arena placement trials on the first large batch (NGZ_OPT_PLACE_TRIALS)
     bool placed = false;
+    std::vector<float> place_ms;                // decode ms of each placement trial (ngz_placement_trials)
+    uint32_t place_kept = 0;                    // the trial whose arena was kept
     uint64_t arena_shift = 0;                   // NGZ_OPT_ARENA_SHIFT: columns start this far into the arena
     bool spin_wait = true;                      // wait for a batch by spinning on h_done (NGZ_SPIN=0: stream sync)
     float t_decode = 0, t_pipeline = 0;

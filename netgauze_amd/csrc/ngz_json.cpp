@@ -745,6 +745,91 @@ extern "C" int64_t ngz_dgram_json(ngz_ctx *ctx, uint32_t dgram, char *buf, size_
     return (int64_t)s.size();
 }
 
+static_assert(DT_octetArray == NGZ_DT_OCTET_ARRAY && DT_string == NGZ_DT_STRING && DT_ipv6Address == NGZ_DT_IPV6_ADDRESS &&
+                  DT_dateTimeNanoseconds == NGZ_DT_DATETIME_NANOSECONDS && DT_unsigned256 == NGZ_DT_UNSIGNED256,
+              "registry data types are the ABI's NGZ_DT_*");
+
+extern "C" int ngz_record_fields(ngz_ctx *ctx, uint32_t dgram, uint32_t set, uint32_t rec, ngz_field_value *out,
+                                 uint32_t cap) {
+    if (!ctx || dgram >= ctx->last_in.n || (cap && !out)) return NGZ_E_INVALID;
+    if (hipSetDevice(ctx->device)) return NGZ_E_DEVICE;
+    if (!ctx->json_view || ctx->json_view->serial != ctx->batch_serial) {
+        auto v = std::make_shared<JsonView>();
+        const int rc = json_view_load(ctx, nullptr, *v);
+        if (rc) return rc;
+        ctx->json_view = v;
+    }
+    JsonView &v = *ctx->json_view;
+    if (v.hdr[dgram].status != NGZ_DG_OK) return NGZ_E_INVALID;
+    const uint32_t s0 = v.set_first[dgram];
+    if (set >= v.set_first[dgram + 1] - s0) return NGZ_E_INVALID;
+    const ngz_set_info &si = v.sets[s0 + set];
+    if (rec >= si.n) return NGZ_E_INVALID;
+    const Version &ver = ctx->versions[ctx->slot_version[si.slot]];
+    const uint8_t *p = v.bytes + v.offs[dgram];
+    // the record's offset in the datagram: fixed records follow each other from the set payload;
+    // variable-length ones are walked once per set (ngz_vlen_walk, the framing's own walk)
+    uint32_t pos;
+    if (ver.plan.has_vlen) {
+        auto it = v.rec_pos.find(s0 + set);
+        if (it == v.rec_pos.end()) {
+            std::vector<uint32_t> starts;
+            uint64_t err = NGZ_NO_ERR;
+            ngz_vlen_walk(p, si.set_pos + 4u, si.set_pos + rd16(p + si.set_pos + 2), ver.plan, &err,
+                          [&](uint32_t, uint32_t at) { starts.push_back(at); });
+            it = v.rec_pos.emplace(s0 + set, std::move(starts)).first;
+        }
+        if (rec >= it->second.size()) return NGZ_E_INVALID;
+        pos = it->second[rec];
+    } else {
+        pos = si.set_pos + 4u + rec * ver.plan.rec_len;
+    }
+    const uint32_t nf = (uint32_t)ver.specs.size();
+    const uint32_t cap_rows = ctx->slot_rt[si.slot].cap;
+    const uint8_t *cols = v.cols[si.slot].data();
+    const uint64_t row = (uint64_t)si.rec0 + rec;
+    for (uint32_t f = 0; f < nf; ++f) {
+        const Spec &sp = ver.specs[f];
+        const DevField &fd = ver.plan.f[f];
+        const uint8_t *cell = cols + (uint64_t)cap_rows * fd.col_off + row * fd.width;
+        ngz_field_value fv{};
+        fv.pen = sp.pen;
+        fv.ie_id = sp.id;
+        fv.kind = fd.kind;
+        fv.dtype = sp.dtype;
+        fv.flags = (sp.scope ? NGZ_FV_SCOPE : 0u) |
+                   (fd.kind == NGZ_K_STR || (fd.kind == NGZ_K_VLEN && (fd.flags & 0x80)) ? NGZ_FV_STRING : 0u) |
+                   (sp.kind == IK_VENDOR || sp.kind == IK_VENDOR_UNKNOWN ? NGZ_FV_VENDOR : 0u) |
+                   (sp.kind == IK_UNKNOWN || sp.kind == IK_VENDOR_UNKNOWN ? NGZ_FV_UNKNOWN : 0u) |
+                   (sp.flags & 4 ? NGZ_FV_SUBREG : 0u) | (sp.flags & 1 ? NGZ_FV_MPLS : 0u) |
+                   (sp.flags & 2 ? NGZ_FV_TCPFLAGS : 0u);
+        fv.wire_length = sp.length;
+        fv.width = fd.width;
+        if (fd.kind == NGZ_K_VLEN) {  // {u64 batch offset, u32 length, u32 0}
+            uint64_t off;
+            uint32_t len;
+            memcpy(&off, cell, 8);
+            memcpy(&len, cell + 8, 4);
+            fv.value = v.bytes + off;
+            fv.len = len;
+            fv.wire_offset = (uint32_t)(off - v.offs[dgram]);
+            pos = fv.wire_offset + len;
+        } else {
+            fv.value = cell;
+            fv.len = fd.width;
+            if (fd.kind == NGZ_K_STR) {  // the string ends at its first NUL (generator.rs:1651-1668)
+                uint32_t n = 0;
+                while (n < fd.width && cell[n]) ++n;
+                fv.len = n;
+            }
+            fv.wire_offset = pos;
+            pos += sp.length;
+        }
+        if (f < cap) out[f] = fv;
+    }
+    return (int)nf;
+}
+
 extern "C" int64_t ngz_batch_json(ngz_ctx *ctx, const uint8_t *host_bytes, ngz_json_line_fn fn, void *user) {
     if (!ctx || !fn) return NGZ_E_INVALID;
     if (hipSetDevice(ctx->device)) return NGZ_E_DEVICE;

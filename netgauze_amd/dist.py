@@ -43,10 +43,11 @@ def shard_range(n, rank, world):
 def shard_by_records(records, rank, world):
     """Contiguous [first, last) message range of this rank, balanced by record count (SURVEY
     §8(e)): records[i] is message i's data-record count (message_records), and the cut between
-    ranks r-1 and r is the message boundary whose record prefix is nearest r/world of the total,
-    so every rank's records are within half a message of total/world and any two ranks differ
-    by at most one message's records -- MTU datagrams of 10 NetFlow v9 records and 64 KB IPFIX
-    messages of 1023 in one stream no longer give ranks 100x different loads."""
+    ranks r-1 and r is the message boundary whose record prefix is nearest r/world of the total.
+    Each cut lands within half of one message's records of its target, so a rank's records are
+    within one message of total/world, and two ranks differ by at most two messages' records
+    (records [3,3,3,3] over 3 ranks: 3/6/3 against 4) -- MTU datagrams of 10 NetFlow v9 records
+    and 64 KB IPFIX messages of 1023 in one stream no longer give ranks 100x different loads."""
     import numpy as np
     rec = np.asarray(records, dtype=np.int64)
     n = rec.size
@@ -65,14 +66,20 @@ def shard_by_records(records, rank, world):
     return cut(rank), cut(rank + 1)
 
 
-def message_records(data, offsets, lengths, record_len):
-    """Data records per message from the headers alone, for shard_by_records: NetFlow v9 takes
+def message_records(data, offsets, lengths, record_len=None, codec=None):
+    """Data records per message, for shard_by_records.  With a codec (a FlowInfoCodec that has
+    learnt the stream's templates): ngz_message_records, the library's count under the codec's
+    templates (variable-length sets walked record by record).  Without one (CPU tests, no
+    device) from the headers alone: NetFlow v9 takes
     the header count (netflow.rs:56-114; a packet carrying template flowsets counts those
     records too), IPFIX the data sets' lengths over their template's record length
     (ipfix.rs:193-214: records while the rest holds one).  record_len maps (version, template
     id) -> fixed record bytes; a data set of another template counts one record per 64 bytes.
     data: bytes-like or uint8 array; offsets / lengths: per-message integers."""
     import numpy as np
+    if codec is not None:
+        return codec.message_records(data, offsets, lengths)
+    record_len = record_len or {}
     buf = memoryview(bytes(data) if not isinstance(data, (bytes, bytearray)) else data)
     out = np.zeros(len(offsets), dtype=np.int64)
     for i, (o, ln) in enumerate(zip(list(offsets), list(lengths))):

@@ -145,6 +145,18 @@ class DecodedBatch:
         lib().ngz_dgram_json(self._codec._ctx, d, buf, n + 1)
         return buf.raw[:n].decode("utf-8")
 
+    def record_fields(self, d, s, r):
+        """ngz_record_fields: the fields of record r of datagram d's data set s (scope first) as
+        [(pen, ie_id, kind, dtype, flags, wire_length, wire_offset, value bytes)] -- the reference's
+        Box<[Field]> of DataRecord::parse (ipfix.rs:335-370), one typed value per IE."""
+        n = lib().ngz_record_fields(self._codec._ctx, d, s, r, None, 0)
+        if n < 0:
+            raise NgzError("ngz_record_fields(%d, %d, %d) = %d" % (d, s, r, n))
+        arr = (_lib.FieldValue * max(n, 1))()
+        lib().ngz_record_fields(self._codec._ctx, d, s, r, arr, n)
+        return [(f.pen, f.ie_id, f.kind, f.dtype, f.flags, f.wire_length, f.wire_offset,
+                 ctypes.string_at(f.value, f.len) if f.len else b"") for f in arr[:n]]
+
     def json_lines(self):
         """[(dgram, status, json, consumed)] for every datagram with a FlowInfo
         or an error (ngz_batch_json: one host copy of the whole batch)."""
@@ -287,6 +299,27 @@ class FlowInfoCodec:
     def last_batch_info(self):
         """ngz_last_batch_info bits: 1 predicted launches, 2 split framing, 4 a pass repeated."""
         return lib().ngz_last_batch_info(self._ctx)
+
+    def message_records(self, data, offsets, lengths):
+        """ngz_message_records: data records per message (host numpy arrays / bytes) under this
+        codec's current templates, for the record-balanced shard plan (dist.shard_by_records)."""
+        buf = np.frombuffer(bytes(data), dtype=np.uint8) if isinstance(data, (bytes, bytearray)) else \
+            np.ascontiguousarray(data, dtype=np.uint8)
+        offs = np.ascontiguousarray(offsets, dtype=np.uint64)
+        lens = np.ascontiguousarray(lengths, dtype=np.uint32)
+        out = np.zeros(len(offs), dtype=np.uint32)
+        self._check(lib().ngz_message_records(self._ctx, buf.ctypes.data, offs.ctypes.data, lens.ctypes.data,
+                                              len(offs), out.ctypes.data))
+        return out.astype(np.int64)
+
+    def placement_trials(self):
+        """ngz_placement_trials: ([decode ms of each arena trial], index of the kept arena), ([], 0)
+        before the context's first large batch placed its arena."""
+        n = lib().ngz_placement_trials(self._ctx, None, 0, None)
+        ms = (ctypes.c_float * max(n, 1))()
+        kept = ctypes.c_uint32()
+        lib().ngz_placement_trials(self._ctx, ms, n, ctypes.byref(kept))
+        return [float(x) for x in ms[:n]], int(kept.value)
 
     def last_timing(self):
         a, b = ctypes.c_float(), ctypes.c_float()

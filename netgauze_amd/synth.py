@@ -216,6 +216,71 @@ def mixed_stream(n, templates=CFG3_TEMPLATES, seed=SEED_CFG3, device="cpu"):
     return buf, torch.cat(offs)[order], torch.cat(lens)[order], recs
 
 
+def stream_index(n, templates=None):
+    """Message index of the stream t20 (templates None: ipfix_data_stream of t20_records, 1023 per
+    message) or mixed_stream(n, templates) builds, without its bytes: per message, numpy arrays
+    (template index, first record within the template's records, records).  A multi-GPU host
+    shards this one index by records (dist.shard_by_records) and builds only its range
+    (stream_range), so the ranks together decode exactly the one stream."""
+    import numpy as np
+    if templates is None:
+        m = (n + 1022) // 1023
+        first = np.arange(m, dtype=np.int64) * 1023
+        return np.zeros(m, dtype=np.int64), first, np.minimum(1023, n - first)
+    T = len(templates)
+    tix, firsts, counts, keys = [], [], [], []
+    for t, (tid, fields) in enumerate(templates):
+        nt = n // T + (1 if t < n % T else 0)
+        _, rl = field_offsets(fields)
+        per = (65535 - 20) // rl
+        m = (nt + per - 1) // per
+        f = np.arange(m, dtype=np.int64) * per
+        tix.append(np.full(m, t, dtype=np.int64))
+        firsts.append(f)
+        counts.append(np.minimum(per, nt - f))
+        keys.append(np.arange(m, dtype=np.int64) * T + t)  # mixed_stream's round-robin order
+    order = np.argsort(np.concatenate(keys), kind="stable")
+    return np.concatenate(tix)[order], np.concatenate(firsts)[order], np.concatenate(counts)[order]
+
+
+def stream_range(n, m0, m1, templates=None, seed=None, device="cpu"):
+    """Messages [m0, m1) of the stream_index(n, templates) stream, byte for byte as the whole
+    stream has them (records from the counter-based generator at their global position; export
+    time and sequence number of their message): (bytes, offsets, lengths, records)."""
+    import numpy as np
+    tix, first, count = stream_index(n, templates)
+    if templates is None:
+        seed = SEED_CFG2 if seed is None else seed
+        r0 = int(first[m0]) if m1 > m0 else 0
+        r1 = int(first[m1 - 1] + count[m1 - 1]) if m1 > m0 else 0
+        rec = t20_records(r1 - r0, seed=seed, device=device, first=r0)
+        buf, offs, lens = ipfix_data_stream(rec, 64, export_time0=1_700_000_000 + m0, seq0=r0)
+        return buf, offs, lens, r1 - r0
+    seed = SEED_CFG3 if seed is None else seed
+    parts, keys = [], []
+    for t, (tid, fields) in enumerate(templates):
+        sel = (np.nonzero(tix[m0:m1] == t)[0] + m0).tolist()
+        if not sel:
+            continue
+        _, rl = field_offsets(fields)
+        per = (65535 - 20) // rl
+        r0, r1 = int(first[sel[0]]), int(first[sel[-1]] + count[sel[-1]])
+        r = template_records(fields, r1 - r0, seed + t, device, first=r0)
+        b, o, ln = ipfix_data_stream(r, rl, tid=tid, rec_per_msg=per, export_time0=1_700_000_000 + r0 // per, seq0=r0)
+        parts.append((b, o, ln))
+        keys.append(torch.tensor(sel, dtype=torch.int64, device=b.device))
+    bufs, offs, lens = [], [], []
+    base = 0
+    for b, o, ln in parts:
+        bufs.append(b[:-16])
+        offs.append(o + base)
+        lens.append(ln)
+        base += b.numel() - 16
+    buf = torch.cat(bufs + [torch.zeros(16, dtype=torch.uint8, device=bufs[0].device)])
+    order = torch.argsort(torch.cat(keys))
+    return buf, torch.cat(offs)[order], torch.cat(lens)[order], int(count[m0:m1].sum())
+
+
 # --- config 4: NetFlow v9 + IPFIX variable-length / enterprise IEs ------------
 # NFv9 template 313 exactly as announced in the reference capture
 # assets/pcaps/101-NFv9-CISCO-cust_primitives (130-byte records, reduced sizes).

@@ -1,6 +1,8 @@
 """The multi-rank product path on the GPU: two processes share the one GPU of
 the test box (gloo carries the collective, as RCCL needs one GPU per rank),
-each decodes its contiguous message shard with libngz on cuda:0, and the
+each cuts its contiguous message range of the one shared stream balanced by
+records (ngz_message_records under its codec's templates, then
+dist.shard_by_records: SURVEY §8(e)), decodes it with libngz on cuda:0, and the
 per-template processed counts of both protocols (NetFlow v9 and IPFIX) are
 exchanged with netgauze_amd.dist.CountExchange.  The node-wide totals must
 equal a single oracle codec's over the whole stream, and every record must be
@@ -82,18 +84,25 @@ def _worker(rank, world, port, n, q):
         from netgauze_amd import dist as ndist
         from netgauze_amd.flow import FlowInfoCodec
         templates, data = _stream(n)
-        first, last = ndist.shard_range(len(data), rank, world)
         # library default: template kernels compiled in the background; a rank may exit with a
         # compile in flight (ngz_rtc.cpp: the exit join runs before hiprtc's / comgr's teardown)
         codec = FlowInfoCodec(0)
         codec.decode_datagrams(templates)
+        # the shard plan: every rank computes the same per-message records of the shared stream
+        # and cuts its own range (no data-path collective)
+        lens = [len(d) for d in data]
+        offs = [0]
+        for ln in lens[:-1]:
+            offs.append(offs[-1] + ln)
+        counts = ndist.message_records(b"".join(data), offs, lens, codec=codec)
+        first, last = ndist.shard_by_records(counts, rank, world)
         batch = codec.decode_datagrams(data[first:last])
         ok = int((batch.dgram_headers()["status"] == 0).sum())
         ex = ndist.CountExchange(codec)
         ex.step(reset=True)
         total, fitted = ex.totals()
         q.put((rank, int(batch.n_records), ok, last - first, total, fitted, codec.template_counts(10),
-               codec.template_counts(9)))
+               codec.template_counts(9), int(counts[first:last].sum()), int(counts.max())))
         import faulthandler  # a rank that does not exit: where it waits
         faulthandler.dump_traceback_later(45, repeat=False)
     except Exception as e:  # surface the failure instead of hanging the parent
@@ -130,6 +139,11 @@ def test_two_ranks_decode_shards_and_exchange_counts():
     assert sum(r[3] for r in res) == len(data)              # every message in exactly one shard
     assert sum(r[1] for r in res) == exp_records            # every record decoded exactly once
     assert sum(r[2] for r in res) == len(data)              # every data message Ok
+    # balanced by records: each rank decoded what the plan counted, and the two ranks are within
+    # two of the largest messages of each other (shard_by_records' bound) although the stream
+    # mixes 10-record NFv9 packets, ~15-record IPFIX MTU packets and 97-record T20 messages
+    assert all(r[1] == r[8] for r in res), [(r[1], r[8]) for r in res]
+    assert abs(res[0][1] - res[1][1]) <= 2 * res[0][9], [(r[1], r[9]) for r in res]
     for r in res:
         total, fitted = r[4], r[5]
         assert fitted and total == exp, (total, exp)        # node-wide templates.usage, protocols 10 and 9
