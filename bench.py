@@ -145,6 +145,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--split", action="store_true",
                     help="split framing (NGZ_OPT_SPLIT: variable-length record walks on a second stream)")
+    ap.add_argument("--place-probe", type=int, choices=[0, 1, 2], default=0,
+                    help="NGZ_OPT_PLACE_PROBE: arena placement trials timed by the batch's decode (0), by a probe "
+                         "of the decode's memory streams (1), or both with the decodes deciding (2)")
     ap.add_argument("--contexts", type=int, default=1,
                     help="decode contexts in flight (one host thread and HIP stream each, the steps dealt round "
                          "robin): batch k+1's framing overlaps batch k's decode")
@@ -187,9 +190,12 @@ def main():
 
     dev = torch.device("cuda", local)
     cdev = dev if dist is None or dist.get_backend() == "nccl" else torch.device("cpu")  # collective tensors
-    from netgauze_amd.flow import OPT_SPLIT
+    from netgauze_amd.flow import OPT_PLACE_PROBE, OPT_SPLIT
     copts = {OPT_SPLIT: 1} if args.split else {}
-    codec = FlowInfoCodec(local, rtc_sync=True, options=copts)  # template kernels compiled when learnt
+    popts = dict(copts)
+    if args.place_probe:
+        popts[OPT_PLACE_PROBE] = args.place_probe
+    codec = FlowInfoCodec(local, rtc_sync=True, options=popts)  # template kernels compiled when learnt
     n = args.records
     learnt = []  # the template messages every context learns before timing
     from netgauze_amd import dist as ndist
@@ -307,13 +313,15 @@ def main():
     traffic = committed_traffic(n, workload_desc)
     # the arena placement lottery of the first large batch (ngz_placement_trials): every trial's
     # decode time, the kept one, and the fraction the median trial would have reached
-    trials, kept = codec.placement_trials()
+    trials, kept, probes = codec.placement_trials(probes=True)
     placement = None
     if trials:
         med = sorted(trials)[len(trials) // 2]
         placement = {"placement_trials_ms": trials, "placement_kept": kept,
                      "placement_median_frac": alg_bytes / (med * 1e-3) / 1e9 / HBM_PEAK_GBS,
                      "placement_best_frac": alg_bytes / (min(trials) * 1e-3) / 1e9 / HBM_PEAK_GBS}
+    if any(probes):
+        placement = dict(placement or {}, placement_probe_ms=probes, placement_kept=kept)
     out = {
         "metric": {"t20": "IPFIX flow records/sec + GB/s (device-resident), 20-field fixed template",
                    "mixed8": "IPFIX flow records/sec (device-resident), config 3: 8 templates",

@@ -179,6 +179,9 @@ const char *ngz_last_error(ngz_ctx *ctx);
                                    launch per template */
 #define NGZ_OPT_PLACE_TRIALS 8  /* column arenas tried for a context's first large batch, the fastest
                                    kept (1..16, default 6; 1 = no trials, DESIGN.md §2 "Arena placement") */
+#define NGZ_OPT_PLACE_PROBE 9   /* how a placement trial is timed: 0 the batch's decode on each arena; 1 a
+                                   probe of the decode's memory streams over a fraction of the windows (one
+                                   decode in all, on the kept arena); 2 both, the decodes decide (diagnostics) */
 /* Options change how a batch runs, never its results.  The library reads no tuning from the
  * environment (only NGZ_DEBUG, stderr traces). */
 int ngz_ctx_set_option(ngz_ctx *ctx, int opt, int64_t value);
@@ -223,10 +226,11 @@ int ngz_message_records(ngz_ctx *ctx, const uint8_t *bytes, const uint64_t *offs
                         uint32_t n, uint32_t *records);
 
 /* The arena placement of the context's first large batch (NGZ_OPT_PLACE_TRIALS, DESIGN.md §2
- * "Arena placement"): the decode milliseconds of every trial arena, in trial order, into
- * decode_ms[0, cap), and in *kept (may be NULL) the trial whose arena the context kept (the
- * fastest).  Returns the number of trials: 0 before the placement ran (or with one trial). */
-int ngz_placement_trials(ngz_ctx *ctx, float *decode_ms, uint32_t cap, uint32_t *kept);
+ * "Arena placement"): per trial arena, in trial order, the batch's decode milliseconds into
+ * decode_ms[0, cap) and the probe's into probe_ms[0, cap) (either may be NULL; 0 where the trial
+ * did not run it, NGZ_OPT_PLACE_PROBE), and in *kept (may be NULL) the trial whose arena the
+ * context kept.  Returns the number of trials: 0 before the placement ran (or with one trial). */
+int ngz_placement_trials(ngz_ctx *ctx, float *decode_ms, float *probe_ms, uint32_t cap, uint32_t *kept);
 
 #define NGZ_BATCH_PREDICTED 1
 #define NGZ_BATCH_SPLIT 2

@@ -246,7 +246,8 @@ def load():
     lib.ngz_dgram_json.argtypes = [P, U32, ctypes.c_char_p, ctypes.c_size_t]
     lib.ngz_record_fields.argtypes = [P, U32, U32, U32, ctypes.POINTER(FieldValue), U32]
     lib.ngz_record_fields.restype = I
-    lib.ngz_placement_trials.argtypes = [P, ctypes.POINTER(ctypes.c_float), U32, ctypes.POINTER(ctypes.c_uint32)]
+    lib.ngz_placement_trials.argtypes = [P, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float), U32,
+                                         ctypes.POINTER(ctypes.c_uint32)]
     lib.ngz_placement_trials.restype = I
     lib.ngz_message_records.argtypes = [P, P, P, P, U32, P]
     lib.ngz_message_records.restype = I

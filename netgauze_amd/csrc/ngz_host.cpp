@@ -54,6 +54,9 @@ int ngz_rtc_compile_source(const std::string &src, std::string *log_out);
 int ngz_rtc_launch(void *fn, const BatchDev *B, uint32_t slot, uint32_t grid, uint32_t block, hipStream_t st);
 extern "C" int ngz_launch_counts(const BatchDev *B, uint64_t set_cap, hipStream_t st);
 extern "C" int ngz_launch_to_host(const void *src, void *dst, uint64_t bytes, hipStream_t st);
+extern "C" int ngz_launch_place_probe(const uint8_t *in, uint64_t in_bytes, uint8_t *blk, uint32_t cap, uint32_t total,
+                                      uint32_t rec_len, uint32_t frac16, const uint32_t *w, const uint32_t *off,
+                                      uint32_t ncol, uint32_t grid, hipStream_t st);
 extern "C" int ngz_launch_export(const BatchDev *B, BatchSummary *h_summary, SlotRT *h_slots,
                                  unsigned long long *h_proc, BatchSummary *next_summary,
                                  unsigned long long *next_proc, unsigned long long *h_done, unsigned long long seq,
@@ -1377,6 +1380,33 @@ static void trace_report(ngz_ctx *ctx, uint32_t S, hipStream_t st) {
 // context is therefore decoded on up to NGZ_PLACE_TRIALS fresh arenas (each
 // kept while the next is allocated, so every trial gets other memory); the
 // fastest is kept and the batch's results are the ones decoded on it.
+// The probe of one arena (k_place_probe over every slot with records, the first frac16 sixteenths of
+// each XCD's windows): device milliseconds.  Overwrites the columns of that arena.
+float place_probe(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st, uint32_t frac16) {
+    const uint32_t S = (uint32_t)ctx->slot_version.size();
+    const uint32_t grid = ctx->lds_blocks_per_cu * (uint32_t)ctx->n_cus;
+    HIPCHK(hipEventRecord(ctx->ev[0], st));
+    for (uint32_t s = 0; s < S; ++s) {
+        const SlotRT &rt = ctx->h_slots[s];
+        if (!rt.total) continue;
+        const Version &v = ctx->versions[ctx->slot_version[s]];
+        std::vector<uint32_t> w, off;
+        for (uint32_t f = 0; f < v.plan.n_fields && f < 32; ++f) {
+            w.push_back(v.plan.f[f].width);
+            off.push_back(v.plan.f[f].col_off);
+        }
+        if (ngz_launch_place_probe(in->bytes, in->bytes_size, ctx->d_arena.p + ctx->arena_shift + rt.block, rt.cap,
+                                   rt.total, std::max<uint32_t>(v.plan.rec_len, 16), frac16, w.data(), off.data(),
+                                   (uint32_t)w.size(), grid, st))
+            return -1.f;
+    }
+    HIPCHK(hipEventRecord(ctx->ev[1], st));
+    HIPCHK(hipEventSynchronize(ctx->ev[1]));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]));
+    return ms;
+}
+
 int place_arena(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st) {
     if (ctx->placed || ctx->place_trials <= 1) return 0;
     if (ctx->t_decode < 0.25f) return 0;  // small batches: launch-bound, placement does not show; try the next
@@ -1385,34 +1415,48 @@ int place_arena(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st) {
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return 0;
     const size_t cap = ctx->d_arena.cap;
     const int trials = (int)std::min<size_t>((size_t)ctx->place_trials, free_b / std::max<size_t>(cap, 1) / 2 + 1);
+    // NGZ_OPT_PLACE_PROBE: 0 every trial decodes the batch; 1 every trial runs the probe (a fraction
+    // of the decode's memory traffic) and only the kept arena decodes; 2 (diagnostics) both, the
+    // decodes decide
+    const int mode = ctx->place_probe;
+    const uint32_t frac16 = (uint32_t)std::max<int64_t>(1, std::min<int64_t>(16, ngz_knob("NGZ_PLACE_PROBE_FRAC", 2)));
     std::vector<DevBuf<uint8_t>> arenas{ctx->d_arena};
-    std::vector<float> ms{ctx->t_decode};
+    std::vector<float> ms{ctx->t_decode}, pms;
+    auto redo = [&]() {
+        int rc;
+        for (int tries = 0; (rc = run_pipeline(ctx, in, st, nullptr)) == 1 && tries < 4; ++tries) {}
+        return rc;
+    };
+    if (mode) pms.push_back(place_probe(ctx, in, st, frac16));  // (arena 0's columns are rewritten below)
     for (int k = 1; k < trials; ++k) {
         DevBuf<uint8_t> a;
         if (a.ensure(cap)) break;  // out of room: keep what was tried
         ctx->d_arena = a;
-        int rc;
-        for (int tries = 0; (rc = run_pipeline(ctx, in, st, nullptr)) == 1 && tries < 4; ++tries) {}
+        if (mode) pms.push_back(place_probe(ctx, in, st, frac16));
+        int rc = mode == 1 ? 0 : redo();
         arenas.push_back(ctx->d_arena);  // (a retry may have regrown it)
         if (rc) {
             ctx->d_arena = arenas[0];
             for (size_t i = 1; i < arenas.size(); ++i) arenas[i].release();
             return rc < 0 ? rc : fail(ctx, NGZ_E_NOMEM, "batch buffers kept overflowing");
         }
-        ms.push_back(ctx->t_decode);
+        if (mode != 1) ms.push_back(ctx->t_decode);
     }
-    const size_t best = (size_t)(std::min_element(ms.begin(), ms.end()) - ms.begin());
-    ctx->place_ms = ms;
+    const std::vector<float> &by = mode == 1 ? pms : ms;
+    const size_t best = (size_t)(std::min_element(by.begin(), by.end()) - by.begin());
+    ctx->place_ms = mode == 1 ? std::vector<float>() : ms;
+    ctx->place_probe_ms = pms;
     ctx->place_kept = (uint32_t)best;
     if (ngz_debug()) {
-        fprintf(stderr, "[ngz] arena placement:");
-        for (float m : ms) fprintf(stderr, " %.3f", m);
+        fprintf(stderr, "[ngz] arena placement (probe mode %d, %u/16):", mode, frac16);
+        for (size_t i = 0; i < by.size(); ++i)
+            fprintf(stderr, " %.3f/%.3f", i < ms.size() ? ms[i] : 0.f, i < pms.size() ? pms[i] : 0.f);
         fprintf(stderr, " ms -> %zu\n", best);
     }
     ctx->d_arena = arenas[best];
     for (size_t i = 0; i < arenas.size(); ++i)
         if (i != best) arenas[i].release();
-    if (best != arenas.size() - 1) {  // leave this batch's results in the kept arena
+    if (mode || best != arenas.size() - 1) {  // leave this batch's results in the kept arena
         int rc;
         for (int tries = 0; (rc = run_pipeline(ctx, in, st, nullptr)) == 1 && tries < 4; ++tries) {}
         if (rc) return rc < 0 ? rc : fail(ctx, NGZ_E_NOMEM, "batch buffers kept overflowing");
@@ -1607,6 +1651,10 @@ int ngz_ctx_set_option(ngz_ctx *ctx, int opt, int64_t value) {
     case NGZ_OPT_PLACE_TRIALS:
         if (value < 1 || value > 16) return fail(ctx, NGZ_E_INVALID, "NGZ_OPT_PLACE_TRIALS takes 1..16");
         ctx->place_trials = (int)value;
+        return NGZ_OK;
+    case NGZ_OPT_PLACE_PROBE:
+        if (value < 0 || value > 2) return fail(ctx, NGZ_E_INVALID, "NGZ_OPT_PLACE_PROBE takes 0, 1 or 2");
+        ctx->place_probe = (int)value;
         return NGZ_OK;
     }
     return fail(ctx, NGZ_E_INVALID, "unknown option");
@@ -1935,11 +1983,15 @@ int ngz_message_records(ngz_ctx *ctx, const uint8_t *bytes, const uint64_t *offs
     return NGZ_OK;
 }
 
-int ngz_placement_trials(ngz_ctx *ctx, float *decode_ms, uint32_t cap, uint32_t *kept) {
-    if (!ctx || (cap && !decode_ms)) return NGZ_E_INVALID;
-    for (size_t i = 0; i < ctx->place_ms.size() && i < cap; ++i) decode_ms[i] = ctx->place_ms[i];
+int ngz_placement_trials(ngz_ctx *ctx, float *decode_ms, float *probe_ms, uint32_t cap, uint32_t *kept) {
+    if (!ctx) return NGZ_E_INVALID;
+    const size_t n = std::max(ctx->place_ms.size(), ctx->place_probe_ms.size());
+    for (size_t i = 0; i < n && i < cap; ++i) {
+        if (decode_ms) decode_ms[i] = i < ctx->place_ms.size() ? ctx->place_ms[i] : 0.f;
+        if (probe_ms) probe_ms[i] = i < ctx->place_probe_ms.size() ? ctx->place_probe_ms[i] : 0.f;
+    }
     if (kept) *kept = ctx->place_kept;
-    return (int)ctx->place_ms.size();
+    return (int)n;
 }
 
 int ngz_slot_kernel(ngz_ctx *ctx, uint32_t slot) {

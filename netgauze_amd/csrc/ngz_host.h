@@ -303,6 +303,8 @@ struct ngz_ctx {
     int place_trials = 6;                       // arena placement trials on the first large batch (NGZ_OPT_PLACE_TRIALS)
     bool placed = false;
     std::vector<float> place_ms;                // decode ms of each placement trial (ngz_placement_trials)
+    std::vector<float> place_probe_ms;          // probe ms of each trial (NGZ_OPT_PLACE_PROBE)
+    int place_probe = 0;                        // NGZ_OPT_PLACE_PROBE
     uint32_t place_kept = 0;                    // the trial whose arena was kept
     uint64_t arena_shift = 0;                   // NGZ_OPT_ARENA_SHIFT: columns start this far into the arena
     bool spin_wait = true;                      // wait for a batch by spinning on h_done (NGZ_SPIN=0: stream sync)

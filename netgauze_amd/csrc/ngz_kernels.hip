@@ -1105,6 +1105,68 @@ __global__ void __launch_bounds__(256) k_to_host_bytes(const uint8_t *__restrict
 // ---------------------------------------------------------------------------
 // launch wrappers (C linkage, used by ngz_host.cpp)
 // ---------------------------------------------------------------------------
+// Arena placement probe (ngz_host.cpp place_arena, NGZ_OPT_PLACE_PROBE): the memory pattern of a
+// slot's LDS-staged decode without the parse -- 1024-row windows dealt XCD-aware as win_seq deals
+// them, each reading its record bytes with 16-byte loads and writing every column's run of the
+// window with 16-byte nontemporal stores at the slot's column stride -- over the first `frac16`
+// sixteenths of each XCD's stretch of windows.  The slow placement mode is DRAM contention among
+// those concurrent streams, set by the arena's pages and the stride, so a short
+// probe of the same streams ranks arenas without decoding the batch on each.
+struct ProbeCols {
+    uint32_t n;
+    uint32_t w[32];    // column widths (the probe takes the slot's first 32 columns)
+    uint32_t off[32];  // column offset factors (bytes per row before the column)
+};
+__global__ void __launch_bounds__(256) k_place_probe(const uint8_t *__restrict__ in, uint64_t in_bytes,
+                                                     uint8_t *__restrict__ blk, uint32_t cap, uint32_t total,
+                                                     uint32_t rec_len, uint32_t frac16, ProbeCols C) {
+    constexpr uint32_t ROWS = 1024;
+    const uint32_t nwin = (total + ROWS - 1) / ROWS;
+    // win_seq's dealing (ngz_dev.h): block b works through the (b % 8)-th contiguous eighth of the windows
+    const uint32_t G = gridDim.x, X = (G % 8 == 0 && G >= 8) ? 8u : 1u;
+    const uint32_t x = blockIdx.x % X, l = blockIdx.x / X;
+    const uint32_t per = (nwin + X - 1) / X;
+    const uint32_t start = min(nwin, x * per), end = min(nwin, start + per);
+    const uint32_t lim = start + ((end - start) * frac16 + 15) / 16;
+    const uint64_t n16 = in_bytes >> 4;
+    const __amdgpu_buffer_rsrc_t ri = __builtin_amdgcn_make_buffer_rsrc((void *)in, (short)0, 0x7FFFFFF0, 0x00020000);
+    for (uint32_t W = start + l; W < end && W < lim; W += G / X) {
+        // the window's record bytes: ROWS * rec_len from the batch (wrapping), 16 B per thread per step
+        const uint64_t b0 = ((uint64_t)W * ROWS * rec_len >> 4) % (n16 ? n16 : 1);
+        const uint32_t pieces = ROWS * rec_len / 16;
+        uint32_t acc = 0;
+        for (uint32_t p = threadIdx.x; p < pieces; p += blockDim.x) {
+            const uint64_t q = (b0 + p) % (n16 ? n16 : 1);
+            const v4u v = __builtin_amdgcn_raw_buffer_load_b128(ri, (uint32_t)(q << 4) & 0x7FFFFFF0u, 0, 0);
+            acc ^= v.x ^ v.y ^ v.z ^ v.w;
+        }
+        const uint32_t rows = min(ROWS, total - W * ROWS);
+        for (uint32_t c = 0; c < C.n; ++c) {
+            const uint32_t w = C.w[c];
+            uint8_t *dst = blk + (uint64_t)cap * C.off[c] + (uint64_t)W * ROWS * w;
+            const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, 0x7FFFFFF0, 0x00020000);
+            const uint32_t n = rows * w / 16;
+            for (uint32_t p = threadIdx.x; p < n; p += blockDim.x) {
+                const v4u x = {acc, acc ^ p, acc + p, acc};
+                __builtin_amdgcn_raw_buffer_store_b128(x, ro, 16 * p, 0, NGZ_ST_AUX);
+            }
+        }
+    }
+}
+
+extern "C" int ngz_launch_place_probe(const uint8_t *in, uint64_t in_bytes, uint8_t *blk, uint32_t cap, uint32_t total,
+                                      uint32_t rec_len, uint32_t frac16, const uint32_t *w, const uint32_t *off,
+                                      uint32_t ncol, uint32_t grid, hipStream_t st) {
+    ProbeCols C{};
+    C.n = ncol < 32 ? ncol : 32;
+    for (uint32_t i = 0; i < C.n; ++i) {
+        C.w[i] = w[i];
+        C.off[i] = off[i];
+    }
+    hipLaunchKernelGGL(k_place_probe, dim3(grid), dim3(256), 0, st, in, in_bytes, blk, cap, total, rec_len, frac16, C);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 extern "C" int ngz_launch_frame(const BatchDev *B, const uint32_t *hf_flag, const uint32_t *hf_first, hipStream_t st) {
     const uint32_t nb = (B->n + kFrameBlock - 1) / kFrameBlock;
     if (nb) hipLaunchKernelGGL(k_frame, dim3(nb), dim3(kFrameBlock), 0, st, *B, hf_flag, hf_first);

@@ -181,6 +181,7 @@ OPT_RTC_SYNC = 5
 OPT_SPLIT = 6         # split framing (flow_decode.h NGZ_OPT_SPLIT)
 OPT_GROUP = 7         # multi-template decode launches
 OPT_PLACE_TRIALS = 8  # column arenas tried for the first large batch
+OPT_PLACE_PROBE = 9   # placement trials timed by a probe (1) / decode and probe (2)
 D2H_KERNEL = 1  # NGZ_D2H_KERNEL
 
 
@@ -312,14 +313,17 @@ class FlowInfoCodec:
                                               len(offs), out.ctypes.data))
         return out.astype(np.int64)
 
-    def placement_trials(self):
+    def placement_trials(self, probes=False):
         """ngz_placement_trials: ([decode ms of each arena trial], index of the kept arena), ([], 0)
-        before the context's first large batch placed its arena."""
-        n = lib().ngz_placement_trials(self._ctx, None, 0, None)
+        before the context's first large batch placed its arena; probes=True adds the probe ms
+        (NGZ_OPT_PLACE_PROBE) as a third item."""
+        n = lib().ngz_placement_trials(self._ctx, None, None, 0, None)
         ms = (ctypes.c_float * max(n, 1))()
+        pm = (ctypes.c_float * max(n, 1))()
         kept = ctypes.c_uint32()
-        lib().ngz_placement_trials(self._ctx, ms, n, ctypes.byref(kept))
-        return [float(x) for x in ms[:n]], int(kept.value)
+        lib().ngz_placement_trials(self._ctx, ms, pm, n, ctypes.byref(kept))
+        out = ([float(x) for x in ms[:n] if x], int(kept.value))
+        return out + ([float(x) for x in pm[:n]],) if probes else out
 
     def last_timing(self):
         a, b = ctypes.c_float(), ctypes.c_float()
