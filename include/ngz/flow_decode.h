@@ -428,9 +428,10 @@ int64_t ngz_columns_to_host_async(ngz_ctx *ctx, void *dst, uint64_t cap, void *h
 /* Introspection (no device needed): the per-template decode kernel for one
  * IPFIX template record (template id u16, field count u16, field specifiers;
  * the body of a template set entry, ipfix.rs:384-413).  Writes the generated
- * HIP source to buf (NUL-terminated, truncated to cap) and, with compile != 0,
+ * HIP source to buf (NUL-terminated, truncated to cap) and, with compile bit 0,
  * compiles it for gfx950 with hiprtc (the build log follows the source on
- * failure).  Returns 0 on success, NGZ_E_INVALID if the template does not
+ * failure).  compile bit 1: the record is a NetFlow v9 template record of the
+ * same layout (netflow.rs:324-353), decoded by the NFv9 kernel shape.  Returns 0 on success, NGZ_E_INVALID if the template does not
  * parse or is not device-decodable, NGZ_E_DEVICE if compilation failed. */
 int ngz_template_kernel(const uint8_t *tmpl, size_t len, int compile, char *buf, size_t cap);
 

@@ -823,7 +823,7 @@ __device__ __forceinline__ void run_windows(const BatchDev &B, uint32_t slot, Sh
 // NGZ_VSTAGE_BYTES per wave decode through global loads as before (row_group).
 // ---------------------------------------------------------------------------
 #ifndef NGZ_VSTAGE_BYTES
-#define NGZ_VSTAGE_BYTES 10240
+#define NGZ_VSTAGE_BYTES NGZ_VSTAGE_IMAGE
 #endif
 constexpr uint32_t kVStageDw = NGZ_VSTAGE_BYTES / 4;
 constexpr uint32_t kVStageWaves = 4;  // the generated kernels run 256-thread workgroups

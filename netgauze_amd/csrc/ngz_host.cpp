@@ -2135,10 +2135,10 @@ extern "C" int ngz_dgram_error_json(ngz_ctx *ctx, uint32_t dgram, char *buf, siz
     ngz_dgram_hdr h;
     if (hipMemcpy(&h, ctx->d_hdr.p + dgram, sizeof h, hipMemcpyDeviceToHost) != hipSuccess) return NGZ_E_DEVICE;
     if (h.err_key == NGZ_NO_ERR) return NGZ_E_INVALID;
-    const uint32_t stop = (uint32_t)(h.err_key >> 48);
-    const uint32_t code = (uint32_t)(h.err_key >> 40) & 0xFF;
-    const uint32_t a = (uint32_t)(h.err_key >> 24) & 0xFFFF;
-    const uint32_t bval = (uint32_t)h.err_key & 0xFFFFFF;
+    uint32_t stop = (uint32_t)(h.err_key >> 48);
+    uint32_t code = (uint32_t)(h.err_key >> 40) & 0xFF;
+    uint32_t a = (uint32_t)(h.err_key >> 24) & 0xFFFF;
+    uint32_t bval = (uint32_t)h.err_key & 0xFFFFFF;
     std::string s;
     char b[256];
     if (code == E_HOST) {
@@ -2176,15 +2176,31 @@ extern "C" int ngz_dgram_error_json(ngz_ctx *ctx, uint32_t dgram, char *buf, siz
             std::vector<ngz_set_info> sets(nsets);
             hipMemcpy(sets.data(), ctx->d_sets.p, nsets * sizeof(ngz_set_info), hipMemcpyDeviceToHost);
             const Version *v = nullptr;
-            uint32_t set_end = 0;
+            uint32_t set_end = 0, set_pos = 0;
             for (auto &si : sets) {
                 const uint32_t e = si.set_pos + rd16(p.data() + si.set_pos + 2);
                 if (si.dgram == dgram && si.set_pos < stop && stop <= e) {
                     v = &ctx->versions[ctx->slot_version[si.slot]];
                     set_end = e;
+                    set_pos = si.set_pos;
                 }
             }
             if (!v || a >= v->specs.size()) { s = "null"; break; }
+            if ((code == E_REC_EOF || code == E_REC_FAIL) && v->plan.has_vlen) {
+                // the framing walk stopped in a record of a variable-length set; its fields before the
+                // failing one were read first, so a value error among them is the record's error
+                // (ngz_partial_record_err, ngz_internal.h)
+                uint64_t werr = NGZ_NO_ERR;
+                uint32_t rstart = set_pos + 4;
+                ngz_vlen_walk_exact(p.data(), set_pos + 4, set_end, v->plan, &werr, [](uint32_t, uint32_t) {}, 0u, &rstart);
+                const uint64_t ve = werr != NGZ_NO_ERR ? ngz_partial_record_err(p.data(), rstart, a, v->plan) : NGZ_NO_ERR;
+                if (ve != NGZ_NO_ERR) {
+                    stop = (uint32_t)(ve >> 48);
+                    code = (uint32_t)(ve >> 40) & 0xFF;
+                    a = (uint32_t)(ve >> 24) & 0xFFFF;
+                    bval = (uint32_t)ve & 0xFFFFFF;
+                }
+            }
             const Spec &sp = v->specs[a];
             std::string fe;
             const char *name = sp.name ? sp.name : "";
@@ -2244,7 +2260,7 @@ extern "C" int ngz_template_kernel(const uint8_t *tmpl, size_t len, int compile,
     const uint32_t count = rd16(tmpl + 2);
     c.pos = 4;
     Version v;
-    v.proto = 10;
+    v.proto = (compile & 2) ? 9 : 10;  // bit 1: a NetFlow v9 template record (netflow.rs:324-353)
     v.tid = tid;
     v.n_scope = 0;
     for (uint32_t i = 0; i < count; ++i) {
@@ -2257,7 +2273,7 @@ extern "C" int ngz_template_kernel(const uint8_t *tmpl, size_t len, int compile,
     if (!rtc_eligible(v.plan)) return NGZ_E_INVALID;
     std::string out = ngz_rtc_source(v.plan);
     int rc = NGZ_OK;
-    if (compile) {
+    if (compile & 1) {
         std::string log;
         if (ngz_rtc_compile_only(v.plan, &log)) {
             out += "\n// hiprtc log:\n" + log;

@@ -17,6 +17,7 @@
 #define NGZ_REG_WINDOW 256    // records per chunk window (4 passes of 64 lanes)
 #define NGZ_LDS_BUDGET 65536  // LDS bytes one workgroup may stage columns in
 #define NGZ_VSTAGE_REC_MAX 160 // longest fixed record of a staged-row kernel (64 records per 10 KiB image)
+#define NGZ_VSTAGE_IMAGE 10240 // bytes of a wave's LDS record image in the staged-row kernels (ngz_dev.h)
 
 #ifndef __HIPCC_RTC__
 // Experiment knobs (ngz_knobs.cpp): `dflt` in the product library; NGZ_<name> from the
@@ -152,11 +153,13 @@ __host__ __device__ inline bool ngz_utf8_ok(const uint8_t *p, uint32_t len, bool
 // DataRecord::parse read its fields before that one and Field::parse checked their values as it
 // read them (ipfix.rs:335-370, generator.rs:1635-1773), so the first value error among them is the
 // record's error -- a dateTime out of chrono's range, a nanosecond fraction of 1e9 outside a leap
-// second, a string that is not UTF-8.  The decode kernels check complete records only, so the walk
-// checks the failing one.  pos = the record's start.  Found by the differential fuzz corpus
-// (tests/test_gpu_fuzz.py: an invalid vlen string before a later field's EOF reported the EOF).
-__host__ __device__ inline uint64_t ngz_partial_record_err(const uint8_t *p, uint32_t pos, uint32_t stop_f,
-                                                           const DevPlan &pl) {
+// second, a string that is not UTF-8.  The decode kernels check complete records only.  The
+// walk's key stays the failure (it decides nothing else: the set is not counted either way), and
+// the host applies this check when it renders the error (ngz_host.cpp render_error): inlined into
+// the framing kernel's walk it took k_frame from 118 to 178 VGPRs with scratch spills (half the
+// occupancy, 0.65 -> 1.45 ms on config 4).  pos = the record's start.  Found by the differential
+// fuzz corpus (tests/test_gpu_fuzz.py: an invalid vlen string before a later field's EOF).
+inline uint64_t ngz_partial_record_err(const uint8_t *p, uint32_t pos, uint32_t stop_f, const DevPlan &pl) {
     for (uint32_t f = 0; f < stop_f; ++f) {
         const DevField &fd = pl.f[f];
         if (fd.kind == NGZ_K_VLEN) {
@@ -194,46 +197,44 @@ __host__ __device__ inline uint64_t ngz_partial_record_err(const uint8_t *p, uin
 // on_rec(n0 + k, record_offset) for each complete record only (a failing
 // record has no row); returns the number of complete records; on
 // UnexpectedEof / a template-constant field failure sets *err to the error
-// key (parsing stops there).  Exact form: one step per field.
+// key (parsing stops there).  Exact form: one step per field.  fail_start (host, error
+// rendering): the start of the record the walk failed in.
 template <class F>
 __host__ __device__ inline uint32_t ngz_vlen_walk_exact(const uint8_t *p, uint32_t pos, uint32_t end, const DevPlan &pl,
-                                                        uint64_t *err, F &&on_rec, uint32_t n0 = 0) {
+                                                        uint64_t *err, F &&on_rec, uint32_t n0 = 0,
+                                                        uint32_t *fail_start = nullptr) {
     const uint32_t minlen = pl.rec_len;  // vlen counted as 1
     uint32_t n = 0;
     while (minlen > 0 && end - pos >= minlen) {
         const uint32_t start = pos;
-        // the record's error: a value error of an earlier field, else the failure at field f
-        auto fail = [&](uint64_t key, uint32_t f) {
-            const uint64_t ve = ngz_partial_record_err(p, start, f, pl);
-            *err = ve != NGZ_NO_ERR ? ve : key;
-        };
+        if (fail_start) *fail_start = start;
         for (uint32_t f = 0; f < pl.n_fields; ++f) {
             const DevField &fd = pl.f[f];
             const uint32_t rem = end - pos;
             if (fd.kind == NGZ_K_FAIL) {  // fails before reading (InvalidLength, ...)
-                fail(ngz_err_key(pos, E_REC_FAIL, f, 0), f);
+                *err = ngz_err_key(pos, E_REC_FAIL, f, 0);
                 return n;
             }
             if (fd.kind == NGZ_K_VLEN) {
-                if (rem < 1) { fail(ngz_err_key(pos, E_REC_EOF, f, 1), f); return n; }
+                if (rem < 1) { *err = ngz_err_key(pos, E_REC_EOF, f, 1); return n; }
                 uint32_t len = p[pos];
                 pos += 1;
                 if (len == 255) {  // read_unsigned32_be(3)
-                    if (end - pos < 3) { fail(ngz_err_key(pos, E_REC_EOF, f, 3), f); return n; }
+                    if (end - pos < 3) { *err = ngz_err_key(pos, E_REC_EOF, f, 3); return n; }
                     len = ((uint32_t)p[pos] << 16) | ((uint32_t)p[pos + 1] << 8) | p[pos + 2];
                     pos += 3;
                 }
-                if (end - pos < len) { fail(ngz_err_key(pos, E_REC_EOF, f, len), f); return n; }
+                if (end - pos < len) { *err = ngz_err_key(pos, E_REC_EOF, f, len); return n; }
                 pos += len;
                 continue;
             }
             if (fd.kind == NGZ_K_DTFRAC) {  // two u32 reads (generator.rs:1748-1773)
-                if (rem < 4) { fail(ngz_err_key(pos, E_REC_EOF, f, 4), f); return n; }
-                if (rem < 8) { fail(ngz_err_key(pos + 4, E_REC_EOF, f, 4), f); return n; }
+                if (rem < 4) { *err = ngz_err_key(pos, E_REC_EOF, f, 4); return n; }
+                if (rem < 8) { *err = ngz_err_key(pos + 4, E_REC_EOF, f, 4); return n; }
                 pos += 8;
                 continue;
             }
-            if (rem < fd.len) { fail(ngz_err_key(pos, E_REC_EOF, f, fd.len), f); return n; }
+            if (rem < fd.len) { *err = ngz_err_key(pos, E_REC_EOF, f, fd.len); return n; }
             pos += fd.len;
         }
         on_rec(n0 + n, start);

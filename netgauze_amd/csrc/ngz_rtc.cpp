@@ -430,6 +430,146 @@ bool staged_rows(const DevPlan &P) {
     return !P.has_vlen && P.rpl && !P.lds_waves && P.proto == 9 && P.rec_len <= NGZ_VSTAGE_REC_MAX;
 }
 
+// Staged-row kernels of fixed records (NetFlow v9, staged_rows): the pass of a row-mode group keeps
+// every decoded cell in registers, then, once the wave's reads of its LDS record image are done,
+// writes the 64 rows' cells into that image column-major (column c at 64 * col_off, its rows
+// contiguous) and stores the image to the columns 16 bytes per lane: piece p of the image is the
+// 16-byte piece p - 4 col_off of column c's run for the group (piece_table).  A wave's 64 rows
+// then go out in ceil(row_bytes / 16) store instructions of 64 x 16 B instead of one narrow store
+// per field (1-8 B per lane: the NFv9 313 launch issued 44 store instructions per group, 215 B
+// each, and waited to issue 49 % of its wave cycles, profiles/r6h/cfg4/pmc_dispatch.txt).  The
+// group's last rows past the slot's total are padding rows of the column capacity (a multiple of
+// 256), so whole pieces are stored.  Chunk-mode batches keep the per-field stores (a chunk's rows
+// end inside a group).  Empty when the plan does not qualify: rows over 160 bytes (the image holds
+// 64 rows of 160 B), or a field too wide for registers.
+std::string piece_table(const DevPlan &P) {
+    std::string t = "__constant__ uint32_t ngz_pt[" + std::to_string(4 * P.row_bytes) + "] = {";
+    char b[32];
+    for (uint32_t f = 0, n = 0; f < P.n_fields; ++f) {
+        const DevField &d = P.f[f];
+        if (!d.width) continue;
+        for (uint32_t k = 0; k < 4 * d.width; ++k, ++n) {
+            snprintf(b, sizeof b, "%s%uu", n ? "," : "", d.col_off | (d.width << 8) | (k << 16));
+            t += b;
+        }
+    }
+    return t + "};\n";
+}
+
+std::string staged_row_body(const DevPlan &P, const std::vector<Item> &items) {
+    if (P.has_vlen || P.row_bytes == 0 || P.row_bytes > 160 || 64 * P.row_bytes > NGZ_VSTAGE_IMAGE) return {};
+    for (uint32_t f = 0, co = 0; f < P.n_fields; ++f) {  // columns back to back in field order
+        if (P.f[f].width && P.f[f].col_off != co) return {};
+        co += P.f[f].width;
+    }
+    for (const Item &it : items)
+        if (it.type == 3 || it.type == 5 || (it.type == 1 && (it.j || it.piece != it.len || it.width > 32 || it.pad_to != it.width)))
+            return {};
+    std::string s;
+    char b[1024];
+    s += "        const Pass &P0 = P[0];\n";
+    s += "        Pass Q = P0;\n";
+    s += "        const uint32_t seg = 0;\n";
+    s += "        (void)seg;\n";
+    // windows: greedy in record order, as generate_vlen plans them
+    std::vector<std::pair<uint32_t, uint32_t>> wins;
+    std::vector<int> item_win(items.size(), -1);
+    for (size_t i = 0; i < items.size(); ++i) {
+        const Item &it = items[i];
+        if (it.type == 4) continue;
+        if (wins.empty() || it.d0 < wins.back().first || it.d1 >= wins.back().first + kWinDw) wins.push_back({it.d0, 1});
+        auto &w = wins.back();
+        w.second = std::max(w.second, it.d1 - w.first + 1);
+        item_win[i] = (int)wins.size() - 1;
+    }
+    std::string stage;  // the cells into the LDS image, after every read of it
+    int cur = -1;
+    for (size_t i = 0; i < items.size(); ++i) {
+        const Item &it = items[i];
+        const int w = item_win[i];
+        if (w >= 0 && w != cur) {
+            snprintf(b, sizeof b, "        win_load_v<%u>(R[0], Q, %uu);\n", wins[w].second, 4 * wins[w].first);
+            s += b;
+            cur = w;
+        }
+        const uint32_t wb = w >= 0 ? 4 * wins[w].first : 0;
+        const uint32_t o = it.off - wb, at = 64 * it.col_off;
+        switch (it.type) {
+        case 0:
+            snprintf(b, sizeof b, "        const uint64_t v%u = num_value(R[0], P0, %uu, %uu, %uu, %uu, %uu);\n", it.f, o,
+                     it.off, it.f, it.len, it.kind);
+            s += b;
+            if (it.width == 1) snprintf(b, sizeof b, "            st[%uu + lane] = (uint8_t)v%u;\n", at, it.f);
+            else if (it.width == 2) snprintf(b, sizeof b, "            *(uint16_t *)&st[%uu + 2 * lane] = (uint16_t)v%u;\n", at, it.f);
+            else if (it.width == 4) snprintf(b, sizeof b, "            *(uint32_t *)&st[%uu + 4 * lane] = (uint32_t)v%u;\n", at, it.f);
+            else snprintf(b, sizeof b, "            *(uint64_t *)&st[%uu + 8 * lane] = v%u;\n", at, it.f);
+            stage += b;
+            break;
+        case 1: {  // raw cell: len bytes, width == len (<= 32), into ceil(width / 4) dwords
+            const uint32_t nd = (it.width + 3) / 4;
+            for (uint32_t m = 0; m < nd; ++m) {
+                if (4 * m + 4 <= it.len) {
+                    snprintf(b, sizeof b, "        const uint32_t c%u_%u = rdw(R[0], %uu);\n", it.f, m, o + 4 * m);
+                } else {
+                    std::string e = "0u";
+                    for (uint32_t q = 4 * m; q < std::min(4 * m + 4, it.len); ++q)
+                        e += " | (rbyte(R[0], " + std::to_string(o + q) + "u) << " + std::to_string(8 * (q - 4 * m)) + ")";
+                    snprintf(b, sizeof b, "        const uint32_t c%u_%u = %s;\n", it.f, m, e.c_str());
+                }
+                s += b;
+            }
+            if ((it.width & 3) == 0) {
+                for (uint32_t m = 0; m < nd; ++m) {
+                    snprintf(b, sizeof b, "            *(uint32_t *)&st[%uu + %uu * lane + %uu] = c%u_%u;\n", at, it.width,
+                             4 * m, it.f, m);
+                    stage += b;
+                }
+            } else {
+                for (uint32_t q = 0; q < it.width; ++q) {
+                    snprintf(b, sizeof b, "            st[%uu + %uu * lane + %uu] = (uint8_t)(c%u_%u >> %u);\n", at,
+                             it.width, q, it.f, q / 4, 8 * (q % 4));
+                    stage += b;
+                }
+            }
+            break;
+        }
+        case 2:
+            snprintf(b, sizeof b, "        check_str(R[0], P0, %uu, %uu, %uu, %uu, true);\n", o, it.off, it.f, it.len);
+            s += b;
+            break;
+        case 4:
+            snprintf(b, sizeof b, "        fail_field(P0, %uu, %uu);\n", it.off, it.f);
+            s += b;
+            break;
+        }
+    }
+    s += "        {  // stage the group's cells in the wave's image (every lane's reads of it are done), then store\n";
+    s += "            const uint32_t lane = threadIdx.x & 63;\n";
+    s += "            uint8_t *st = (uint8_t *)&ngz_vstage[(threadIdx.x >> 6) * kVStageDw];\n";
+    s += "            __builtin_amdgcn_fence(__ATOMIC_RELEASE, \"wavefront\");\n"
+         "            __builtin_amdgcn_wave_barrier();\n"
+         "            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, \"wavefront\");\n";
+    s += stage;
+    s += "            __builtin_amdgcn_fence(__ATOMIC_RELEASE, \"wavefront\");\n"
+         "            __builtin_amdgcn_wave_barrier();\n"
+         "            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, \"wavefront\");\n";
+    snprintf(b, sizeof b,
+             "            for (uint32_t p = lane; p < %uu; p += 64) {\n"
+             "                const uint32_t e = ngz_pt[p];\n"
+             "                const v4u x = *(const v4u *)&st[16 * p];\n"
+             "                uint8_t *d = P0.blk + (uint64_t)P0.cap * (e & 0xFFu) + (uint64_t)P0.prow * ((e >> 8) & 0xFFu) +\n"
+             "                             16u * (e >> 16);\n"
+             "                __builtin_nontemporal_store(x, (v4u *)d);\n"
+             "            }\n"
+             "            __builtin_amdgcn_fence(__ATOMIC_RELEASE, \"wavefront\");\n"
+             "            __builtin_amdgcn_wave_barrier();\n"
+             "            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, \"wavefront\");\n"
+             "        }\n",
+             4 * P.row_bytes);
+    s += b;
+    return s;
+}
+
 std::string generate_vlen(const DevPlan &P) {
     struct Seg {
         std::vector<Item> items;   // fixed fields, offsets relative to the segment start
@@ -593,17 +733,37 @@ std::string generate_vlen(const DevPlan &P) {
             if (it.type != 5) body += b;
         }
     }
+    const std::string sbody = P.has_vlen ? std::string() : staged_row_body(P, segs[0].items);
     std::string src;
     src += "// generated by ngz_rtc.cpp for plan " + signature(P) + "\n";
     src += cpol_defines() + "#define NGZ_VSTAGE 1\n#include \"ngz_dev.h\"\nusing namespace ngzdev;\n";
+    if (!sbody.empty()) src += piece_table(P);
     src += "extern \"C\" __global__ void __launch_bounds__(256) ngz_tpl(BatchDev B, uint32_t slot) {\n";
     src += "    if (sload(&B.summary->overflow)) return;\n";
     src += "    auto pass = [&](const Pass (&P)[1]) {\n";
     src += "        uint32_t R[1][WIN_DW];\n";
     src += (vexp & 8) ? std::string("        (void)P; (void)R;\n") : body;
     src += "    };\n";
+    if (!sbody.empty()) {
+        src += "    auto pass_rows = [&](const Pass (&P)[1]) {\n";
+        src += "        uint32_t R[1][WIN_DW];\n";
+        src += sbody;
+        src += "    };\n";
+    }
     if (P.has_vlen) {
         src += "    run_windows_staged(B, slot, pass);\n}\n";
+    } else if (!sbody.empty()) {
+        snprintf(b, sizeof b,
+                 "    const SlotRT rt = sload(&B.slots[slot]);\n"
+                 "    if (rt.mode == NGZ_MODE_ROW) {\n"
+                 "        run_windows_staged(B, slot, pass_rows);\n"
+                 "    } else {\n"
+                 "        auto want = [&](uint32_t s) { return s == slot; };\n"
+                 "        auto shape = [](uint32_t) { return RecShape{%uu, 0u, false}; };\n"
+                 "        run_chunks<1, false>(B, rt.chunk0, rt.chunk0 + rt.nchunks, want, shape, pass);\n"
+                 "    }\n}\n",
+                 P.rec_len);
+        src += b;
     } else {
         snprintf(b, sizeof b,
                  "    const SlotRT rt = sload(&B.slots[slot]);\n"
