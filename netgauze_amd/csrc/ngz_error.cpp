@@ -242,6 +242,7 @@ extern "C" int ngz_dgram_error(ngz_ctx *ctx, uint32_t dgram, ngz_error *err) {
         // IE named in the error for host-framed datagrams
         ngz_dgram_hdr h;
         if (hipMemcpy(&h, ctx->d_hdr.p + dgram, sizeof h, hipMemcpyDeviceToHost) != hipSuccess) return NGZ_E_DEVICE;
+        h.err_key = record_err_key(ctx, dgram, h.err_key);
         const uint32_t code = (uint32_t)(h.err_key >> 40) & 0xFF;
         if (code >= E_REC_DTMS && code <= E_REC_EOF && code != E_HOST) {
             const uint32_t stop = (uint32_t)(h.err_key >> 48);

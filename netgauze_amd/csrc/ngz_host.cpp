@@ -2130,15 +2130,52 @@ std::string utf8_error_msg(const uint8_t *s, uint32_t n) {
 
 }  // namespace
 
+namespace ngzh {
+// The error key of a datagram as the reference reports it.  The framing walk of a variable-length
+// set stops in a record at an UnexpectedEof or a template-constant failure, and that key is the
+// datagram's; DataRecord::parse had read the record's fields before the failing one, so a value
+// error among them is the record's error (ngz_partial_record_err, ngz_internal.h).  Applied here,
+// on the host, whenever an error is rendered (JSON text and ngz_dgram_error alike).
+uint64_t record_err_key(ngz_ctx *ctx, uint32_t dgram, uint64_t key) {
+    const uint32_t code = (uint32_t)(key >> 40) & 0xFF;
+    if (key == NGZ_NO_ERR || (code != E_REC_EOF && code != E_REC_FAIL)) return key;
+    const uint32_t stop = (uint32_t)(key >> 48), f = (uint32_t)(key >> 24) & 0xFFFF;
+    uint64_t off = 0;
+    uint32_t len = 0;
+    if (hipMemcpy(&off, ctx->last_in.offsets + dgram, 8, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(&len, ctx->last_in.lengths + dgram, 4, hipMemcpyDeviceToHost) != hipSuccess)
+        return key;
+    std::vector<uint8_t> p(len + 16, 0);
+    std::vector<ngz_set_info> sets(ctx->summary.n_sets);
+    if (hipMemcpy(p.data(), ctx->last_in.bytes + off, len, hipMemcpyDeviceToHost) != hipSuccess ||
+        (!sets.empty() &&
+         hipMemcpy(sets.data(), ctx->d_sets.p, sets.size() * sizeof(ngz_set_info), hipMemcpyDeviceToHost) != hipSuccess))
+        return key;
+    for (const auto &si : sets) {
+        const uint32_t e = si.set_pos + rd16(p.data() + si.set_pos + 2);
+        if (si.dgram != dgram || si.set_pos >= stop || stop > e) continue;
+        const Version &v = ctx->versions[ctx->slot_version[si.slot]];
+        if (!v.plan.has_vlen || f >= v.specs.size()) return key;
+        uint64_t werr = NGZ_NO_ERR;
+        uint32_t rstart = si.set_pos + 4u;
+        ngz_vlen_walk_exact(p.data(), si.set_pos + 4u, e, v.plan, &werr, [](uint32_t, uint32_t) {}, 0u, &rstart);
+        const uint64_t ve = werr != NGZ_NO_ERR ? ngz_partial_record_err(p.data(), rstart, f, v.plan) : NGZ_NO_ERR;
+        return ve != NGZ_NO_ERR ? ve : key;
+    }
+    return key;
+}
+}  // namespace ngzh
+
 extern "C" int ngz_dgram_error_json(ngz_ctx *ctx, uint32_t dgram, char *buf, size_t cap) {
     if (!ctx || dgram >= ctx->last_in.n) return NGZ_E_INVALID;
     ngz_dgram_hdr h;
     if (hipMemcpy(&h, ctx->d_hdr.p + dgram, sizeof h, hipMemcpyDeviceToHost) != hipSuccess) return NGZ_E_DEVICE;
     if (h.err_key == NGZ_NO_ERR) return NGZ_E_INVALID;
-    uint32_t stop = (uint32_t)(h.err_key >> 48);
-    uint32_t code = (uint32_t)(h.err_key >> 40) & 0xFF;
-    uint32_t a = (uint32_t)(h.err_key >> 24) & 0xFFFF;
-    uint32_t bval = (uint32_t)h.err_key & 0xFFFFFF;
+    h.err_key = record_err_key(ctx, dgram, h.err_key);
+    const uint32_t stop = (uint32_t)(h.err_key >> 48);
+    const uint32_t code = (uint32_t)(h.err_key >> 40) & 0xFF;
+    const uint32_t a = (uint32_t)(h.err_key >> 24) & 0xFFFF;
+    const uint32_t bval = (uint32_t)h.err_key & 0xFFFFFF;
     std::string s;
     char b[256];
     if (code == E_HOST) {
@@ -2176,31 +2213,15 @@ extern "C" int ngz_dgram_error_json(ngz_ctx *ctx, uint32_t dgram, char *buf, siz
             std::vector<ngz_set_info> sets(nsets);
             hipMemcpy(sets.data(), ctx->d_sets.p, nsets * sizeof(ngz_set_info), hipMemcpyDeviceToHost);
             const Version *v = nullptr;
-            uint32_t set_end = 0, set_pos = 0;
+            uint32_t set_end = 0;
             for (auto &si : sets) {
                 const uint32_t e = si.set_pos + rd16(p.data() + si.set_pos + 2);
                 if (si.dgram == dgram && si.set_pos < stop && stop <= e) {
                     v = &ctx->versions[ctx->slot_version[si.slot]];
                     set_end = e;
-                    set_pos = si.set_pos;
                 }
             }
             if (!v || a >= v->specs.size()) { s = "null"; break; }
-            if ((code == E_REC_EOF || code == E_REC_FAIL) && v->plan.has_vlen) {
-                // the framing walk stopped in a record of a variable-length set; its fields before the
-                // failing one were read first, so a value error among them is the record's error
-                // (ngz_partial_record_err, ngz_internal.h)
-                uint64_t werr = NGZ_NO_ERR;
-                uint32_t rstart = set_pos + 4;
-                ngz_vlen_walk_exact(p.data(), set_pos + 4, set_end, v->plan, &werr, [](uint32_t, uint32_t) {}, 0u, &rstart);
-                const uint64_t ve = werr != NGZ_NO_ERR ? ngz_partial_record_err(p.data(), rstart, a, v->plan) : NGZ_NO_ERR;
-                if (ve != NGZ_NO_ERR) {
-                    stop = (uint32_t)(ve >> 48);
-                    code = (uint32_t)(ve >> 40) & 0xFF;
-                    a = (uint32_t)(ve >> 24) & 0xFFFF;
-                    bval = (uint32_t)ve & 0xFFFFFF;
-                }
-            }
             const Spec &sp = v->specs[a];
             std::string fe;
             const char *name = sp.name ? sp.name : "";

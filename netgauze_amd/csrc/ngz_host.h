@@ -213,6 +213,8 @@ struct TemplateState {
     std::vector<int32_t> cur[2];
 };
 void state_save(ngz_ctx *ctx, TemplateState &s);
+// a datagram's error key as the reference reports it (a value error before a walk's failure, ngz_host.cpp)
+uint64_t record_err_key(ngz_ctx *ctx, uint32_t dgram, uint64_t key);
 void state_restore(ngz_ctx *ctx, const TemplateState &s);
 // D2H of the last batch (host_bytes: the batch bytes already in host memory, or null)
 int json_view_load(ngz_ctx *ctx, const uint8_t *host_bytes, JsonView &v);
