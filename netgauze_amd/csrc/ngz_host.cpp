@@ -1994,6 +1994,41 @@ int ngz_placement_trials(ngz_ctx *ctx, float *decode_ms, float *probe_ms, uint32
     return (int)n;
 }
 
+#ifdef NGZ_EXPERIMENTS
+extern "C" int ngz_launch_walk_probe(const uint8_t *bytes, uint64_t bytes_size, const uint64_t *offsets,
+                                     const ngz_set_info *sets, uint32_t nsets, const DevPlan *plans, uint32_t mode,
+                                     uint32_t lds_kb, uint32_t grid, uint32_t *out, hipStream_t st);
+// Experiment builds: the walk probe (k_walk_probe, ngz_kernels.hip) over the last batch's sets, `reps`
+// launches; out[0] records walked per launch, out[1] sets whose count differs; returns device ms per launch
+extern "C" float ngz_exp_walk_probe(ngz_ctx *ctx, uint32_t mode, uint32_t lds_kb, uint32_t blocks_per_cu, uint32_t reps,
+                                    uint32_t *out2) {
+    if (!ctx || !ctx->summary.n_sets || !reps) return -1.f;
+    hipStream_t st = ctx->stream;
+    uint32_t *d_out = nullptr;
+    if (hipMalloc(&d_out, 8) != hipSuccess) return -1.f;
+    const uint32_t grid = blocks_per_cu * (uint32_t)ctx->n_cus;
+    float ms = -1.f;
+    uint32_t h[2] = {0, 0};
+    hipMemsetAsync(d_out, 0, 8, st);
+    hipEventRecord(ctx->ev[0], st);
+    for (uint32_t r = 0; r < reps; ++r)
+        if (ngz_launch_walk_probe(ctx->last_in.bytes, ctx->last_in.bytes_size, ctx->last_in.offsets, ctx->d_sets.p,
+                                  ctx->summary.n_sets, ctx->d_plans.p, mode, lds_kb, grid, d_out, st))
+            break;
+    hipEventRecord(ctx->ev[1], st);
+    if (hipEventSynchronize(ctx->ev[1]) == hipSuccess && hipEventElapsedTime(&ms, ctx->ev[0], ctx->ev[1]) == hipSuccess &&
+        hipMemcpy(h, d_out, 8, hipMemcpyDeviceToHost) == hipSuccess) {
+        ms /= (float)reps;
+        out2[0] = h[0] / reps;
+        out2[1] = h[1] / reps;
+    } else {
+        ms = -1.f;
+    }
+    hipFree(d_out);
+    return ms;
+}
+#endif
+
 int ngz_slot_kernel(ngz_ctx *ctx, uint32_t slot) {
     if (!ctx || slot >= ctx->slot_spec.size()) return NGZ_E_INVALID;
     return ctx->slot_spec[slot];

@@ -1167,6 +1167,149 @@ extern "C" int ngz_launch_place_probe(const uint8_t *in, uint64_t in_bytes, uint
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+#ifdef NGZ_EXPERIMENTS
+// Experiment builds only ("walk the variable-length records next to the data they
+// decode"): how fast can the record walk run once the sets' bytes sit in LDS?  Over the last batch's
+// set table, the variable-length sets only:
+//   mode 0: one lane per set walks it from HBM (the walk of k_frame, alone);
+//   mode 1: each wave stages up to 64 consecutive sets (as many as fit its kWaveLds bytes) with
+//           coalesced 16-byte loads, 8 in flight per lane, then one lane per staged set walks it in LDS;
+//   mode 2: mode 1's staging without the walk.
+// out[0] += records walked, out[1] += sets whose count differs from the framing's.  kWaveLds sets the
+// waves per CU (four waves per workgroup): 8 KB 20, 12 KB 12, 16 KB 8, 36 KB 4.
+template <uint32_t kWaveLds>
+__global__ void __launch_bounds__(256) k_walk_probe(const uint8_t *__restrict__ bytes, uint64_t bytes_size,
+                                                    const uint64_t *__restrict__ offsets,
+                                                    const ngz_set_info *__restrict__ sets, uint32_t nsets,
+                                                    const DevPlan *__restrict__ plans, uint32_t mode,
+                                                    uint32_t *__restrict__ out) {
+    constexpr uint32_t kPieces = kWaveLds / 16;
+    __shared__ uint4 stage[4][kPieces];
+    __shared__ uint32_t tab[4][65];
+    __shared__ uint64_t atab[4][64];
+    const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t gw = blockIdx.x * 4 + wv, nw = gridDim.x * 4;
+    uint32_t recs = 0, bad = 0;
+    if (mode == 0) {
+        for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < nsets; j += gridDim.x * blockDim.x) {
+            const ngz_set_info si = sets[j];
+            const DevPlan &pl = plans[si.slot];
+            if (!pl.has_vlen) continue;
+            const uint8_t *p = bytes + offsets[si.dgram];
+            const uint32_t len = ((uint32_t)p[si.set_pos + 2] << 8) | p[si.set_pos + 3];
+            uint64_t err = NGZ_NO_ERR;
+            const uint32_t n = ngz_vlen_walk(p, si.set_pos + 4u, si.set_pos + len, pl, &err, [](uint32_t, uint32_t) {});
+            recs += n;
+            bad += n != si.n;
+        }
+    } else {
+        const uint32_t per = (nsets + nw - 1) / nw;
+        uint32_t s = min(nsets, gw * per);
+        const uint32_t se = min(nsets, s + per);
+        while (s < se) {
+            const uint32_t j = s + lane;
+            ngz_set_info si{};
+            bool v = false;
+            uint32_t len = 0, pieces = 0;
+            uint64_t a = 0, a0 = 0;
+            if (j < se) {
+                si = sets[j];
+                v = plans[si.slot].has_vlen;
+                a = offsets[si.dgram] + si.set_pos;
+                len = ((uint32_t)bytes[a + 2] << 8) | bytes[a + 3];
+                a0 = a & ~15ull;
+                if (v) pieces = (uint32_t)((a + len + 15 - a0) >> 4);
+            }
+            uint32_t inc = pieces;
+#pragma unroll
+            for (uint32_t o = 1; o < 64; o <<= 1) {
+                const uint32_t t = __shfl_up(inc, o);
+                if (lane >= o) inc += t;
+            }
+            const uint64_t take = __ballot(j < se && inc <= kPieces);
+            const uint32_t k = take == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~take);
+            if (k == 0) {  // one set larger than the wave's stage: walk it from HBM
+                if (lane == 0 && v) {
+                    uint64_t err = NGZ_NO_ERR;
+                    const uint8_t *p = bytes + offsets[si.dgram];
+                    const uint32_t n = ngz_vlen_walk(p, si.set_pos + 4u, si.set_pos + len, plans[si.slot], &err,
+                                                     [](uint32_t, uint32_t) {});
+                    recs += n;
+                    bad += n != si.n;
+                }
+                s += 1;
+                continue;
+            }
+            if (lane < k) {
+                tab[wv][lane] = inc - pieces;
+                atab[wv][lane] = a0;
+            }
+            if (lane == k - 1) tab[wv][k] = inc;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const uint32_t total = tab[wv][k];
+            for (uint32_t b = 0; b < total; b += 8 * 64) {
+                uint4 x[8];
+                uint32_t at[8];
+#pragma unroll
+                for (uint32_t i = 0; i < 8; ++i) {
+                    const uint32_t q = b + 64 * i + lane;
+                    at[i] = q;
+                    x[i] = make_uint4(0, 0, 0, 0);
+                    if (q < total) {
+                        uint32_t lo = 0, hi = k;  // owner: the last set whose first piece is <= q
+                        while (hi - lo > 1) {
+                            const uint32_t m = (lo + hi) >> 1;
+                            if (tab[wv][m] <= q) lo = m; else hi = m;
+                        }
+                        const uint64_t g = atab[wv][lo] + 16ull * (q - tab[wv][lo]);
+                        if (g + 16 <= bytes_size) x[i] = *(const uint4 *)(bytes + g);
+                    }
+                }
+#pragma unroll
+                for (uint32_t i = 0; i < 8; ++i)
+                    if (at[i] < total) stage[wv][at[i]] = x[i];
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (mode == 1 && lane < k && v) {
+                const uint8_t *ps = (const uint8_t *)&stage[wv][tab[wv][lane]] + (uint32_t)(a - a0);
+                uint64_t err = NGZ_NO_ERR;
+                const uint32_t n = ngz_vlen_walk(ps, 4u, len, plans[si.slot], &err, [](uint32_t, uint32_t) {});
+                recs += n;
+                bad += n != si.n;
+            } else if (mode == 2 && lane < k && v) {
+                recs += ((const uint8_t *)&stage[wv][tab[wv][lane]])[(uint32_t)(a - a0) + 3] != 0xEEu;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            s += k;
+        }
+    }
+    if (recs) atomicAdd(&out[0], recs);
+    if (bad) atomicAdd(&out[1], bad);
+}
+
+extern "C" int ngz_launch_walk_probe(const uint8_t *bytes, uint64_t bytes_size, const uint64_t *offsets,
+                                     const ngz_set_info *sets, uint32_t nsets, const DevPlan *plans, uint32_t mode,
+                                     uint32_t lds_kb, uint32_t grid, uint32_t *out, hipStream_t st) {
+    if (lds_kb == 8)
+        hipLaunchKernelGGL(k_walk_probe<8192>, dim3(grid), dim3(256), 0, st, bytes, bytes_size, offsets, sets, nsets, plans, mode, out);
+    else if (lds_kb == 12)
+        hipLaunchKernelGGL(k_walk_probe<12288>, dim3(grid), dim3(256), 0, st, bytes, bytes_size, offsets, sets, nsets, plans, mode, out);
+    else if (lds_kb == 16)
+        hipLaunchKernelGGL(k_walk_probe<16384>, dim3(grid), dim3(256), 0, st, bytes, bytes_size, offsets, sets, nsets, plans, mode, out);
+    else if (lds_kb == 36)
+        hipLaunchKernelGGL(k_walk_probe<36864>, dim3(grid), dim3(256), 0, st, bytes, bytes_size, offsets, sets, nsets, plans, mode, out);
+    else
+        return -1;
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+#endif
+
 extern "C" int ngz_launch_frame(const BatchDev *B, const uint32_t *hf_flag, const uint32_t *hf_first, hipStream_t st) {
     const uint32_t nb = (B->n + kFrameBlock - 1) / kFrameBlock;
     if (nb) hipLaunchKernelGGL(k_frame, dim3(nb), dim3(kFrameBlock), 0, st, *B, hf_flag, hf_first);
