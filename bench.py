@@ -151,6 +151,9 @@ def main():
     ap.add_argument("--contexts", type=int, default=1,
                     help="decode contexts in flight (one host thread and HIP stream each, the steps dealt round "
                          "robin): batch k+1's framing overlaps batch k's decode")
+    ap.add_argument("--submit", action="store_true",
+                    help="with --contexts P: one host thread keeps the P contexts' batches in flight through "
+                         "ngz_decode_batch_submit / ngz_decode_batch_wait instead of a thread per context")
     ap.add_argument("--e2e-contexts", type=int, default=3, help="--e2e: contexts (host threads) in flight")
     ap.add_argument("--e2e-ranges", type=int, default=12, help="--e2e: message ranges per batch")
     ap.add_argument("--e2e-duplex-contexts", type=int, default=6, help="--e2e duplex modes: contexts")
@@ -268,6 +271,20 @@ def main():
         for _ in range(args.steps):
             step()
             dec_ms.append(codec.last_timing()[0])
+    elif args.submit:
+        # one host thread: step k goes to context k % P once that context's previous batch is collected
+        pending = [False] * P
+        for k in range(args.steps):
+            c, st = ctxs[k % P]
+            if pending[k % P]:
+                c.decode_batch_wait()
+                dec_ms.append(c.last_timing()[0])
+            c.decode_batch_submit(buf, offs, lens, stream=st)
+            pending[k % P] = True
+        for i, (c, st) in enumerate(ctxs):
+            if pending[i]:
+                c.decode_batch_wait()
+                dec_ms.append(c.last_timing()[0])
     else:
         import threading
 
@@ -347,7 +364,7 @@ def main():
                    "records_per_gpu": n, "messages_per_gpu": int(offs.numel()),
                    "parallelism": ("record-balanced message ranges of one stream, one per GPU"
                                    if args.workload != "cfg4" else "a stream per GPU") if world > 1 else "single",
-                   **({"contexts": P} if P > 1 else {}), **({"split_framing": True} if args.split else {})},
+                   **({"contexts": P} if P > 1 else {}), **({"one_thread_submit": True} if P > 1 and args.submit else {}), **({"split_framing": True} if args.split else {})},
         "gbps_step": alg_bytes * world * args.steps / elapsed / 1e9,
         "templates_usage_exchange": usage,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -40,10 +40,10 @@
 extern "C" {
 #endif
 
-#define NGZ_ABI_VERSION 5  /* 2: ngz_slot_info.n_fields is 32-bit (no field cap), ngz_dgram_error,
+#define NGZ_ABI_VERSION 6  /* 2: ngz_slot_info.n_fields is 32-bit (no field cap), ngz_dgram_error,
                               ngz_template_counts_device; 3: ngz_abi_version, ngz_ctx_destroy joins the
                               context's background compiles; 4: ngz_columns_to_host_async;
-                              5: ngz_record_fields */
+                              5: ngz_record_fields; 6: ngz_decode_batch_submit / _wait */
 
 /* return codes */
 #define NGZ_OK 0
@@ -200,6 +200,18 @@ int ngz_rtc_drain(void);
  * stay valid until the next ngz_decode_batch on this context.
  * hip_stream: a hipStream_t (NULL = the context's own stream). */
 int ngz_decode_batch(ngz_ctx *ctx, const ngz_batch_in *in, ngz_batch_out *out, void *hip_stream);
+
+/* ngz_decode_batch without blocking the caller: the context's decode worker (one host thread per
+ * context, started on first use) runs it, and ngz_decode_batch_wait returns its result once *out
+ * is filled.  One host thread can so keep batches of several contexts in flight, each context on
+ * its own stream, as a collector with one socket thread does (FlowCollectorActor's loop).  Until
+ * the wait returns, the context takes no other call and *in / *out / the input bytes must stay
+ * valid.  Returns NGZ_OK when queued, NGZ_E_INVALID if a batch is already pending. */
+int ngz_decode_batch_submit(ngz_ctx *ctx, const ngz_batch_in *in, ngz_batch_out *out, void *hip_stream);
+
+/* Wait for the batch ngz_decode_batch_submit queued on ctx: ngz_decode_batch's return code, or
+ * NGZ_E_INVALID when nothing is pending. */
+int ngz_decode_batch_wait(ngz_ctx *ctx);
 
 /* Same, with the datagrams in host memory (pinned staging, H2D included). */
 int ngz_decode_batch_host(ngz_ctx *ctx, const uint8_t *bytes, uint64_t bytes_size,

@@ -35,9 +35,9 @@ ABI_FUNCTIONS = [
     "ngz_template_kernel", "ngz_group_kernel", "ngz_columns_to_host", "ngz_columns_to_host_async", "ngz_dgram_json", "ngz_batch_json",
     "ngz_dgram_error", "ngz_template_counts_device", "ngz_slot_kernel", "ngz_rtc_drain", "ngz_abi_version",
     "ngz_last_batch_info", "ngz_record_fields", "ngz_placement_trials",
-    "ngz_message_records",
+    "ngz_message_records", "ngz_decode_batch_submit", "ngz_decode_batch_wait",
 ]
-NGZ_ABI_VERSION = 5
+NGZ_ABI_VERSION = 6
 # ngz_field_value.flags
 FV_SCOPE, FV_STRING, FV_VENDOR, FV_UNKNOWN, FV_SUBREG, FV_MPLS, FV_TCPFLAGS = 1, 2, 4, 8, 16, 32, 64
 NGZ_BATCH_PREDICTED, NGZ_BATCH_SPLIT, NGZ_BATCH_RERUN = 1, 2, 4  # ngz_last_batch_info
@@ -221,6 +221,10 @@ def load():
     lib.ngz_last_error.restype = ctypes.c_char_p
     lib.ngz_decode_batch.argtypes = [P, ctypes.POINTER(BatchIn), ctypes.POINTER(BatchOut), P]
     lib.ngz_decode_batch.restype = I
+    lib.ngz_decode_batch_submit.argtypes = [P, ctypes.POINTER(BatchIn), ctypes.POINTER(BatchOut), P]
+    lib.ngz_decode_batch_submit.restype = I
+    lib.ngz_decode_batch_wait.argtypes = [P]
+    lib.ngz_decode_batch_wait.restype = I
     lib.ngz_decode_batch_host.argtypes = [P, P, U64, P, P, U32, ctypes.POINTER(BatchOut)]
     lib.ngz_decode_batch_host.restype = I
     lib.ngz_slot_fields.argtypes = [P, U32, ctypes.POINTER(FieldInfo), U32]

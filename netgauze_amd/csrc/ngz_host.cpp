@@ -1564,6 +1564,14 @@ int ngz_ctx_create(int device, ngz_ctx **out) {
 
 void ngz_ctx_destroy(ngz_ctx *ctx) {
     if (!ctx) return;
+    if (ctx->async.th.joinable()) {  // the decode worker finishes a submitted batch, then exits
+        {
+            std::lock_guard<std::mutex> lk(ctx->async.m);
+            ctx->async.stop = true;
+        }
+        ctx->async.cv.notify_all();
+        ctx->async.th.join();
+    }
     {
         // Synchronous drop, as the reference codec's (codec.rs:68-82): no kernel compile this context
         // started or waits on is still running once it returns, so a C / Rust host may return from main
@@ -1664,6 +1672,8 @@ static int wait_d2h(ngz_ctx *ctx);
 
 int ngz_decode_batch(ngz_ctx *ctx, const ngz_batch_in *in, ngz_batch_out *out, void *hip_stream) {
     if (!ctx || !in || !out) return NGZ_E_INVALID;
+    if (ctx->async.pending.load() && std::this_thread::get_id() != ctx->async.th.get_id())
+        return NGZ_E_INVALID;  // (no message: the worker may be writing the context's error text)
     if (in->n && (!in->bytes || !in->offsets || !in->lengths)) return fail(ctx, NGZ_E_INVALID, "null batch arrays");
     HIPCHK(hipSetDevice(ctx->device));
     hipStream_t st = hip_stream ? (hipStream_t)hip_stream : ctx->stream;
@@ -1849,9 +1859,64 @@ int ngz_decode_batch(ngz_ctx *ctx, const ngz_batch_in *in, ngz_batch_out *out, v
     return finish_batch(ctx, in, out, st);
 }
 
+// The decode worker of ngz_decode_batch_submit: runs one submitted batch at a time through
+// ngz_decode_batch on its own thread; exits when the context is destroyed (after a pending batch)
+static void async_worker(ngz_ctx *ctx) {
+    ngz_ctx::AsyncDecode &A = ctx->async;
+    std::unique_lock<std::mutex> lk(A.m);
+    for (;;) {
+        A.cv.wait(lk, [&] { return A.job || A.stop; });
+        if (!A.job) return;
+        const ngz_batch_in in = A.in;
+        ngz_batch_out *out = A.out;
+        void *stream = A.stream;
+        lk.unlock();
+        const int rc = ngz_decode_batch(ctx, &in, out, stream);
+        lk.lock();
+        A.rc = rc;
+        A.job = false;
+        A.result = true;
+        A.cv.notify_all();
+    }
+}
+
+int ngz_decode_batch_submit(ngz_ctx *ctx, const ngz_batch_in *in, ngz_batch_out *out, void *hip_stream) {
+    if (!ctx || !in || !out) return NGZ_E_INVALID;
+    if (in->n && (!in->bytes || !in->offsets || !in->lengths)) return fail(ctx, NGZ_E_INVALID, "null batch arrays");
+    ngz_ctx::AsyncDecode &A = ctx->async;
+    std::unique_lock<std::mutex> lk(A.m);
+    if (A.job || A.result) return NGZ_E_INVALID;  // pending: ngz_decode_batch_wait first (no message, see above)
+    if (!A.th.joinable()) {
+        try {
+            A.th = std::thread(async_worker, ctx);
+        } catch (...) {
+            return fail(ctx, NGZ_E_NOMEM, "decode worker thread");
+        }
+    }
+    A.in = *in;
+    A.out = out;
+    A.stream = hip_stream;
+    A.job = true;
+    A.pending.store(true);
+    A.cv.notify_all();
+    return NGZ_OK;
+}
+
+int ngz_decode_batch_wait(ngz_ctx *ctx) {
+    if (!ctx) return NGZ_E_INVALID;
+    ngz_ctx::AsyncDecode &A = ctx->async;
+    std::unique_lock<std::mutex> lk(A.m);
+    if (!A.job && !A.result) return NGZ_E_INVALID;
+    A.cv.wait(lk, [&] { return A.result; });
+    A.result = false;
+    A.pending.store(false);
+    return A.rc;
+}
+
 int ngz_decode_batch_host(ngz_ctx *ctx, const uint8_t *bytes, uint64_t bytes_size, const uint64_t *offsets,
                           const uint32_t *lengths, uint32_t n, ngz_batch_out *out) {
     if (!ctx || !out || (n && (!bytes || !offsets || !lengths))) return NGZ_E_INVALID;
+    if (ctx->async.pending.load()) return NGZ_E_INVALID;  // a submitted batch is pending
     HIPCHK(hipSetDevice(ctx->device));
     if (wait_d2h(ctx)) return NGZ_E_DEVICE;
     if (ctx->d_in_bytes.ensure(bytes_size + 16) || ctx->d_in_off.ensure(n + 1) || ctx->d_in_len.ensure(n + 1))

@@ -6,10 +6,14 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <cstdint>
 #include <cstdio>
 #include <memory>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <map>
 #include <vector>
 
@@ -308,6 +312,20 @@ struct ngz_ctx {
     std::vector<float> place_probe_ms;          // probe ms of each trial (NGZ_OPT_PLACE_PROBE)
     int place_probe = 0;                        // NGZ_OPT_PLACE_PROBE
     uint32_t place_kept = 0;                    // the trial whose arena was kept
+    // ngz_decode_batch_submit / _wait: the context's decode worker, started on first use
+    struct AsyncDecode {
+        std::thread th;
+        std::mutex m;
+        std::condition_variable cv;
+        bool job = false;     // a submitted batch the worker has not finished
+        bool result = false;  // a finished batch whose result the host has not collected
+        bool stop = false;
+        std::atomic<bool> pending{false};  // job || result: other calls on the context are refused
+        ngz_batch_in in{};
+        ngz_batch_out *out = nullptr;
+        void *stream = nullptr;
+        int rc = 0;
+    } async;
     uint64_t arena_shift = 0;                   // NGZ_OPT_ARENA_SHIFT: columns start this far into the arena
     bool spin_wait = true;                      // wait for a batch by spinning on h_done (NGZ_SPIN=0: stream sync)
     float t_decode = 0, t_pipeline = 0;

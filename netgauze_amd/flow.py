@@ -235,6 +235,28 @@ class FlowInfoCodec:
                                            ctypes.c_void_p(stream) if stream else None))
         return DecodedBatch(self, out, data)
 
+    def decode_batch_submit(self, data, offsets, lengths, n=None, stream=None):
+        """ngz_decode_batch_submit: queue decode_batch on the context's decode worker and return at
+        once; decode_batch_wait() gives the DecodedBatch.  One host thread can so keep several
+        contexts' batches in flight.  The tensors must stay alive until the wait returns."""
+        if getattr(self, "_pending", None) is not None:
+            raise RuntimeError("netgauze_amd: a submitted batch is pending (decode_batch_wait first)")
+        n = int(offsets.numel()) if n is None else n
+        bi = _lib.BatchIn(data.data_ptr(), data.numel(), offsets.data_ptr(), lengths.data_ptr(), n)
+        out = _lib.BatchOut()
+        self._check(lib().ngz_decode_batch_submit(self._ctx, ctypes.byref(bi), ctypes.byref(out),
+                                                  ctypes.c_void_p(stream) if stream else None))
+        self._pending = (bi, out, data, offsets, lengths)
+        return self
+
+    def decode_batch_wait(self):
+        """ngz_decode_batch_wait: the DecodedBatch of the submitted batch."""
+        p, self._pending = getattr(self, "_pending", None), None
+        if p is None:
+            raise RuntimeError("netgauze_amd: no submitted batch")
+        self._check(lib().ngz_decode_batch_wait(self._ctx))
+        return DecodedBatch(self, p[1], p[2])
+
     def decode_datagrams(self, datagrams):
         """Host-memory datagrams (list of bytes): H2D through the library."""
         lens = np.array([len(d) for d in datagrams], dtype=np.uint32)
