@@ -1456,7 +1456,12 @@ int place_arena(ngz_ctx *ctx, const ngz_batch_in *in, hipStream_t st) {
     ctx->d_arena = arenas[best];
     for (size_t i = 0; i < arenas.size(); ++i)
         if (i != best) arenas[i].release();
-    if (mode || best != arenas.size() - 1) {  // leave this batch's results in the kept arena
+    if (mode != 1) ctx->t_decode = ms[best];
+    // Every trial decoded the batch into its own arena (its columns and row tables; the headers, sets,
+    // chunks and counts outside the arena are the same for every trial), so the kept arena already
+    // holds this batch's results -- unless the probe ran over it after its decode (every arena in
+    // mode 1; arena 0, decoded before the trials, in mode 2): decode it there once more
+    if (mode == 1 || (mode == 2 && best == 0)) {
         int rc;
         for (int tries = 0; (rc = run_pipeline(ctx, in, st, nullptr)) == 1 && tries < 4; ++tries) {}
         if (rc) return rc < 0 ? rc : fail(ctx, NGZ_E_NOMEM, "batch buffers kept overflowing");
@@ -1871,7 +1876,12 @@ static void async_worker(ngz_ctx *ctx) {
         ngz_batch_out *out = A.out;
         void *stream = A.stream;
         lk.unlock();
-        const int rc = ngz_decode_batch(ctx, &in, out, stream);
+        int rc;
+        try {
+            rc = ngz_decode_batch(ctx, &in, out, stream);
+        } catch (...) {  // (host allocation failure: no exception may leave the worker thread)
+            rc = NGZ_E_NOMEM;
+        }
         lk.lock();
         A.rc = rc;
         A.job = false;
